@@ -1,0 +1,11 @@
+#!/usr/bin/env bash
+# Build libgwn.so (HIP, gfx950) in-tree.  Used by __graft_entry__.build() and by hand.
+set -euo pipefail
+ROOT="$(cd "$(dirname "$0")" && pwd)"
+SRC="$ROOT/graph-wavenet_amd/csrc"
+OUT="$ROOT/graph-wavenet_amd/gwn_amd/libgwn.so"
+HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
+"$HIPCC" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-result \
+  -I"$ROOT/include" -o "$OUT.tmp" "$SRC/gemm.hip" "$SRC/ops.hip"
+mv "$OUT.tmp" "$OUT"
+echo "built $OUT"

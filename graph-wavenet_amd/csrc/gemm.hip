@@ -1,0 +1,253 @@
+// Generic fp32 GEMM on the CDNA4 f32-input MFMA (v_mfma_f32_32x32x2_f32, exact fp32 fma chain).
+//
+// One kernel template serves every matrix-shaped step of the Graph WaveNet hot path:
+//   * diffusion  y_s = A^T x_s   (nconv, model.py:12-14)   M = nodes, N = slices*C, K = nodes
+//   * 1x1 / dilated convs        (model.py:135-151, 161-169) M = positions, N = C_out, K = C_in*taps
+//   * weight / adjacency grads   (their backward)           K = positions or slices*C, split-K
+// Tiles are staged k-major through LDS (double buffered, register prefetch of the next k-tile,
+// one barrier per k-tile); every wave owns TM x TN 32x32 accumulator tiles (16 VGPRs each).
+#include "gwn_internal.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int BK = 16;
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// Shared epilogue for EPI_STORE / EPI_MASKGRAD (also used by the split-K reduction).
+__device__ __forceinline__ void epi_store(const GemmParams& p, int m, int n, float v,
+                                          unsigned long long seed) {
+  if (p.epi == EPI_MASKGRAD) {
+    v = (p.mask[(long)m * p.ldmask_m + n] > 0.0f) ? v : 0.0f;
+  } else {
+    if (p.bias_n) v += p.bias_n[n];
+    if (p.relu) v = fmaxf(v, 0.0f);
+    if (p.drop_p > 0.0f) {
+      float u = gwn_uniform(seed, p.seed_salt, (unsigned long long)m * (unsigned)p.N + n);
+      v = (u >= p.drop_p) ? v * (1.0f / (1.0f - p.drop_p)) : 0.0f;
+    }
+  }
+  const int no = n / p.c_nin, ni = n - no * p.c_nin;  // C0 shares the column map of C
+  if (p.C0) v += p.beta * p.C0[(long)m * p.ldc0_m + (long)ni * p.ldc0_n + (long)no * p.c0_no_stride];
+  p.C[(long)m * p.ldc_m + (long)ni * p.ldc_n + (long)no * p.c_no_stride] = v;
+}
+
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int LDA = BM + 4;
+  constexpr int LDB = BN + 4;
+  constexpr int A_PER = (BM * BK + NT - 1) / NT;
+  constexpr int B_PER = (BN * BK + NT - 1) / NT;
+  __shared__ float As[2][BK * LDA];
+  __shared__ float Bs[2][BK * LDB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int split = blockIdx.z;
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+
+  const bool a_tiled = (p.a_kin % BK == 0) || (p.a_kin >= p.K);
+  const bool b_tiled = (p.b_kin % BK == 0) || (p.b_kin >= p.K);
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  float ra[A_PER], rb[B_PER];
+
+  auto load = [&](int k0) {
+    {
+      // k-tiles never straddle an a_kin block when a_kin % BK == 0 (the hot configurations);
+      // otherwise (e.g. NCHW slices with T = 12 inner steps) the block is resolved per element.
+      const int ko0 = k0 / p.a_kin;
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i) {
+        const int e = tid + i * NT;
+        int kk, mm;
+        if (AKC) { kk = e % BK; mm = e / BK; } else { kk = e / BM; mm = e % BM; }
+        const int m = m0 + mm, k = k0 + kk;
+        const int ko = a_tiled ? ko0 : (int)((unsigned)k / (unsigned)p.a_kin);
+        const int ki = k - ko * p.a_kin;
+        const int srow = m + ko * p.a_row_shift;
+        float v = 0.0f;
+        if (e < BM * BK && m < p.M && k < kend && srow >= 0 && srow < p.a_rows)
+          v = p.A[(long)srow * p.lda_m + (long)ki * p.lda_k + (long)ko * p.a_ko_stride];
+        ra[i] = v;
+      }
+    }
+    {
+      const int kb0 = k0 / p.b_kin;
+#pragma unroll
+      for (int i = 0; i < B_PER; ++i) {
+        const int e = tid + i * NT;
+        int kk, nn;
+        if (BKC) { kk = e % BK; nn = e / BK; } else { kk = e / BN; nn = e % BN; }
+        const int n = n0 + nn, k = k0 + kk;
+        float v = 0.0f;
+        if (e < BN * BK && n < p.N && k < kend) {
+          const int kb = b_tiled ? kb0 : (int)((unsigned)k / (unsigned)p.b_kin);
+          const int kj = k - kb * p.b_kin;
+          const int no = (unsigned)n / (unsigned)p.b_nin, ni = n - no * p.b_nin;
+          v = p.B[(long)kj * p.ldb_k + (long)kb * p.b_ko_stride + (long)ni * p.ldb_n +
+                  (long)no * p.b_no_stride];
+        }
+        rb[i] = v;
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int e = tid + i * NT;
+      int kk, mm;
+      if (AKC) { kk = e % BK; mm = e / BK; } else { kk = e / BM; mm = e % BM; }
+      if (e < BM * BK) As[buf][kk * LDA + mm] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int e = tid + i * NT;
+      int kk, nn;
+      if (BKC) { kk = e % BK; nn = e / BK; } else { kk = e / BN; nn = e % BN; }
+      if (e < BN * BK) Bs[buf][kk * LDB + nn] = rb[i];
+    }
+  };
+
+  const int nkt = (kend > kbeg) ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nkt > 0) {
+    load(kbeg);
+    store(0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) load(kbeg + (kt + 1) * BK);
+    const float* as = &As[buf][0];
+    const float* bs = &Bs[buf][0];
+#pragma unroll
+    for (int kp = 0; kp < BK / 2; ++kp) {
+      const int krow = 2 * kp + (lane >> 5);
+      float a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = as[krow * LDA + (wm * TM + i) * 32 + (lane & 31)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = bs[krow * LDB + (wn * TN + j) * 32 + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nkt) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  const unsigned long long seed = p.seed_ptr ? *p.seed_ptr : 0ull;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + (wn * TN + j) * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        float v = p.alpha * acc[i][j][r];
+        if (p.ksplit > 1) {
+          if (m < p.M && n < p.N) p.part[((long)split * p.M + m) * p.N + n] = v;
+        } else if (p.epi == EPI_GATE) {
+          // column n = 2c + g: g=0 filter (tanh), g=1 gate (sigmoid); partner lives in lane^1
+          v += (n < p.N) ? p.bias_n[n] : 0.0f;
+          const float other = __shfl_xor(v, 1);
+          if (((lane & 1) == 0) && m < p.M && n < p.N) {
+            const float f = tanhf(v), g = sigmoidf_(other);
+            const float xg = f * g;
+            const int c = n >> 1;
+            p.C[(long)m * p.ldc_m + c] = xg;
+            p.aux[(long)m * p.ld_aux + n] = f;
+            p.aux[(long)m * p.ld_aux + n + 1] = g;
+            if (p.aux2 && m >= p.aux2_row0) p.aux2[(long)(m - p.aux2_row0) * p.ld_aux2 + c] = xg;
+          }
+        } else if (m < p.M && n < p.N) {
+          epi_store(p, m, n, v, seed);
+        }
+      }
+    }
+  }
+}
+
+__global__ void splitk_reduce_kernel(const GemmParams p) {
+  const long total = (long)p.M * p.N;
+  const unsigned long long seed = p.seed_ptr ? *p.seed_ptr : 0ull;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    float v = 0.0f;
+    for (int s = 0; s < p.ksplit; ++s) v += p.part[(long)s * total + idx];
+    const int m = (int)(idx / p.N), n = (int)(idx - (long)m * p.N);
+    epi_store(p, m, n, v, seed);
+  }
+}
+
+template <int WM, int WN, int TM, int TN>
+int launch_cfg(const GemmParams& p, bool akc, bool bkc, hipStream_t s) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.ksplit);
+  dim3 block(64 * WM * WN);
+  if (akc && bkc) gemm_kernel<WM, WN, TM, TN, true, true><<<grid, block, 0, s>>>(p);
+  else if (akc) gemm_kernel<WM, WN, TM, TN, true, false><<<grid, block, 0, s>>>(p);
+  else if (bkc) gemm_kernel<WM, WN, TM, TN, false, true><<<grid, block, 0, s>>>(p);
+  else gemm_kernel<WM, WN, TM, TN, false, false><<<grid, block, 0, s>>>(p);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+}  // namespace
+
+int gwn_gemm_launch(const GemmParams& pin, hipStream_t s) {
+  GemmParams p = pin;
+  GWN_REQUIRE(p.M > 0 && p.N > 0 && p.K >= 0, "gemm: bad shape");
+  if (p.a_kin <= 0 || p.a_kin > p.K) p.a_kin = (p.K > 0 ? p.K : 1);
+  if (p.b_kin <= 0 || p.b_kin > p.K) p.b_kin = (p.K > 0 ? p.K : 1);
+  if (p.b_nin <= 0 || p.b_nin > p.N) p.b_nin = p.N;
+  if (p.c_nin <= 0 || p.c_nin > p.N) p.c_nin = p.N;
+  if (p.a_rows <= 0) p.a_rows = 0x7fffffff;
+  GWN_REQUIRE(p.C != nullptr && p.A != nullptr && p.B != nullptr, "gemm: null operand");
+  GWN_REQUIRE(p.epi != EPI_GATE || (p.ksplit <= 1 && p.aux && p.bias_n && (p.N % 2) == 0),
+              "gemm: gate epilogue needs aux, bias, even N and no split-K");
+  GWN_REQUIRE(p.epi != EPI_MASKGRAD || p.mask, "gemm: mask-grad epilogue needs a mask");
+  if (p.ksplit < 1) p.ksplit = 1;
+  if (p.ksplit > 1) {
+    GWN_REQUIRE(p.part != nullptr, "gemm: split-K needs a partial buffer");
+    int chunk = (p.K + p.ksplit - 1) / p.ksplit;
+    chunk = (chunk + BK - 1) / BK * BK;
+    p.kchunk = chunk;
+    p.ksplit = (p.K + chunk - 1) / chunk;
+    if (p.ksplit < 1) p.ksplit = 1;
+  } else {
+    p.kchunk = p.K > 0 ? (p.K + BK - 1) / BK * BK : BK;
+  }
+  const bool akc = (p.lda_k == 1 && p.lda_m != 1);
+  const bool bkc = (p.ldb_k == 1 && p.ldb_n != 1);
+  int rc;
+  if (p.N <= 32) rc = launch_cfg<4, 1, 2, 1>(p, akc, bkc, s);          // 256 x 32
+  else if (p.N <= 64 && p.M > 128 && p.M <= 224) rc = launch_cfg<7, 1, 1, 2>(p, akc, bkc, s);  // 224 x 64
+  else if (p.N <= 64) rc = launch_cfg<4, 1, 1, 2>(p, akc, bkc, s);     // 128 x 64
+  else if (p.M > 160 && p.M <= 224) rc = launch_cfg<7, 1, 1, 2>(p, akc, bkc, s);
+  else if (p.M >= 128) rc = launch_cfg<2, 2, 2, 2>(p, akc, bkc, s);    // 128 x 128
+  else rc = launch_cfg<2, 2, 1, 1>(p, akc, bkc, s);                    // 64 x 64
+  if (rc != GWN_OK || p.ksplit <= 1) return rc;
+  const long total = (long)p.M * p.N;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  splitk_reduce_kernel<<<blocks, 256, 0, s>>>(p);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}

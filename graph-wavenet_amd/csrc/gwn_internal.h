@@ -1,0 +1,50 @@
+// Internal helpers shared by the HIP translation units of libgwn (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/gwn.h"
+
+#define GWN_CHECK_LAUNCH()                                   \
+  do {                                                       \
+    hipError_t e_ = hipGetLastError();                       \
+    if (e_ != hipSuccess) return gwn_set_error(GWN_ERR_HIP, hipGetErrorString(e_)); \
+  } while (0)
+
+#define GWN_REQUIRE(cond, msg)                                \
+  do {                                                        \
+    if (!(cond)) return gwn_set_error(GWN_ERR_ARG, msg);      \
+  } while (0)
+
+int gwn_set_error(int code, const char* msg);
+
+// ---------------------------------------------------------------------------------------------
+// Generic fp32 MFMA GEMM (gemm.hip).  C(m,n) = epi(alpha * sum_k A(m,k) B(k,n)).
+//
+// Two-level indices let one launch walk "slices" that are not a single stride apart:
+//   A(m,k): ko = k / a_kin, ki = k % a_kin; src_row = m + ko*a_row_shift (valid iff
+//           0 <= src_row < a_rows); addr = A + src_row*lda_m + ki*lda_k + ko*a_ko_stride
+//   B(k,n): kb = k / b_kin, kj = k % b_kin; no = n / b_nin, ni = n % b_nin;
+//           addr = B + kj*ldb_k + kb*b_ko_stride + ni*ldb_n + no*b_no_stride
+//   C(m,n): no = n / c_nin, ni = n % c_nin; addr = C + m*ldc_m + ni*ldc_n + no*c_no_stride
+// a_kin / b_kin must be multiples of 16 (or >= K); b_nin / c_nin multiples of 32 (or >= N).
+// ---------------------------------------------------------------------------------------------
+enum GemmEpi {
+  EPI_STORE = 0,      // v = alpha*acc + bias_n[n] (+relu) (+dropout) + beta*C0
+  EPI_GATE = 1,       // n = 2c+g: (tanh(f) * sigmoid(g)) -> C[m][c]; aux = (tanh f, sigmoid g); aux2 dual store
+  EPI_MASKGRAD = 2,   // v = alpha*acc * (mask[m][n] > 0) + beta*C0   (relu backward)
+};
+
+typedef gwn_gemm_desc GemmParams;
+
+int gwn_gemm_launch(const GemmParams& p, hipStream_t stream);
+
+// Deterministic counter-based dropout RNG (splitmix64 finaliser), identical in every kernel
+// that applies or differentiates the same mask.
+__host__ __device__ inline float gwn_uniform(unsigned long long seed, unsigned long long salt,
+                                             unsigned long long idx) {
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (salt + 1) + idx * 0xD1B54A32D192ED03ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z = z ^ (z >> 31);
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}

@@ -1,0 +1,899 @@
+// Op-level C-ABI of libgwn: the Graph WaveNet hot-path operators (reference model.py /
+// engine.py / Utils/util.py) built from the MFMA GEMM (gemm.hip) and the reduction /
+// element-wise kernels below.  All reductions use a fixed order (per-block partials, then an
+// in-order merge), so every result is bitwise reproducible.
+#include <math.h>
+#include <string.h>
+#include "gwn_internal.h"
+
+namespace {
+thread_local char g_err[512] = "";
+
+constexpr int RED_BLOCKS = 512;  // partial-reduction blocks (fixed -> fixed summation order)
+
+gwn_gemm_desc gemm_zero() {
+  gwn_gemm_desc d;
+  memset(&d, 0, sizeof(d));
+  d.alpha = 1.0f;
+  d.beta = 1.0f;
+  d.ksplit = 1;
+  return d;
+}
+
+int pick_ksplit(int M, int N, int K) {
+  // aim for ~1024 blocks over the output tiles (see gemm.hip launch configs: >= 64x64 tiles)
+  long tiles = ((M + 127) / 128) * (long)((N + 63) / 64);
+  if (tiles < 1) tiles = 1;
+  long ks = 1024 / tiles;
+  long maxks = K / 256;
+  if (ks > maxks) ks = maxks;
+  if (ks < 1) ks = 1;
+  return (int)ks;
+}
+
+// ---------------------------------------------------------------------------------------------
+// block-level fixed-order sum over blockDim.x (power of two) threads
+template <int NT>
+__device__ float block_sum(float v, float* sh) {
+  sh[threadIdx.x] = v;
+  __syncthreads();
+#pragma unroll
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
+    __syncthreads();
+  }
+  float r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+template <int NT>
+__device__ float block_max(float v, float* sh) {
+  sh[threadIdx.x] = v;
+  __syncthreads();
+#pragma unroll
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) sh[threadIdx.x] = fmaxf(sh[threadIdx.x], sh[threadIdx.x + s]);
+    __syncthreads();
+  }
+  float r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// adaptive adjacency: one block per row v.  logits l[w] = relu(sum_k e1[v][k] e2[k][w])
+__global__ void adp_fwd_kernel(const float* e1, const float* e2, int n, int d, float* adp, int ld) {
+  __shared__ float sh[256];
+  const int v = blockIdx.x;
+  float mx = -INFINITY;
+  for (int w = threadIdx.x; w < n; w += 256) {
+    float l = 0.0f;
+    for (int k = 0; k < d; ++k) l = fmaf(e1[(long)v * d + k], e2[(long)k * n + w], l);
+    l = fmaxf(l, 0.0f);
+    mx = fmaxf(mx, l);
+  }
+  mx = block_max<256>(mx, sh);
+  float sum = 0.0f;
+  for (int w = threadIdx.x; w < n; w += 256) {
+    float l = 0.0f;
+    for (int k = 0; k < d; ++k) l = fmaf(e1[(long)v * d + k], e2[(long)k * n + w], l);
+    l = fmaxf(l, 0.0f);
+    const float ex = expf(l - mx);
+    adp[(long)v * ld + w] = ex;
+    sum += ex;
+  }
+  sum = block_sum<256>(sum, sh);
+  const float inv = 1.0f / sum;
+  for (int w = threadIdx.x; w < ld; w += 256)
+    adp[(long)v * ld + w] = (w < n) ? adp[(long)v * ld + w] * inv : 0.0f;
+}
+
+// dlogit[v][w] = adp*(dadp - sum_w' adp*dadp) * [pre > 0]
+__global__ void adp_bwd_kernel(const float* e1, const float* e2, const float* adp, const float* dadp,
+                               int n, int d, int ld, float* dl) {
+  __shared__ float sh[256];
+  const int v = blockIdx.x;
+  float dot = 0.0f;
+  for (int w = threadIdx.x; w < n; w += 256) dot += adp[(long)v * ld + w] * dadp[(long)v * ld + w];
+  dot = block_sum<256>(dot, sh);
+  for (int w = threadIdx.x; w < ld; w += 256) {
+    float g = 0.0f;
+    if (w < n) {
+      float l = 0.0f;
+      for (int k = 0; k < d; ++k) l = fmaf(e1[(long)v * d + k], e2[(long)k * n + w], l);
+      const float a = adp[(long)v * ld + w];
+      g = (l > 0.0f) ? a * (dadp[(long)v * ld + w] - dot) : 0.0f;
+    }
+    dl[(long)v * ld + w] = g;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ void start_conv_kernel(const float* x, long sb, long sc, long sn, long st, int B, int cin,
+                                  int n, int t, int t0, const float* W, const float* bias, int c,
+                                  float* out, float* xin) {
+  const long rows = (long)t0 * B * n;
+  const long total = rows * c;
+  const int pad = t0 - t;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const long row = idx / c;
+    const int co = (int)(idx - row * c);
+    const int v = (int)(row % n);
+    const long tb = row / n;
+    const int b = (int)(tb % B);
+    const int tt = (int)(tb / B);
+    const int ts = tt - pad;
+    float acc = bias[co];
+    for (int ci = 0; ci < cin; ++ci) {
+      const float xv = (ts >= 0) ? x[b * sb + ci * sc + v * sn + (long)ts * st] : 0.0f;
+      acc = fmaf(W[co * cin + ci], xv, acc);
+      if (co == 0 && xin) xin[row * cin + ci] = xv;
+    }
+    out[idx] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// gated TCN backward element-wise part: dfg from dxg (+ skip grad) and the saved tanh/sigmoid.
+__global__ void gate_bwd_kernel(const float* dxg, long ld_dxg, const float* dskip, long ld_dskip,
+                                int skip_row0, const float* fg, long rows, int c, float* dfg) {
+  const long total = rows * c;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const long r = idx / c;
+    const int ch = (int)(idx - r * c);
+    float g = dxg ? dxg[r * ld_dxg + ch] : 0.0f;
+    if (dskip && r >= skip_row0) g += dskip[(r - skip_row0) * ld_dskip + ch];
+    const float f = fg[r * 2 * c + 2 * ch], s = fg[r * 2 * c + 2 * ch + 1];
+    dfg[r * 2 * c + 2 * ch] = g * s * (1.0f - f * f);
+    dfg[r * 2 * c + 2 * ch + 1] = g * f * s * (1.0f - s);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// column partial sums: partial[blk][j] = sum over the block's row chunk of f(a[r][j])
+//   mode 0: a;  mode 1: a * ((b - mean[j]) * rstd[j])
+template <int MODE>
+__global__ void colsum_partial_kernel(const float* a, long lda, const float* b, long ldb,
+                                      const float* mean, const float* rstd, long rows, int ncol,
+                                      float* partial) {
+  __shared__ float sh[256];
+  const long chunk = (rows + gridDim.x - 1) / gridDim.x;
+  const long r0 = blockIdx.x * chunk;
+  const long r1 = (r0 + chunk < rows) ? r0 + chunk : rows;
+  if (ncol <= 256) {
+    const int lanes = 256 / ncol;  // row lanes per column
+    const int col = threadIdx.x % ncol, rl = threadIdx.x / ncol;
+    float acc = 0.0f;
+    if (rl < lanes) {
+      for (long r = r0 + rl; r < r1; r += lanes) {
+        float v = a[r * lda + col];
+        if (MODE == 1) v *= (b[r * ldb + col] - mean[col]) * rstd[col];
+        acc += v;
+      }
+    }
+    sh[threadIdx.x] = (rl < lanes) ? acc : 0.0f;
+    __syncthreads();
+    if ((int)threadIdx.x < ncol) {
+      float s = 0.0f;
+      for (int i = 0; i < lanes; ++i) s += sh[i * ncol + threadIdx.x];
+      partial[(long)blockIdx.x * ncol + threadIdx.x] = s;
+    }
+  } else {
+    for (int col = threadIdx.x; col < ncol; col += 256) {
+      float acc = 0.0f;
+      for (long r = r0; r < r1; ++r) {
+        float v = a[r * lda + col];
+        if (MODE == 1) v *= (b[r * ldb + col] - mean[col]) * rstd[col];
+        acc += v;
+      }
+      partial[(long)blockIdx.x * ncol + col] = acc;
+    }
+  }
+}
+
+__global__ void colsum_final_kernel(const float* partial, int nparts, int ncol, float* out,
+                                    int accumulate) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < ncol; j += gridDim.x * blockDim.x) {
+    float s = 0.0f;
+    for (int i = 0; i < nparts; ++i) s += partial[(long)i * ncol + j];
+    out[j] = accumulate ? out[j] + s : s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// BatchNorm statistics: per block (count, mean, M2) over its row chunk (two passes over the chunk),
+// merged in block order with Chan's formula.
+__global__ void bn_partial_kernel(const float* z, long rows, int c, float* part) {
+  __shared__ float sh[256];
+  const long chunk = (rows + gridDim.x - 1) / gridDim.x;
+  const long r0 = blockIdx.x * chunk;
+  const long r1 = (r0 + chunk < rows) ? r0 + chunk : rows;
+  const long cnt = (r1 > r0) ? r1 - r0 : 0;
+  const int lanes = 256 / c;
+  const int col = threadIdx.x % c, rl = threadIdx.x / c;
+  float s = 0.0f;
+  if (rl < lanes)
+    for (long r = r0 + rl; r < r1; r += lanes) s += z[r * c + col];
+  sh[threadIdx.x] = (rl < lanes) ? s : 0.0f;
+  __syncthreads();
+  float mean = 0.0f;
+  if (cnt > 0) {
+    float t = 0.0f;
+    for (int i = 0; i < lanes; ++i) t += sh[i * c + col];
+    mean = t / (float)cnt;
+  }
+  __syncthreads();
+  float q = 0.0f;
+  if (rl < lanes)
+    for (long r = r0 + rl; r < r1; r += lanes) {
+      const float dlt = z[r * c + col] - mean;
+      q += dlt * dlt;
+    }
+  sh[threadIdx.x] = (rl < lanes) ? q : 0.0f;
+  __syncthreads();
+  if ((int)threadIdx.x < c) {
+    float m2 = 0.0f;
+    for (int i = 0; i < lanes; ++i) m2 += sh[i * c + threadIdx.x];
+    float* pp = part + (long)blockIdx.x * 3 * c;
+    pp[threadIdx.x] = (float)cnt;
+    pp[c + threadIdx.x] = mean;
+    pp[2 * c + threadIdx.x] = m2;
+  }
+}
+
+__global__ void bn_finalize_kernel(const float* part, int nparts, int c, float momentum, float eps,
+                                   float* running_mean, float* running_var, float* save_mean,
+                                   float* save_rstd) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= c) return;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int i = 0; i < nparts; ++i) {
+    const float* pp = part + (long)i * 3 * c;
+    const double nb = pp[j];
+    if (nb <= 0.0) continue;
+    const double mb = pp[c + j], m2b = pp[2 * c + j];
+    const double nn = n + nb;
+    const double delta = mb - mean;
+    mean += delta * nb / nn;
+    m2 += m2b + delta * delta * n * nb / nn;
+    n = nn;
+  }
+  const double var = (n > 0.0) ? m2 / n : 0.0;
+  save_mean[j] = (float)mean;
+  save_rstd[j] = (float)(1.0 / sqrt(var + (double)eps));
+  if (running_mean) {
+    const double unbiased = (n > 1.0) ? m2 / (n - 1.0) : var;
+    running_mean[j] = (float)((1.0 - momentum) * running_mean[j] + momentum * mean);
+    running_var[j] = (float)((1.0 - momentum) * running_var[j] + momentum * unbiased);
+  }
+}
+
+__global__ void bn_apply_kernel(const float* z, long rows, int c, const float* mean,
+                                const float* rstd, const float* rvar, float eps,
+                                const float* gamma, const float* beta, float* out) {
+  const long total = rows * c;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(idx % c);
+    const float rs = rstd ? rstd[j] : 1.0f / sqrtf(rvar[j] + eps);
+    out[idx] = (z[idx] - mean[j]) * rs * gamma[j] + beta[j];
+  }
+}
+
+// dz = gamma*rstd*(dy - k1 - xhat*k2); dres[r + row0] = dz; dres rows < row0 zeroed; dh = dropout'(dz)
+__global__ void bn_bwd_apply_kernel(const float* dy, const float* z, long rows, int c,
+                                    const float* gamma, const float* mean, const float* rstd,
+                                    const float* sums, float* dres, int res_row0, float* dh,
+                                    const unsigned long long* seed_ptr, unsigned long long salt,
+                                    float drop_p) {
+  const long total = rows * c;
+  const unsigned long long seed = seed_ptr ? *seed_ptr : 0ull;
+  const float inv_n = 1.0f / (float)rows;
+  const long zero_total = (long)res_row0 * c;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total + zero_total;
+       idx += (long)gridDim.x * blockDim.x) {
+    if (idx >= total) {
+      if (dres) dres[idx - total] = 0.0f;
+      continue;
+    }
+    const long r = idx / c;
+    const int j = (int)(idx - r * c);
+    const float xhat = (z[idx] - mean[j]) * rstd[j];
+    const float k1 = sums[j] * inv_n, k2 = sums[c + j] * inv_n;
+    const float dz = gamma[j] * rstd[j] * (dy[idx] - k1 - xhat * k2);
+    if (dres) dres[(r + res_row0) * c + j] = dz;
+    if (dh) {
+      float v = dz;
+      if (drop_p > 0.0f) {
+        const float u = gwn_uniform(seed, salt, (unsigned long long)r * (unsigned)c + j);
+        v = (u >= drop_p) ? v * (1.0f / (1.0f - drop_p)) : 0.0f;
+      }
+      dh[idx] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// masked metrics (util.py:510-552, null_val = 0).  ws layout: [0] nonzero count,
+// [1 .. 1+3*RED_BLOCKS) partial (mae, mape, mse) sums
+__global__ void loss_count_kernel(const float* real, long rsb, long rsn, long rso, int B, int n,
+                                  int o, float* ws) {
+  __shared__ float sh[1024];
+  const long total = (long)B * n * o;
+  float cnt = 0.0f;
+  for (long i = threadIdx.x; i < total; i += 1024) {
+    const int oo = (int)(i % o);
+    const long bv = i / o;
+    const int v = (int)(bv % n);
+    const int b = (int)(bv / n);
+    cnt += (real[b * rsb + v * rsn + oo * rso] != 0.0f) ? 1.0f : 0.0f;
+  }
+  cnt = block_sum<1024>(cnt, sh);
+  if (threadIdx.x == 0) ws[0] = cnt;
+}
+
+__global__ void loss_terms_kernel(const float* out, const float* real, long rsb, long rsn, long rso,
+                                  int B, int o, int n, int tf, float mean, float std, float* dout,
+                                  float* ws) {
+  __shared__ float sh[256];
+  const long total = (long)B * o * n * tf;  // out is [B][o][n][tf]
+  const float cnt = ws[0];
+  const float label_total = (float)((long)B * n * o);
+  const float mask_scale = (cnt > 0.0f) ? label_total / cnt : 0.0f;  // 1 / mean(mask)
+  const float inv_total = 1.0f / (float)total;
+  float s_mae = 0.0f, s_mape = 0.0f, s_mse = 0.0f;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int t = (int)(idx % tf);
+    const long r1 = idx / tf;
+    const int v = (int)(r1 % n);
+    const long r2 = r1 / n;
+    const int oo = (int)(r2 % o);
+    const int b = (int)(r2 / o);
+    const float y = real[b * rsb + v * rsn + oo * rso];
+    const float pred = out[idx] * std + mean;
+    const float mask = (y != 0.0f) ? mask_scale : 0.0f;
+    const float diff = pred - y;
+    float mae = fabsf(diff) * mask;
+    if (isnan(mae)) mae = 0.0f;
+    float mape = fabsf(diff) / y * mask;
+    if (isnan(mape)) mape = 0.0f;
+    float mse = diff * diff * mask;
+    if (isnan(mse)) mse = 0.0f;
+    s_mae += mae;
+    s_mape += mape;
+    s_mse += mse;
+    (void)t;
+    if (dout) {
+      const float sg = (diff > 0.0f) ? 1.0f : ((diff < 0.0f) ? -1.0f : 0.0f);
+      const float g = fabsf(diff) * mask;
+      dout[idx] = isnan(g) ? 0.0f : sg * mask * inv_total * std;
+    }
+  }
+  s_mae = block_sum<256>(s_mae, sh);
+  s_mape = block_sum<256>(s_mape, sh);
+  s_mse = block_sum<256>(s_mse, sh);
+  if (threadIdx.x == 0) {
+    ws[1 + blockIdx.x * 3] = s_mae;
+    ws[2 + blockIdx.x * 3] = s_mape;
+    ws[3 + blockIdx.x * 3] = s_mse;
+  }
+}
+
+__global__ void loss_final_kernel(const float* ws, int nblocks, long total, float* metrics) {
+  if (threadIdx.x != 0) return;
+  double a = 0.0, b = 0.0, c = 0.0;
+  for (int i = 0; i < nblocks; ++i) {
+    a += ws[1 + i * 3];
+    b += ws[2 + i * 3];
+    c += ws[3 + i * 3];
+  }
+  metrics[0] = (float)(a / (double)total);
+  metrics[1] = (float)(b / (double)total);
+  metrics[2] = sqrtf((float)(c / (double)total));
+}
+
+// ---------------------------------------------------------------------------------------------
+// clip_grad_norm_ + Adam over ranges of the flat buffers.  ws: [0 .. RED_BLOCKS) partial sq-sums,
+// [RED_BLOCKS] clip coefficient.
+__device__ __forceinline__ bool range_index(const long* lo, const long* hi, int nr, long i, long* out) {
+  for (int r = 0; r < nr; ++r) {
+    const long len = hi[r] - lo[r];
+    if (i < len) { *out = lo[r] + i; return true; }
+    i -= len;
+  }
+  return false;
+}
+
+__global__ void sqnorm_partial_kernel(const float* g, const long* lo, const long* hi, int nr,
+                                      long active, float* ws) {
+  __shared__ float sh[256];
+  float s = 0.0f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < active;
+       i += (long)gridDim.x * blockDim.x) {
+    long k;
+    if (range_index(lo, hi, nr, i, &k)) s += g[k] * g[k];
+  }
+  s = block_sum<256>(s, sh);
+  if (threadIdx.x == 0) ws[blockIdx.x] = s;
+}
+
+__global__ void clip_coef_kernel(float* ws, int nparts, float max_norm, long long* step,
+                                 float* total_norm_out) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < nparts; ++i) s += ws[i];
+  const float norm = sqrtf((float)s);
+  const float coef = max_norm / (norm + 1e-6f);
+  ws[RED_BLOCKS] = coef < 1.0f ? coef : 1.0f;
+  if (total_norm_out) *total_norm_out = norm;
+  *step += 1;
+}
+
+__global__ void adam_kernel(float* p, float* g, float* m, float* v, const long* lo, const long* hi,
+                            int nr, long active, const float* ws, const long long* step, float lr,
+                            float beta1, float beta2, float eps, float wd) {
+  const float coef = ws[RED_BLOCKS];
+  const double t = (double)(*step);
+  const double bc1 = 1.0 - pow((double)beta1, t);
+  const double bc2 = 1.0 - pow((double)beta2, t);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < active;
+       i += (long)gridDim.x * blockDim.x) {
+    long k;
+    if (!range_index(lo, hi, nr, i, &k)) continue;
+    float gr = g[k] * coef;
+    g[k] = gr;
+    const float pv = p[k];
+    if (wd != 0.0f) gr = gr + wd * pv;
+    float mv = m[k];
+    mv = mv + (1.0f - beta1) * (gr - mv);
+    float vv = v[k] * beta2 + (1.0f - beta2) * gr * gr;
+    m[k] = mv;
+    v[k] = vv;
+    const float denom = sqrtf(vv) / bc2_sqrt + eps;
+    p[k] = pv - step_size * (mv / denom);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ void gather_kernel(const float* src, const int* idx, float* dst, long count) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count;
+       i += (long)gridDim.x * blockDim.x)
+    dst[i] = src[idx[i]];
+}
+
+__global__ void to_nchw_kernel(const float* y, int B, int o, int n, int t, float* out) {
+  const long total = (long)B * o * n * t;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int tt = (int)(idx % t);
+    const long r1 = idx / t;
+    const int v = (int)(r1 % n);
+    const long r2 = r1 / n;
+    const int oo = (int)(r2 % o);
+    const int b = (int)(r2 / o);
+    out[idx] = y[(((long)tt * B + b) * n + v) * o + oo];
+  }
+}
+
+__global__ void from_nchw_kernel(const float* dout, int B, int o, int n, int t, float* dy) {
+  const long total = (long)B * o * n * t;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int tt = (int)(idx % t);
+    const long r1 = idx / t;
+    const int v = (int)(r1 % n);
+    const long r2 = r1 / n;
+    const int oo = (int)(r2 % o);
+    const int b = (int)(r2 / o);
+    dy[(((long)tt * B + b) * n + v) * o + oo] = dout[idx];
+  }
+}
+
+__global__ void sum_vectors_kernel(const float* x, int count, int len, long stride, float* out) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < len; j += gridDim.x * blockDim.x) {
+    float s = 0.0f;
+    for (int i = 0; i < count; ++i) s += x[(long)i * stride + j];
+    out[j] = s;
+  }
+}
+
+__global__ void increment_kernel(unsigned long long* c, unsigned long long inc) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *c += inc;
+}
+
+int grid_for(long total, int block = 256) {
+  long g = (total + block - 1) / block;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+// =============================================================================================
+int gwn_set_error(int code, const char* msg) {
+  strncpy(g_err, msg ? msg : "", sizeof(g_err) - 1);
+  g_err[sizeof(g_err) - 1] = 0;
+  return code;
+}
+
+extern "C" {
+
+int gwn_version(void) { return 1; }
+const char* gwn_last_error(void) { return g_err; }
+
+int gwn_gemm(const gwn_gemm_desc* d, hipStream_t s) {
+  GWN_REQUIRE(d != nullptr, "gemm: null descriptor");
+  return gwn_gemm_launch(*d, s);
+}
+
+long gwn_gemm_workspace_floats(int M, int N, int ksplit) { return (long)M * N * (ksplit > 1 ? ksplit : 0); }
+
+// ---------------------------------------------------------------------------------------------
+int gwn_nconv(const float* A, int lda, int transpose_a, const float* x, long ldx, float* y, long ldy,
+              const float* y0, long ldy0, int n, int c, int slices, hipStream_t s) {
+  GWN_REQUIRE(n > 0 && c > 0 && slices > 0, "nconv: bad shape");
+  gwn_gemm_desc d = gemm_zero();
+  d.A = A;
+  if (transpose_a) { d.lda_m = 1; d.lda_k = lda; } else { d.lda_m = lda; d.lda_k = 1; }
+  d.B = x; d.ldb_k = ldx; d.ldb_n = 1; d.b_nin = c; d.b_no_stride = (long)n * ldx;
+  d.C = y; d.ldc_m = ldy; d.ldc_n = 1; d.c_nin = c; d.c_no_stride = (long)n * ldy;
+  if (y0) { d.C0 = y0; d.ldc0_m = ldy0; d.ldc0_n = 1; d.c0_no_stride = (long)n * ldy0; d.beta = 1.0f; }
+  d.M = n; d.N = c * slices; d.K = n;
+  return gwn_gemm_launch(d, s);
+}
+
+static int adj_grad_ksplit(int n, int c, int slices) {
+  return pick_ksplit(n, n, c * slices);
+}
+
+long gwn_nconv_adj_grad_workspace_floats(int n, int c, int slices) {
+  const int ks = adj_grad_ksplit(n, c, slices);
+  return ks > 1 ? (long)ks * n * n : 0;
+}
+
+int gwn_nconv_adj_grad(const float* x, long ldx, const float* dy, long lddy, int n, int c, int slices,
+                       float* dA, int ld_dA, int accumulate, float* ws, hipStream_t s) {
+  gwn_gemm_desc d = gemm_zero();
+  d.A = x; d.lda_m = ldx; d.lda_k = 1; d.a_kin = c; d.a_ko_stride = (long)n * ldx;
+  d.B = dy; d.ldb_k = 1; d.ldb_n = lddy; d.b_kin = c; d.b_ko_stride = (long)n * lddy;
+  d.C = dA; d.ldc_m = ld_dA; d.ldc_n = 1;
+  if (accumulate) { d.C0 = dA; d.ldc0_m = ld_dA; d.ldc0_n = 1; d.beta = 1.0f; }
+  d.M = n; d.N = n; d.K = c * slices;
+  d.ksplit = adj_grad_ksplit(n, c, slices);
+  d.part = ws;
+  return gwn_gemm_launch(d, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+int gwn_adaptive_adj_fwd(const float* e1, const float* e2, int n, int dd, float* adp, int ld,
+                         hipStream_t s) {
+  GWN_REQUIRE(n > 0 && dd > 0 && ld >= n, "adaptive_adj_fwd: bad shape");
+  adp_fwd_kernel<<<n, 256, 0, s>>>(e1, e2, n, dd, adp, ld);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_adaptive_adj_bwd(const float* e1, const float* e2, const float* adp, const float* dadp, int n,
+                         int dd, int ld, float* de1, float* de2, float* ws, hipStream_t s) {
+  GWN_REQUIRE(n > 0 && dd > 0 && ld >= n, "adaptive_adj_bwd: bad shape");
+  adp_bwd_kernel<<<n, 256, 0, s>>>(e1, e2, adp, dadp, n, dd, ld, ws);
+  GWN_CHECK_LAUNCH();
+  // dE1[v][k] = sum_w dl[v][w] * e2[k][w]
+  gwn_gemm_desc d = gemm_zero();
+  d.A = ws; d.lda_m = ld; d.lda_k = 1;
+  d.B = e2; d.ldb_k = 1; d.ldb_n = n;
+  d.C = de1; d.ldc_m = dd; d.ldc_n = 1;
+  d.M = n; d.N = dd; d.K = n;
+  int rc = gwn_gemm_launch(d, s);
+  if (rc) return rc;
+  // dE2[k][w] = sum_v e1[v][k] * dl[v][w]
+  d = gemm_zero();
+  d.A = e1; d.lda_m = 1; d.lda_k = dd;
+  d.B = ws; d.ldb_k = ld; d.ldb_n = 1;
+  d.C = de2; d.ldc_m = n; d.ldc_n = 1;
+  d.M = dd; d.N = n; d.K = n;
+  return gwn_gemm_launch(d, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+int gwn_start_conv_fwd(const float* x, long sb, long sc, long sn, long st, int B, int cin, int n,
+                       int t, int t0, const float* W, const float* bias, int c, float* out, float* xin,
+                       hipStream_t s) {
+  GWN_REQUIRE(t0 >= t && B > 0 && n > 0 && c > 0 && cin > 0, "start_conv: bad shape");
+  const long total = (long)t0 * B * n * c;
+  start_conv_kernel<<<grid_for(total), 256, 0, s>>>(x, sb, sc, sn, st, B, cin, n, t, t0, W, bias, c,
+                                                    out, xin);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+int gwn_gated_tcn_fwd(const gwn_tcn_args* a, hipStream_t s) {
+  GWN_REQUIRE(a && a->t_in > a->dilation && a->c > 0 && a->P > 0, "gated_tcn_fwd: bad shape");
+  GWN_REQUIRE(a->c % 16 == 0, "gated_tcn_fwd: channels must be a multiple of 16");
+  const int c = a->c, P = a->P, t_out = a->t_in - a->dilation;
+  gwn_gemm_desc d = gemm_zero();
+  d.A = a->x; d.lda_m = c; d.lda_k = 1; d.a_kin = c; d.a_row_shift = a->dilation * P;
+  d.a_rows = a->t_in * P;
+  d.B = a->w_fg; d.ldb_k = 1; d.ldb_n = 2 * c;
+  d.C = a->xg; d.ldc_m = a->ld_xg; d.ldc_n = 1;
+  d.bias_n = a->b_fg;
+  d.epi = EPI_GATE;
+  d.aux = a->fg; d.ld_aux = 2 * c;
+  d.aux2 = a->skipcat; d.ld_aux2 = a->ld_skip; d.aux2_row0 = a->skip_row0;
+  d.M = t_out * P; d.N = 2 * c; d.K = 2 * c;
+  return gwn_gemm_launch(d, s);
+}
+
+static int tcn_w_ksplit(int rows, int c) { return pick_ksplit(2 * c, 2 * c, rows); }
+
+long gwn_gated_tcn_bwd_workspace_floats(int t_in, int P, int c, int dilation) {
+  const int rows = (t_in - dilation) * P;
+  const long wk = (long)tcn_w_ksplit(rows, c) * 4 * c * c;
+  const long cs = gwn_colsum_workspace_floats(rows, 2 * c);
+  return wk > cs ? wk : cs;
+}
+
+int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
+  GWN_REQUIRE(a && a->t_in > a->dilation && a->c % 16 == 0, "gated_tcn_bwd: bad shape");
+  const int c = a->c, P = a->P, t_out = a->t_in - a->dilation;
+  const long rows = (long)t_out * P;
+  gate_bwd_kernel<<<grid_for(rows * c), 256, 0, s>>>(a->dxg, a->ld_dxg, a->dskip, a->ld_dskip,
+                                                     a->skip_row0, a->fg, rows, c, a->dfg);
+  GWN_CHECK_LAUNCH();
+  // dW_fg[j][tap*c + ci] = sum_r dfg[r][j] * x[r + tap*d*P][ci]
+  gwn_gemm_desc d = gemm_zero();
+  d.A = a->dfg; d.lda_m = 1; d.lda_k = 2 * c;
+  d.B = a->x; d.ldb_k = c; d.ldb_n = 1; d.b_nin = c; d.b_no_stride = (long)a->dilation * P * c;
+  d.C = a->dw_fg; d.ldc_m = 2 * c; d.ldc_n = 1;
+  d.M = 2 * c; d.N = 2 * c; d.K = (int)rows;
+  d.ksplit = tcn_w_ksplit((int)rows, c);
+  d.part = a->workspace;
+  int rc = gwn_gemm_launch(d, s);
+  if (rc) return rc;
+  rc = gwn_colsum(a->dfg, (int)rows, 2 * c, 2 * c, a->db_fg, 0, a->workspace, s);
+  if (rc) return rc;
+  // dx[r'][ci] (+)= sum_tap sum_j dfg[r' - tap*d*P][j] * Wfg[j][tap*c + ci]
+  d = gemm_zero();
+  d.A = a->dfg; d.lda_m = 2 * c; d.lda_k = 1; d.a_kin = 2 * c; d.a_row_shift = -a->dilation * P;
+  d.a_rows = (int)rows;
+  d.B = a->w_fg; d.ldb_k = 2 * c; d.ldb_n = 1; d.b_kin = 2 * c; d.b_ko_stride = c;
+  d.C = a->dx; d.ldc_m = c; d.ldc_n = 1;
+  if (a->accumulate_dx) { d.C0 = a->dx; d.ldc0_m = c; d.ldc0_n = 1; d.beta = 1.0f; }
+  d.M = a->t_in * P; d.N = c; d.K = 4 * c;
+  return gwn_gemm_launch(d, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
+  GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_fwd: rows must be slices*n");
+  const int c = a->c, n = a->n, slices = a->rows / n;
+  const int width = (2 * a->nsup + 1) * c;
+  for (int k = 0; k < a->nsup; ++k) {
+    float* x1 = a->h + (1 + 2 * k) * c;
+    float* x2 = a->h + (2 + 2 * k) * c;
+    int rc = gwn_nconv(a->sup[k], a->ld_sup, 1, a->h, a->ld_h, x1, a->ld_h, nullptr, 0, n, c, slices, s);
+    if (rc) return rc;
+    rc = gwn_nconv(a->sup[k], a->ld_sup, 1, x1, a->ld_h, x2, a->ld_h, nullptr, 0, n, c, slices, s);
+    if (rc) return rc;
+  }
+  gwn_gemm_desc d = gemm_zero();
+  d.A = a->h; d.lda_m = a->ld_h; d.lda_k = 1;
+  d.B = a->w_mlp; d.ldb_k = 1; d.ldb_n = width;
+  d.C = a->z; d.ldc_m = c; d.ldc_n = 1;
+  d.bias_n = a->b_mlp;
+  d.C0 = a->residual; d.ldc0_m = c; d.ldc0_n = 1; d.beta = 1.0f;
+  d.seed_ptr = a->seed_ptr; d.seed_salt = a->salt; d.drop_p = a->drop_p;
+  d.M = a->rows; d.N = c; d.K = width;
+  return gwn_gemm_launch(d, s);
+}
+
+static int gcn_w_ksplit(int rows, int c, int width) { return pick_ksplit(c, width, rows); }
+
+long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup) {
+  const int width = (2 * nsup + 1) * c;
+  long w = (long)gcn_w_ksplit(rows, c, width) * c * width;
+  const long g = gwn_nconv_adj_grad_workspace_floats(n, c, rows / n);
+  const long cs = gwn_colsum_workspace_floats(rows, c);
+  if (g > w) w = g;
+  if (cs > w) w = cs;
+  return w;
+}
+
+int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
+  GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_bwd: rows must be slices*n");
+  const int c = a->c, n = a->n, slices = a->rows / n;
+  const int width = (2 * a->nsup + 1) * c;
+  // dW_mlp[j][k] = sum_r dh[r][j] h[r][k]
+  gwn_gemm_desc d = gemm_zero();
+  d.A = a->dh; d.lda_m = 1; d.lda_k = c;
+  d.B = a->h; d.ldb_k = a->ld_h; d.ldb_n = 1;
+  d.C = a->dw_mlp; d.ldc_m = width; d.ldc_n = 1;
+  d.M = c; d.N = width; d.K = a->rows;
+  d.ksplit = gcn_w_ksplit(a->rows, c, width);
+  d.part = a->workspace;
+  int rc = gwn_gemm_launch(d, s);
+  if (rc) return rc;
+  rc = gwn_colsum(a->dh, a->rows, c, c, a->db_mlp, 0, a->workspace, s);
+  if (rc) return rc;
+  // dhcat[r][k] = sum_j dh[r][j] W[j][k]
+  d = gemm_zero();
+  d.A = a->dh; d.lda_m = c; d.lda_k = 1;
+  d.B = a->w_mlp; d.ldb_k = width; d.ldb_n = 1;
+  d.C = a->dhcat; d.ldc_m = a->ld_dhcat; d.ldc_n = 1;
+  d.M = a->rows; d.N = width; d.K = c;
+  rc = gwn_gemm_launch(d, s);
+  if (rc) return rc;
+  for (int k = 0; k < a->nsup; ++k) {
+    float* t1 = a->dhcat + (1 + 2 * k) * c;        // dL/dx1 (gets the x2 path added)
+    const float* t2 = a->dhcat + (2 + 2 * k) * c;  // dL/dx2
+    // x2 = A^T x1  =>  dx1 += A dx2
+    rc = gwn_nconv(a->sup[k], a->ld_sup, 0, t2, a->ld_dhcat, t1, a->ld_dhcat, t1, a->ld_dhcat, n, c,
+                   slices, s);
+    if (rc) return rc;
+    if (k == a->adp_index && a->dadp) {
+      // dA = sum xg (x) dx1  +  sum x1 (x) dx2
+      rc = gwn_nconv_adj_grad(a->h, a->ld_h, t1, a->ld_dhcat, n, c, slices, a->dadp, a->ld_sup,
+                              a->accumulate_dadp, a->workspace, s);
+      if (rc) return rc;
+      rc = gwn_nconv_adj_grad(a->h + (1 + 2 * k) * c, a->ld_h, t2, a->ld_dhcat, n, c, slices, a->dadp,
+                              a->ld_sup, 1, a->workspace, s);
+      if (rc) return rc;
+    }
+    // x1 = A^T xg  =>  dxg += A dx1   (dxg is piece 0 of dhcat)
+    rc = gwn_nconv(a->sup[k], a->ld_sup, 0, t1, a->ld_dhcat, a->dhcat, a->ld_dhcat, a->dhcat,
+                   a->ld_dhcat, n, c, slices, s);
+    if (rc) return rc;
+  }
+  return GWN_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+long gwn_batchnorm_workspace_floats(int rows, int c) {
+  (void)rows;
+  return (long)RED_BLOCKS * 3 * (c > 0 ? c : 1) + 2L * c;
+}
+
+int gwn_batchnorm_fwd(const float* z, int rows, int c, const float* gamma, const float* beta,
+                      float* running_mean, float* running_var, float momentum, float eps, int training,
+                      float* out, float* save_mean, float* save_rstd, float* ws, hipStream_t s) {
+  GWN_REQUIRE(rows > 0 && c > 0 && c <= 256 && 256 % c == 0, "batchnorm_fwd: c must divide 256");
+  const long total = (long)rows * c;
+  if (training) {
+    bn_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(z, rows, c, ws);
+    GWN_CHECK_LAUNCH();
+    bn_finalize_kernel<<<1, 256, 0, s>>>(ws, RED_BLOCKS, c, momentum, eps, running_mean, running_var,
+                                         save_mean, save_rstd);
+    GWN_CHECK_LAUNCH();
+    bn_apply_kernel<<<grid_for(total), 256, 0, s>>>(z, rows, c, save_mean, save_rstd, nullptr, eps,
+                                                    gamma, beta, out);
+  } else {
+    bn_apply_kernel<<<grid_for(total), 256, 0, s>>>(z, rows, c, running_mean, nullptr, running_var,
+                                                    eps, gamma, beta, out);
+  }
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_batchnorm_bwd(const float* dy, const float* z, int rows, int c, const float* gamma,
+                      const float* save_mean, const float* save_rstd, float* dgamma, float* dbeta,
+                      float* dres, int res_row0, float* dh, const unsigned long long* seed_ptr,
+                      unsigned long long salt, float drop_p, float* ws, hipStream_t s) {
+  GWN_REQUIRE(rows > 0 && c > 0 && c <= 256, "batchnorm_bwd: bad shape");
+  float* part = ws;
+  float* sums = ws + (long)RED_BLOCKS * 3 * c;  // [2][c]: sum dy, sum dy*xhat
+  colsum_partial_kernel<0><<<RED_BLOCKS, 256, 0, s>>>(dy, c, nullptr, 0, nullptr, nullptr, rows, c, part);
+  GWN_CHECK_LAUNCH();
+  colsum_final_kernel<<<1, 256, 0, s>>>(part, RED_BLOCKS, c, sums, 0);
+  GWN_CHECK_LAUNCH();
+  colsum_partial_kernel<1><<<RED_BLOCKS, 256, 0, s>>>(dy, c, z, c, save_mean, save_rstd, rows, c, part);
+  GWN_CHECK_LAUNCH();
+  colsum_final_kernel<<<1, 256, 0, s>>>(part, RED_BLOCKS, c, sums + c, 0);
+  GWN_CHECK_LAUNCH();
+  if (dbeta && hipMemcpyAsync(dbeta, sums, sizeof(float) * c, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return gwn_set_error(GWN_ERR_HIP, "batchnorm_bwd: dbeta copy");
+  if (dgamma && hipMemcpyAsync(dgamma, sums + c, sizeof(float) * c, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return gwn_set_error(GWN_ERR_HIP, "batchnorm_bwd: dgamma copy");
+  const long total = (long)rows * c + (long)res_row0 * c;
+  bn_bwd_apply_kernel<<<grid_for(total), 256, 0, s>>>(dy, z, rows, c, gamma, save_mean, save_rstd, sums,
+                                                      dres, res_row0, dh, seed_ptr, salt, drop_p);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+long gwn_colsum_workspace_floats(int rows, int ncol) {
+  (void)rows;
+  return (long)RED_BLOCKS * ncol;
+}
+
+int gwn_colsum(const float* dy, int rows, int ncol, long ld, float* out, int accumulate, float* ws,
+               hipStream_t s) {
+  GWN_REQUIRE(rows > 0 && ncol > 0, "colsum: bad shape");
+  colsum_partial_kernel<0><<<RED_BLOCKS, 256, 0, s>>>(dy, ld, nullptr, 0, nullptr, nullptr, rows, ncol, ws);
+  GWN_CHECK_LAUNCH();
+  colsum_final_kernel<<<(ncol + 255) / 256, 256, 0, s>>>(ws, RED_BLOCKS, ncol, out, accumulate);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+long gwn_masked_loss_workspace_floats(int B, int o, int n, int tf) {
+  (void)B; (void)o; (void)n; (void)tf;
+  return 1 + 3L * RED_BLOCKS;
+}
+
+int gwn_masked_loss(const float* out, const float* real, long rsb, long rsn, long rso, int B, int o,
+                    int n, int tf, float mean, float std, float* metrics, float* dout, float* ws,
+                    hipStream_t s) {
+  GWN_REQUIRE(B > 0 && o > 0 && n > 0 && tf > 0, "masked_loss: bad shape");
+  loss_count_kernel<<<1, 1024, 0, s>>>(real, rsb, rsn, rso, B, n, o, ws);
+  GWN_CHECK_LAUNCH();
+  loss_terms_kernel<<<RED_BLOCKS, 256, 0, s>>>(out, real, rsb, rsn, rso, B, o, n, tf, mean, std, dout, ws);
+  GWN_CHECK_LAUNCH();
+  loss_final_kernel<<<1, 64, 0, s>>>(ws, RED_BLOCKS, (long)B * o * n * tf, metrics);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+long gwn_clip_adam_workspace_floats(long total) {
+  (void)total;
+  return RED_BLOCKS + 1;
+}
+
+int gwn_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, const long* lo,
+                  const long* hi, int nranges, long active, float max_norm, float lr, float beta1,
+                  float beta2, float eps, float wd, long long* step_ptr, float* ws,
+                  float* total_norm_out, hipStream_t s) {
+  GWN_REQUIRE(nranges > 0 && active > 0, "clip_adam: empty");
+  sqnorm_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(grads, lo, hi, nranges, active, ws);
+  GWN_CHECK_LAUNCH();
+  clip_coef_kernel<<<1, 64, 0, s>>>(ws, RED_BLOCKS, max_norm, step_ptr, total_norm_out);
+  GWN_CHECK_LAUNCH();
+  adam_kernel<<<grid_for(active), 256, 0, s>>>(params, grads, exp_avg, exp_avg_sq, lo, hi, nranges, active,
+                                               ws, step_ptr, lr, beta1, beta2, eps, wd);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_gather(const float* src, const int* idx, float* dst, long count, hipStream_t s) {
+  if (count <= 0) return GWN_OK;
+  gather_kernel<<<grid_for(count), 256, 0, s>>>(src, idx, dst, count);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_to_nchw(const float* y, int B, int o, int n, int t, float* out, hipStream_t s) {
+  const long total = (long)B * o * n * t;
+  to_nchw_kernel<<<grid_for(total), 256, 0, s>>>(y, B, o, n, t, out);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_from_nchw(const float* dout, int B, int o, int n, int t, float* dy, hipStream_t s) {
+  const long total = (long)B * o * n * t;
+  from_nchw_kernel<<<grid_for(total), 256, 0, s>>>(dout, B, o, n, t, dy);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_sum_vectors(const float* x, int count, int len, long stride, float* out, hipStream_t s) {
+  sum_vectors_kernel<<<(len + 255) / 256, 256, 0, s>>>(x, count, len, stride, out);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_increment_u64(unsigned long long* counter, unsigned long long inc, hipStream_t s) {
+  increment_kernel<<<1, 64, 0, s>>>(counter, inc);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+}  // extern "C"

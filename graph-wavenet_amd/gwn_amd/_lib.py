@@ -1,0 +1,177 @@
+"""ctypes binding of libgwn.so (include/gwn.h).
+
+The library is the only compute path of this package: if it is missing or fails to load, every
+product entry point raises (there is no CPU or eager-PyTorch fallback).  PyTorch is used only as
+the device-memory / stream provider: tensors are passed as raw device pointers together with
+``torch.cuda.current_stream().cuda_stream``.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgwn.so")
+
+c_int, c_long, c_float, c_void_p, c_u64 = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
+                                          ctypes.c_void_p, ctypes.c_ulonglong)
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("A", c_void_p), ("lda_m", c_long), ("lda_k", c_long), ("a_ko_stride", c_long),
+        ("a_kin", c_int), ("a_row_shift", c_int), ("a_rows", c_int),
+        ("B", c_void_p), ("ldb_k", c_long), ("ldb_n", c_long), ("b_ko_stride", c_long),
+        ("b_no_stride", c_long), ("b_kin", c_int), ("b_nin", c_int),
+        ("C", c_void_p), ("ldc_m", c_long), ("ldc_n", c_long), ("c_no_stride", c_long), ("c_nin", c_int),
+        ("C0", c_void_p), ("ldc0_m", c_long), ("ldc0_n", c_long), ("c0_no_stride", c_long), ("beta", c_float),
+        ("bias_n", c_void_p),
+        ("mask", c_void_p), ("ldmask_m", c_long),
+        ("M", c_int), ("N", c_int), ("K", c_int),
+        ("alpha", c_float),
+        ("epi", c_int), ("relu", c_int),
+        ("aux", c_void_p), ("ld_aux", c_long),
+        ("aux2", c_void_p), ("ld_aux2", c_long), ("aux2_row0", c_int),
+        ("seed_ptr", c_void_p), ("seed_salt", c_u64), ("drop_p", c_float),
+        ("ksplit", c_int), ("kchunk", c_int), ("part", c_void_p),
+    ]
+
+
+class TcnArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p), ("t_in", c_int), ("P", c_int), ("c", c_int), ("dilation", c_int),
+        ("w_fg", c_void_p), ("b_fg", c_void_p),
+        ("xg", c_void_p), ("ld_xg", c_long),
+        ("fg", c_void_p),
+        ("skipcat", c_void_p), ("ld_skip", c_long), ("skip_row0", c_int),
+    ]
+
+
+class TcnBwdArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p), ("t_in", c_int), ("P", c_int), ("c", c_int), ("dilation", c_int),
+        ("w_fg", c_void_p), ("fg", c_void_p),
+        ("dxg", c_void_p), ("ld_dxg", c_long),
+        ("dskip", c_void_p), ("ld_dskip", c_long), ("skip_row0", c_int),
+        ("dfg", c_void_p),
+        ("dw_fg", c_void_p), ("db_fg", c_void_p),
+        ("dx", c_void_p), ("accumulate_dx", c_int),
+        ("workspace", c_void_p),
+    ]
+
+
+class GcnArgs(ctypes.Structure):
+    _fields_ = [
+        ("rows", c_int), ("n", c_int), ("c", c_int), ("nsup", c_int),
+        ("sup", ctypes.POINTER(c_void_p)), ("ld_sup", c_int),
+        ("h", c_void_p), ("ld_h", c_long),
+        ("w_mlp", c_void_p), ("b_mlp", c_void_p),
+        ("residual", c_void_p),
+        ("z", c_void_p),
+        ("seed_ptr", c_void_p), ("salt", c_u64), ("drop_p", c_float),
+    ]
+
+
+class GcnBwdArgs(ctypes.Structure):
+    _fields_ = [
+        ("rows", c_int), ("n", c_int), ("c", c_int), ("nsup", c_int),
+        ("sup", ctypes.POINTER(c_void_p)), ("ld_sup", c_int),
+        ("h", c_void_p), ("ld_h", c_long),
+        ("w_mlp", c_void_p),
+        ("dh", c_void_p),
+        ("dhcat", c_void_p), ("ld_dhcat", c_long),
+        ("dw_mlp", c_void_p), ("db_mlp", c_void_p),
+        ("adp_index", c_int), ("dadp", c_void_p), ("accumulate_dadp", c_int),
+        ("workspace", c_void_p),
+    ]
+
+
+# (name, restype, argtypes) of every exported entry point declared in include/gwn.h
+_SIGS = [
+    ("gwn_version", c_int, []),
+    ("gwn_last_error", ctypes.c_char_p, []),
+    ("gwn_gemm", c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
+    ("gwn_gemm_workspace_floats", c_long, [c_int, c_int, c_int]),
+    ("gwn_nconv", c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,
+                          c_int, c_int, c_int, c_void_p]),
+    ("gwn_nconv_adj_grad", c_int, [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_void_p,
+                                   c_int, c_int, c_void_p, c_void_p]),
+    ("gwn_nconv_adj_grad_workspace_floats", c_long, [c_int, c_int, c_int]),
+    ("gwn_adaptive_adj_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    ("gwn_adaptive_adj_bwd", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                     c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("gwn_start_conv_fwd", c_int, [c_void_p, c_long, c_long, c_long, c_long, c_int, c_int, c_int, c_int,
+                                   c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    ("gwn_gated_tcn_fwd", c_int, [ctypes.POINTER(TcnArgs), c_void_p]),
+    ("gwn_gated_tcn_bwd", c_int, [ctypes.POINTER(TcnBwdArgs), c_void_p]),
+    ("gwn_gated_tcn_bwd_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
+    ("gwn_gcn_fwd", c_int, [ctypes.POINTER(GcnArgs), c_void_p]),
+    ("gwn_gcn_bwd", c_int, [ctypes.POINTER(GcnBwdArgs), c_void_p]),
+    ("gwn_gcn_bwd_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
+    ("gwn_batchnorm_fwd", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+                                  c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("gwn_batchnorm_workspace_floats", c_long, [c_int, c_int]),
+    ("gwn_batchnorm_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_u64, c_float, c_void_p,
+                                  c_void_p]),
+    ("gwn_colsum", c_int, [c_void_p, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p]),
+    ("gwn_colsum_workspace_floats", c_long, [c_int, c_int]),
+    ("gwn_masked_loss", c_int, [c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_int, c_int, c_int,
+                                c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("gwn_masked_loss_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
+    ("gwn_clip_adam", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_long,
+                              c_float, c_float, c_float, c_float, c_float, c_float, c_void_p, c_void_p,
+                              c_void_p, c_void_p]),
+    ("gwn_clip_adam_workspace_floats", c_long, [c_long]),
+    ("gwn_gather", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p]),
+    ("gwn_to_nchw", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    ("gwn_from_nchw", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    ("gwn_sum_vectors", c_int, [c_void_p, c_int, c_int, c_long, c_void_p, c_void_p]),
+    ("gwn_increment_u64", c_int, [c_void_p, c_u64, c_void_p]),
+]
+
+EXPORTED = [s[0] for s in _SIGS]
+
+_lib = None
+
+
+class GwnError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libgwn.so (raises if it is missing: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise GwnError("libgwn.so not found at %s; run build.sh (or __graft_entry__.build())" % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, res, args in _SIGS:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = load().gwn_last_error().decode(errors="replace")
+        raise GwnError("libgwn %s failed (%d): %s" % (what, rc, msg))
+
+
+def ptr(t):
+    """Raw device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def call(name, *args):
+    """Invoke an int-returning entry point and raise on failure."""
+    rc = getattr(load(), name)(*args)
+    check(rc, name)

@@ -1,0 +1,203 @@
+"""Drop-in ``trainer`` (reference engine.py:9-58, 119-130) on the libgwn hot path.
+
+``trainer.train`` is one fused step: pad (engine.py:44) -> gwnet forward -> masked MAE + its
+gradient (engine.py:46-51, util.py:527-538) -> hand-written backward -> clip_grad_norm_(5) ->
+Adam (engine.py:52-55), all as libgwn launches on the current stream, followed by ONE device->host
+copy of (loss, mape, rmse) -- the reference does three ``.item()`` syncs (engine.py:56-58).
+"""
+import torch
+
+from . import _lib, util
+from ._lib import ptr
+from .model import gwnet
+
+F32 = torch.float32
+_NO_CLIP = 3.0e38
+
+
+class FlatAdam(torch.optim.Optimizer):
+    """``torch.optim.Adam`` semantics (L2 weight decay, bias correction, amsgrad=False) over the
+    model's flat parameter buffer, executed by ``gwn_clip_adam`` in one pass."""
+
+    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        super().__init__(model.parameters(), dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.model = model
+        flat = model._flat
+        self.exp_avg = torch.zeros_like(flat)
+        self.exp_avg_sq = torch.zeros_like(flat)
+        self.grad_flat = torch.zeros_like(flat)
+        self.step_t = torch.zeros(1, device=flat.device, dtype=torch.long)
+        self.total_norm = torch.zeros(1, device=flat.device, dtype=F32)
+        self._ranges_key = None
+        self._ws = torch.empty(_lib.load().gwn_clip_adam_workspace_floats(flat.numel()) + 16,
+                               device=flat.device, dtype=F32)
+
+    def _ranges(self, names):
+        key = tuple(names)
+        if key != self._ranges_key:
+            lay = self.model._executor.layout
+            rs = []
+            for n in names:
+                off, shape = lay.flat_off[n]
+                numel = 1
+                for s in shape:
+                    numel *= s
+                if rs and rs[-1][1] == off:
+                    rs[-1][1] = off + numel
+                else:
+                    rs.append([off, off + numel])
+            dev = self.model._flat.device
+            self._lo = torch.tensor([r[0] for r in rs], dtype=torch.long, device=dev)
+            self._hi = torch.tensor([r[1] for r in rs], dtype=torch.long, device=dev)
+            self._nr = len(rs)
+            self._active = sum(r[1] - r[0] for r in rs)
+            self._ranges_key = key
+        return self._lo, self._hi, self._nr, self._active
+
+    def apply(self, names, max_norm):
+        """clip (max_norm; huge = off) + Adam over the flat ranges of ``names``; grads in grad_flat."""
+        g = self.param_groups[0]
+        lo, hi, nr, active = self._ranges(names)
+        _lib.call("gwn_clip_adam", ptr(self.model._flat), ptr(self.grad_flat), ptr(self.exp_avg),
+                  ptr(self.exp_avg_sq), ptr(lo), ptr(hi), nr, active, float(max_norm), float(g["lr"]),
+                  float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), float(g["weight_decay"]),
+                  ptr(self.step_t), ptr(self._ws), ptr(self.total_norm), _lib.stream())
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        """Generic path (grads left in ``p.grad`` by autograd): gather them and run Adam."""
+        loss = closure() if closure is not None else None
+        model = self.model
+        model._ensure_flat()
+        lay = model.executor().layout
+        names = []
+        for name, p in model.named_parameters():
+            if p.grad is None:
+                continue
+            off, shape = lay.flat_off[name]
+            self.grad_flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
+            names.append(name)
+        if names:
+            self.apply(names, _NO_CLIP)
+        return loss
+
+
+class trainer():
+    def __init__(self, scaler, in_dim, seq_length, num_nodes, nhid, dropout, lrate, wdecay, device, supports,
+                 gcn_bool, addaptadj, aptinit, blocks, layers):
+        if isinstance(supports, dict):
+            raise NotImplementedError("per-sample graphs (gwnet_diff_G, engine.py:14-25) are out of scope")
+        self.model = gwnet(device, num_nodes, dropout, supports=supports, gcn_bool=gcn_bool,
+                           addaptadj=addaptadj, aptinit=aptinit, in_dim=in_dim, out_dim=seq_length,
+                           residual_channels=nhid, dilation_channels=nhid, skip_channels=nhid * 8,
+                           end_channels=nhid * 16, blocks=blocks, layers=layers)
+        self.model.to(device)
+        self.optimizer = FlatAdam(self.model, lr=lrate, weight_decay=wdecay)
+        self.loss = util.masked_mae
+        self.scaler = scaler
+        self.clip = 5
+        self.supports = supports
+        self.aptinit = aptinit
+        self.state = None
+        self._acts = {}
+        self._host_metrics = torch.zeros(4, dtype=F32).pin_memory() if torch.cuda.is_available() else None
+
+    # ------------------------------------------------------------------------------------------
+    def _step(self, input, real_val, training):
+        """Fused step; returns the device metrics tensor [mae, mape, rmse]."""
+        model = self.model
+        model.train(training)
+        ex = model.executor()
+        B, _, _, T = input.shape
+        ts = ex.cfg.times(T + 1)  # engine.py:44 pads one step on the left before the forward
+        key = (B, tuple(ts), training)
+        acts = self._acts.get(key)
+        out, acts = ex.forward(model._flat, model._fixed_supports(), input, training, model._bn_bufs(),
+                               acts=acts, lead_pad=1)
+        self._acts[key] = acts
+        if training:
+            model._nbt.add_(1)
+        sc = ex.scratch(B, ts)
+        dout = torch.empty_like(out) if training else None
+        rs = real_val.stride()
+        _lib.call("gwn_masked_loss", ptr(out), ptr(real_val), rs[0], rs[1], rs[2], B, ex.cfg.O, ex.cfg.N,
+                  ts[-1], float(self.scaler.mean), float(self.scaler.std), ptr(sc["metrics"]), ptr(dout),
+                  ptr(sc["ws"]), _lib.stream())
+        if training:
+            ex.backward(acts, dout)
+            ex.unpack_grads(self.optimizer.grad_flat)
+            clip = self.clip if self.clip is not None else _NO_CLIP
+            self.optimizer.apply(ex.layout.active, clip)
+            if model.dropout > 0:
+                _lib.call("gwn_increment_u64", ptr(ex.seed), 1, _lib.stream())
+        return sc["metrics"]
+
+    def _fused_ok(self, input, real_val):
+        return (self.loss is util.masked_mae and input.is_cuda and input.dtype == F32
+                and real_val.dtype == F32 and real_val.dim() == 3)
+
+    def train(self, input, real_val):
+        if not self._fused_ok(input, real_val):
+            return self._train_autograd(input, real_val)
+        m = self._step(input, real_val, True)
+        self._expose_grads()
+        return self._read(m)
+
+    def eval(self, input, real_val):
+        if not self._fused_ok(input, real_val):
+            return self._eval_autograd(input, real_val)
+        with torch.no_grad():
+            m = self._step(input, real_val, False)
+        return self._read(m)
+
+    def _read(self, m):
+        if self._host_metrics is not None:
+            self._host_metrics[:3].copy_(m[:3], non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            v = self._host_metrics.tolist()
+        else:
+            v = m.tolist()
+        return v[0], v[1], v[2]
+
+    def _expose_grads(self):
+        """Make ``p.grad`` views of the flat gradient buffer (as after the reference's step)."""
+        lay = self.model._executor.layout
+        active = set(lay.active)
+        for name, p in self.model.named_parameters():
+            if name in active:
+                off, shape = lay.flat_off[name]
+                g = self.optimizer.grad_flat[off:off + p.numel()].view(shape)
+                if p.grad is None or p.grad.data_ptr() != g.data_ptr():
+                    p.grad = g
+
+    # ------------------------------------------------------------------------------------------
+    # generic path for a user-supplied loss: the model is still one libgwn autograd node
+    def _train_autograd(self, input, real_val):
+        self.model.train()
+        self.optimizer.zero_grad()
+        input = torch.nn.functional.pad(input, (1, 0, 0, 0))
+        output = self.model(input).transpose(1, 3)
+        real = torch.unsqueeze(real_val, dim=1)
+        predict = self.scaler.inverse_transform(output)
+        loss = self.loss(predict, real, 0.0)
+        loss.backward()
+        if self.clip is not None:
+            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip)
+        self.optimizer.step()
+        mape = util.masked_mape(predict, real, 0.0).item()
+        rmse = util.masked_rmse(predict, real, 0.0).item()
+        return loss.item(), mape, rmse
+
+    def _eval_autograd(self, input, real_val):
+        self.model.eval()
+        input = torch.nn.functional.pad(input, (1, 0, 0, 0))
+        output = self.model(input).transpose(1, 3)
+        real = torch.unsqueeze(real_val, dim=1)
+        predict = self.scaler.inverse_transform(output)
+        loss = self.loss(predict, real, 0.0)
+        mape = util.masked_mape(predict, real, 0.0).item()
+        rmse = util.masked_rmse(predict, real, 0.0).item()
+        return loss.item(), mape, rmse
+
+
+__all__ = ["trainer", "FlatAdam"]

@@ -1,0 +1,496 @@
+"""Step executor: runs gwnet's forward / backward as a fixed schedule of libgwn launches.
+
+Reference semantics (model.py:175-241 forward, engine.py:41-58 train step) restated on the
+internal "slab-major, channels-last" layout of include/gwn.h: a reference NCHW tensor
+[B, C, N, T] lives here as rows (t, b, n) x C channels.  One time step = a slab of P = B*N rows.
+
+Per layer i (input X_i with T_i steps, dilation d_i, output T_{i+1} = T_i - d_i):
+  gated TCN   -> xg (piece 0 of the gcn concat H_i), (tanh, sigmoid) saved in FG_i,
+                 last T_f slabs copied into SKIPCAT[:, i*C:(i+1)*C]       (model.py:206-222)
+  gcn         -> H_i pieces 1..2K by diffusion, Z_i = dropout(mlp(H_i)) + X_i[last T_{i+1}]
+                                                                        (model.py:41-55, 234)
+  batchnorm   -> X_{i+1}                                                   (model.py:236)
+After the layers: SKR = relu(SKIPCAT Wskip^T + sum_i b_i) (only the last T_f steps of every
+skip term reach the output, model.py:216-222, 238), E1 = relu(end_conv_1), Y = end_conv_2.
+"""
+import ctypes
+from collections import OrderedDict
+
+import torch
+
+from . import _lib
+from ._lib import ptr
+
+F32 = torch.float32
+
+
+class PackedLayout:
+    """Kernel-friendly packing of the parameters (and, with the same offsets, of their grads).
+
+    ``pidx``: packed[i] = flat[pidx[i]];  ``uidx``: grad_flat[j] = grad_packed[uidx[j]] (inactive
+    parameters point at a trailing zero slot).  ``flat`` is the model's parameter buffer in
+    registration (== state_dict) order.
+    """
+
+    def __init__(self, model, cfg=None):
+        cfg = cfg if cfg is not None else Config(model)
+        C, Cin, S, E, O, L = cfg.C, cfg.Cin, cfg.S, cfg.E, cfg.O, cfg.L
+        offs = {}
+        names = [n for n, _ in model.named_parameters()]
+        flat_off = {}
+        o = 0
+        for n, p in model.named_parameters():
+            flat_off[n] = (o, p.shape)
+            o += p.numel()
+        self.flat_total = o
+        segs = OrderedDict()
+        pidx = []
+        grad_src = {}  # flat param name -> packed index tensor (same shape as the param)
+
+        def add(name, numel):
+            segs[name] = (len(pidx), numel)
+
+        def gather_seg(name, src_index):
+            # src_index: LongTensor of flat indices, in packed order
+            segs[name] = (len(pidx), src_index.numel())
+            pidx.extend(src_index.tolist())
+
+        def flat_range(pname):
+            off, shape = flat_off[pname]
+            n = 1
+            for s in shape:
+                n *= s
+            return torch.arange(off, off + n, dtype=torch.long).view(shape)
+
+        def map_grad(pname, packed_index):
+            grad_src[pname] = packed_index
+
+        def seg_index(name, shape):
+            start, numel = segs[name]
+            return torch.arange(start, start + numel, dtype=torch.long).view(shape)
+
+        # start conv
+        gather_seg("start_w", flat_range("start_conv.weight").reshape(C, Cin).reshape(-1))
+        map_grad("start_conv.weight", seg_index("start_w", (C, Cin, 1, 1)))
+        gather_seg("start_b", flat_range("start_conv.bias"))
+        map_grad("start_conv.bias", seg_index("start_b", (C,)))
+        if cfg.adaptive:
+            gather_seg("nv1", flat_range("nodevec1").reshape(-1))
+            map_grad("nodevec1", seg_index("nv1", tuple(flat_off["nodevec1"][1])))
+            gather_seg("nv2", flat_range("nodevec2").reshape(-1))
+            map_grad("nodevec2", seg_index("nv2", tuple(flat_off["nodevec2"][1])))
+        for i in range(L):
+            fw = flat_range("filter_convs.%d.weight" % i).reshape(C, C, 2)   # [co][ci][tap]
+            gw = flat_range("gate_convs.%d.weight" % i).reshape(C, C, 2)
+            # packed [2C rows j=2co+g][2C cols k=tap*C+ci]
+            both = torch.stack([fw, gw], dim=1)  # [co][g][ci][tap]
+            packed = both.permute(0, 1, 3, 2).reshape(2 * C, 2 * C)
+            gather_seg("fg_w%d" % i, packed.reshape(-1))
+            idx = seg_index("fg_w%d" % i, (C, 2, 2, C))  # [co][g][tap][ci]
+            map_grad("filter_convs.%d.weight" % i, idx[:, 0].permute(0, 2, 1).reshape(C, C, 1, 2))
+            map_grad("gate_convs.%d.weight" % i, idx[:, 1].permute(0, 2, 1).reshape(C, C, 1, 2))
+            fb = flat_range("filter_convs.%d.bias" % i)
+            gb = flat_range("gate_convs.%d.bias" % i)
+            gather_seg("fg_b%d" % i, torch.stack([fb, gb], dim=1).reshape(-1))
+            bidx = seg_index("fg_b%d" % i, (C, 2))
+            map_grad("filter_convs.%d.bias" % i, bidx[:, 0].clone())
+            map_grad("gate_convs.%d.bias" % i, bidx[:, 1].clone())
+            if cfg.use_gcn:
+                wname, bname = "gconv.%d.mlp.mlp.weight" % i, "gconv.%d.mlp.mlp.bias" % i
+            else:
+                wname, bname = "residual_convs.%d.weight" % i, "residual_convs.%d.bias" % i
+            W = cfg.W
+            gather_seg("mlp_w%d" % i, flat_range(wname).reshape(-1))
+            gather_seg("mlp_b%d" % i, flat_range(bname))
+            gather_seg("bn_g%d" % i, flat_range("bn.%d.weight" % i))
+            gather_seg("bn_b%d" % i, flat_range("bn.%d.bias" % i))
+            if i < L - 1:  # the last layer's gcn / bn never reach the output (no grad)
+                map_grad(wname, seg_index("mlp_w%d" % i, tuple(flat_off[wname][1])))
+                map_grad(bname, seg_index("mlp_b%d" % i, (C,)))
+                map_grad("bn.%d.weight" % i, seg_index("bn_g%d" % i, (C,)))
+                map_grad("bn.%d.bias" % i, seg_index("bn_b%d" % i, (C,)))
+            assert flat_off[wname][1][1] == W
+        # skip convs concatenated along K: [S][L*C]
+        sk = torch.stack([flat_range("skip_convs.%d.weight" % i).reshape(S, C) for i in range(L)], dim=1)
+        gather_seg("skip_w", sk.reshape(-1))
+        skidx = seg_index("skip_w", (S, L, C))
+        for i in range(L):
+            map_grad("skip_convs.%d.weight" % i, skidx[:, i].reshape(S, C, 1, 1).clone())
+        gather_seg("skip_b", torch.cat([flat_range("skip_convs.%d.bias" % i) for i in range(L)]))
+        # computed slot: sum_i skip bias (and, for grads, the shared bias gradient)
+        segs["skip_bsum"] = (len(pidx), S)
+        pidx.extend([0] * S)
+        for i in range(L):
+            map_grad("skip_convs.%d.bias" % i, seg_index("skip_bsum", (S,)))
+        gather_seg("e1_w", flat_range("end_conv_1.weight").reshape(-1))
+        map_grad("end_conv_1.weight", seg_index("e1_w", (E, S, 1, 1)))
+        gather_seg("e1_b", flat_range("end_conv_1.bias"))
+        map_grad("end_conv_1.bias", seg_index("e1_b", (E,)))
+        gather_seg("e2_w", flat_range("end_conv_2.weight").reshape(-1))
+        map_grad("end_conv_2.weight", seg_index("e2_w", (O, E, 1, 1)))
+        gather_seg("e2_b", flat_range("end_conv_2.bias"))
+        map_grad("end_conv_2.bias", seg_index("e2_b", (O,)))
+        self.zero_slot = len(pidx)
+        pidx.append(0)
+        self.total = len(pidx)
+        self.segs = segs
+        uidx = torch.full((self.flat_total,), self.zero_slot, dtype=torch.long)
+        self.active = []  # names of parameters that receive gradients
+        for n in names:
+            if n in grad_src:
+                off, shape = flat_off[n]
+                src = grad_src[n].reshape(-1)
+                uidx[off:off + src.numel()] = src
+                self.active.append(n)
+        self.flat_off = flat_off
+        self.pidx_cpu = torch.tensor(pidx, dtype=torch.int32)
+        self.uidx_cpu = uidx.to(torch.int32)
+        # contiguous [lo, hi) flat ranges of the active parameters (clip + Adam)
+        ranges = []
+        for n in names:
+            if n not in grad_src:
+                continue
+            off, shape = flat_off[n]
+            numel = 1
+            for s in shape:
+                numel *= s
+            if ranges and ranges[-1][1] == off:
+                ranges[-1][1] = off + numel
+            else:
+                ranges.append([off, off + numel])
+        self.ranges = ranges
+
+    def view(self, buf, name, shape=None):
+        start, numel = self.segs[name]
+        v = buf[start:start + numel]
+        return v.view(shape) if shape is not None else v
+
+
+class Config:
+    """Static model configuration (mirrors the gwnet ctor, model.py:83-171)."""
+
+    def __init__(self, model):
+        self.N = model.num_nodes
+        self.C = model.residual_channels
+        self.Cin = model.in_dim
+        self.S = model.skip_channels
+        self.E = model.end_channels
+        self.O = model.out_dim
+        self.L = model.blocks * model.layers
+        self.dilations = []
+        for _ in range(model.blocks):
+            d = 1
+            for _ in range(model.layers):
+                self.dilations.append(d)
+                d *= 2
+        self.R = model.receptive_field
+        self.adaptive = bool(model.gcn_bool and model.addaptadj)
+        self.use_gcn = bool(model.gcn_bool and model.supports is not None)
+        self.nfixed = len(model.supports) if (self.use_gcn and model.supports is not None) else 0
+        self.nsup = self.nfixed + (1 if (self.use_gcn and self.adaptive) else 0)
+        self.W = (2 * self.nsup + 1) * self.C if self.use_gcn else self.C
+        if model.residual_channels != model.dilation_channels:
+            raise ValueError("gwn_amd: residual_channels must equal dilation_channels")
+        if model.kernel_size != 2:
+            raise ValueError("gwn_amd: only kernel_size=2 (the reference default) is implemented")
+        if self.C % 16 != 0 or 256 % self.C != 0:
+            raise ValueError("gwn_amd: residual channels must be 16, 32, 64, 128 or 256")
+
+    def times(self, t_in):
+        t0 = max(t_in, self.R)
+        ts = [t0]
+        for d in self.dilations:
+            ts.append(ts[-1] - d)
+        return ts
+
+
+class Acts:
+    """Activations of one forward (kept for its backward)."""
+
+    def __init__(self, cfg, B, ts, device, training):
+        C, N, L = cfg.C, cfg.N, cfg.L
+        P = B * N
+        self.B, self.ts, self.P = B, ts, P
+        tf = ts[-1]
+        e = lambda *s: torch.empty(*s, device=device, dtype=F32)  # noqa: E731
+        self.xin = e(ts[0] * P, cfg.Cin)
+        self.X = [e(ts[0] * P, C)]
+        self.FG, self.H, self.Z, self.mean, self.rstd = [], [], [], [], []
+        for i in range(L):
+            rows = ts[i + 1] * P
+            self.FG.append(e(rows, 2 * C))
+            self.H.append(e(rows, cfg.W))
+            self.Z.append(e(rows, C))
+            self.X.append(e(rows, C))
+            self.mean.append(e(C))
+            self.rstd.append(e(C))
+        self.skipcat = e(tf * P, L * C)
+        self.skr = e(tf * P, cfg.S)
+        self.e1 = e(tf * P, cfg.E)
+        self.y = e(tf * P, cfg.O)
+        self.adp = e(N, N) if cfg.adaptive else None
+        self.training = training
+
+
+class Executor:
+    def __init__(self, model):
+        self.cfg = Config(model)
+        self.layout = PackedLayout(model, self.cfg)
+        self.dropout = model.dropout
+        self.device = None
+        self._scratch = {}
+
+    # ---------------------------------------------------------------------------------------
+    def bind(self, device):
+        if self.device == device:
+            return
+        self.device = device
+        lay = self.layout
+        self.pidx = lay.pidx_cpu.to(device)
+        self.uidx = lay.uidx_cpu.to(device)
+        self.packed = torch.zeros(lay.total, device=device, dtype=F32)
+        self.gpacked = torch.zeros(lay.total, device=device, dtype=F32)
+        self.seed = torch.zeros(1, device=device, dtype=torch.int64)
+        self.seed.fill_(int(torch.randint(0, 2 ** 62, (1,)).item()))
+        self._scratch = {}
+
+    def pk(self, name, buf=None):
+        return self.layout.view(self.packed if buf is None else buf, name)
+
+    def gk(self, name):
+        return self.layout.view(self.gpacked, name)
+
+    def scratch(self, B, ts):
+        key = (B, tuple(ts))
+        s = self._scratch.get(key)
+        if s is not None:
+            return s
+        cfg = self.cfg
+        C, N, L = cfg.C, cfg.N, cfg.L
+        P = B * N
+        tf = ts[-1]
+        e = lambda *s_: torch.empty(*s_, device=self.device, dtype=F32)  # noqa: E731
+        maxrows = max(ts[i + 1] for i in range(L)) * P
+        s = {
+            "dy": e(tf * P, cfg.O),
+            "de1": e(tf * P, cfg.E),
+            "dsk": e(tf * P, cfg.S),
+            "dskipcat": e(tf * P, L * C),
+            "dxa": e(ts[0] * P, C),
+            "dxb": e(ts[0] * P, C),
+            "dfg": e(maxrows, 2 * C),
+            "dh": e(maxrows, C),
+            "dhc": e(maxrows, cfg.W),
+            "dadp": e(N, N),
+            "metrics": e(4),
+        }
+        lib = _lib.load()
+        need = [
+            lib.gwn_gated_tcn_bwd_workspace_floats(ts[0], P, C, 1),
+            lib.gwn_gcn_bwd_workspace_floats(maxrows, N, C, max(cfg.nsup, 0)),
+            lib.gwn_batchnorm_workspace_floats(maxrows, C),
+            lib.gwn_colsum_workspace_floats(maxrows, max(cfg.E, cfg.S, cfg.L * C)),
+            lib.gwn_masked_loss_workspace_floats(B, cfg.O, N, tf),
+            lib.gwn_clip_adam_workspace_floats(self.layout.flat_total),
+            N * N,
+        ]
+        # split-K partials of the head / start weight grads
+        for (M_, N_, K_) in ((cfg.O, cfg.E, tf * P), (cfg.E, cfg.S, tf * P), (cfg.S, L * C, tf * P),
+                             (C, cfg.Cin, ts[0] * P)):
+            need.append(lib.gwn_gemm_workspace_floats(M_, N_, _ksplit(M_, N_, K_)))
+        s["ws"] = e(int(max(need)) + 16)
+        self._scratch[key] = s
+        return s
+
+    # ---------------------------------------------------------------------------------------
+    def pack_params(self, flat):
+        st = _lib.stream()
+        lay = self.layout
+        _lib.call("gwn_gather", ptr(flat), ptr(self.pidx), ptr(self.packed), lay.total, st)
+        cfg = self.cfg
+        _lib.call("gwn_sum_vectors", ptr(self.pk("skip_b")), cfg.L, cfg.S, cfg.S,
+                  ptr(self.pk("skip_bsum")), st)
+
+    def supports(self, fixed, acts):
+        sups = list(fixed) if self.cfg.use_gcn else []
+        if self.cfg.use_gcn and self.cfg.adaptive:
+            sups.append(acts.adp)
+        arr = (ctypes.c_void_p * max(len(sups), 1))(*[s.data_ptr() for s in sups])
+        return sups, arr
+
+    def forward(self, flat, fixed_sups, x, training, bn_bufs, acts=None, lead_pad=0):
+        """x: reference NCHW input [B, Cin, N, T] (any strides).  ``lead_pad`` extra zero steps
+        are prepended (engine.py:44) before the receptive-field pad (model.py:176-178).
+        Returns (out [B, O, N, T_f], acts)."""
+        cfg = self.cfg
+        C, N, L = cfg.C, cfg.N, cfg.L
+        if x.dim() != 4:
+            raise RuntimeError("gwnet: expected a 4-D input [B, C, N, T], got %d-D" % x.dim())
+        B, cin, n, t_in = x.shape
+        if n != N or cin != cfg.Cin:
+            raise RuntimeError("gwnet: expected input [B, %d, %d, T], got %s" % (cfg.Cin, N, tuple(x.shape)))
+        if x.dtype != F32 or not x.is_cuda:
+            raise RuntimeError("gwnet (gwn_amd): input must be a float32 CUDA/HIP tensor")
+        ts = cfg.times(t_in + lead_pad)
+        if acts is not None and (acts.B != B or list(acts.ts) != list(ts)):
+            acts = None
+        if ts[-1] < 1:
+            raise RuntimeError("gwnet: input too short for the receptive field")
+        st = _lib.stream()
+        self.pack_params(flat)
+        if acts is None:
+            acts = Acts(cfg, B, ts, self.device, training)
+        acts.training = training
+        P = B * N
+        tf = ts[-1]
+        lib = _lib
+        if cfg.adaptive and cfg.use_gcn:
+            lib.call("gwn_adaptive_adj_fwd", ptr(self.pk("nv1")), ptr(self.pk("nv2")), N, 10,
+                     ptr(acts.adp), N, st)
+        sups, sup_arr = self.supports(fixed_sups, acts)
+        acts.sups, acts.sup_arr = sups, sup_arr
+        sx = x.stride()
+        lib.call("gwn_start_conv_fwd", ptr(x), sx[0], sx[1], sx[2], sx[3], B, cin, N, t_in, ts[0],
+                 ptr(self.pk("start_w")), ptr(self.pk("start_b")), C, ptr(acts.X[0]), ptr(acts.xin), st)
+        ws = self.scratch(B, ts)["ws"]
+        for i in range(L):
+            d = cfg.dilations[i]
+            rows = ts[i + 1] * P
+            ta = _lib.TcnArgs(x=ptr(acts.X[i]), t_in=ts[i], P=P, c=C, dilation=d,
+                              w_fg=ptr(self.pk("fg_w%d" % i)), b_fg=ptr(self.pk("fg_b%d" % i)),
+                              xg=ptr(acts.H[i]), ld_xg=cfg.W, fg=ptr(acts.FG[i]),
+                              skipcat=acts.skipcat.data_ptr() + 4 * i * C, ld_skip=L * C,
+                              skip_row0=(ts[i + 1] - tf) * P)
+            lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), st)
+            if i == L - 1 and not training:
+                continue  # the last gcn / bn output is dead in eval (only skip reaches the output)
+            drop = float(self.dropout) if (training and cfg.use_gcn) else 0.0
+            ga = _lib.GcnArgs(rows=rows, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
+                              sup=ctypes.cast(sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=N,
+                              h=ptr(acts.H[i]), ld_h=cfg.W,
+                              w_mlp=ptr(self.pk("mlp_w%d" % i)), b_mlp=ptr(self.pk("mlp_b%d" % i)),
+                              residual=acts.X[i].data_ptr() + 4 * d * P * C, z=ptr(acts.Z[i]),
+                              seed_ptr=ptr(self.seed), salt=i, drop_p=drop)
+            lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
+            rm, rv, mom, eps = bn_bufs[i]
+            lib.call("gwn_batchnorm_fwd", ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
+                     ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps, 1 if training else 0,
+                     ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(ws), st)
+        rows_f = tf * P
+        # skip sum (relu'd) -> end_conv_1 (+relu) -> end_conv_2
+        gemm(acts.skipcat, L * C, 1, self.pk("skip_w"), 1, L * C, acts.skr, cfg.S, 1,
+             M=rows_f, N=cfg.S, K=L * C, bias=self.pk("skip_bsum"), relu=1)
+        gemm(acts.skr, cfg.S, 1, self.pk("e1_w"), 1, cfg.S, acts.e1, cfg.E, 1,
+             M=rows_f, N=cfg.E, K=cfg.S, bias=self.pk("e1_b"), relu=1)
+        gemm(acts.e1, cfg.E, 1, self.pk("e2_w"), 1, cfg.E, acts.y, cfg.O, 1,
+             M=rows_f, N=cfg.O, K=cfg.E, bias=self.pk("e2_b"))
+        out = torch.empty(B, cfg.O, N, tf, device=self.device, dtype=F32)
+        lib.call("gwn_to_nchw", ptr(acts.y), B, cfg.O, N, tf, ptr(out), st)
+        return out, acts
+
+    # ---------------------------------------------------------------------------------------
+    def backward(self, acts, dout):
+        """Gradients of every active parameter into self.gpacked (kernel layout)."""
+        cfg = self.cfg
+        C, N, L, S, E, O = cfg.C, cfg.N, cfg.L, cfg.S, cfg.E, cfg.O
+        B, ts, P = acts.B, acts.ts, acts.P
+        tf = ts[-1]
+        rows_f = tf * P
+        sc = self.scratch(B, ts)
+        ws = sc["ws"]
+        st = _lib.stream()
+        lib = _lib
+        dout = dout.contiguous()
+        lib.call("gwn_from_nchw", ptr(dout), B, O, N, tf, ptr(sc["dy"]), st)
+        # end_conv_2
+        wgrad(sc["dy"], O, acts.e1, E, rows_f, self.gk("e2_w"), ws)
+        lib.call("gwn_colsum", ptr(sc["dy"]), rows_f, O, O, ptr(self.gk("e2_b")), 0, ptr(ws), st)
+        gemm(sc["dy"], O, 1, self.pk("e2_w"), E, 1, sc["de1"], E, 1, M=rows_f, N=E, K=O,
+             epi=2, mask=acts.e1, ldmask=E)
+        # end_conv_1
+        wgrad(sc["de1"], E, acts.skr, S, rows_f, self.gk("e1_w"), ws)
+        lib.call("gwn_colsum", ptr(sc["de1"]), rows_f, E, E, ptr(self.gk("e1_b")), 0, ptr(ws), st)
+        gemm(sc["de1"], E, 1, self.pk("e1_w"), S, 1, sc["dsk"], S, 1, M=rows_f, N=S, K=E,
+             epi=2, mask=acts.skr, ldmask=S)
+        # skip convs
+        wgrad(sc["dsk"], S, acts.skipcat, L * C, rows_f, self.gk("skip_w"), ws)
+        lib.call("gwn_colsum", ptr(sc["dsk"]), rows_f, S, S, ptr(self.gk("skip_bsum")), 0, ptr(ws), st)
+        gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * C, 1, sc["dskipcat"], L * C, 1, M=rows_f, N=L * C, K=S)
+        # layers in reverse
+        dnext = None
+        bufs = [sc["dxa"], sc["dxb"]]
+        first_adp = True
+        for i in range(L - 1, -1, -1):
+            d = cfg.dilations[i]
+            rows = ts[i + 1] * P
+            dx = bufs[i % 2]
+            dxg, ld_dxg, acc = None, 0, 0
+            if dnext is not None:
+                lib.call("gwn_batchnorm_bwd", ptr(dnext), ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
+                         ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(self.gk("bn_g%d" % i)),
+                         ptr(self.gk("bn_b%d" % i)), ptr(dx), d * P, ptr(sc["dh"]), ptr(self.seed), i,
+                         float(self.dropout) if (acts.training and cfg.use_gcn) else 0.0, ptr(ws), st)
+                adp_index = cfg.nsup - 1 if (cfg.use_gcn and cfg.adaptive) else -1
+                gb = _lib.GcnBwdArgs(rows=rows, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
+                                     sup=ctypes.cast(acts.sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=N,
+                                     h=ptr(acts.H[i]), ld_h=cfg.W, w_mlp=ptr(self.pk("mlp_w%d" % i)),
+                                     dh=ptr(sc["dh"]), dhcat=ptr(sc["dhc"]), ld_dhcat=cfg.W,
+                                     dw_mlp=ptr(self.gk("mlp_w%d" % i)), db_mlp=ptr(self.gk("mlp_b%d" % i)),
+                                     adp_index=adp_index, dadp=ptr(sc["dadp"]),
+                                     accumulate_dadp=0 if first_adp else 1, workspace=ptr(ws))
+                lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)
+                if adp_index >= 0:
+                    first_adp = False
+                dxg, ld_dxg, acc = sc["dhc"], cfg.W, 1
+            tb = _lib.TcnBwdArgs(x=ptr(acts.X[i]), t_in=ts[i], P=P, c=C, dilation=d,
+                                 w_fg=ptr(self.pk("fg_w%d" % i)), fg=ptr(acts.FG[i]),
+                                 dxg=ptr(dxg), ld_dxg=ld_dxg,
+                                 dskip=sc["dskipcat"].data_ptr() + 4 * i * C, ld_dskip=L * C,
+                                 skip_row0=(ts[i + 1] - tf) * P, dfg=ptr(sc["dfg"]),
+                                 dw_fg=ptr(self.gk("fg_w%d" % i)), db_fg=ptr(self.gk("fg_b%d" % i)),
+                                 dx=ptr(dx), accumulate_dx=acc, workspace=ptr(ws))
+            lib.call("gwn_gated_tcn_bwd", ctypes.byref(tb), st)
+            dnext = dx
+        # start conv
+        rows0 = ts[0] * P
+        wgrad(dnext, C, acts.xin, cfg.Cin, rows0, self.gk("start_w"), ws)
+        lib.call("gwn_colsum", ptr(dnext), rows0, C, C, ptr(self.gk("start_b")), 0, ptr(ws), st)
+        if cfg.use_gcn and cfg.adaptive:
+            lib.call("gwn_adaptive_adj_bwd", ptr(self.pk("nv1")), ptr(self.pk("nv2")), ptr(acts.adp),
+                     ptr(sc["dadp"]), N, 10, N, ptr(self.gk("nv1")), ptr(self.gk("nv2")), ptr(ws), st)
+
+    def unpack_grads(self, gflat):
+        _lib.call("gwn_gather", ptr(self.gpacked), ptr(self.uidx), ptr(gflat), self.layout.flat_total,
+                  _lib.stream())
+
+
+def _ksplit(M, N, K):
+    tiles = ((M + 127) // 128) * ((N + 63) // 64)
+    ks = max(1, min(1024 // max(tiles, 1), K // 256))
+    return ks
+
+
+def gemm(A, lda_m, lda_k, B, ldb_k, ldb_n, Cout, ldc_m, ldc_n, M, N, K, bias=None, relu=0, epi=0,
+         mask=None, ldmask=0, C0=None, ldc0=0, beta=1.0, ksplit=1, part=None):
+    d = _lib.GemmDesc()
+    d.A, d.lda_m, d.lda_k = ptr(A), lda_m, lda_k
+    d.B, d.ldb_k, d.ldb_n = ptr(B), ldb_k, ldb_n
+    d.C, d.ldc_m, d.ldc_n = ptr(Cout), ldc_m, ldc_n
+    d.M, d.N, d.K = M, N, K
+    d.alpha = 1.0
+    d.beta = beta
+    d.bias_n = ptr(bias)
+    d.relu = relu
+    d.epi = epi
+    d.mask, d.ldmask_m = ptr(mask), ldmask
+    if C0 is not None:
+        d.C0, d.ldc0_m, d.ldc0_n = ptr(C0), ldc0, 1
+    d.ksplit = ksplit
+    d.part = ptr(part)
+    _lib.call("gwn_gemm", ctypes.byref(d), _lib.stream())
+
+
+def wgrad(dY, J, X, Kc, rows, out, ws):
+    """out[j][k] = sum_r dY[r][j] * X[r][k]   (1x1 conv weight gradient, split over rows)."""
+    ks = _ksplit(J, Kc, rows)
+    gemm(dY, 1, J, X, Kc, 1, out, Kc, 1, M=J, N=Kc, K=rows, ksplit=ks, part=ws)

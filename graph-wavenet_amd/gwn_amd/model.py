@@ -1,0 +1,264 @@
+"""Drop-in ``gwnet`` (reference model.py:82-241) whose forward/backward run on libgwn (HIP, gfx950).
+
+Constructor signature, attributes (``nodevec1``, ``nodevec2``, ``supports``, ``receptive_field``,
+``supports_len``), submodule tree and therefore ``state_dict`` keys / shapes are those of the
+reference, and parameters are created in the reference's order with the same init functions, so
+``torch.manual_seed(s); gwnet(...)`` yields the reference's initial weights bit for bit.
+
+Below the module boundary nothing is PyTorch compute: every parameter lives in one flat fp32
+device buffer (``_flat``), the forward is a fixed schedule of libgwn launches (executor.py) and
+the backward is the matching hand-written gradient schedule, wrapped as ONE autograd node.
+"""
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .executor import Executor, gemm  # noqa: F401  (gemm re-exported for the op-level modules)
+
+F32 = torch.float32
+
+
+class nconv(nn.Module):
+    """``einsum('ncvl,vw->ncwl')`` (reference model.py:8-14) on libgwn's batched MFMA GEMM."""
+
+    def forward(self, x, A):
+        return _NconvFn.apply(x, A)
+
+
+class _NconvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, A):
+        _require_device(x, A)
+        x = x.contiguous()
+        A = A.contiguous()
+        B, C, N, T = x.shape
+        y = torch.empty_like(x)
+        # NCHW slices: rows = nodes, "channels" = the T time steps of one (b, c) pair
+        _lib.call("gwn_nconv", A.data_ptr(), N, 1, x.data_ptr(), T, y.data_ptr(), T, None, 0, N, T, B * C,
+                  _lib.stream())
+        ctx.save_for_backward(x, A)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, A = ctx.saved_tensors
+        dy = dy.contiguous()
+        B, C, N, T = x.shape
+        dx = dA = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _lib.call("gwn_nconv", A.data_ptr(), N, 0, dy.data_ptr(), T, dx.data_ptr(), T, None, 0, N, T,
+                      B * C, _lib.stream())
+        if ctx.needs_input_grad[1]:
+            dA = torch.empty_like(A)
+            lib = _lib.load()
+            ws = torch.empty(max(1, lib.gwn_nconv_adj_grad_workspace_floats(N, T, B * C)), device=x.device,
+                             dtype=F32)
+            _lib.call("gwn_nconv_adj_grad", x.data_ptr(), T, dy.data_ptr(), T, N, T, B * C, dA.data_ptr(), N,
+                      0, ws.data_ptr(), _lib.stream())
+        return dx, dA
+
+
+class linear(nn.Module):
+    """1x1 convolution container (reference model.py:24-30); holds ``mlp`` for state_dict parity."""
+
+    def __init__(self, c_in, c_out):
+        super().__init__()
+        self.mlp = torch.nn.Conv2d(c_in, c_out, kernel_size=(1, 1), padding=(0, 0), stride=(1, 1), bias=True)
+
+    def forward(self, x):
+        raise NotImplementedError("gwn_amd.linear is evaluated inside gwnet's fused schedule")
+
+
+class gcn(nn.Module):
+    """Diffusion graph convolution container (reference model.py:32-55).  Inside ``gwnet`` its
+    arithmetic is executed by ``gwn_gcn_fwd`` / ``gwn_gcn_bwd``; the module keeps the parameters
+    (``mlp.mlp``: Conv2d((order*support_len+1)*c_in -> c_out)) and the hyper-parameters."""
+
+    def __init__(self, c_in, c_out, dropout, support_len=3, order=2):
+        super().__init__()
+        if order != 2:
+            raise ValueError("gwn_amd: diffusion order 2 (the reference default) is implemented")
+        self.nconv = nconv()
+        self.mlp = linear((order * support_len + 1) * c_in, c_out)
+        self.dropout = dropout
+        self.order = order
+
+    def forward(self, x, support):
+        raise NotImplementedError("gwn_amd.gcn is evaluated inside gwnet's fused schedule")
+
+
+def _require_device(*ts):
+    for t in ts:
+        if not (t.is_cuda and t.dtype == F32):
+            raise RuntimeError("gwn_amd: the HIP path needs float32 tensors on a GPU device "
+                               "(there is no CPU fallback)")
+
+
+class gwnet(nn.Module):
+    def __init__(self, device, num_nodes, dropout=0.3, supports=None, gcn_bool=True, addaptadj=True,
+                 aptinit=None, in_dim=2, out_dim=12, residual_channels=32, dilation_channels=32,
+                 skip_channels=256, end_channels=512, kernel_size=2, blocks=4, layers=2):
+        super().__init__()
+        self.dropout = dropout
+        self.blocks = blocks
+        self.layers = layers
+        self.gcn_bool = gcn_bool
+        self.addaptadj = addaptadj
+        self.num_nodes = num_nodes
+        self.in_dim, self.out_dim = in_dim, out_dim
+        self.residual_channels, self.dilation_channels = residual_channels, dilation_channels
+        self.skip_channels, self.end_channels = skip_channels, end_channels
+        self.kernel_size = kernel_size
+
+        # Submodule registration order == reference state_dict order (model.py:95-100).
+        for name in ("filter_convs", "gate_convs", "residual_convs", "skip_convs", "bn", "gconv"):
+            setattr(self, name, nn.ModuleList())
+        # RNG consumption order == reference (model.py:102-169): start_conv, node embeddings,
+        # then per layer filter, gate, residual, skip, bn, gcn-mlp; then the two end convs.
+        self.start_conv = nn.Conv2d(in_channels=in_dim, out_channels=residual_channels, kernel_size=(1, 1))
+        self.supports = supports
+        self.supports_len = len(supports) if supports is not None else 0
+        if gcn_bool and addaptadj:
+            if self.supports is None:
+                self.supports = []
+            if aptinit is None:
+                e1 = torch.randn(num_nodes, 10)
+                e2 = torch.randn(10, num_nodes)
+            else:
+                # SVD initialisation (model.py:123-127): E1 = U_10 sqrt(S_10), E2 = sqrt(S_10) V_10^T
+                u, s, v = torch.svd(aptinit.detach().to("cpu", F32))
+                root = torch.diag(s[:10] ** 0.5)
+                e1 = torch.mm(u[:, :10], root)
+                e2 = torch.mm(root, v[:, :10].t())
+            self.nodevec1 = nn.Parameter(e1, requires_grad=True)
+            self.nodevec2 = nn.Parameter(e2, requires_grad=True)
+            self.supports_len += 1
+
+        receptive_field = 1
+        for _ in range(blocks):
+            scope, dilation = kernel_size - 1, 1
+            for _ in range(layers):
+                self._add_layer(dilation)
+                dilation *= 2
+                receptive_field += scope
+                scope *= 2
+        self.end_conv_1 = nn.Conv2d(in_channels=skip_channels, out_channels=end_channels, kernel_size=(1, 1),
+                                    bias=True)
+        self.end_conv_2 = nn.Conv2d(in_channels=end_channels, out_channels=out_dim, kernel_size=(1, 1), bias=True)
+        self.receptive_field = receptive_field
+
+        self._executor = None
+        self._flat = None
+        self._flat_ptrs = None
+        self._nbt = None
+        self._sup_cache = (None, None)
+        self._place(device)
+
+    def _add_layer(self, dilation):
+        rc, dc, k = self.residual_channels, self.dilation_channels, self.kernel_size
+        self.filter_convs.append(nn.Conv2d(in_channels=rc, out_channels=dc, kernel_size=(1, k), dilation=dilation))
+        # legacy Conv1d with a 2-D kernel (model.py:139-151): weight [out, in, 1, k]
+        self.gate_convs.append(nn.Conv1d(in_channels=rc, out_channels=dc, kernel_size=(1, k), dilation=dilation))
+        self.residual_convs.append(nn.Conv1d(in_channels=dc, out_channels=rc, kernel_size=(1, 1)))
+        self.skip_convs.append(nn.Conv1d(in_channels=dc, out_channels=self.skip_channels, kernel_size=(1, 1)))
+        self.bn.append(nn.BatchNorm2d(rc))
+        if self.gcn_bool:
+            self.gconv.append(gcn(dc, rc, self.dropout, support_len=self.supports_len))
+
+    # -----------------------------------------------------------------------------------------
+    def _place(self, device):
+        """Move to ``device`` and alias every parameter into one flat fp32 buffer."""
+        device = torch.device(device)
+        super().to(device)
+        params = list(self.parameters())
+        total = sum(p.numel() for p in params)
+        flat = torch.empty(total, device=device, dtype=F32)
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                n = p.numel()
+                flat[off:off + n].copy_(p.data.reshape(-1))
+                p.data = flat[off:off + n].view_as(p)
+                off += n
+            nbt = torch.zeros(len(self.bn), device=device, dtype=torch.long)
+            for i, m in enumerate(self.bn):
+                nbt[i] = m.num_batches_tracked
+                m.num_batches_tracked = nbt[i]
+        self._flat = flat
+        self._nbt = nbt
+        self._flat_ptrs = tuple(p.data_ptr() for p in params)
+
+    def _ensure_flat(self):
+        params = list(self.parameters())
+        ptrs = tuple(p.data_ptr() for p in params)
+        if ptrs != self._flat_ptrs or params[0].device != self._flat.device:
+            if any(p.dtype != F32 for p in params):
+                raise RuntimeError("gwn_amd: gwnet runs in float32 only")
+            self._place(params[0].device)
+            self._executor = None
+
+    def executor(self):
+        self._ensure_flat()
+        if self._executor is None:
+            self._executor = Executor(self)
+        ex = self._executor
+        ex.dropout = self.dropout
+        ex.bind(self._flat.device)
+        return ex
+
+    def _fixed_supports(self):
+        if self.supports is None or len(self.supports) == 0:
+            return []
+        key = tuple((s.data_ptr(), s._version) for s in self.supports)
+        if self._sup_cache[0] != key:
+            dev = self._flat.device
+            self._sup_cache = (key, [s.detach().to(dev, F32).contiguous() for s in self.supports])
+        return self._sup_cache[1]
+
+    def _bn_bufs(self):
+        out = []
+        for m in self.bn:
+            mom = 0.1 if m.momentum is None else m.momentum
+            out.append((m.running_mean, m.running_var, float(mom), float(m.eps)))
+        return out
+
+    def forward(self, input):
+        self.executor()
+        return _GwnetFn.apply(self, input, *self.parameters())
+
+
+class _GwnetFn(torch.autograd.Function):
+    """The whole gwnet forward as one autograd node; its backward is libgwn's gradient schedule.
+    Parameters that never reach the output (``residual_convs`` on the gcn path, the last layer's
+    gconv / bn, model.py:225-236) get ``None`` gradients, exactly as under reference autograd."""
+
+    @staticmethod
+    def forward(ctx, model, x, *params):
+        ex = model._executor
+        training = model.training
+        out, acts = ex.forward(model._flat, model._fixed_supports(), x, training, model._bn_bufs())
+        if training:
+            model._nbt.add_(1)
+        ctx.model = model
+        ctx.acts = acts
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        model = ctx.model
+        ex = model._executor
+        ex.backward(ctx.acts, dout)
+        gflat = torch.zeros_like(model._flat)
+        ex.unpack_grads(gflat)
+        ctx.acts = None
+        grads = []
+        lay = ex.layout
+        active = set(lay.active)
+        for name, p in model.named_parameters():
+            if name in active:
+                off, shape = lay.flat_off[name]
+                grads.append(gflat[off:off + p.numel()].view(shape))
+            else:
+                grads.append(None)
+        return (None, None, *grads)

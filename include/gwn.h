@@ -1,0 +1,249 @@
+/*
+ * libgwn — MI355X (gfx950) native kernels for the Graph WaveNet gwnet.forward()/backward hot path.
+ *
+ * C-ABI only: plain device pointers, sizes and a hipStream_t; no torch types.  Every entry point
+ * is asynchronous on the given stream, never allocates, never synchronises the host, and keeps
+ * no mutable global state besides a thread-local error string.  Workspaces are owned by the
+ * caller (see the *_workspace_floats queries).  Return value: 0 on success, otherwise a GWN_ERR_*
+ * code; gwn_last_error() gives the message.  All arithmetic is fp32 with fixed-order reductions
+ * (bitwise reproducible run to run).
+ *
+ * Internal activation layout ("slab-major, channels-last"): a tensor that the reference holds as
+ * NCHW [B, C, N, T] (model.py:175-241) is held as [T][B][N][C], i.e. a row-major matrix with
+ * rows = T*B*N positions and C contiguous channels.  One time step is a "slab" of P = B*N rows;
+ * one (t, b) pair is a "slice" of N consecutive rows (the operand of one diffusion step).
+ *
+ * The reference (sklin93/Graph-WaveNet) is pure Python with no FFI; each entry below names the
+ * reference function whose arithmetic it replaces (file:line in the reference tree).
+ */
+#ifndef GWN_H_
+#define GWN_H_
+
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GWN_OK 0
+#define GWN_ERR_ARG 1
+#define GWN_ERR_HIP 2
+
+int gwn_version(void);
+const char* gwn_last_error(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Generic fp32 MFMA GEMM:  C(m,n) = epi(alpha * sum_k A(m,k) * B(k,n)).
+ * Used for the 1x1 / dilated convolutions (model.py:102-104, 135-151, 161-169, 27) and their
+ * gradients.  Index maps (two-level so one launch can walk strided slices):
+ *   A(m,k): ko=k/a_kin, ki=k%a_kin, row=m+ko*a_row_shift (0<=row<a_rows else 0)
+ *           -> A[row*lda_m + ki*lda_k + ko*a_ko_stride]
+ *   B(k,n): kb=k/b_kin, kj=k%b_kin, no=n/b_nin, ni=n%b_nin
+ *           -> B[kj*ldb_k + kb*b_ko_stride + ni*ldb_n + no*b_no_stride]
+ *   C(m,n): no=n/c_nin, ni=n%c_nin -> C[m*ldc_m + ni*ldc_n + no*c_no_stride] (C0 alike)
+ * epi: 0 = store (+bias_n, relu, dropout, +beta*C0); 1 = gated tanh*sigmoid (columns 2c+g);
+ *      2 = relu-backward mask (keep where mask(m,n) > 0).
+ * ksplit > 1 splits K over blocks; the partial sums go to `part` ([ksplit][M][N] floats, see
+ * gwn_gemm_workspace_floats) and are reduced in a fixed order.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct gwn_gemm_desc {
+  const float* A; long lda_m, lda_k, a_ko_stride; int a_kin, a_row_shift, a_rows;
+  const float* B; long ldb_k, ldb_n, b_ko_stride, b_no_stride; int b_kin, b_nin;
+  float* C; long ldc_m, ldc_n, c_no_stride; int c_nin;
+  const float* C0; long ldc0_m, ldc0_n, c0_no_stride; float beta;
+  const float* bias_n;
+  const float* mask; long ldmask_m;
+  int M, N, K;
+  float alpha;
+  int epi, relu;
+  float* aux; long ld_aux;
+  float* aux2; long ld_aux2; int aux2_row0;
+  const unsigned long long* seed_ptr; unsigned long long seed_salt; float drop_p;
+  int ksplit, kchunk; float* part;
+} gwn_gemm_desc;
+
+int gwn_gemm(const gwn_gemm_desc* desc, hipStream_t stream);
+long gwn_gemm_workspace_floats(int M, int N, int ksplit);
+
+/* ---------------------------------------------------------------------------------------------
+ * nconv (model.py:12-14): einsum('ncvl,vw->ncwl', x, A), i.e. for every slice s
+ *   y_s[w][c] = sum_v A[v][w] * x_s[v][c]            (transpose_a = 1, the forward)
+ *   y_s[v][c] = sum_w A[v][w] * x_s[w][c]            (transpose_a = 0, its input gradient)
+ * plus an optional addend y0 (may alias y).  A is [n][lda]; slices are `slices` blocks of n rows
+ * of C channels, row stride ldx / ldy / ldy0 (floats), consecutive slices n rows apart.
+ * ------------------------------------------------------------------------------------------- */
+int gwn_nconv(const float* A, int lda, int transpose_a, const float* x, long ldx, float* y,
+              long ldy, const float* y0, long ldy0, int n, int c, int slices, hipStream_t stream);
+
+/* Adjacency gradient of nconv (the backward of model.py:13 w.r.t. A, used for the adaptive
+ * support): dA[v][w] (+)= sum_{s,c} x_s[v][c] * dy_s[w][c].  `accumulate` adds to dA.  Needs
+ * gwn_nconv_adj_grad_workspace_floats(n, slices*c) floats of workspace. */
+int gwn_nconv_adj_grad(const float* x, long ldx, const float* dy, long lddy, int n, int c,
+                       int slices, float* dA, int ld_dA, int accumulate, float* workspace,
+                       hipStream_t stream);
+long gwn_nconv_adj_grad_workspace_floats(int n, int c, int slices);
+
+/* ---------------------------------------------------------------------------------------------
+ * Adaptive adjacency (model.py:185-188): adp = softmax(relu(E1 @ E2), dim=1), E1 [n][d],
+ * E2 [d][n]; adp is written as [n][ld_adp].  Backward (autograd of the same expression):
+ * given dadp [n][ld_adp] -> dE1 [n][d], dE2 [d][n]; workspace = n*ld_adp floats.
+ * ------------------------------------------------------------------------------------------- */
+int gwn_adaptive_adj_fwd(const float* e1, const float* e2, int n, int d, float* adp, int ld_adp,
+                         hipStream_t stream);
+int gwn_adaptive_adj_bwd(const float* e1, const float* e2, const float* adp, const float* dadp,
+                         int n, int d, int ld_adp, float* de1, float* de2, float* workspace,
+                         hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Input padding + start_conv (model.py:176-181): x is the reference NCHW input [B][cin][n][t]
+ * given by element strides (may be a non-contiguous transpose view, train.py:245); it is
+ * left-padded with zeros to t0 >= t steps and mapped 1x1 cin -> c:
+ *   out[(tt*B + b)*n + v][co] = bias[co] + sum_ci W[co][ci] * xpad[b][ci][v][tt]
+ * xin (optional, [t0*B*n][cin]) receives the padded input channels-last (for the weight grad).
+ * ------------------------------------------------------------------------------------------- */
+int gwn_start_conv_fwd(const float* x, long sb, long sc, long sn, long st, int B, int cin, int n,
+                       int t, int t0, const float* W, const float* bias, int c, float* out,
+                       float* xin, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Gated dilated TCN (model.py:206-212; filter_convs Conv2d 135-137, gate_convs legacy Conv1d
+ * 139-141):  for output row r (t < t_out = t_in - dilation):
+ *   f = Wf0 x[r] + Wf1 x[r + d*P] + bf,  g = Wg0 x[r] + Wg1 x[r + d*P] + bg,
+ *   xg[r] = tanh(f) * sigmoid(g)
+ * w_fg is the packed [2c][2c] matrix (row 2co+gate, column tap*c+ci), b_fg [2c] interleaved the
+ * same way.  fg [rows][2c] receives (tanh f, sigmoid g) for the backward.  xg is written with
+ * row stride ld_xg (it is piece 0 of the gcn concat, model.py:42).  skipcat (optional) receives
+ * the rows >= skip_row0 at column offset given by its pointer (the skip path only reads the last
+ * T_final steps, model.py:216-222).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct gwn_tcn_args {
+  const float* x; int t_in, P, c, dilation;
+  const float* w_fg; const float* b_fg;
+  float* xg; long ld_xg;
+  float* fg;
+  float* skipcat; long ld_skip; int skip_row0;
+} gwn_tcn_args;
+int gwn_gated_tcn_fwd(const gwn_tcn_args* a, hipStream_t stream);
+
+/* Backward: dxg [rows][ld_dxg] (NULL = zero) (+ dskip [rows-skip_row0][ld_dskip] for rows >= skip_row0) ->
+ *   dfg (scratch [rows][2c]), dW_fg [2c][2c] (packed like w_fg), db_fg [2c],
+ *   dx [t_in*P][c]  (+)= tap-0 rows and tap-1 rows (accumulate_dx adds to existing content).
+ * workspace: gwn_gated_tcn_bwd_workspace_floats(...) floats. */
+typedef struct gwn_tcn_bwd_args {
+  const float* x; int t_in, P, c, dilation;
+  const float* w_fg; const float* fg;
+  const float* dxg; long ld_dxg;
+  const float* dskip; long ld_dskip; int skip_row0;
+  float* dfg;
+  float* dw_fg; float* db_fg;
+  float* dx; int accumulate_dx;
+  float* workspace;
+} gwn_tcn_bwd_args;
+int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t stream);
+long gwn_gated_tcn_bwd_workspace_floats(int t_in, int P, int c, int dilation);
+
+/* ---------------------------------------------------------------------------------------------
+ * Graph convolution + residual (gcn.forward model.py:41-55 and model.py:234):
+ *   h = [xg, A1^T xg, (A1^T)^2 xg, ..., AK^T xg, (AK^T)^2 xg]  (piece-major concat, order=2)
+ *   z = dropout(W_mlp h + b_mlp) + residual[rows shifted by d*P]
+ * h is a [rows][(2K+1)c] buffer whose piece 0 already holds xg (written by the TCN);
+ * supports [K] point to [n][ld_sup] matrices (the adaptive one included).  If nsup == 0 the
+ * residual_convs 1x1 conv (model.py:232) is applied instead: z = W xg + b + residual.
+ * Dropout keeps h(m, c) iff hash(*seed, salt, m*c_out + c) >= p, scaled by 1/(1-p)
+ * (train mode only; p = 0 disables).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct gwn_gcn_args {
+  int rows, n, c, nsup;
+  const float* const* sup; int ld_sup;
+  float* h; long ld_h;
+  const float* w_mlp; const float* b_mlp;
+  const float* residual;
+  float* z;
+  const unsigned long long* seed_ptr; unsigned long long salt; float drop_p;
+} gwn_gcn_args;
+int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t stream);
+
+/* Backward of gwn_gcn_fwd given dh (gradient w.r.t. the dropout output, i.e. dz with the
+ * dropout mask and scale already applied).  Produces dW_mlp [c][(2K+1)c], db_mlp [c], the
+ * concat gradient dhcat [rows][ld_dhcat] whose piece 0 (columns 0..c) ends up holding dxg, and,
+ * for support `adp_index` (-1 = none), the adjacency gradient dadp [n][ld_sup].  Workspace
+ * floats from gwn_gcn_bwd_workspace_floats. */
+typedef struct gwn_gcn_bwd_args {
+  int rows, n, c, nsup;
+  const float* const* sup; int ld_sup;
+  const float* h; long ld_h;
+  const float* w_mlp;
+  const float* dh;
+  float* dhcat; long ld_dhcat;
+  float* dw_mlp; float* db_mlp;
+  int adp_index; float* dadp; int accumulate_dadp;
+  float* workspace;
+} gwn_gcn_bwd_args;
+int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
+long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);
+
+/* ---------------------------------------------------------------------------------------------
+ * BatchNorm2d (model.py:236, bn = nn.BatchNorm2d(c) model.py:152) over the rows of z [rows][c].
+ * train: batch mean / biased variance (eps), running stats updated with `momentum` and the
+ * unbiased variance; mean/rstd saved for the backward.  eval: running stats.
+ * ------------------------------------------------------------------------------------------- */
+int gwn_batchnorm_fwd(const float* z, int rows, int c, const float* gamma, const float* beta,
+                      float* running_mean, float* running_var, float momentum, float eps,
+                      int training, float* out, float* save_mean, float* save_rstd,
+                      float* workspace, hipStream_t stream);
+long gwn_batchnorm_workspace_floats(int rows, int c);
+
+/* BN backward fused with the residual split and the dropout backward of the same layer:
+ *   dz = gamma*rstd*(dy - mean(dy) - xhat*mean(dy*xhat));  dgamma, dbeta
+ *   dres[r + res_row0] = dz[r]   (the residual path, model.py:234; rows < res_row0 zeroed)
+ *   dh[r] = dz[r] * mask(r) / (1-p)   (dropout backward, model.py:54)  */
+int gwn_batchnorm_bwd(const float* dy, const float* z, int rows, int c, const float* gamma,
+                      const float* save_mean, const float* save_rstd, float* dgamma,
+                      float* dbeta, float* dres, int res_row0, float* dh,
+                      const unsigned long long* seed_ptr, unsigned long long salt,
+                      float drop_p, float* workspace, hipStream_t stream);
+
+/* Column sums db[j] = sum_r dy[r][j] (bias gradients), fixed order. */
+int gwn_colsum(const float* dy, int rows, int ncol, long ld, float* out, int accumulate,
+               float* workspace, hipStream_t stream);
+long gwn_colsum_workspace_floats(int rows, int ncol);
+
+/* ---------------------------------------------------------------------------------------------
+ * Masked metrics + loss gradient (engine.py:46-58, util.py:510-552 with null_val = 0):
+ *   pred[b][t][v][o] = out[b][o][v][t] * std + mean,   real[b][v][o] broadcast over t
+ *   metrics[0..2] = masked MAE, MAPE, RMSE;  dout = d(MAE)/d(out) (if dout != NULL)
+ * ------------------------------------------------------------------------------------------- */
+int gwn_masked_loss(const float* out, const float* real, long rsb, long rsn, long rso, int B,
+                    int o, int n, int tf, float mean, float std, float* metrics, float* dout,
+                    float* workspace, hipStream_t stream);
+long gwn_masked_loss_workspace_floats(int B, int o, int n, int tf);
+
+/* ---------------------------------------------------------------------------------------------
+ * Optimiser tail (engine.py:53-55): clip_grad_norm_(max_norm) over the listed ranges of the flat
+ * gradient buffer, then torch.optim.Adam (L2 weight decay, bias correction) on the same ranges.
+ * range_lo / range_hi: DEVICE arrays of nranges [lo, hi) element ranges; `total` = the number of
+ * elements they cover.  step_ptr: device int64 step counter (incremented before use).
+ * ------------------------------------------------------------------------------------------- */
+int gwn_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                  const long* range_lo, const long* range_hi, int nranges, long total,
+                  float max_norm, float lr, float beta1, float beta2, float eps,
+                  float weight_decay, long long* step_ptr, float* workspace,
+                  float* total_norm_out, hipStream_t stream);
+long gwn_clip_adam_workspace_floats(long total);
+
+/* dst[i] = src[idx[i]] (parameter repacking into kernel layouts and back). */
+int gwn_gather(const float* src, const int* idx, float* dst, long count, hipStream_t stream);
+/* out[b][o][v][t] = y[(t*B + b)*n + v][o]  (head output back to the reference NCHW layout) */
+int gwn_to_nchw(const float* y, int B, int o, int n, int t, float* out, hipStream_t stream);
+/* dy[(t*B + b)*n + v][o] = dout[b][o][v][t] */
+int gwn_from_nchw(const float* dout, int B, int o, int n, int t, float* dy, hipStream_t stream);
+/* sum of `count` vectors of length len spaced by stride: out[j] = sum_i x[i*stride + j] */
+int gwn_sum_vectors(const float* x, int count, int len, long stride, float* out,
+                    hipStream_t stream);
+/* (*counter) += inc  on the device (dropout seed / step bookkeeping inside graphs) */
+int gwn_increment_u64(unsigned long long* counter, unsigned long long inc, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GWN_H_ */

@@ -1,0 +1,231 @@
+"""ORACLE (test infrastructure only) — CPU restatement of Graph WaveNet's hot path.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module, and only as the checker / CPU baseline.  The product (graph-wavenet_amd/gwn_amd)
+never imports it.
+
+It restates, with plain torch-CPU tensor algebra written independently of the reference source,
+the arithmetic of:
+  * nconv               reference model.py:12-14     ('ncvl,vw->ncwl')
+  * gcn                 reference model.py:41-55     (K supports x order 2, concat, 1x1, dropout)
+  * gwnet.forward       reference model.py:175-241   (pad, start conv, 8 gated/dilated layers,
+                                                      skip, residual, BN, head)
+  * adaptive adjacency  reference model.py:185-188
+  * SVD node-embedding init  reference model.py:123-127
+  * trainer.train       reference engine.py:41-58    (pad, masked MAE, clip 5, Adam)
+  * masked metrics      reference Utils/util.py:510-552
+  * asym_adj            reference Utils/util.py:130-136
+
+Parity is PINNED: tests/test_oracle.py checks this restatement against the golden vectors in
+tests/golden/*.npz, which tests/golden/make_golden.py produced by running the reference itself.
+Default dtype is float64 (the "truth" the fp32 HIP path is compared against).
+"""
+import math
+
+import numpy as np
+import torch
+
+F64 = torch.float64
+
+
+class Cfg:
+    """Hyper-parameters of one gwnet (reference ctor, model.py:83-86)."""
+
+    def __init__(self, num_nodes, nfixed=2, gcn_bool=True, addaptadj=True, in_dim=2, out_dim=12, nhid=32,
+                 skip=None, end=None, blocks=4, layers=2, dropout=0.0):
+        self.N, self.nfixed = num_nodes, nfixed
+        self.gcn_bool, self.addaptadj = gcn_bool, addaptadj
+        self.Cin, self.O, self.C = in_dim, out_dim, nhid
+        self.S = skip if skip is not None else 8 * nhid
+        self.E = end if end is not None else 16 * nhid
+        self.blocks, self.layers, self.dropout = blocks, layers, dropout
+        self.dilations = [2 ** j for _ in range(blocks) for j in range(layers)]
+        self.receptive_field = 1 + sum(self.dilations)   # kernel 2: each layer adds its dilation
+        self.adaptive = gcn_bool and addaptadj
+        # model.py:110-128 + 225: the gcn path runs iff gcn_bool and supports is not None (the
+        # adaptive branch turns supports=None into [])
+        self.use_gcn = gcn_bool and (nfixed > 0 or self.adaptive)
+
+    @property
+    def L(self):
+        return self.blocks * self.layers
+
+
+def asym_adj(adj):
+    a = np.asarray(adj, dtype=np.float64)
+    rs = a.sum(1)
+    with np.errstate(divide="ignore"):
+        inv = 1.0 / rs
+    inv[~np.isfinite(inv)] = 0.0
+    return (inv[:, None] * a).astype(np.float32)
+
+
+def svd_embeddings(aptinit, rank=10):
+    u, s, v = torch.svd(torch.as_tensor(aptinit, dtype=torch.float32))
+    r = torch.diag(s[:rank].sqrt())
+    return u[:, :rank] @ r, r @ v[:, :rank].t()
+
+
+def adaptive_adjacency(e1, e2):
+    """softmax over rows of relu(E1 E2)."""
+    logits = torch.clamp(e1 @ e2, min=0.0)
+    logits = logits - logits.max(dim=1, keepdim=True).values
+    ex = torch.exp(logits)
+    return ex / ex.sum(dim=1, keepdim=True)
+
+
+def diffuse(x, a):
+    """y[b,c,w,t] = sum_v x[b,c,v,t] a[v,w]   (nconv)."""
+    b, c, n, t = x.shape
+    xt = x.permute(0, 1, 3, 2).reshape(b * c * t, n)
+    return (xt @ a).reshape(b, c, t, n).permute(0, 1, 3, 2)
+
+
+def pointwise(x, w, bias=None):
+    """1x1 convolution over NCHW: y[b,o,n,t] = sum_i w[o,i] x[b,i,n,t] + bias[o]."""
+    y = torch.einsum("oi,bint->bont", w.reshape(w.shape[0], -1), x)
+    return y if bias is None else y + bias.view(1, -1, 1, 1)
+
+
+def dilated_pair(x, w, bias, d):
+    """Conv with kernel (1,2), dilation d, no padding: taps at t and t+d."""
+    w0, w1 = w[:, :, 0, 0], w[:, :, 0, 1]
+    return pointwise(x[..., :-d], w0) + pointwise(x[..., d:], w1) + bias.view(1, -1, 1, 1)
+
+
+def batchnorm(x, gamma, beta, rmean, rvar, training, momentum=0.1, eps=1e-5):
+    if training:
+        n = x.numel() // x.shape[1]
+        mu = x.mean(dim=(0, 2, 3))
+        var = ((x - mu.view(1, -1, 1, 1)) ** 2).mean(dim=(0, 2, 3))
+        if rmean is not None:
+            with torch.no_grad():
+                rmean.mul_(1 - momentum).add_(momentum * mu.detach().to(rmean.dtype))
+                rvar.mul_(1 - momentum).add_(momentum * (var.detach() * n / max(n - 1, 1)).to(rvar.dtype))
+    else:
+        mu, var = rmean.to(x.dtype), rvar.to(x.dtype)
+    return (x - mu.view(1, -1, 1, 1)) / torch.sqrt(var.view(1, -1, 1, 1) + eps) * gamma.view(1, -1, 1, 1) \
+        + beta.view(1, -1, 1, 1)
+
+
+def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None):
+    """gwnet forward.  p: dict of parameter tensors (state_dict names); supports: list of [N,N]
+    fixed supports; x: [B, Cin, N, T]; bn_state: dict name->buffer updated in train mode."""
+    t = x.shape[-1]
+    if t < cfg.receptive_field:
+        x = torch.nn.functional.pad(x, (cfg.receptive_field - t, 0, 0, 0))
+    h = pointwise(x, p["start_conv.weight"], p["start_conv.bias"])
+    sups = list(supports) if cfg.use_gcn else []
+    if cfg.use_gcn and cfg.adaptive:
+        sups.append(adaptive_adjacency(p["nodevec1"], p["nodevec2"]))
+    skip = None
+    for i, d in enumerate(cfg.dilations):
+        res = h
+        filt = torch.tanh(dilated_pair(res, p["filter_convs.%d.weight" % i], p["filter_convs.%d.bias" % i], d))
+        gate = torch.sigmoid(dilated_pair(res, p["gate_convs.%d.weight" % i], p["gate_convs.%d.bias" % i], d))
+        g = filt * gate
+        s = pointwise(g, p["skip_convs.%d.weight" % i], p["skip_convs.%d.bias" % i])
+        skip = s if skip is None else s + skip[..., -s.shape[-1]:]
+        if cfg.use_gcn:
+            pieces = [g]
+            for a in sups:
+                y1 = diffuse(g, a)
+                y2 = diffuse(y1, a)
+                pieces += [y1, y2]
+            h = pointwise(torch.cat(pieces, dim=1), p["gconv.%d.mlp.mlp.weight" % i], p["gconv.%d.mlp.mlp.bias" % i])
+            if training and cfg.dropout > 0:
+                m = dropout_masks[i] if dropout_masks is not None else \
+                    (torch.rand_like(h) >= cfg.dropout).to(h.dtype)
+                h = h * m / (1 - cfg.dropout)
+        else:
+            h = pointwise(g, p["residual_convs.%d.weight" % i], p["residual_convs.%d.bias" % i])
+        h = h + res[..., -h.shape[-1]:]
+        rm = bn_state["bn.%d.running_mean" % i] if bn_state is not None else None
+        rv = bn_state["bn.%d.running_var" % i] if bn_state is not None else None
+        h = batchnorm(h, p["bn.%d.weight" % i], p["bn.%d.bias" % i], rm, rv, training)
+    y = torch.relu(pointwise(torch.relu(skip), p["end_conv_1.weight"], p["end_conv_1.bias"]))
+    return pointwise(y, p["end_conv_2.weight"], p["end_conv_2.bias"])
+
+
+def masked_metrics(pred, real, null_val=0.0):
+    """(mae, mape, rmse) with the zero-label mask renormalised by its mean (util.py:510-552)."""
+    mask = (real != null_val).float()          # the reference builds the mask in fp32 (.float())
+    mask = mask / mask.mean()
+    mask = torch.where(torch.isnan(mask), torch.zeros_like(mask), mask)
+
+    def fin(v):
+        return torch.where(torch.isnan(v), torch.zeros_like(v), v).mean()
+
+    diff = pred - real
+    mae = fin(diff.abs() * mask)
+    mape = fin(diff.abs() / real * mask)
+    rmse = torch.sqrt(fin(diff * diff * mask))
+    return mae, mape, rmse
+
+
+def engine_loss(p, supports, x, real_val, cfg, scaler_mean, scaler_std, bn_state=None, training=True):
+    """engine.py:41-51 up to the loss: pad 1, forward, inverse scale, masked MAE."""
+    x = torch.nn.functional.pad(x, (1, 0, 0, 0))
+    out = forward(p, supports, x, cfg, training, bn_state)
+    pred = out.transpose(1, 3) * scaler_std + scaler_mean
+    real = real_val.unsqueeze(1)
+    mae, mape, rmse = masked_metrics(pred, real)
+    return out, mae, mape, rmse
+
+
+def grads(sd, supports, x, real_val, cfg, scaler_mean, scaler_std, dtype=F64):
+    """Per-parameter gradients of the engine loss (train mode); params that do not reach the
+    output get no entry (the reference leaves their .grad None)."""
+    p = {k: torch.tensor(np.asarray(v), dtype=dtype, requires_grad=True) for k, v in sd.items()
+         if not _is_buffer(k)}
+    bn = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in sd.items() if "running" in k}
+    sups = [torch.tensor(np.asarray(a), dtype=dtype) for a in supports]
+    out, mae, mape, rmse = engine_loss(p, sups, torch.tensor(x, dtype=dtype), torch.tensor(real_val, dtype=dtype),
+                                       cfg, scaler_mean, scaler_std, bn)
+    names = list(p.keys())
+    gs = torch.autograd.grad(mae, [p[n] for n in names], allow_unused=True)
+    g = {n: gi for n, gi in zip(names, gs) if gi is not None}
+    return out.detach(), (mae.item(), mape.item(), rmse.item()), g, bn
+
+
+def _is_buffer(k):
+    return ("running_" in k) or ("num_batches_tracked" in k)
+
+
+class Trainer:
+    """engine.trainer restated (engine.py:41-58): clip_grad_norm_(5) + torch.optim.Adam math."""
+
+    def __init__(self, sd, supports, cfg, lr=1e-3, wd=1e-4, clip=5.0, scaler=(54.4, 19.5), dtype=F64):
+        self.cfg, self.lr, self.wd, self.clip = cfg, lr, wd, clip
+        self.scaler = scaler
+        self.dtype = dtype
+        self.p = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in sd.items() if not _is_buffer(k)}
+        self.bn = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in sd.items() if "running" in k}
+        self.m = {k: torch.zeros_like(v) for k, v in self.p.items()}
+        self.v = {k: torch.zeros_like(v) for k, v in self.p.items()}
+        self.t = 0
+        self.sups = [torch.tensor(np.asarray(a), dtype=dtype) for a in supports]
+
+    def train(self, x, real_val):
+        for v in self.p.values():
+            v.requires_grad_(True)
+        out, mae, mape, rmse = engine_loss(self.p, self.sups, torch.as_tensor(x, dtype=self.dtype),
+                                           torch.as_tensor(real_val, dtype=self.dtype), self.cfg,
+                                           self.scaler[0], self.scaler[1], self.bn)
+        names = list(self.p.keys())
+        gs = torch.autograd.grad(mae, [self.p[n] for n in names], allow_unused=True)
+        g = {n: gi for n, gi in zip(names, gs) if gi is not None}
+        with torch.no_grad():
+            total = math.sqrt(sum(float((gi.double() ** 2).sum()) for gi in g.values()))
+            coef = min(self.clip / (total + 1e-6), 1.0)
+            self.t += 1
+            b1, b2, eps = 0.9, 0.999, 1e-8
+            for n, gi in g.items():
+                gi = gi * coef + self.wd * self.p[n]
+                self.m[n] = self.m[n] + (1 - b1) * (gi - self.m[n])
+                self.v[n] = self.v[n] * b2 + (1 - b2) * gi * gi
+                denom = self.v[n].sqrt() / math.sqrt(1 - b2 ** self.t) + eps
+                self.p[n] = self.p[n] - (self.lr / (1 - b1 ** self.t)) * self.m[n] / denom
+        for v in self.p.values():
+            v.requires_grad_(False)
+        return mae.item(), mape.item(), rmse.item()

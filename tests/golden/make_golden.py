@@ -1,0 +1,248 @@
+"""Generate the golden vectors in tests/golden/*.npz by running the REFERENCE implementation.
+
+Runs ONLY in the build container, where /root/reference exists (read-only).  Nothing from the
+reference is copied into the repo: the reference modules are imported from their own path and
+only their numeric outputs (inputs, state_dicts, outputs, grads, metrics) are written as .npz.
+
+Harness-side shims needed to import the reference under torch 2.10:
+  1. stub ``ipdb``      (imported at model.py:6, engine.py:7, util.py:11; not installed)
+  2. stub ``nibabel``   (Utils/CRASH_loader.py:7, pulled in by util.py:9)
+  3. matplotlib ``Agg`` and a no-op ``matplotlib.use`` (engine.py:5 asks for TkAgg)
+  4. legacy ``nn.Conv1d`` on 4-D input (model.py:139-151): torch 1.x expanded the 1-tuple
+     stride/padding/dilation to both dims and ran a 2-D conv; torch >= 1.11 raises.  The shim
+     routes 4-D input to ``F.conv2d`` with the expanded params (kernel height 1, so the
+     H-dilation is irrelevant).
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "graph-wavenet_amd"))
+from gwn_amd import synthetic  # noqa: E402  (numpy-only input generator, shared with tests)
+
+
+def _install_shims():
+    sys.dont_write_bytecode = True
+    sys.modules.setdefault("ipdb", types.ModuleType("ipdb"))
+    sys.modules["ipdb"].set_trace = lambda *a, **k: None
+    sys.modules.setdefault("nibabel", types.ModuleType("nibabel"))
+    import matplotlib
+    matplotlib.use("Agg")
+    matplotlib.use = lambda *a, **k: None
+
+    orig = nn.Conv1d._conv_forward
+
+    def _conv_forward(self, input, weight, bias):
+        if input.dim() == 4:
+            s, p, d = self.stride[0], self.padding[0], self.dilation[0]
+            return F.conv2d(input, weight, bias, (s, s), (p, p), (d, d), self.groups)
+        return orig(self, input, weight, bias)
+
+    nn.Conv1d._conv_forward = _conv_forward
+    sys.path.insert(0, REF)
+
+
+def _sd(model):
+    return {"sd/" + k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+
+
+def _grads(model, prefix="grad/"):
+    out = {}
+    for k, p in model.named_parameters():
+        if p.grad is not None:
+            # f64 truth stored as f32: the 6e-8 rounding is far below the 1e-4 grad tolerance
+            out[prefix + k] = p.grad.detach().cpu().float().numpy().copy()
+    return out
+
+
+def _ref_model(ref_model, num_nodes, supports, seed=999, dropout=0.0, **kw):
+    torch.manual_seed(seed)
+    sup = None if supports is None else [torch.tensor(a) for a in supports]
+    return ref_model.gwnet("cpu", num_nodes, dropout, supports=sup, **kw)
+
+
+def _loss_grads(ref_model, util, model, x, y, dtype):
+    """engine.py:41-52 up to (and including) loss.backward(), on a model cast to ``dtype``."""
+    m = model.to(dtype)
+    if m.supports is not None:
+        m.supports = [a.to(dtype) for a in m.supports]
+    m.train()
+    m.zero_grad()
+    scaler = util.StandardScaler(synthetic.SCALER_MEAN, synthetic.SCALER_STD)
+    inp = nn.functional.pad(torch.tensor(x, dtype=dtype), (1, 0, 0, 0))
+    out = m(inp)
+    pred = scaler.inverse_transform(out.transpose(1, 3))
+    real = torch.unsqueeze(torch.tensor(y, dtype=dtype), dim=1)
+    loss = util.masked_mae(pred, real, 0.0)
+    loss.backward()
+    mape = util.masked_mape(pred, real, 0.0)
+    rmse = util.masked_rmse(pred, real, 0.0)
+    return out, loss, mape, rmse
+
+
+def main():
+    _install_shims()
+    import model as ref_model  # /root/reference/model.py
+    import engine as ref_engine  # /root/reference/engine.py
+    import Utils.util as util  # /root/reference/Utils/util.py
+
+    torch.set_num_threads(8)
+    N = 207
+    adj = synthetic.random_sensor_graph(N, seed=0)
+    sup = synthetic.double_transition(adj)
+
+    # ---- G1+G2 (METR-LA shape, nhid 32, randomadj, seed 999 init shared by both) ----
+    # G1: eval forward, B=4, T=12 (the forward pads to 13 itself, model.py:176-178)
+    # G2: train mode, dropout=0, engine.py:41-52 loss + backward, B=4
+    g = {"adj": adj, "sup0": sup[0], "sup1": sup[1]}
+    m = _ref_model(ref_model, N, sup, dropout=0.3, gcn_bool=True, addaptadj=True)
+    g.update(_sd(m))
+    x, _ = synthetic.synthetic_batch(4, N, 12, seed=1)
+    g["g1_x"] = x
+    m.eval()
+    with torch.no_grad():
+        g["g1_out_f32"] = m(torch.tensor(x)).numpy()
+        md = m.double()
+        md.supports = [a.double() for a in md.supports]
+        g["g1_out_f64"] = md(torch.tensor(x, dtype=torch.float64)).float().numpy()
+    x, y = synthetic.synthetic_batch(4, N, 12, seed=2)
+    g["g2_x"], g["g2_y"] = x, y
+    for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        mm = _ref_model(ref_model, N, sup, dropout=0.0, gcn_bool=True, addaptadj=True)
+        out, loss, mape, rmse = _loss_grads(ref_model, util, mm, x, y, dt)
+        g["g2_out_" + tag] = out.detach().float().numpy()
+        g["g2_metrics_" + tag] = np.array([loss.item(), mape.item(), rmse.item()])
+        if tag == "f64":
+            g.update(_grads(mm, "g2_grad_f64/"))
+            for k, v in mm.state_dict().items():
+                if k.startswith("bn.") and ("running" in k or "num_batches" in k):
+                    g["g2_bnpost_f64/" + k] = v.detach().double().numpy().copy()
+    np.savez_compressed(os.path.join(HERE, "g12_metr_n207.npz"), **g)
+
+    # small-config fixtures: N=16, nhid=16 (skip 128, end 256 as engine.py:27-31 derives them)
+    n16 = 16
+    small = dict(residual_channels=16, dilation_channels=16, skip_channels=128, end_channels=256)
+    adj16 = synthetic.random_sensor_graph(n16, density=0.3, seed=3)
+    sup16 = synthetic.double_transition(adj16)
+    scaler = util.StandardScaler(synthetic.SCALER_MEAN, synthetic.SCALER_STD)
+
+    # ---- G3: three full trainer.train steps (clip 5 + Adam lr 1e-3 wd 1e-4), f64 truth ----
+    g3 = {"adj": adj16, "sup0": sup16[0], "sup1": sup16[1]}
+    torch.manual_seed(999)
+    eng = ref_engine.trainer(scaler, 2, 12, n16, 16, 0.0, 1e-3, 1e-4, "cpu",
+                             [torch.tensor(a) for a in sup16], True, True, None, 4, 2)
+    g3.update(_sd(eng.model))
+    eng.model.double()
+    eng.model.supports = [a.double() for a in eng.model.supports]
+    eng.optimizer = torch.optim.Adam(eng.model.parameters(), lr=1e-3, weight_decay=1e-4)
+    for step in range(3):
+        xs, ys = synthetic.synthetic_batch(4, n16, 12, seed=30 + step)
+        g3["x%d" % step], g3["y%d" % step] = xs, ys
+        met = eng.train(torch.tensor(xs, dtype=torch.float64), torch.tensor(ys, dtype=torch.float64))
+        g3["metrics%d_f64" % step] = np.array(met, dtype=np.float64)
+    for k, v in eng.model.state_dict().items():
+        g3["post_f64/" + k] = v.detach().double().numpy().copy()
+    np.savez_compressed(os.path.join(HERE, "g3_trainer_steps_n16.npz"), **g3)
+
+    # ---- G4: aptinit SVD initialisation (model.py:120-128): E1@E2 is sign-invariant ----
+    g4 = {"adj": adj16, "sup0": sup16[0], "sup1": sup16[1]}
+    m = _ref_model(ref_model, n16, sup16, dropout=0.3, gcn_bool=True, addaptadj=True,
+                   aptinit=torch.tensor(sup16[0]), **small)
+    g4["e1e2"] = (m.nodevec1 @ m.nodevec2).detach().numpy()
+    x, _ = synthetic.synthetic_batch(2, n16, 12, seed=4)
+    g4["x"] = x
+    m.eval()
+    with torch.no_grad():
+        g4["out_f32"] = m(torch.tensor(x)).numpy()
+    g4.update(_sd(m))
+    np.savez_compressed(os.path.join(HERE, "g4_aptinit_n16.npz"), **g4)
+
+    # ---- G5: variants (N=16, B=2): eval output + train-mode f64 grads ----
+    variants = {
+        "nogcn": dict(sup=sup16, gcn_bool=False, addaptadj=True),
+        "noadp": dict(sup=sup16, gcn_bool=True, addaptadj=False),
+        "aptonly": dict(sup=None, gcn_bool=True, addaptadj=True),
+        "blocks3": dict(sup=sup16, gcn_bool=True, addaptadj=True, blocks=3, layers=3),
+        "seq24": dict(sup=sup16, gcn_bool=True, addaptadj=True, seq=24),
+    }
+    for name, kw in variants.items():
+        kw = dict(kw)
+        s = kw.pop("sup")
+        seq = kw.pop("seq", 12)
+        kw.update(small)
+        kw["out_dim"] = seq
+        x, y = synthetic.synthetic_batch(2, n16, seq, seed=5)
+        g5 = {"x": x, "y": y, "adj": adj16, "sup0": sup16[0], "sup1": sup16[1]}
+        m = _ref_model(ref_model, n16, s, dropout=0.0, **kw)
+        g5.update(_sd(m))
+        m.eval()
+        with torch.no_grad():
+            g5["out_f32"] = m(torch.tensor(x)).numpy()
+        m2 = _ref_model(ref_model, n16, s, dropout=0.0, **kw)
+        out, loss, _, _ = _loss_grads(ref_model, util, m2, x, y, torch.float64)
+        g5["loss_f64"] = np.float64(loss.item())
+        g5["trainout_f64"] = out.detach().float().numpy()
+        g5.update(_grads(m2, "grad_f64/"))
+        np.savez_compressed(os.path.join(HERE, "g5_variant_%s_n16.npz" % name), **g5)
+
+    # ---- G5b: PEMS-BAY shape N=325 eval forward, B=2, nhid 32 ----
+    n325 = 325
+    adj325 = synthetic.random_sensor_graph(n325, seed=6)
+    sup325 = synthetic.double_transition(adj325)
+    x, _ = synthetic.synthetic_batch(2, n325, 12, seed=7)
+    m = _ref_model(ref_model, n325, sup325, dropout=0.3, gcn_bool=True, addaptadj=True)
+    m.eval()
+    g5b = {"x": x, "adj": adj325, "sup0": sup325[0], "sup1": sup325[1]}
+    g5b.update(_sd(m))
+    with torch.no_grad():
+        md = m.double()
+        md.supports = [a.double() for a in md.supports]
+        g5b["out_f64"] = md(torch.tensor(x, dtype=torch.float64)).float().numpy()
+    np.savez_compressed(os.path.join(HERE, "g5b_fwd_eval_n325.npz"), **g5b)
+
+    # ---- G6: op level: nconv (model.py:12-14), adaptive adjacency (model.py:187), gated TCN ----
+    rng = np.random.default_rng(8)
+    xo = rng.standard_normal((1, 32, N, 12)).astype(np.float32)
+    g6 = {"x": xo, "A": sup[0]}
+    g6["nconv"] = ref_model.nconv()(torch.tensor(xo), torch.tensor(sup[0])).numpy()
+    e1 = rng.standard_normal((N, 10)).astype(np.float32)
+    e2 = rng.standard_normal((10, N)).astype(np.float32)
+    g6["e1"], g6["e2"] = e1, e2
+    g6["adp"] = F.softmax(F.relu(torch.mm(torch.tensor(e1), torch.tensor(e2))), dim=1).numpy()
+    m = _ref_model(ref_model, N, sup, dropout=0.0)
+    with torch.no_grad():
+        xt = torch.tensor(xo)
+        filt = torch.tanh(m.filter_convs[1](xt))
+        gate = torch.sigmoid(m.gate_convs[1](xt))
+        g6["tcn_d2"] = (filt * gate).numpy()
+    for k in ("filter_convs.1.weight", "filter_convs.1.bias", "gate_convs.1.weight", "gate_convs.1.bias"):
+        g6["w/" + k] = m.state_dict()[k].numpy()
+    np.savez_compressed(os.path.join(HERE, "g6_ops_n207.npz"), **g6)
+
+    # ---- G7: data parallel: mean of per-shard f64 grads, 2 shards of B=2 (BN per replica) ----
+    x, y = synthetic.synthetic_batch(4, n16, 12, seed=9)
+    g7 = {"x": x, "y": y, "adj": adj16, "sup0": sup16[0], "sup1": sup16[1]}
+    m = _ref_model(ref_model, n16, sup16, dropout=0.0, gcn_bool=True, addaptadj=True, **small)
+    g7.update(_sd(m))
+    shard_grads = []
+    for r in range(2):
+        mm = _ref_model(ref_model, n16, sup16, dropout=0.0, gcn_bool=True, addaptadj=True, **small)
+        _loss_grads(ref_model, util, mm, x[2 * r:2 * r + 2], y[2 * r:2 * r + 2], torch.float64)
+        shard_grads.append(_grads(mm, ""))
+    for k in shard_grads[0]:
+        g7["gradmean_f64/" + k] = 0.5 * (shard_grads[0][k] + shard_grads[1][k])
+    np.savez_compressed(os.path.join(HERE, "g7_ddp_n16.npz"), **g7)
+    print("golden vectors written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,235 @@
+"""libgwn kernels vs fp64 CPU references (op level).  Tolerances are written per test."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _gemm(**kw):
+    from gwn_amd import _lib
+    d = _lib.GemmDesc()
+    d.alpha, d.beta, d.ksplit = 1.0, 1.0, 1
+    for k, v in kw.items():
+        if isinstance(v, torch.Tensor):
+            v = v.data_ptr()
+        setattr(d, k, v)
+    _lib.call("gwn_gemm", ctypes.byref(d), _lib.stream())
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (37, 29, 53), (256, 32, 32), (207, 64, 207), (300, 200, 100),
+                                   (1000, 512, 256), (13, 7, 1000)])
+@pytest.mark.parametrize("akc,bkc", [(True, False), (False, False), (True, True), (False, True)])
+def test_gemm_layouts(gpu, M, N, K, akc, bkc):
+    torch.manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, dtype=torch.float64)
+    B = torch.randn(K, N, dtype=torch.float64)
+    ref = A @ B
+    Ad = (A if akc else A.t()).contiguous().float().to(gpu)   # akc: [M][K]; else [K][M]
+    Bd = (B.t() if bkc else B).contiguous().float().to(gpu)   # bkc: [N][K]; else [K][N]
+    C = torch.full((M, N), float("nan"), device=gpu)
+    _gemm(A=Ad, lda_m=K if akc else 1, lda_k=1 if akc else M, B=Bd, ldb_k=1 if bkc else N, ldb_n=K if bkc else 1,
+          C=C, ldc_m=N, ldc_n=1, M=M, N=N, K=K)
+    torch.cuda.synchronize()
+    got = C.double().cpu()
+    # exact fp32 fma chain: |err| <= ~K * 2^-24 * sum|a||b|
+    bound = 2.0 ** -22 * K * (A.abs() @ B.abs())
+    assert torch.all((got - ref).abs() <= bound + 1e-30), float(((got - ref).abs() / (bound + 1e-30)).max())
+
+
+def test_mfma_layout_identity_asymmetric(gpu):
+    """A = I with an asymmetric B must reproduce B exactly (catches a transposed C write)."""
+    n = 64
+    A = torch.eye(n, device=gpu)
+    B = torch.arange(n * n, dtype=torch.float32, device=gpu).reshape(n, n) * 0.5 + 3
+    C = torch.zeros(n, n, device=gpu)
+    _gemm(A=A, lda_m=n, lda_k=1, B=B, ldb_k=n, ldb_n=1, C=C, ldc_m=n, ldc_n=1, M=n, N=n, K=n)
+    torch.cuda.synchronize()
+    assert torch.equal(C, B)
+
+
+def test_gemm_splitk_bias_relu_residual(gpu):
+    M, N, K = 96, 160, 5000
+    torch.manual_seed(3)
+    A = torch.randn(M, K, device=gpu)
+    B = torch.randn(K, N, device=gpu)
+    bias = torch.randn(N, device=gpu)
+    C0 = torch.randn(M, N, device=gpu)
+    part = torch.empty(8 * M * N, device=gpu)
+    C = torch.empty(M, N, device=gpu)
+    _gemm(A=A, lda_m=K, lda_k=1, B=B, ldb_k=N, ldb_n=1, C=C, ldc_m=N, ldc_n=1, M=M, N=N, K=K, ksplit=8, part=part,
+          bias_n=bias, relu=1, C0=C0, ldc0_m=N, ldc0_n=1, beta=0.5)
+    ref = torch.relu(A.double() @ B.double() + bias.double()) + 0.5 * C0.double()
+    torch.cuda.synchronize()
+    assert rel_err(C.cpu().numpy(), ref.cpu().numpy()) < 1e-5
+
+
+def test_gemm_two_level_taps_and_slices(gpu):
+    """Dilated two-tap rows (a_kin / a_row_shift / a_rows) and strided slices (b_nin / c_nin)."""
+    P, T, Cc, d = 10, 6, 16, 2
+    torch.manual_seed(4)
+    X = torch.randn(T * P, Cc, device=gpu)
+    W = torch.randn(2 * Cc, 24, device=gpu)  # [k=tap*C+ci][n]
+    rows = (T - d) * P
+    Y = torch.empty(rows, 24, device=gpu)
+    _gemm(A=X, lda_m=Cc, lda_k=1, a_kin=Cc, a_row_shift=d * P, a_rows=T * P, B=W, ldb_k=24, ldb_n=1,
+          C=Y, ldc_m=24, ldc_n=1, M=rows, N=24, K=2 * Cc)
+    Xd, Wd = X.double().cpu(), W.double().cpu()
+    ref = Xd[:rows] @ Wd[:Cc] + Xd[d * P:] @ Wd[Cc:]
+    torch.cuda.synchronize()
+    assert rel_err(Y.cpu().numpy(), ref.numpy()) < 1e-5
+    # backward-data form: negative shift with validity window
+    dY = torch.randn(rows, 2 * Cc, device=gpu)
+    Wt = torch.randn(2 * Cc, 2 * Cc, device=gpu)  # [j][tap*C+ci]
+    dX = torch.empty(T * P, Cc, device=gpu)
+    _gemm(A=dY, lda_m=2 * Cc, lda_k=1, a_kin=2 * Cc, a_row_shift=-d * P, a_rows=rows, B=Wt, ldb_k=2 * Cc, ldb_n=1,
+          b_kin=2 * Cc, b_ko_stride=Cc, C=dX, ldc_m=Cc, ldc_n=1, M=T * P, N=Cc, K=4 * Cc)
+    dYd, Wtd = dY.double().cpu(), Wt.double().cpu()
+    ref = torch.zeros(T * P, Cc, dtype=torch.float64)
+    ref[:rows] += dYd @ Wtd[:, :Cc]
+    ref[d * P:] += dYd @ Wtd[:, Cc:]
+    torch.cuda.synchronize()
+    assert rel_err(dX.cpu().numpy(), ref.numpy()) < 1e-5
+
+
+def test_nconv_matches_reference_golden(gpu):
+    from gwn_amd.model import nconv
+    g = load_golden("g6_ops_n207.npz")
+    x = torch.tensor(g["x"], device=gpu)
+    A = torch.tensor(g["A"], device=gpu)
+    y = nconv()(x, A)
+    torch.cuda.synchronize()
+    assert rel_err(y.cpu().numpy(), g["nconv"]) < 1e-5
+
+
+def test_nconv_backward(gpu):
+    from gwn_amd.model import nconv
+    torch.manual_seed(5)
+    x = torch.randn(2, 3, 29, 12, device=gpu, requires_grad=True)
+    A = torch.rand(29, 29, device=gpu, requires_grad=True)
+    y = nconv()(x, A)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xc = x.detach().double().cpu().requires_grad_(True)
+    Ac = A.detach().double().cpu().requires_grad_(True)
+    torch.einsum("ncvl,vw->ncwl", xc, Ac).backward(gy.double().cpu())
+    assert rel_err(x.grad.cpu().numpy(), xc.grad.numpy()) < 1e-5
+    assert rel_err(A.grad.cpu().numpy(), Ac.grad.numpy()) < 1e-5
+
+
+def test_adaptive_adjacency_fwd_bwd(gpu):
+    from gwn_amd import _lib
+    from oracle import gwnet_oracle as orc
+    g = load_golden("g6_ops_n207.npz")
+    n = 207
+    e1 = torch.tensor(g["e1"], device=gpu)
+    e2 = torch.tensor(g["e2"], device=gpu)
+    adp = torch.empty(n, n, device=gpu)
+    _lib.call("gwn_adaptive_adj_fwd", e1.data_ptr(), e2.data_ptr(), n, 10, adp.data_ptr(), n, _lib.stream())
+    torch.cuda.synchronize()
+    assert rel_err(adp.cpu().numpy(), g["adp"]) < 1e-5
+    dadp = torch.randn(n, n, device=gpu)
+    de1, de2 = torch.empty(n, 10, device=gpu), torch.empty(10, n, device=gpu)
+    ws = torch.empty(n * n, device=gpu)
+    _lib.call("gwn_adaptive_adj_bwd", e1.data_ptr(), e2.data_ptr(), adp.data_ptr(), dadp.data_ptr(), n, 10, n,
+              de1.data_ptr(), de2.data_ptr(), ws.data_ptr(), _lib.stream())
+    a = torch.tensor(g["e1"], dtype=torch.float64, requires_grad=True)
+    b = torch.tensor(g["e2"], dtype=torch.float64, requires_grad=True)
+    orc.adaptive_adjacency(a, b).backward(dadp.double().cpu())
+    torch.cuda.synchronize()
+    assert rel_err(de1.cpu().numpy(), a.grad.numpy()) < 1e-4
+    assert rel_err(de2.cpu().numpy(), b.grad.numpy()) < 1e-4
+
+
+def test_gated_tcn_matches_reference_golden(gpu):
+    from gwn_amd import _lib
+    g = load_golden("g6_ops_n207.npz")
+    x = torch.tensor(g["x"])  # [1, 32, 207, 12] NCHW
+    B, C, N, T = x.shape
+    d = 2
+    P = B * N
+    xl = x.permute(3, 0, 2, 1).contiguous().to(gpu)  # [T][B][N][C]
+    fw = torch.tensor(g["w/filter_convs.1.weight"]).reshape(C, C, 2)
+    gw = torch.tensor(g["w/gate_convs.1.weight"]).reshape(C, C, 2)
+    wfg = torch.stack([fw, gw], 1).permute(0, 1, 3, 2).reshape(2 * C, 2 * C).contiguous().to(gpu)
+    bfg = torch.stack([torch.tensor(g["w/filter_convs.1.bias"]), torch.tensor(g["w/gate_convs.1.bias"])],
+                      1).reshape(-1).contiguous().to(gpu)
+    rows = (T - d) * P
+    xg = torch.empty(rows, C, device=gpu)
+    fg = torch.empty(rows, 2 * C, device=gpu)
+    a = _lib.TcnArgs(x=xl.data_ptr(), t_in=T, P=P, c=C, dilation=d, w_fg=wfg.data_ptr(), b_fg=bfg.data_ptr(),
+                     xg=xg.data_ptr(), ld_xg=C, fg=fg.data_ptr(), skipcat=None, ld_skip=0, skip_row0=0)
+    _lib.call("gwn_gated_tcn_fwd", ctypes.byref(a), _lib.stream())
+    torch.cuda.synchronize()
+    got = xg.cpu().reshape(T - d, B, N, C).permute(1, 3, 2, 0).numpy()
+    assert rel_err(got, g["tcn_d2"]) < 1e-5
+
+
+def test_batchnorm_fwd_bwd(gpu):
+    from gwn_amd import _lib
+    torch.manual_seed(6)
+    rows, c = 5000, 32
+    z = (torch.randn(rows, c) * 3 + 1).to(gpu)
+    gamma, beta = torch.randn(c, device=gpu), torch.randn(c, device=gpu)
+    rm, rv = torch.zeros(c, device=gpu), torch.ones(c, device=gpu)
+    out = torch.empty_like(z)
+    mean, rstd = torch.empty(c, device=gpu), torch.empty(c, device=gpu)
+    ws = torch.empty(_lib.load().gwn_batchnorm_workspace_floats(rows, c), device=gpu)
+    _lib.call("gwn_batchnorm_fwd", z.data_ptr(), rows, c, gamma.data_ptr(), beta.data_ptr(), rm.data_ptr(),
+              rv.data_ptr(), 0.1, 1e-5, 1, out.data_ptr(), mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(),
+              _lib.stream())
+    zc = z.double().cpu().requires_grad_(True)
+    bn = torch.nn.BatchNorm1d(c).double()
+    with torch.no_grad():
+        bn.weight.copy_(gamma.double().cpu())
+        bn.bias.copy_(beta.double().cpu())
+    ref = bn(zc)
+    torch.cuda.synchronize()
+    assert rel_err(out.cpu().numpy(), ref.detach().numpy()) < 1e-5
+    assert rel_err(rm.cpu().numpy(), bn.running_mean.numpy()) < 1e-5
+    assert rel_err(rv.cpu().numpy(), bn.running_var.numpy()) < 1e-5
+    dy = torch.randn(rows, c, device=gpu)
+    ref.backward(dy.double().cpu())
+    dg, db = torch.empty(c, device=gpu), torch.empty(c, device=gpu)
+    dres = torch.full((rows + 7, c), float("nan"), device=gpu)
+    dh = torch.empty(rows, c, device=gpu)
+    _lib.call("gwn_batchnorm_bwd", dy.data_ptr(), z.data_ptr(), rows, c, gamma.data_ptr(), mean.data_ptr(),
+              rstd.data_ptr(), dg.data_ptr(), db.data_ptr(), dres.data_ptr(), 7, dh.data_ptr(), None, 0, 0.0,
+              ws.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    assert rel_err(dh.cpu().numpy(), zc.grad.numpy()) < 1e-4
+    assert torch.all(dres[:7] == 0)
+    assert torch.equal(dres[7:], dh)
+    assert rel_err(dg.cpu().numpy(), bn.weight.grad.numpy()) < 1e-5
+    assert rel_err(db.cpu().numpy(), bn.bias.grad.numpy()) < 1e-5
+
+
+def test_masked_loss_and_grad(gpu):
+    from gwn_amd import _lib
+    from oracle import gwnet_oracle as orc
+    torch.manual_seed(7)
+    B, O, N, tf = 8, 12, 50, 3
+    out = torch.randn(B, O, N, tf, device=gpu)
+    real = torch.clamp(54.4 + 19.5 * torch.randn(B, O, N), 0, 80)
+    real[torch.rand_like(real) < 0.1] = 0
+    real_t = real.permute(0, 2, 1).contiguous().to(gpu).transpose(1, 2)  # non-contiguous [B][N][O] view... 
+    real_v = real.permute(0, 2, 1).contiguous().to(gpu)  # [B][N][O]
+    metrics = torch.empty(4, device=gpu)
+    dout = torch.empty_like(out)
+    ws = torch.empty(_lib.load().gwn_masked_loss_workspace_floats(B, O, N, tf), device=gpu)
+    rs = real_v.stride()
+    _lib.call("gwn_masked_loss", out.data_ptr(), real_v.data_ptr(), rs[0], rs[1], rs[2], B, O, N, tf, 54.4, 19.5,
+              metrics.data_ptr(), dout.data_ptr(), ws.data_ptr(), _lib.stream())
+    oc = out.double().cpu().requires_grad_(True)
+    pred = oc.transpose(1, 3) * 19.5 + 54.4
+    mae, mape, rmse = orc.masked_metrics(pred, real_v.double().cpu().unsqueeze(1))
+    mae.backward()
+    torch.cuda.synchronize()
+    m = metrics.cpu().numpy()
+    np.testing.assert_allclose(m[:3], [mae.item(), mape.item(), rmse.item()], rtol=2e-5)
+    assert rel_err(dout.cpu().numpy(), oc.grad.numpy()) < 1e-5
+    del real_t
