@@ -23,13 +23,20 @@ def _model(g, device, n, dropout=0.0, sups=2, **kw):
     return m
 
 
-def _check_grads(model, ref, tag):
+def _bn_cancelled(name):
+    """Biases added right before a BatchNorm (no dropout in between) have an analytically zero
+    gradient: the batch mean removes any per-channel shift."""
+    return (name.startswith("gconv.") and name.endswith("mlp.bias")) or \
+        (name.startswith("residual_convs.") and name.endswith(".bias"))
+
+
+def _check_grads(model, ref, tag, dropout=False):
     got = {n: p.grad for n, p in model.named_parameters() if p.grad is not None}
     assert set(got) == set(ref), (tag, sorted(set(got) ^ set(ref)))
     scale = max(np.max(np.abs(v)) for v in ref.values())
     for k, v in ref.items():
         g = got[k].detach().cpu().numpy()
-        if k.startswith("gconv.") and k.endswith("mlp.bias"):
+        if _bn_cancelled(k) and not dropout:
             assert np.max(np.abs(g)) <= 1e-5 * scale, (tag, k)
         elif np.linalg.norm(v) > 0:
             assert norm_rel(g, v) <= 1e-4, (tag, k, norm_rel(g, v))
@@ -115,6 +122,9 @@ def test_g3_trainer_three_steps(gpu):
             got = sd[name].cpu().numpy()
             if "num_batches" in name:
                 assert int(got) == int(v), name
+            elif name.startswith("gconv.") and name.endswith("mlp.bias"):
+                # true gradient is 0 (BN cancels it): Adam turns fp noise into +-lr steps
+                assert np.max(np.abs(got - v)) <= 2 * 3 * 1e-3 + 1e-6, name
             else:
                 assert norm_rel(got, v) <= 1e-4, (name, norm_rel(got, v))
 
@@ -255,7 +265,7 @@ def test_dropout_forward_backward_exact_masks(gpu):
     names = list(p)
     gs = torch.autograd.grad(rl, [p[n] for n in names], allow_unused=True)
     refg = {n: gi.numpy() for n, gi in zip(names, gs) if gi is not None}
-    _check_grads(m, refg, "dropout")
+    _check_grads(m, refg, "dropout", dropout=True)
 
 
 def test_full_size_forward_and_batch_independence(gpu):
