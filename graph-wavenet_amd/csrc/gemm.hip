@@ -184,15 +184,26 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
   }
 }
 
+// 8 outputs per block x 32 split lanes (lane l sums splits l, l+32, ...), then a fixed-order tree.
 __global__ void splitk_reduce_kernel(const GemmParams p) {
+  __shared__ float sh[256];
   const long total = (long)p.M * p.N;
-  const unsigned long long seed = p.seed_ptr ? *p.seed_ptr : 0ull;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long)gridDim.x * blockDim.x) {
-    float v = 0.0f;
-    for (int s = 0; s < p.ksplit; ++s) v += p.part[(long)s * total + idx];
+  const int ej = threadIdx.x & 7, lane = threadIdx.x >> 3;
+  const long idx = blockIdx.x * 8L + ej;
+  float v = 0.0f;
+  if (idx < total)
+    for (int s = lane; s < p.ksplit; s += 32) v += p.part[(long)s * total + idx];
+  sh[threadIdx.x] = v;
+  __syncthreads();
+#pragma unroll
+  for (int w = 16; w > 0; w >>= 1) {
+    if (lane < w) sh[threadIdx.x] += sh[threadIdx.x + 8 * w];
+    __syncthreads();
+  }
+  if (lane == 0 && idx < total) {
+    const unsigned long long seed = p.seed_ptr ? *p.seed_ptr : 0ull;
     const int m = (int)(idx / p.N), n = (int)(idx - (long)m * p.N);
-    epi_store(p, m, n, v, seed);
+    epi_store(p, m, n, sh[ej], seed);
   }
 }
 
@@ -245,9 +256,7 @@ int gwn_gemm_launch(const GemmParams& pin, hipStream_t s) {
   else rc = launch_cfg<2, 2, 1, 1>(p, akc, bkc, s);                    // 64 x 64
   if (rc != GWN_OK || p.ksplit <= 1) return rc;
   const long total = (long)p.M * p.N;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  splitk_reduce_kernel<<<blocks, 256, 0, s>>>(p);
+  splitk_reduce_kernel<<<(unsigned)((total + 7) / 8), 256, 0, s>>>(p);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

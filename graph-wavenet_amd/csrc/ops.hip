@@ -21,7 +21,8 @@ gwn_gemm_desc gemm_zero() {
 }
 
 int pick_ksplit(int M, int N, int K) {
-  // aim for ~1024 blocks over the output tiles (see gemm.hip launch configs: >= 64x64 tiles)
+  // aim for ~1024 blocks over the output tiles (see gemm.hip launch configs: >= 64x64 tiles),
+  // K-slices of >= 256 rows; the split reduction is a parallel fixed-order tree (gemm.hip)
   long tiles = ((M + 127) / 128) * (long)((N + 63) / 64);
   if (tiles < 1) tiles = 1;
   long ks = 1024 / tiles;
@@ -194,13 +195,23 @@ __global__ void colsum_partial_kernel(const float* a, long lda, const float* b, 
   }
 }
 
+// 8 columns per block x 32 partial lanes, then a fixed-order tree over the lanes.
 __global__ void colsum_final_kernel(const float* partial, int nparts, int ncol, float* out,
                                     int accumulate) {
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < ncol; j += gridDim.x * blockDim.x) {
-    float s = 0.0f;
-    for (int i = 0; i < nparts; ++i) s += partial[(long)i * ncol + j];
-    out[j] = accumulate ? out[j] + s : s;
+  __shared__ float sh[256];
+  const int cj = threadIdx.x & 7, lane = threadIdx.x >> 3;
+  const int j = blockIdx.x * 8 + cj;
+  float s = 0.0f;
+  if (j < ncol)
+    for (int i = lane; i < nparts; i += 32) s += partial[(long)i * ncol + j];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+#pragma unroll
+  for (int w = 16; w > 0; w >>= 1) {
+    if (lane < w) sh[threadIdx.x] += sh[threadIdx.x + 8 * w];
+    __syncthreads();
   }
+  if (lane == 0 && j < ncol) out[j] = accumulate ? out[j] + sh[cj] : sh[cj];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -247,10 +258,12 @@ __global__ void bn_partial_kernel(const float* z, long rows, int c, float* part)
 __global__ void bn_finalize_kernel(const float* part, int nparts, int c, float momentum, float eps,
                                    float* running_mean, float* running_var, float* save_mean,
                                    float* save_rstd) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= c) return;
+  // one block per channel: each thread merges a strided subset of the partials (Chan), then a
+  // fixed-order tree merge over the 256 threads
+  __shared__ double sn[256], sm[256], sq[256];
+  const int j = blockIdx.x;
   double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int i = 0; i < nparts; ++i) {
+  for (int i = threadIdx.x; i < nparts; i += 256) {
     const float* pp = part + (long)i * 3 * c;
     const double nb = pp[j];
     if (nb <= 0.0) continue;
@@ -261,6 +274,23 @@ __global__ void bn_finalize_kernel(const float* part, int nparts, int c, float m
     m2 += m2b + delta * delta * n * nb / nn;
     n = nn;
   }
+  sn[threadIdx.x] = n; sm[threadIdx.x] = mean; sq[threadIdx.x] = m2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const double na = sn[threadIdx.x], nb = sn[threadIdx.x + w];
+      const double nn = na + nb;
+      if (nb > 0.0) {
+        const double delta = sm[threadIdx.x + w] - sm[threadIdx.x];
+        sm[threadIdx.x] += delta * nb / nn;
+        sq[threadIdx.x] += sq[threadIdx.x + w] + delta * delta * na * nb / nn;
+        sn[threadIdx.x] = nn;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  n = sn[0]; mean = sm[0]; m2 = sq[0];
   const double var = (n > 0.0) ? m2 / n : 0.0;
   save_mean[j] = (float)mean;
   save_rstd[j] = (float)(1.0 / sqrt(var + (double)eps));
@@ -318,21 +348,24 @@ __global__ void bn_bwd_apply_kernel(const float* dy, const float* z, long rows, 
 
 // ---------------------------------------------------------------------------------------------
 // masked metrics (util.py:510-552, null_val = 0).  ws layout: [0] nonzero count,
-// [1 .. 1+3*RED_BLOCKS) partial (mae, mape, mse) sums
+// [1 .. 1+3*RED_BLOCKS) partial (mae, mape, mse) sums, [LOSS_CNT ..) partial nonzero-label counts
+constexpr int LOSS_CNT_BLOCKS = 128;
+constexpr int LOSS_CNT = 1 + 3 * RED_BLOCKS;
+
 __global__ void loss_count_kernel(const float* real, long rsb, long rsn, long rso, int B, int n,
                                   int o, float* ws) {
-  __shared__ float sh[1024];
+  __shared__ float sh[256];
   const long total = (long)B * n * o;
   float cnt = 0.0f;
-  for (long i = threadIdx.x; i < total; i += 1024) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += 256L * gridDim.x) {
     const int oo = (int)(i % o);
     const long bv = i / o;
     const int v = (int)(bv % n);
     const int b = (int)(bv / n);
     cnt += (real[b * rsb + v * rsn + oo * rso] != 0.0f) ? 1.0f : 0.0f;
   }
-  cnt = block_sum<1024>(cnt, sh);
-  if (threadIdx.x == 0) ws[0] = cnt;
+  cnt = block_sum<256>(cnt, sh);
+  if (threadIdx.x == 0) ws[LOSS_CNT + blockIdx.x] = cnt;
 }
 
 __global__ void loss_terms_kernel(const float* out, const float* real, long rsb, long rsn, long rso,
@@ -340,7 +373,8 @@ __global__ void loss_terms_kernel(const float* out, const float* real, long rsb,
                                   float* ws) {
   __shared__ float sh[256];
   const long total = (long)B * o * n * tf;  // out is [B][o][n][tf]
-  const float cnt = ws[0];
+  // every block re-derives the (exact, integer-valued) label count from the count partials
+  const float cnt = block_sum<256>((threadIdx.x < LOSS_CNT_BLOCKS) ? ws[LOSS_CNT + threadIdx.x] : 0.0f, sh);
   const float label_total = (float)((long)B * n * o);
   const float mask_scale = (cnt > 0.0f) ? label_total / cnt : 0.0f;  // 1 / mean(mask)
   const float inv_total = 1.0f / (float)total;
@@ -384,16 +418,21 @@ __global__ void loss_terms_kernel(const float* out, const float* real, long rsb,
 }
 
 __global__ void loss_final_kernel(const float* ws, int nblocks, long total, float* metrics) {
-  if (threadIdx.x != 0) return;
-  double a = 0.0, b = 0.0, c = 0.0;
-  for (int i = 0; i < nblocks; ++i) {
+  __shared__ float sh[256];
+  float a = 0.0f, b = 0.0f, c = 0.0f;
+  for (int i = threadIdx.x; i < nblocks; i += 256) {
     a += ws[1 + i * 3];
     b += ws[2 + i * 3];
     c += ws[3 + i * 3];
   }
-  metrics[0] = (float)(a / (double)total);
-  metrics[1] = (float)(b / (double)total);
-  metrics[2] = sqrtf((float)(c / (double)total));
+  a = block_sum<256>(a, sh);
+  b = block_sum<256>(b, sh);
+  c = block_sum<256>(c, sh);
+  if (threadIdx.x == 0) {
+    metrics[0] = (float)((double)a / (double)total);
+    metrics[1] = (float)((double)b / (double)total);
+    metrics[2] = sqrtf((float)((double)c / (double)total));
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -423,10 +462,12 @@ __global__ void sqnorm_partial_kernel(const float* g, const long* lo, const long
 
 __global__ void clip_coef_kernel(float* ws, int nparts, float max_norm, long long* step,
                                  float* total_norm_out) {
+  __shared__ float sh[256];
+  float part = 0.0f;
+  for (int i = threadIdx.x; i < nparts; i += 256) part += ws[i];
+  const float s = block_sum<256>(part, sh);
   if (threadIdx.x != 0) return;
-  double s = 0.0;
-  for (int i = 0; i < nparts; ++i) s += ws[i];
-  const float norm = sqrtf((float)s);
+  const float norm = sqrtf(s);
   const float coef = max_norm / (norm + 1e-6f);
   ws[RED_BLOCKS] = coef < 1.0f ? coef : 1.0f;
   if (total_norm_out) *total_norm_out = norm;
@@ -769,7 +810,7 @@ int gwn_batchnorm_fwd(const float* z, int rows, int c, const float* gamma, const
   if (training) {
     bn_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(z, rows, c, ws);
     GWN_CHECK_LAUNCH();
-    bn_finalize_kernel<<<1, 256, 0, s>>>(ws, RED_BLOCKS, c, momentum, eps, running_mean, running_var,
+    bn_finalize_kernel<<<c, 256, 0, s>>>(ws, RED_BLOCKS, c, momentum, eps, running_mean, running_var,
                                          save_mean, save_rstd);
     GWN_CHECK_LAUNCH();
     bn_apply_kernel<<<grid_for(total), 256, 0, s>>>(z, rows, c, save_mean, save_rstd, nullptr, eps,
@@ -791,11 +832,11 @@ int gwn_batchnorm_bwd(const float* dy, const float* z, int rows, int c, const fl
   float* sums = ws + (long)RED_BLOCKS * 3 * c;  // [2][c]: sum dy, sum dy*xhat
   colsum_partial_kernel<0><<<RED_BLOCKS, 256, 0, s>>>(dy, c, nullptr, 0, nullptr, nullptr, rows, c, part);
   GWN_CHECK_LAUNCH();
-  colsum_final_kernel<<<1, 256, 0, s>>>(part, RED_BLOCKS, c, sums, 0);
+  colsum_final_kernel<<<(c + 7) / 8, 256, 0, s>>>(part, RED_BLOCKS, c, sums, 0);
   GWN_CHECK_LAUNCH();
   colsum_partial_kernel<1><<<RED_BLOCKS, 256, 0, s>>>(dy, c, z, c, save_mean, save_rstd, rows, c, part);
   GWN_CHECK_LAUNCH();
-  colsum_final_kernel<<<1, 256, 0, s>>>(part, RED_BLOCKS, c, sums + c, 0);
+  colsum_final_kernel<<<(c + 7) / 8, 256, 0, s>>>(part, RED_BLOCKS, c, sums + c, 0);
   GWN_CHECK_LAUNCH();
   if (dbeta && hipMemcpyAsync(dbeta, sums, sizeof(float) * c, hipMemcpyDeviceToDevice, s) != hipSuccess)
     return gwn_set_error(GWN_ERR_HIP, "batchnorm_bwd: dbeta copy");
@@ -818,7 +859,7 @@ int gwn_colsum(const float* dy, int rows, int ncol, long ld, float* out, int acc
   GWN_REQUIRE(rows > 0 && ncol > 0, "colsum: bad shape");
   colsum_partial_kernel<0><<<RED_BLOCKS, 256, 0, s>>>(dy, ld, nullptr, 0, nullptr, nullptr, rows, ncol, ws);
   GWN_CHECK_LAUNCH();
-  colsum_final_kernel<<<(ncol + 255) / 256, 256, 0, s>>>(ws, RED_BLOCKS, ncol, out, accumulate);
+  colsum_final_kernel<<<(ncol + 7) / 8, 256, 0, s>>>(ws, RED_BLOCKS, ncol, out, accumulate);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -826,18 +867,18 @@ int gwn_colsum(const float* dy, int rows, int ncol, long ld, float* out, int acc
 // ---------------------------------------------------------------------------------------------
 long gwn_masked_loss_workspace_floats(int B, int o, int n, int tf) {
   (void)B; (void)o; (void)n; (void)tf;
-  return 1 + 3L * RED_BLOCKS;
+  return LOSS_CNT + LOSS_CNT_BLOCKS;
 }
 
 int gwn_masked_loss(const float* out, const float* real, long rsb, long rsn, long rso, int B, int o,
                     int n, int tf, float mean, float std, float* metrics, float* dout, float* ws,
                     hipStream_t s) {
   GWN_REQUIRE(B > 0 && o > 0 && n > 0 && tf > 0, "masked_loss: bad shape");
-  loss_count_kernel<<<1, 1024, 0, s>>>(real, rsb, rsn, rso, B, n, o, ws);
+  loss_count_kernel<<<LOSS_CNT_BLOCKS, 256, 0, s>>>(real, rsb, rsn, rso, B, n, o, ws);
   GWN_CHECK_LAUNCH();
   loss_terms_kernel<<<RED_BLOCKS, 256, 0, s>>>(out, real, rsb, rsn, rso, B, o, n, tf, mean, std, dout, ws);
   GWN_CHECK_LAUNCH();
-  loss_final_kernel<<<1, 64, 0, s>>>(ws, RED_BLOCKS, (long)B * o * n * tf, metrics);
+  loss_final_kernel<<<1, 256, 0, s>>>(ws, RED_BLOCKS, (long)B * o * n * tf, metrics);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -855,7 +896,7 @@ int gwn_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq
   GWN_REQUIRE(nranges > 0 && active > 0, "clip_adam: empty");
   sqnorm_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(grads, lo, hi, nranges, active, ws);
   GWN_CHECK_LAUNCH();
-  clip_coef_kernel<<<1, 64, 0, s>>>(ws, RED_BLOCKS, max_norm, step_ptr, total_norm_out);
+  clip_coef_kernel<<<1, 256, 0, s>>>(ws, RED_BLOCKS, max_norm, step_ptr, total_norm_out);
   GWN_CHECK_LAUNCH();
   adam_kernel<<<grid_for(active), 256, 0, s>>>(params, grads, exp_avg, exp_avg_sq, lo, hi, nranges, active,
                                                ws, step_ptr, lr, beta1, beta2, eps, wd);

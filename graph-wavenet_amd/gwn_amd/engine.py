@@ -126,11 +126,36 @@ class trainer():
         if training:
             ex.backward(acts, dout)
             ex.unpack_grads(self.optimizer.grad_flat)
+            self._allreduce_grads()
             clip = self.clip if self.clip is not None else _NO_CLIP
             self.optimizer.apply(ex.layout.active, clip)
             if model.dropout > 0:
                 _lib.call("gwn_increment_u64", ptr(ex.seed), 1, _lib.stream())
         return sc["metrics"]
+
+    def _allreduce_grads(self):
+        """Data parallel (one process per GPU): average the flat gradient over ranks with ONE
+        collective (RCCL all-reduce over xGMI for the "nccl" backend), before clip + Adam, i.e.
+        DistributedDataParallel semantics with per-replica BatchNorm (the reference has no
+        SyncBN).  A no-op without an initialised process group."""
+        dist = torch.distributed
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return
+        g = self.optimizer.grad_flat
+        if dist.get_backend() == "nccl":
+            dist.all_reduce(g, op=dist.ReduceOp.AVG)
+        else:
+            dist.all_reduce(g, op=dist.ReduceOp.SUM)
+            g.div_(dist.get_world_size())
+
+    def broadcast_parameters(self, src=0):
+        """Make every rank start from rank ``src``'s weights (DDP's construction-time broadcast)."""
+        dist = torch.distributed
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.broadcast(self.model._flat, src)
+            for m in self.model.bn:
+                dist.broadcast(m.running_mean, src)
+                dist.broadcast(m.running_var, src)
 
     def _fused_ok(self, input, real_val):
         return (self.loss is util.masked_mae and input.is_cuda and input.dtype == F32

@@ -465,6 +465,7 @@ class Executor:
 
 
 def _ksplit(M, N, K):
+    """Same policy as pick_ksplit() in csrc/ops.hip."""
     tiles = ((M + 127) // 128) * ((N + 63) // 64)
     ks = max(1, min(1024 // max(tiles, 1), K // 256))
     return ks
