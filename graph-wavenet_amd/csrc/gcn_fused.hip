@@ -1,0 +1,331 @@
+// Fused diffusion graph convolution (gcn.forward, reference model.py:41-55, + residual model.py:234)
+// and its backward, for C = 32 channels and N <= 512 nodes.
+//
+// One workgroup = one slice (a (t, b) pair: N nodes x 32 channels, contiguous rows of the
+// channels-last activation).  Wave w owns node tile [32w, 32w+32).  All products run on
+// v_mfma_f32_32x32x2_f32 in the transposed orientation
+//     D'[c][w] = sum_v X[v][c] * G[v][w]            (M = channel, N = node, K = node)
+// so that
+//   * the A operand X[v][c] is an LDS row read (conflict-free, rows padded to 33 floats),
+//   * the B operand G[v][w] is a coalesced 128-B global (L2-resident) read, prefetched 8 deep,
+//   * the accumulator D'[c][w] (channel on registers, node on lanes) is directly the B operand
+//     of the next product that contracts over channels (the 1x1 mlp): no lane shuffles.
+// The node features never leave LDS between hops; only the pieces needed by the backward
+// (x1, x2 per support) and the layer output are written to HBM, with full-row coalesced stores.
+#include "gwn_internal.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int CH = 32;   // channels (one MFMA tile)
+constexpr int LDR = 33;  // LDS row stride (floats): conflict-free row and column reads
+
+struct FusedFwd {
+  const float* h; long ld_h;
+  const float* sup[8]; int nsup, ld_sup;
+  const float* w_mlp; int ld_w; const float* b_mlp;
+  const float* residual; float* z; float* bn_part;
+  const unsigned long long* seed_ptr; unsigned long long salt; float drop_p;
+  int n;
+};
+
+struct FusedBwd {
+  const float* dh;
+  const float* supT[8]; int nsup, ld_sup;
+  const float* w_mlp; int ld_w;
+  float* dxg; long ld_dxg;
+  float* t1; float* t2; long ld_t; int adp_index;
+  int n;
+};
+
+__device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+// D'[c][w0+col] = sum_v buf[v][c] * G[v][w0+col]   (buf rows >= n are zero)
+__device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int ld, int n, int w0,
+                                          int lane, f32x16 acc) {
+  const int half = lane >> 5, col = lane & 31;
+  const int w = w0 + col;
+  const bool wok = w < n;
+  const float* gp = G + (long)half * ld + w;
+  const int nkp = (n + 1) >> 1;
+  float gq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int v = 2 * j + half;
+    gq[j] = (wok && v < n) ? gp[(long)(2 * j) * ld] : 0.0f;
+  }
+  for (int kp0 = 0; kp0 < nkp; kp0 += 8) {
+    float gn[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kp = kp0 + 8 + j;
+      const int v = 2 * kp + half;
+      gn[j] = (wok && v < n) ? gp[(long)(2 * kp) * ld] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kp = kp0 + j;
+      if (kp < nkp) {
+        const float a = buf[(2 * kp + half) * LDR + col];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, gq[j], acc, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gq[j] = gn[j];
+  }
+  return acc;
+}
+
+// acc_out[c'][w] += sum_c W[c'][off + c] * D'[c][w]   with D' = the accumulator `d`
+__device__ __forceinline__ f32x16 mlp_from_acc(const float* W, int ld_w, int off, const f32x16& d,
+                                               int lane, f32x16 acc) {
+  const int half = lane >> 5, col = lane & 31;
+  const float* wp = W + (long)col * ld_w + off;
+#pragma unroll
+  for (int s = 0; s < 16; ++s)
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wp[crow(s, half)], d[s], acc, 0, 0, 0);
+  return acc;
+}
+
+// acc[c'][w] += sum_c W[c'][off + c] * buf[w][c]      (buf = LDS rows)
+__device__ __forceinline__ f32x16 mlp_from_lds(const float* W, int ld_w, int off, const float* buf,
+                                               int w0, int lane, f32x16 acc) {
+  const int half = lane >> 5, col = lane & 31;
+  const float* wp = W + (long)col * ld_w + off;
+  const float* bp = buf + (w0 + col) * LDR;
+#pragma unroll
+  for (int s = 0; s < 16; ++s)
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wp[2 * s + half], bp[2 * s + half], acc, 0, 0, 0);
+  return acc;
+}
+
+// acc[c][w] += sum_c' W[c'][off + c] * buf[w][c']      (transposed weights: dP = W^T dh)
+__device__ __forceinline__ f32x16 mlpT_from_lds(const float* W, int ld_w, int off, const float* buf,
+                                                int w0, int lane, f32x16 acc) {
+  const int half = lane >> 5, col = lane & 31;
+  const float* bp = buf + (w0 + col) * LDR;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int cp = 2 * s + half;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(W[(long)cp * ld_w + off + col], bp[cp], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void acc_to_lds(float* buf, const f32x16& d, int w0, int lane) {
+  const int half = lane >> 5, col = lane & 31;
+  float* bp = buf + (w0 + col) * LDR;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) bp[crow(r, half)] = d[r];
+}
+
+__device__ __forceinline__ void lds_to_global(const float* buf, float* dst, long ld, int n) {
+  for (int e = threadIdx.x; e < n * CH; e += blockDim.x) {
+    const int w = e >> 5, c = e & 31;
+    dst[(long)w * ld + c] = buf[w * LDR + c];
+  }
+}
+
+__device__ __forceinline__ void global_to_lds(const float* src, long ld, int n, int np, float* buf) {
+  for (int e = threadIdx.x; e < np * CH; e += blockDim.x) {
+    const int w = e >> 5, c = e & 31;
+    buf[w * LDR + c] = (w < n) ? src[(long)w * ld + c] : 0.0f;
+  }
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.0f;
+  return z;
+}
+
+__global__ void gcn_fwd_fused_kernel(const FusedFwd a) {
+  extern __shared__ float lds[];
+  const int n = a.n;
+  const int np = (int)(blockDim.x >> 6) * 32;
+  float* xs = lds;
+  float* ys = lds + np * LDR;
+  const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
+  const long row0 = (long)blockIdx.x * n;
+  const float* hs = a.h + row0 * a.ld_h;
+
+  global_to_lds(hs, a.ld_h, n, np, xs);
+  __syncthreads();
+  f32x16 hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
+  for (int k = 0; k < a.nsup; ++k) {
+    const float* G = a.sup[k];
+    f32x16 d = diffuse(xs, G, a.ld_sup, n, w0, lane, zero16());
+    hacc = mlp_from_acc(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, d, lane, hacc);
+    __syncthreads();
+    acc_to_lds(ys, d, w0, lane);
+    __syncthreads();
+    lds_to_global(ys, (float*)hs + (1 + 2 * k) * CH, a.ld_h, n);
+    d = diffuse(ys, G, a.ld_sup, n, w0, lane, zero16());
+    hacc = mlp_from_acc(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, d, lane, hacc);
+    __syncthreads();
+    acc_to_lds(ys, d, w0, lane);
+    __syncthreads();
+    lds_to_global(ys, (float*)hs + (2 + 2 * k) * CH, a.ld_h, n);
+  }
+  __syncthreads();
+  acc_to_lds(ys, hacc, w0, lane);
+  __syncthreads();
+  // epilogue: bias, dropout (same counter hash as the GEMM epilogue: index m*32 + c), residual
+  const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
+  const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  for (int e = threadIdx.x; e < n * CH; e += blockDim.x) {
+    const int w = e >> 5, c = e & 31;
+    const long m = row0 + w;
+    float v = ys[w * LDR + c] + a.b_mlp[c];
+    if (a.drop_p > 0.0f) {
+      const float u = gwn_uniform(seed, a.salt, (unsigned long long)m * CH + c);
+      v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
+    }
+    v += a.residual[m * CH + c];
+    a.z[m * CH + c] = v;
+    ys[w * LDR + c] = v;
+  }
+  if (a.bn_part == nullptr) return;
+  __syncthreads();
+  // per-slice BN partials (count, mean, M2) per channel, fixed order
+  __shared__ float red[2][1024];
+  const int ngroups = blockDim.x >> 5;
+  const int c = threadIdx.x & 31, g = threadIdx.x >> 5;
+  float s = 0.0f;
+  for (int w = g; w < n; w += ngroups) s += ys[w * LDR + c];
+  red[0][threadIdx.x] = s;
+  __syncthreads();
+  float mean = 0.0f;
+  for (int i = 0; i < ngroups; ++i) mean += red[0][i * 32 + c];
+  mean /= (float)n;
+  float q = 0.0f;
+  for (int w = g; w < n; w += ngroups) {
+    const float dlt = ys[w * LDR + c] - mean;
+    q += dlt * dlt;
+  }
+  red[1][threadIdx.x] = q;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float m2 = 0.0f;
+    for (int i = 0; i < ngroups; ++i) m2 += red[1][i * 32 + c];
+    float* pp = a.bn_part + (long)blockIdx.x * 3 * CH;
+    pp[c] = (float)n;
+    pp[CH + c] = mean;
+    pp[2 * CH + c] = m2;
+  }
+}
+
+__global__ void gcn_bwd_fused_kernel(const FusedBwd a) {
+  extern __shared__ float lds[];
+  const int n = a.n;
+  const int np = (int)(blockDim.x >> 6) * 32;
+  float* dhs = lds;
+  float* buf = lds + np * LDR;
+  const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
+  const long row0 = (long)blockIdx.x * n;
+
+  global_to_lds(a.dh + row0 * CH, CH, n, np, dhs);
+  __syncthreads();
+  f32x16 dx = mlpT_from_lds(a.w_mlp, a.ld_w, 0, dhs, w0, lane, zero16());
+  for (int k = 0; k < a.nsup; ++k) {
+    const float* GT = a.supT[k];
+    f32x16 t = mlpT_from_lds(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, w0, lane, zero16());
+    const f32x16 u = mlpT_from_lds(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, w0, lane, zero16());
+    __syncthreads();
+    acc_to_lds(buf, u, w0, lane);
+    __syncthreads();
+    if (k == a.adp_index) lds_to_global(buf, a.t2 + row0 * a.ld_t, a.ld_t, n);
+    t = diffuse(buf, GT, a.ld_sup, n, w0, lane, t);          // dx1 = dP_x1 + A dP_x2
+    __syncthreads();
+    acc_to_lds(buf, t, w0, lane);
+    __syncthreads();
+    if (k == a.adp_index) lds_to_global(buf, a.t1 + row0 * a.ld_t, a.ld_t, n);
+    dx = diffuse(buf, GT, a.ld_sup, n, w0, lane, dx);        // dxg += A dx1
+  }
+  __syncthreads();
+  acc_to_lds(buf, dx, w0, lane);
+  __syncthreads();
+  lds_to_global(buf, a.dxg + row0 * a.ld_dxg, a.ld_dxg, n);
+}
+
+__global__ void transpose_kernel(const float* src, int n, int ld_src, float* dst, int ld_dst) {
+  __shared__ float tile[32][33];
+  const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
+  for (int r = ty; r < 32; r += 8) {
+    const int i = by + r, j = bx + tx;
+    tile[r][tx] = (i < n && j < n) ? src[(long)i * ld_src + j] : 0.0f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int i = bx + r, j = by + tx;
+    if (i < n && j < n) dst[(long)i * ld_dst + j] = tile[tx][r];
+  }
+}
+
+size_t fused_lds_bytes(int n) {
+  const int np = (n + 31) / 32 * 32;
+  return (size_t)2 * np * LDR * sizeof(float);
+}
+
+}  // namespace
+
+bool gwn_gcn_fused_eligible(int c, int n, int nsup) {
+  return c == CH && n > 0 && n <= 512 && nsup >= 0 && nsup <= 8;
+}
+
+int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
+  FusedFwd a;
+  a.h = g->h; a.ld_h = g->ld_h;
+  for (int k = 0; k < 8; ++k) a.sup[k] = (k < g->nsup) ? g->sup[k] : nullptr;
+  a.nsup = g->nsup; a.ld_sup = g->ld_sup;
+  a.w_mlp = g->w_mlp; a.ld_w = (2 * g->nsup + 1) * CH; a.b_mlp = g->b_mlp;
+  a.residual = g->residual; a.z = g->z; a.bn_part = bn_part;
+  a.seed_ptr = g->seed_ptr; a.salt = g->salt; a.drop_p = g->drop_p;
+  a.n = g->n;
+  const int nwt = (g->n + 31) / 32;
+  const size_t lds = fused_lds_bytes(g->n);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gcn_fwd_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)fused_lds_bytes(512));
+    (void)hipFuncSetAttribute((const void*)gcn_bwd_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)fused_lds_bytes(512));
+    attr_set = true;
+  }
+  gcn_fwd_fused_kernel<<<g->rows / g->n, 64 * nwt, lds, s>>>(a);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT, float* dxg, long ld_dxg,
+                             float* t1, float* t2, long ld_t, hipStream_t s) {
+  FusedBwd a;
+  a.dh = g->dh;
+  for (int k = 0; k < 8; ++k) a.supT[k] = (k < g->nsup) ? supT[k] : nullptr;
+  a.nsup = g->nsup; a.ld_sup = g->ld_sup;
+  a.w_mlp = g->w_mlp; a.ld_w = (2 * g->nsup + 1) * CH;
+  a.dxg = dxg; a.ld_dxg = ld_dxg;
+  a.t1 = t1; a.t2 = t2; a.ld_t = ld_t; a.adp_index = g->adp_index;
+  a.n = g->n;
+  const int nwt = (g->n + 31) / 32;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gcn_bwd_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)fused_lds_bytes(512));
+    attr_set = true;
+  }
+  gcn_bwd_fused_kernel<<<g->rows / g->n, 64 * nwt, fused_lds_bytes(g->n), s>>>(a);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+extern "C" int gwn_transpose(const float* src, int n, int ld_src, float* dst, int ld_dst, hipStream_t s) {
+  GWN_REQUIRE(n > 0, "transpose: bad shape");
+  dim3 grid((n + 31) / 32, (n + 31) / 32);
+  transpose_kernel<<<grid, 256, 0, s>>>(src, n, ld_src, dst, ld_dst);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}

@@ -716,6 +716,7 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
 int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_fwd: rows must be slices*n");
   const int c = a->c, n = a->n, slices = a->rows / n;
+  if (gwn_gcn_fused_eligible(c, n, a->nsup)) return gwn_gcn_fused_fwd_launch(a, a->bn_partials, s);
   const int width = (2 * a->nsup + 1) * c;
   for (int k = 0; k < a->nsup; ++k) {
     float* x1 = a->h + (1 + 2 * k) * c;
@@ -733,7 +734,12 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   d.C0 = a->residual; d.ldc0_m = c; d.ldc0_n = 1; d.beta = 1.0f;
   d.seed_ptr = a->seed_ptr; d.seed_salt = a->salt; d.drop_p = a->drop_p;
   d.M = a->rows; d.N = c; d.K = width;
-  return gwn_gemm_launch(d, s);
+  int rc = gwn_gemm_launch(d, s);
+  if (rc || !a->bn_partials) return rc;
+  GWN_REQUIRE(c <= 256 && 256 % c == 0, "gcn_fwd: BN partials need c | 256");
+  bn_partial_kernel<<<slices, 256, 0, s>>>(a->z, a->rows, c, a->bn_partials);  // one chunk per slice
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
 }
 
 static int gcn_w_ksplit(int rows, int c, int width) { return pick_ksplit(c, width, rows); }
@@ -764,6 +770,22 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   if (rc) return rc;
   rc = gwn_colsum(a->dh, a->rows, c, c, a->db_mlp, 0, a->workspace, s);
   if (rc) return rc;
+  if (a->sup_t && gwn_gcn_fused_eligible(c, n, a->nsup)) {
+    // fused: dxg -> dhcat piece 0; for the adaptive support dx1 -> piece 1, dx2 -> piece 2
+    float* t1 = a->dhcat + c;
+    float* t2 = a->dhcat + 2 * c;
+    rc = gwn_gcn_fused_bwd_launch(a, a->sup_t, a->dhcat, a->ld_dhcat, t1, t2, a->ld_dhcat, s);
+    if (rc) return rc;
+    if (a->adp_index >= 0 && a->adp_index < a->nsup && a->dadp) {
+      const int k = a->adp_index;
+      rc = gwn_nconv_adj_grad(a->h, a->ld_h, t1, a->ld_dhcat, n, c, slices, a->dadp, a->ld_sup,
+                              a->accumulate_dadp, a->workspace, s);
+      if (rc) return rc;
+      rc = gwn_nconv_adj_grad(a->h + (1 + 2 * k) * c, a->ld_h, t2, a->ld_dhcat, n, c, slices, a->dadp,
+                              a->ld_sup, 1, a->workspace, s);
+    }
+    return rc;
+  }
   // dhcat[r][k] = sum_j dh[r][j] W[j][k]
   d = gemm_zero();
   d.A = a->dh; d.lda_m = c; d.lda_k = 1;
@@ -819,6 +841,21 @@ int gwn_batchnorm_fwd(const float* z, int rows, int c, const float* gamma, const
     bn_apply_kernel<<<grid_for(total), 256, 0, s>>>(z, rows, c, running_mean, nullptr, running_var,
                                                     eps, gamma, beta, out);
   }
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_batchnorm_fwd_partials(const float* z, int rows, int c, const float* partials, int nparts,
+                               const float* gamma, const float* beta, float* running_mean, float* running_var,
+                               float momentum, float eps, float* out, float* save_mean, float* save_rstd,
+                               hipStream_t s) {
+  GWN_REQUIRE(rows > 0 && c > 0 && nparts > 0, "batchnorm_fwd_partials: bad shape");
+  bn_finalize_kernel<<<c, 256, 0, s>>>(partials, nparts, c, momentum, eps, running_mean, running_var,
+                                       save_mean, save_rstd);
+  GWN_CHECK_LAUNCH();
+  const long total = (long)rows * c;
+  bn_apply_kernel<<<grid_for(total), 256, 0, s>>>(z, rows, c, save_mean, save_rstd, nullptr, eps, gamma,
+                                                  beta, out);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

@@ -69,6 +69,7 @@ class GcnArgs(ctypes.Structure):
         ("residual", c_void_p),
         ("z", c_void_p),
         ("seed_ptr", c_void_p), ("salt", c_u64), ("drop_p", c_float),
+        ("bn_partials", c_void_p),
     ]
 
 
@@ -83,6 +84,7 @@ class GcnBwdArgs(ctypes.Structure):
         ("dw_mlp", c_void_p), ("db_mlp", c_void_p),
         ("adp_index", c_int), ("dadp", c_void_p), ("accumulate_dadp", c_int),
         ("workspace", c_void_p),
+        ("sup_t", ctypes.POINTER(c_void_p)),
     ]
 
 
@@ -111,6 +113,9 @@ _SIGS = [
     ("gwn_batchnorm_fwd", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                   c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gwn_batchnorm_workspace_floats", c_long, [c_int, c_int]),
+    ("gwn_batchnorm_fwd_partials", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("gwn_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     ("gwn_batchnorm_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_u64, c_float, c_void_p,
                                   c_void_p]),

@@ -283,6 +283,7 @@ class Executor:
             "dhc": e(maxrows, cfg.W),
             "dadp": e(N, N),
             "metrics": e(4),
+            "bnpart": e(ts[0] * B * 3 * C),  # per-slice BN partials of one layer
         }
         lib = _lib.load()
         need = [
@@ -349,10 +350,19 @@ class Executor:
                      ptr(acts.adp), N, st)
         sups, sup_arr = self.supports(fixed_sups, acts)
         acts.sups, acts.sup_arr = sups, sup_arr
+        acts.supT_arr = None
+        if training and sups:
+            # transposed supports: the fused backward computes A·x as (A^T)^T·x on the forward kernel path
+            if getattr(acts, "supT", None) is None or len(acts.supT) != len(sups):
+                acts.supT = [torch.empty(N, N, device=self.device, dtype=F32) for _ in sups]
+            for s_, t_ in zip(sups, acts.supT):
+                lib.call("gwn_transpose", ptr(s_), N, N, ptr(t_), N, st)
+            acts.supT_arr = (ctypes.c_void_p * len(sups))(*[t.data_ptr() for t in acts.supT])
         sx = x.stride()
         lib.call("gwn_start_conv_fwd", ptr(x), sx[0], sx[1], sx[2], sx[3], B, cin, N, t_in, ts[0],
                  ptr(self.pk("start_w")), ptr(self.pk("start_b")), C, ptr(acts.X[0]), ptr(acts.xin), st)
-        ws = self.scratch(B, ts)["ws"]
+        scr = self.scratch(B, ts)
+        ws, bnpart = scr["ws"], scr["bnpart"]
         for i in range(L):
             d = cfg.dilations[i]
             rows = ts[i + 1] * P
@@ -370,12 +380,18 @@ class Executor:
                               h=ptr(acts.H[i]), ld_h=cfg.W,
                               w_mlp=ptr(self.pk("mlp_w%d" % i)), b_mlp=ptr(self.pk("mlp_b%d" % i)),
                               residual=acts.X[i].data_ptr() + 4 * d * P * C, z=ptr(acts.Z[i]),
-                              seed_ptr=ptr(self.seed), salt=i, drop_p=drop)
+                              seed_ptr=ptr(self.seed), salt=i, drop_p=drop,
+                              bn_partials=ptr(bnpart) if training else None)
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             rm, rv, mom, eps = bn_bufs[i]
-            lib.call("gwn_batchnorm_fwd", ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
-                     ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps, 1 if training else 0,
-                     ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(ws), st)
+            if training:
+                lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnpart), rows // N,
+                         ptr(self.pk("bn_g%d" % i)), ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps,
+                         ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), st)
+            else:
+                lib.call("gwn_batchnorm_fwd", ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
+                         ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps, 0,
+                         ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(ws), st)
         rows_f = tf * P
         # skip sum (relu'd) -> end_conv_1 (+relu) -> end_conv_2
         gemm(acts.skipcat, L * C, 1, self.pk("skip_w"), 1, L * C, acts.skr, cfg.S, 1,
@@ -437,7 +453,9 @@ class Executor:
                                      dh=ptr(sc["dh"]), dhcat=ptr(sc["dhc"]), ld_dhcat=cfg.W,
                                      dw_mlp=ptr(self.gk("mlp_w%d" % i)), db_mlp=ptr(self.gk("mlp_b%d" % i)),
                                      adp_index=adp_index, dadp=ptr(sc["dadp"]),
-                                     accumulate_dadp=0 if first_adp else 1, workspace=ptr(ws))
+                                     accumulate_dadp=0 if first_adp else 1, workspace=ptr(ws),
+                                     sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
+                                     if acts.supT_arr is not None else None)
                 lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)
                 if adp_index >= 0:
                     first_adp = False

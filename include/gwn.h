@@ -160,7 +160,14 @@ typedef struct gwn_gcn_args {
   const float* residual;
   float* z;
   const unsigned long long* seed_ptr; unsigned long long salt; float drop_p;
+  /* optional: per-slice BatchNorm partials [rows/n][3][c] (count, mean, M2) of z, written by the
+   * fused path (c == 32, n <= 512) for gwn_batchnorm_fwd_partials; NULL = not wanted.  When the
+   * generic path runs instead, they are computed from z by a separate pass. */
+  float* bn_partials;
 } gwn_gcn_args;
+/* c == 32 and n <= 512: one fused launch (gcn_fused.hip: node features LDS-resident through the
+ * whole diffusion chain, mlp accumulated from the MFMA accumulators, residual + dropout +
+ * BN partials in the epilogue).  Otherwise: 2K nconv GEMMs + one mlp GEMM. */
 int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t stream);
 
 /* Backward of gwn_gcn_fwd given dh (gradient w.r.t. the dropout output, i.e. dz with the
@@ -178,6 +185,9 @@ typedef struct gwn_gcn_bwd_args {
   float* dw_mlp; float* db_mlp;
   int adp_index; float* dadp; int accumulate_dadp;
   float* workspace;
+  /* optional transposed supports (gwn_transpose) enabling the fused backward (c == 32,
+   * n <= 512); NULL = generic path */
+  const float* const* sup_t;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);
@@ -192,6 +202,14 @@ int gwn_batchnorm_fwd(const float* z, int rows, int c, const float* gamma, const
                       int training, float* out, float* save_mean, float* save_rstd,
                       float* workspace, hipStream_t stream);
 long gwn_batchnorm_workspace_floats(int rows, int c);
+/* train-mode BN from precomputed partials [nparts][3][c] (count, mean, M2), e.g. written by the
+ * fused gwn_gcn_fwd: merge (fixed order), update running stats, normalise z into out. */
+int gwn_batchnorm_fwd_partials(const float* z, int rows, int c, const float* partials, int nparts,
+                               const float* gamma, const float* beta, float* running_mean,
+                               float* running_var, float momentum, float eps, float* out,
+                               float* save_mean, float* save_rstd, hipStream_t stream);
+/* dst[j][i] = src[i][j] for an n x n matrix (supports for the fused backward) */
+int gwn_transpose(const float* src, int n, int ld_src, float* dst, int ld_dst, hipStream_t stream);
 
 /* BN backward fused with the residual split and the dropout backward of the same layer:
  *   dz = gamma*rstd*(dy - mean(dy) - xhat*mean(dy*xhat));  dgamma, dbeta
