@@ -7,11 +7,15 @@
 //     D'[c][w] = sum_v X[v][c] * G[v][w]            (M = channel, N = node, K = node)
 // so that
 //   * the A operand X[v][c] is an LDS row read (conflict-free, rows padded to 33 floats),
-//   * the B operand G[v][w] is a coalesced 128-B global (L2-resident) read, prefetched 8 deep,
+//   * the B operand G[v][w] is a coalesced 128-B buffer_load of the (L2-resident) support with a
+//     scalar row offset (1 VGPR of addressing for the whole K loop), rolled 16 k-steps ahead,
 //   * the accumulator D'[c][w] (channel on registers, node on lanes) is directly the B operand
 //     of the next product that contracts over channels (the 1x1 mlp): no lane shuffles.
 // The node features never leave LDS between hops; only the pieces needed by the backward
-// (x1, x2 per support) and the layer output are written to HBM, with full-row coalesced stores.
+// (x1, x2 per support) and the layer output are written to HBM, as full coalesced rows.
+//
+// Contract on the supports: [np][ld] with np = 32*ceil(n/32) <= ld, ZERO outside [n][n]
+// (the executor keeps padded copies), so the K loop runs whole 32-node batches unguarded.
 #include "gwn_internal.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -20,6 +24,7 @@ namespace {
 
 constexpr int CH = 32;   // channels (one MFMA tile)
 constexpr int LDR = 33;  // LDS row stride (floats): conflict-free row and column reads
+constexpr int KB = 16;   // k-steps (32 nodes) per batch of the K loop
 
 struct FusedFwd {
   const float* h; long ld_h;
@@ -41,38 +46,34 @@ struct FusedBwd {
 
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
-// D'[c][w0+col] = sum_v buf[v][c] * G[v][w0+col]   (buf rows >= n are zero)
-__device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int ld, int n, int w0,
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+// D'[c][w0+col] += sum_v buf[v][c] * G[v][w0+col]
+__device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int ld, int nkb, int w0,
                                           int lane, f32x16 acc) {
   const int half = lane >> 5, col = lane & 31;
-  const int w = w0 + col;
-  const bool wok = w < n;
-  const float* gp = G + (long)half * ld + w;
-  const int nkp = (n + 1) >> 1;
-  float gq[8];
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, nkb * 32 * ld * 4, 0x00020000);
+  const int voff = (half * ld + w0 + col) * 4;
+  const int rowb = 2 * ld * 4;  // bytes between k-steps (2 nodes)
+  float gq[KB];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int v = 2 * j + half;
-    gq[j] = (wok && v < n) ? gp[(long)(2 * j) * ld] : 0.0f;
-  }
-  for (int kp0 = 0; kp0 < nkp; kp0 += 8) {
-    float gn[8];
+  for (int j = 0; j < KB; ++j) gq[j] = bload(rs, voff, j * rowb);
+  for (int kb = 0; kb < nkb; ++kb) {
+    float av[KB];
+    const float* bp = buf + (32 * kb + half) * LDR + col;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int kp = kp0 + 8 + j;
-      const int v = 2 * kp + half;
-      gn[j] = (wok && v < n) ? gp[(long)(2 * kp) * ld] : 0.0f;
+    for (int j = 0; j < KB; ++j) av[j] = bp[2 * j * LDR];
+    const bool more = kb + 1 < nkb;
+    const int nb = (kb + 1) * KB * rowb;
+    // rolling prefetch: slot j is refilled with batch kb+1 right after its MFMA consumed it
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], gq[j], acc, 0, 0, 0);
+      if (more) gq[j] = bload(rs, voff, nb + j * rowb);
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int kp = kp0 + j;
-      if (kp < nkp) {
-        const float a = buf[(2 * kp + half) * LDR + col];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, gq[j], acc, 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) gq[j] = gn[j];
   }
   return acc;
 }
@@ -82,9 +83,11 @@ __device__ __forceinline__ f32x16 mlp_from_acc(const float* W, int ld_w, int off
                                                int lane, f32x16 acc) {
   const int half = lane >> 5, col = lane & 31;
   const float* wp = W + (long)col * ld_w + off;
+  float wf[16];
 #pragma unroll
-  for (int s = 0; s < 16; ++s)
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wp[crow(s, half)], d[s], acc, 0, 0, 0);
+  for (int s = 0; s < 16; ++s) wf[s] = wp[crow(s, half)];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s], d[s], acc, 0, 0, 0);
   return acc;
 }
 
@@ -104,12 +107,14 @@ __device__ __forceinline__ f32x16 mlp_from_lds(const float* W, int ld_w, int off
 __device__ __forceinline__ f32x16 mlpT_from_lds(const float* W, int ld_w, int off, const float* buf,
                                                 int w0, int lane, f32x16 acc) {
   const int half = lane >> 5, col = lane & 31;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, CH * ld_w * 4, 0x00020000);
+  const int voff = (half * ld_w + off + col) * 4;
   const float* bp = buf + (w0 + col) * LDR;
+  float wf[16];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int cp = 2 * s + half;
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(W[(long)cp * ld_w + off + col], bp[cp], acc, 0, 0, 0);
-  }
+  for (int s = 0; s < 16; ++s) wf[s] = bload(rs, voff, 2 * s * ld_w * 4);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s], bp[2 * s + half], acc, 0, 0, 0);
   return acc;
 }
 
@@ -141,10 +146,13 @@ __device__ __forceinline__ f32x16 zero16() {
   return z;
 }
 
-__global__ void gcn_fwd_fused_kernel(const FusedFwd a) {
+template <int MAXT>
+__global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
   extern __shared__ float lds[];
+  __shared__ float red[2][MAXT];
   const int n = a.n;
-  const int np = (int)(blockDim.x >> 6) * 32;
+  const int nkb = (int)(blockDim.x >> 6);
+  const int np = nkb * 32;
   float* xs = lds;
   float* ys = lds + np * LDR;
   const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
@@ -156,13 +164,13 @@ __global__ void gcn_fwd_fused_kernel(const FusedFwd a) {
   f32x16 hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
   for (int k = 0; k < a.nsup; ++k) {
     const float* G = a.sup[k];
-    f32x16 d = diffuse(xs, G, a.ld_sup, n, w0, lane, zero16());
+    f32x16 d = diffuse(xs, G, a.ld_sup, nkb, w0, lane, zero16());
     hacc = mlp_from_acc(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, d, lane, hacc);
     __syncthreads();
     acc_to_lds(ys, d, w0, lane);
     __syncthreads();
     lds_to_global(ys, (float*)hs + (1 + 2 * k) * CH, a.ld_h, n);
-    d = diffuse(ys, G, a.ld_sup, n, w0, lane, zero16());
+    d = diffuse(ys, G, a.ld_sup, nkb, w0, lane, zero16());
     hacc = mlp_from_acc(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, d, lane, hacc);
     __syncthreads();
     acc_to_lds(ys, d, w0, lane);
@@ -190,7 +198,6 @@ __global__ void gcn_fwd_fused_kernel(const FusedFwd a) {
   if (a.bn_part == nullptr) return;
   __syncthreads();
   // per-slice BN partials (count, mean, M2) per channel, fixed order
-  __shared__ float red[2][1024];
   const int ngroups = blockDim.x >> 5;
   const int c = threadIdx.x & 31, g = threadIdx.x >> 5;
   float s = 0.0f;
@@ -217,10 +224,12 @@ __global__ void gcn_fwd_fused_kernel(const FusedFwd a) {
   }
 }
 
-__global__ void gcn_bwd_fused_kernel(const FusedBwd a) {
+template <int MAXT>
+__global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
   extern __shared__ float lds[];
   const int n = a.n;
-  const int np = (int)(blockDim.x >> 6) * 32;
+  const int nkb = (int)(blockDim.x >> 6);
+  const int np = nkb * 32;
   float* dhs = lds;
   float* buf = lds + np * LDR;
   const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
@@ -231,18 +240,20 @@ __global__ void gcn_bwd_fused_kernel(const FusedBwd a) {
   f32x16 dx = mlpT_from_lds(a.w_mlp, a.ld_w, 0, dhs, w0, lane, zero16());
   for (int k = 0; k < a.nsup; ++k) {
     const float* GT = a.supT[k];
-    f32x16 t = mlpT_from_lds(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, w0, lane, zero16());
-    const f32x16 u = mlpT_from_lds(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, w0, lane, zero16());
-    __syncthreads();
-    acc_to_lds(buf, u, w0, lane);
+    {
+      const f32x16 u = mlpT_from_lds(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, w0, lane, zero16());
+      __syncthreads();
+      acc_to_lds(buf, u, w0, lane);
+    }
     __syncthreads();
     if (k == a.adp_index) lds_to_global(buf, a.t2 + row0 * a.ld_t, a.ld_t, n);
-    t = diffuse(buf, GT, a.ld_sup, n, w0, lane, t);          // dx1 = dP_x1 + A dP_x2
+    f32x16 t = mlpT_from_lds(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, w0, lane, zero16());
+    t = diffuse(buf, GT, a.ld_sup, nkb, w0, lane, t);  // dx1 = dP_x1 + A dP_x2
     __syncthreads();
     acc_to_lds(buf, t, w0, lane);
     __syncthreads();
     if (k == a.adp_index) lds_to_global(buf, a.t1 + row0 * a.ld_t, a.ld_t, n);
-    dx = diffuse(buf, GT, a.ld_sup, n, w0, lane, dx);        // dxg += A dx1
+    dx = diffuse(buf, GT, a.ld_sup, nkb, w0, lane, dx);  // dxg += A dx1
   }
   __syncthreads();
   acc_to_lds(buf, dx, w0, lane);
@@ -250,7 +261,9 @@ __global__ void gcn_bwd_fused_kernel(const FusedBwd a) {
   lds_to_global(buf, a.dxg + row0 * a.ld_dxg, a.ld_dxg, n);
 }
 
-__global__ void transpose_kernel(const float* src, int n, int ld_src, float* dst, int ld_dst) {
+// dst (padded [np][ld_dst], zero outside n x n) = src or src^T
+__global__ void pad_copy_kernel(const float* src, int n, int ld_src, float* dst, int ld_dst, int np,
+                                int transpose) {
   __shared__ float tile[32][33];
   const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
@@ -260,8 +273,13 @@ __global__ void transpose_kernel(const float* src, int n, int ld_src, float* dst
   }
   __syncthreads();
   for (int r = ty; r < 32; r += 8) {
-    const int i = bx + r, j = by + tx;
-    if (i < n && j < n) dst[(long)i * ld_dst + j] = tile[tx][r];
+    if (transpose) {
+      const int i = bx + r, j = by + tx;
+      if (i < np && j < np) dst[(long)i * ld_dst + j] = tile[tx][r];
+    } else {
+      const int i = by + r, j = bx + tx;
+      if (i < np && j < np) dst[(long)i * ld_dst + j] = tile[r][tx];
+    }
   }
 }
 
@@ -270,13 +288,21 @@ size_t fused_lds_bytes(int n) {
   return (size_t)2 * np * LDR * sizeof(float);
 }
 
+template <typename K>
+void ensure_lds_attr(K kern) {
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)fused_lds_bytes(512));
+}
+
 }  // namespace
 
-bool gwn_gcn_fused_eligible(int c, int n, int nsup) {
-  return c == CH && n > 0 && n <= 512 && nsup >= 0 && nsup <= 8;
+bool gwn_gcn_fused_eligible(int c, int n, int nsup, int ld_sup) {
+  return c == CH && n > 0 && n <= 512 && nsup >= 0 && nsup <= 8 && ld_sup >= (n + 31) / 32 * 32;
 }
 
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
+  const int nwt = (g->n + 31) / 32;
+  GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_fwd (fused): supports must be padded to 32*ceil(n/32)");
   FusedFwd a;
   a.h = g->h; a.ld_h = g->ld_h;
   for (int k = 0; k < 8; ++k) a.sup[k] = (k < g->nsup) ? g->sup[k] : nullptr;
@@ -285,23 +311,23 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.residual = g->residual; a.z = g->z; a.bn_part = bn_part;
   a.seed_ptr = g->seed_ptr; a.salt = g->salt; a.drop_p = g->drop_p;
   a.n = g->n;
-  const int nwt = (g->n + 31) / 32;
   const size_t lds = fused_lds_bytes(g->n);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gcn_fwd_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)fused_lds_bytes(512));
-    (void)hipFuncSetAttribute((const void*)gcn_bwd_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)fused_lds_bytes(512));
+    ensure_lds_attr(gcn_fwd_fused_kernel<512>);
+    ensure_lds_attr(gcn_fwd_fused_kernel<1024>);
     attr_set = true;
   }
-  gcn_fwd_fused_kernel<<<g->rows / g->n, 64 * nwt, lds, s>>>(a);
+  if (nwt <= 8) gcn_fwd_fused_kernel<512><<<g->rows / g->n, 64 * nwt, lds, s>>>(a);
+  else gcn_fwd_fused_kernel<1024><<<g->rows / g->n, 64 * nwt, lds, s>>>(a);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
 
 int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT, float* dxg, long ld_dxg,
                              float* t1, float* t2, long ld_t, hipStream_t s) {
+  const int nwt = (g->n + 31) / 32;
+  GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_bwd (fused): supports must be padded to 32*ceil(n/32)");
   FusedBwd a;
   a.dh = g->dh;
   for (int k = 0; k < 8; ++k) a.supT[k] = (k < g->nsup) ? supT[k] : nullptr;
@@ -310,14 +336,15 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   a.dxg = dxg; a.ld_dxg = ld_dxg;
   a.t1 = t1; a.t2 = t2; a.ld_t = ld_t; a.adp_index = g->adp_index;
   a.n = g->n;
-  const int nwt = (g->n + 31) / 32;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gcn_bwd_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)fused_lds_bytes(512));
+    ensure_lds_attr(gcn_bwd_fused_kernel<512>);
+    ensure_lds_attr(gcn_bwd_fused_kernel<1024>);
     attr_set = true;
   }
-  gcn_bwd_fused_kernel<<<g->rows / g->n, 64 * nwt, fused_lds_bytes(g->n), s>>>(a);
+  const size_t lds = fused_lds_bytes(g->n);
+  if (nwt <= 8) gcn_bwd_fused_kernel<512><<<g->rows / g->n, 64 * nwt, lds, s>>>(a);
+  else gcn_bwd_fused_kernel<1024><<<g->rows / g->n, 64 * nwt, lds, s>>>(a);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -325,7 +352,16 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
 extern "C" int gwn_transpose(const float* src, int n, int ld_src, float* dst, int ld_dst, hipStream_t s) {
   GWN_REQUIRE(n > 0, "transpose: bad shape");
   dim3 grid((n + 31) / 32, (n + 31) / 32);
-  transpose_kernel<<<grid, 256, 0, s>>>(src, n, ld_src, dst, ld_dst);
+  pad_copy_kernel<<<grid, 256, 0, s>>>(src, n, ld_src, dst, ld_dst, n, 1);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+extern "C" int gwn_pad_square(const float* src, int n, int ld_src, float* dst, int np, int ld_dst, int transpose,
+                              hipStream_t s) {
+  GWN_REQUIRE(n > 0 && np >= n && ld_dst >= np, "pad_square: bad shape");
+  dim3 grid((np + 31) / 32, (np + 31) / 32);
+  pad_copy_kernel<<<grid, 256, 0, s>>>(src, n, ld_src, dst, ld_dst, np, transpose);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

@@ -39,7 +39,7 @@ typedef gwn_gemm_desc GemmParams;
 int gwn_gemm_launch(const GemmParams& p, hipStream_t stream);
 
 // Fused diffusion GCN (gcn_fused.hip)
-bool gwn_gcn_fused_eligible(int c, int n, int nsup);
+bool gwn_gcn_fused_eligible(int c, int n, int nsup, int ld_sup);
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s);
 int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT, float* dxg, long ld_dxg,
                              float* t1, float* t2, long ld_t, hipStream_t s);

@@ -716,7 +716,7 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
 int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_fwd: rows must be slices*n");
   const int c = a->c, n = a->n, slices = a->rows / n;
-  if (gwn_gcn_fused_eligible(c, n, a->nsup)) return gwn_gcn_fused_fwd_launch(a, a->bn_partials, s);
+  if (gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup)) return gwn_gcn_fused_fwd_launch(a, a->bn_partials, s);
   const int width = (2 * a->nsup + 1) * c;
   for (int k = 0; k < a->nsup; ++k) {
     float* x1 = a->h + (1 + 2 * k) * c;
@@ -770,7 +770,7 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   if (rc) return rc;
   rc = gwn_colsum(a->dh, a->rows, c, c, a->db_mlp, 0, a->workspace, s);
   if (rc) return rc;
-  if (a->sup_t && gwn_gcn_fused_eligible(c, n, a->nsup)) {
+  if (a->sup_t && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup)) {
     // fused: dxg -> dhcat piece 0; for the adaptive support dx1 -> piece 1, dx2 -> piece 2
     float* t1 = a->dhcat + c;
     float* t2 = a->dhcat + 2 * c;

@@ -116,6 +116,7 @@ _SIGS = [
     ("gwn_batchnorm_fwd_partials", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gwn_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    ("gwn_pad_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
     ("gwn_batchnorm_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_u64, c_float, c_void_p,
                                   c_void_p]),

@@ -189,6 +189,7 @@ class Config:
         self.nfixed = len(model.supports) if (self.use_gcn and model.supports is not None) else 0
         self.nsup = self.nfixed + (1 if (self.use_gcn and self.adaptive) else 0)
         self.W = (2 * self.nsup + 1) * self.C if self.use_gcn else self.C
+        self.NP = (self.N + 31) // 32 * 32  # padded support side (zero outside N x N)
         if model.residual_channels != model.dilation_channels:
             raise ValueError("gwn_amd: residual_channels must equal dilation_channels")
         if model.kernel_size != 2:
@@ -228,7 +229,7 @@ class Acts:
         self.skr = e(tf * P, cfg.S)
         self.e1 = e(tf * P, cfg.E)
         self.y = e(tf * P, cfg.O)
-        self.adp = e(N, N) if cfg.adaptive else None
+        self.adp = torch.zeros(cfg.NP, cfg.NP, device=device, dtype=F32) if cfg.adaptive else None
         self.training = training
 
 
@@ -281,7 +282,7 @@ class Executor:
             "dfg": e(maxrows, 2 * C),
             "dh": e(maxrows, C),
             "dhc": e(maxrows, cfg.W),
-            "dadp": e(N, N),
+            "dadp": torch.zeros(cfg.NP, cfg.NP, device=self.device, dtype=F32),
             "metrics": e(4),
             "bnpart": e(ts[0] * B * 3 * C),  # per-slice BN partials of one layer
         }
@@ -293,7 +294,7 @@ class Executor:
             lib.gwn_colsum_workspace_floats(maxrows, max(cfg.E, cfg.S, cfg.L * C)),
             lib.gwn_masked_loss_workspace_floats(B, cfg.O, N, tf),
             lib.gwn_clip_adam_workspace_floats(self.layout.flat_total),
-            N * N,
+            cfg.NP * cfg.NP,
         ]
         # split-K partials of the head / start weight grads
         for (M_, N_, K_) in ((cfg.O, cfg.E, tf * P), (cfg.E, cfg.S, tf * P), (cfg.S, L * C, tf * P),
@@ -347,16 +348,16 @@ class Executor:
         lib = _lib
         if cfg.adaptive and cfg.use_gcn:
             lib.call("gwn_adaptive_adj_fwd", ptr(self.pk("nv1")), ptr(self.pk("nv2")), N, 10,
-                     ptr(acts.adp), N, st)
+                     ptr(acts.adp), cfg.NP, st)
         sups, sup_arr = self.supports(fixed_sups, acts)
         acts.sups, acts.sup_arr = sups, sup_arr
         acts.supT_arr = None
         if training and sups:
             # transposed supports: the fused backward computes A·x as (A^T)^T·x on the forward kernel path
             if getattr(acts, "supT", None) is None or len(acts.supT) != len(sups):
-                acts.supT = [torch.empty(N, N, device=self.device, dtype=F32) for _ in sups]
+                acts.supT = [torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32) for _ in sups]
             for s_, t_ in zip(sups, acts.supT):
-                lib.call("gwn_transpose", ptr(s_), N, N, ptr(t_), N, st)
+                lib.call("gwn_pad_square", ptr(s_), N, cfg.NP, ptr(t_), cfg.NP, cfg.NP, 1, st)
             acts.supT_arr = (ctypes.c_void_p * len(sups))(*[t.data_ptr() for t in acts.supT])
         sx = x.stride()
         lib.call("gwn_start_conv_fwd", ptr(x), sx[0], sx[1], sx[2], sx[3], B, cin, N, t_in, ts[0],
@@ -376,7 +377,7 @@ class Executor:
                 continue  # the last gcn / bn output is dead in eval (only skip reaches the output)
             drop = float(self.dropout) if (training and cfg.use_gcn) else 0.0
             ga = _lib.GcnArgs(rows=rows, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
-                              sup=ctypes.cast(sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=N,
+                              sup=ctypes.cast(sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=cfg.NP,
                               h=ptr(acts.H[i]), ld_h=cfg.W,
                               w_mlp=ptr(self.pk("mlp_w%d" % i)), b_mlp=ptr(self.pk("mlp_b%d" % i)),
                               residual=acts.X[i].data_ptr() + 4 * d * P * C, z=ptr(acts.Z[i]),
@@ -448,7 +449,8 @@ class Executor:
                          float(self.dropout) if (acts.training and cfg.use_gcn) else 0.0, ptr(ws), st)
                 adp_index = cfg.nsup - 1 if (cfg.use_gcn and cfg.adaptive) else -1
                 gb = _lib.GcnBwdArgs(rows=rows, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
-                                     sup=ctypes.cast(acts.sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=N,
+                                     sup=ctypes.cast(acts.sup_arr, ctypes.POINTER(ctypes.c_void_p)),
+                                     ld_sup=cfg.NP,
                                      h=ptr(acts.H[i]), ld_h=cfg.W, w_mlp=ptr(self.pk("mlp_w%d" % i)),
                                      dh=ptr(sc["dh"]), dhcat=ptr(sc["dhc"]), ld_dhcat=cfg.W,
                                      dw_mlp=ptr(self.gk("mlp_w%d" % i)), db_mlp=ptr(self.gk("mlp_b%d" % i)),
@@ -475,7 +477,7 @@ class Executor:
         lib.call("gwn_colsum", ptr(dnext), rows0, C, C, ptr(self.gk("start_b")), 0, ptr(ws), st)
         if cfg.use_gcn and cfg.adaptive:
             lib.call("gwn_adaptive_adj_bwd", ptr(self.pk("nv1")), ptr(self.pk("nv2")), ptr(acts.adp),
-                     ptr(sc["dadp"]), N, 10, N, ptr(self.gk("nv1")), ptr(self.gk("nv2")), ptr(ws), st)
+                     ptr(sc["dadp"]), N, 10, cfg.NP, ptr(self.gk("nv1")), ptr(self.gk("nv2")), ptr(ws), st)
 
     def unpack_grads(self, gflat):
         _lib.call("gwn_gather", ptr(self.gpacked), ptr(self.uidx), ptr(gflat), self.layout.flat_total,

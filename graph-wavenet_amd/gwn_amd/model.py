@@ -208,12 +208,24 @@ class gwnet(nn.Module):
         return ex
 
     def _fixed_supports(self):
+        """Device copies of the fixed supports, zero-padded to [NP][NP] (NP = 32*ceil(N/32)), the
+        layout the fused diffusion kernel streams (include/gwn.h, gwn_gcn_fwd)."""
         if self.supports is None or len(self.supports) == 0:
             return []
         key = tuple((s.data_ptr(), s._version) for s in self.supports)
         if self._sup_cache[0] != key:
             dev = self._flat.device
-            self._sup_cache = (key, [s.detach().to(dev, F32).contiguous() for s in self.supports])
+            n = self.num_nodes
+            np_ = (n + 31) // 32 * 32
+            padded = []
+            for s in self.supports:
+                src = s.detach().to(dev, F32).contiguous()
+                if tuple(src.shape) != (n, n):
+                    raise RuntimeError("gwnet: supports must be [%d, %d], got %s" % (n, n, tuple(src.shape)))
+                dst = torch.empty(np_, np_, device=dev, dtype=F32)
+                _lib.call("gwn_pad_square", src.data_ptr(), n, n, dst.data_ptr(), np_, np_, 0, _lib.stream())
+                padded.append(dst)
+            self._sup_cache = (key, padded)
         return self._sup_cache[1]
 
     def _bn_bufs(self):

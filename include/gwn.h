@@ -165,9 +165,11 @@ typedef struct gwn_gcn_args {
    * generic path runs instead, they are computed from z by a separate pass. */
   float* bn_partials;
 } gwn_gcn_args;
-/* c == 32 and n <= 512: one fused launch (gcn_fused.hip: node features LDS-resident through the
- * whole diffusion chain, mlp accumulated from the MFMA accumulators, residual + dropout +
- * BN partials in the epilogue).  Otherwise: 2K nconv GEMMs + one mlp GEMM. */
+/* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
+ * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
+ * accumulators, residual + dropout + BN partials in the epilogue).  In that case the supports
+ * must be [np][ld_sup] and ZERO outside [n][n] (gwn_pad_square makes such copies).
+ * Otherwise: 2K nconv GEMMs + one mlp GEMM. */
 int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t stream);
 
 /* Backward of gwn_gcn_fwd given dh (gradient w.r.t. the dropout output, i.e. dz with the
@@ -210,6 +212,9 @@ int gwn_batchnorm_fwd_partials(const float* z, int rows, int c, const float* par
                                float* save_mean, float* save_rstd, hipStream_t stream);
 /* dst[j][i] = src[i][j] for an n x n matrix (supports for the fused backward) */
 int gwn_transpose(const float* src, int n, int ld_src, float* dst, int ld_dst, hipStream_t stream);
+/* dst [np][ld_dst] = src (or src^T if transpose) inside [n][n], zero elsewhere (np >= n) */
+int gwn_pad_square(const float* src, int n, int ld_src, float* dst, int np, int ld_dst, int transpose,
+                   hipStream_t stream);
 
 /* BN backward fused with the residual split and the dropout backward of the same layer:
  *   dz = gamma*rstd*(dy - mean(dy) - xhat*mean(dy*xhat));  dgamma, dbeta
