@@ -343,6 +343,7 @@ class Executor:
         if acts is None:
             acts = Acts(cfg, B, ts, self.device, training)
         acts.training = training
+        acts.gcn_args = {}
         P = B * N
         tf = ts[-1]
         lib = _lib
@@ -384,6 +385,7 @@ class Executor:
                               seed_ptr=ptr(self.seed), salt=i, drop_p=drop,
                               bn_partials=ptr(bnpart) if training else None)
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
+            acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
             rm, rv, mom, eps = bn_bufs[i]
             if training:
                 lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnpart), rows // N,
