@@ -34,17 +34,22 @@ __device__ __forceinline__ void epi_store(const GemmParams& p, int m, int n, flo
   p.C[(long)m * p.ldc_m + (long)ni * p.ldc_n + (long)no * p.c_no_stride] = v;
 }
 
+// Operands are staged as "quads": 4 consecutive elements along the operand's contiguous
+// dimension (k for AKC/BKC, m or n otherwise).  vec_a / vec_b (host-checked alignment) turn a
+// quad into one 16-B global load; otherwise the quad is 4 guarded scalar loads.
 template <int WM, int WN, int TM, int TN, bool AKC, bool BKC>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) {
+__global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, const int vec_a,
+                                                           const int vec_b) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
   constexpr int LDA = BM + 4;
   constexpr int LDB = BN + 4;
-  constexpr int A_PER = (BM * BK + NT - 1) / NT;
-  constexpr int B_PER = (BN * BK + NT - 1) / NT;
-  __shared__ float As[2][BK * LDA];
-  __shared__ float Bs[2][BK * LDB];
+  constexpr int AQ = BM * BK / 4, BQ = BN * BK / 4;
+  constexpr int A_PER = (AQ + NT - 1) / NT;
+  constexpr int B_PER = (BQ + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) float As[2][BK * LDA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -63,62 +68,117 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  float ra[A_PER], rb[B_PER];
+  float4 ra[A_PER], rb[B_PER];
+
+  // scalar element loads (any layout; per-element two-level index when the tile straddles)
+  auto a_elem = [&](int m, int k, int ko0) -> float {
+    if (m >= p.M || k >= kend) return 0.0f;
+    const int ko = a_tiled ? ko0 : (int)((unsigned)k / (unsigned)p.a_kin);
+    const int ki = k - ko * p.a_kin;
+    const int srow = m + ko * p.a_row_shift;
+    if (srow < 0 || srow >= p.a_rows) return 0.0f;
+    return p.A[(long)srow * p.lda_m + (long)ki * p.lda_k + (long)ko * p.a_ko_stride];
+  };
+  auto b_elem = [&](int k, int n, int kb0) -> float {
+    if (n >= p.N || k >= kend) return 0.0f;
+    const int kb = b_tiled ? kb0 : (int)((unsigned)k / (unsigned)p.b_kin);
+    const int kj = k - kb * p.b_kin;
+    const int no = (unsigned)n / (unsigned)p.b_nin, ni = n - no * p.b_nin;
+    return p.B[(long)kj * p.ldb_k + (long)kb * p.b_ko_stride + (long)ni * p.ldb_n + (long)no * p.b_no_stride];
+  };
 
   auto load = [&](int k0) {
-    {
-      // k-tiles never straddle an a_kin block when a_kin % BK == 0 (the hot configurations);
-      // otherwise (e.g. NCHW slices with T = 12 inner steps) the block is resolved per element.
-      const int ko0 = k0 / p.a_kin;
+    // k-tiles never straddle an a_kin block when a_kin % BK == 0 (the hot configurations);
+    // otherwise (e.g. NCHW slices with T = 12 inner steps) the block is resolved per element.
+    const int ko0 = k0 / p.a_kin;
 #pragma unroll
-      for (int i = 0; i < A_PER; ++i) {
-        const int e = tid + i * NT;
-        int kk, mm;
-        if (AKC) { kk = e % BK; mm = e / BK; } else { kk = e / BM; mm = e % BM; }
-        const int m = m0 + mm, k = k0 + kk;
-        const int ko = a_tiled ? ko0 : (int)((unsigned)k / (unsigned)p.a_kin);
-        const int ki = k - ko * p.a_kin;
-        const int srow = m + ko * p.a_row_shift;
-        float v = 0.0f;
-        if (e < BM * BK && m < p.M && k < kend && srow >= 0 && srow < p.a_rows)
-          v = p.A[(long)srow * p.lda_m + (long)ki * p.lda_k + (long)ko * p.a_ko_stride];
-        ra[i] = v;
-      }
-    }
-    {
-      const int kb0 = k0 / p.b_kin;
-#pragma unroll
-      for (int i = 0; i < B_PER; ++i) {
-        const int e = tid + i * NT;
-        int kk, nn;
-        if (BKC) { kk = e % BK; nn = e / BK; } else { kk = e / BN; nn = e % BN; }
-        const int n = n0 + nn, k = k0 + kk;
-        float v = 0.0f;
-        if (e < BN * BK && n < p.N && k < kend) {
-          const int kb = b_tiled ? kb0 : (int)((unsigned)k / (unsigned)p.b_kin);
-          const int kj = k - kb * p.b_kin;
-          const int no = (unsigned)n / (unsigned)p.b_nin, ni = n - no * p.b_nin;
-          v = p.B[(long)kj * p.ldb_k + (long)kb * p.b_ko_stride + (long)ni * p.ldb_n +
-                  (long)no * p.b_no_stride];
+    for (int i = 0; i < A_PER; ++i) {
+      const int q = tid + i * NT;
+      float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (q < AQ) {
+        if (AKC) {  // quad = 4 consecutive k of row m
+          const int m = m0 + q / (BK / 4), k = k0 + (q % (BK / 4)) * 4;
+          const int srow = m + ko0 * p.a_row_shift;
+          if (vec_a && m < p.M && k + 3 < kend && srow >= 0 && srow < p.a_rows) {
+            v = *(const float4*)(p.A + (long)srow * p.lda_m + (k - ko0 * p.a_kin) + (long)ko0 * p.a_ko_stride);
+          } else {
+            v.x = a_elem(m, k, ko0); v.y = a_elem(m, k + 1, ko0);
+            v.z = a_elem(m, k + 2, ko0); v.w = a_elem(m, k + 3, ko0);
+          }
+        } else {  // quad = 4 consecutive m at one k
+          const int k = k0 + q / (BM / 4), m = m0 + (q % (BM / 4)) * 4;
+          const int srow = m + ko0 * p.a_row_shift;
+          if (vec_a && k < kend && m + 3 < p.M && srow >= 0 && srow + 3 < p.a_rows) {
+            v = *(const float4*)(p.A + srow + (long)(k - ko0 * p.a_kin) * p.lda_k + (long)ko0 * p.a_ko_stride);
+          } else {
+            v.x = a_elem(m, k, ko0); v.y = a_elem(m + 1, k, ko0);
+            v.z = a_elem(m + 2, k, ko0); v.w = a_elem(m + 3, k, ko0);
+          }
         }
-        rb[i] = v;
       }
+      ra[i] = v;
+    }
+    const int kb0 = k0 / p.b_kin;
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int q = tid + i * NT;
+      float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (q < BQ) {
+        if (BKC) {  // quad = 4 consecutive k of column n
+          const int n = n0 + q / (BK / 4), k = k0 + (q % (BK / 4)) * 4;
+          if (vec_b && n < p.N && k + 3 < kend) {
+            const int no = (unsigned)n / (unsigned)p.b_nin, ni = n - no * p.b_nin;
+            v = *(const float4*)(p.B + (k - kb0 * p.b_kin) + (long)kb0 * p.b_ko_stride + (long)ni * p.ldb_n +
+                                 (long)no * p.b_no_stride);
+          } else {
+            v.x = b_elem(k, n, kb0); v.y = b_elem(k + 1, n, kb0);
+            v.z = b_elem(k + 2, n, kb0); v.w = b_elem(k + 3, n, kb0);
+          }
+        } else {  // quad = 4 consecutive n at one k
+          const int k = k0 + q / (BN / 4), n = n0 + (q % (BN / 4)) * 4;
+          if (vec_b && k < kend && n + 3 < p.N) {
+            const int no = (unsigned)n / (unsigned)p.b_nin, ni = n - no * p.b_nin;
+            v = *(const float4*)(p.B + (long)(k - kb0 * p.b_kin) * p.ldb_k + (long)kb0 * p.b_ko_stride + ni +
+                                 (long)no * p.b_no_stride);
+          } else {
+            v.x = b_elem(k, n, kb0); v.y = b_elem(k, n + 1, kb0);
+            v.z = b_elem(k, n + 2, kb0); v.w = b_elem(k, n + 3, kb0);
+          }
+        }
+      }
+      rb[i] = v;
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      const int e = tid + i * NT;
-      int kk, mm;
-      if (AKC) { kk = e % BK; mm = e / BK; } else { kk = e / BM; mm = e % BM; }
-      if (e < BM * BK) As[buf][kk * LDA + mm] = ra[i];
+      const int q = tid + i * NT;
+      if (q >= AQ) continue;
+      if (AKC) {
+        const int mm = q / (BK / 4), kk = (q % (BK / 4)) * 4;
+        As[buf][kk * LDA + mm] = ra[i].x;
+        As[buf][(kk + 1) * LDA + mm] = ra[i].y;
+        As[buf][(kk + 2) * LDA + mm] = ra[i].z;
+        As[buf][(kk + 3) * LDA + mm] = ra[i].w;
+      } else {
+        const int kk = q / (BM / 4), mm = (q % (BM / 4)) * 4;
+        *(float4*)&As[buf][kk * LDA + mm] = ra[i];
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int e = tid + i * NT;
-      int kk, nn;
-      if (BKC) { kk = e % BK; nn = e / BK; } else { kk = e / BN; nn = e % BN; }
-      if (e < BN * BK) Bs[buf][kk * LDB + nn] = rb[i];
+      const int q = tid + i * NT;
+      if (q >= BQ) continue;
+      if (BKC) {
+        const int nn = q / (BK / 4), kk = (q % (BK / 4)) * 4;
+        Bs[buf][kk * LDB + nn] = rb[i].x;
+        Bs[buf][(kk + 1) * LDB + nn] = rb[i].y;
+        Bs[buf][(kk + 2) * LDB + nn] = rb[i].z;
+        Bs[buf][(kk + 3) * LDB + nn] = rb[i].w;
+      } else {
+        const int kk = q / (BN / 4), nn = (q % (BN / 4)) * 4;
+        *(float4*)&Bs[buf][kk * LDB + nn] = rb[i];
+      }
     }
   };
 
@@ -208,17 +268,20 @@ __global__ void splitk_reduce_kernel(const GemmParams p) {
 }
 
 template <int WM, int WN, int TM, int TN>
-int launch_cfg(const GemmParams& p, bool akc, bool bkc, hipStream_t s) {
+int launch_cfg(const GemmParams& p, bool akc, bool bkc, int va, int vb, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.ksplit);
   dim3 block(64 * WM * WN);
-  if (akc && bkc) gemm_kernel<WM, WN, TM, TN, true, true><<<grid, block, 0, s>>>(p);
-  else if (akc) gemm_kernel<WM, WN, TM, TN, true, false><<<grid, block, 0, s>>>(p);
-  else if (bkc) gemm_kernel<WM, WN, TM, TN, false, true><<<grid, block, 0, s>>>(p);
-  else gemm_kernel<WM, WN, TM, TN, false, false><<<grid, block, 0, s>>>(p);
+  if (akc && bkc) gemm_kernel<WM, WN, TM, TN, true, true><<<grid, block, 0, s>>>(p, va, vb);
+  else if (akc) gemm_kernel<WM, WN, TM, TN, true, false><<<grid, block, 0, s>>>(p, va, vb);
+  else if (bkc) gemm_kernel<WM, WN, TM, TN, false, true><<<grid, block, 0, s>>>(p, va, vb);
+  else gemm_kernel<WM, WN, TM, TN, false, false><<<grid, block, 0, s>>>(p, va, vb);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
+
+inline bool al16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
+inline bool m4(long v) { return (v & 3) == 0; }
 
 }  // namespace
 
@@ -247,13 +310,24 @@ int gwn_gemm_launch(const GemmParams& pin, hipStream_t s) {
   }
   const bool akc = (p.lda_k == 1 && p.lda_m != 1);
   const bool bkc = (p.ldb_k == 1 && p.ldb_n != 1);
+  const bool a_tiled = (p.a_kin % BK == 0) || (p.a_kin >= p.K);
+  const bool b_tiled = (p.b_kin % BK == 0) || (p.b_kin >= p.K);
+  // 16-B quads are legal when the quad never straddles an index block and every stride that
+  // moves between quads is a multiple of 4 floats
+  const int va = al16(p.A) && a_tiled && m4(p.a_ko_stride) && m4(p.a_kin) &&
+                 (akc ? m4(p.lda_m) : (p.lda_m == 1 && m4(p.lda_k) && m4(p.a_row_shift)));
+  const int vb = al16(p.B) && b_tiled && m4(p.b_ko_stride) && m4(p.b_no_stride) && m4(p.b_kin) &&
+                 (bkc ? m4(p.ldb_n) : (p.ldb_n == 1 && m4(p.ldb_k) && m4(p.b_nin)));
   int rc;
-  if (p.N <= 32) rc = launch_cfg<4, 1, 2, 1>(p, akc, bkc, s);          // 256 x 32
-  else if (p.N <= 64 && p.M > 128 && p.M <= 224) rc = launch_cfg<7, 1, 1, 2>(p, akc, bkc, s);  // 224 x 64
-  else if (p.N <= 64) rc = launch_cfg<4, 1, 1, 2>(p, akc, bkc, s);     // 128 x 64
-  else if (p.M > 160 && p.M <= 224) rc = launch_cfg<7, 1, 1, 2>(p, akc, bkc, s);
-  else if (p.M >= 128) rc = launch_cfg<2, 2, 2, 2>(p, akc, bkc, s);    // 128 x 128
-  else rc = launch_cfg<2, 2, 1, 1>(p, akc, bkc, s);                    // 64 x 64
+  if (p.M <= 32 && p.N <= 32) rc = launch_cfg<1, 1, 1, 1>(p, akc, bkc, va, vb, s);        // 32 x 32
+  else if (p.M <= 32 && p.N <= 224) rc = launch_cfg<1, 7, 1, 1>(p, akc, bkc, va, vb, s);  // 32 x 224
+  else if (p.N <= 32) rc = launch_cfg<4, 1, 2, 1>(p, akc, bkc, va, vb, s);                // 256 x 32
+  else if (p.N <= 64 && p.M <= 64) rc = launch_cfg<2, 2, 1, 1>(p, akc, bkc, va, vb, s);   // 64 x 64
+  else if (p.N <= 64 && p.M > 128 && p.M <= 224) rc = launch_cfg<7, 1, 1, 2>(p, akc, bkc, va, vb, s);  // 224 x 64
+  else if (p.N <= 64) rc = launch_cfg<4, 1, 1, 2>(p, akc, bkc, va, vb, s);                // 128 x 64
+  else if (p.M > 160 && p.M <= 224) rc = launch_cfg<7, 1, 1, 2>(p, akc, bkc, va, vb, s);
+  else if (p.M >= 128) rc = launch_cfg<2, 2, 2, 2>(p, akc, bkc, va, vb, s);               // 128 x 128
+  else rc = launch_cfg<2, 2, 1, 1>(p, akc, bkc, va, vb, s);                               // 64 x 64
   if (rc != GWN_OK || p.ksplit <= 1) return rc;
   const long total = (long)p.M * p.N;
   splitk_reduce_kernel<<<(unsigned)((total + 7) / 8), 256, 0, s>>>(p);

@@ -41,6 +41,43 @@ def test_gemm_layouts(gpu, M, N, K, akc, bkc):
     assert torch.all((got - ref).abs() <= bound + 1e-30), float(((got - ref).abs() / (bound + 1e-30)).max())
 
 
+@pytest.mark.parametrize("M,N,K", [(207, 207, 197), (61, 222, 99), (300, 30, 1001), (13, 5, 7), (33, 224, 513)])
+@pytest.mark.parametrize("akc,bkc", [(True, False), (False, False), (True, True), (False, True)])
+def test_gemm_vector_quads_ragged(gpu, M, N, K, akc, bkc):
+    """Leading dims padded to multiples of 4 (16-B quad loads enabled) with ragged M, N, K:
+    the edge quads fall back to guarded scalar loads."""
+    def pad4(v):
+        return (v + 3) // 4 * 4 + 4
+    torch.manual_seed(M + 3 * N + 7 * K)
+    A = torch.randn(M, K, dtype=torch.float64)
+    B = torch.randn(K, N, dtype=torch.float64)
+    ref = A @ B
+    if akc:
+        lda = pad4(K)
+        Ad = torch.zeros(M, lda, device=gpu); Ad[:, :K] = A.float().to(gpu)
+        a_kw = dict(lda_m=lda, lda_k=1)
+    else:
+        lda = pad4(M)
+        Ad = torch.zeros(K, lda, device=gpu); Ad[:, :M] = A.t().float().to(gpu)
+        a_kw = dict(lda_m=1, lda_k=lda)
+    if bkc:
+        ldb = pad4(K)
+        Bd = torch.zeros(N, ldb, device=gpu); Bd[:, :K] = B.t().float().to(gpu)
+        b_kw = dict(ldb_k=1, ldb_n=ldb)
+    else:
+        ldb = pad4(N)
+        Bd = torch.zeros(K, ldb, device=gpu); Bd[:, :N] = B.float().to(gpu)
+        b_kw = dict(ldb_k=ldb, ldb_n=1)
+    C = torch.full((M, N), float("nan"), device=gpu)
+    part = torch.empty(4 * M * N, device=gpu)
+    _gemm(A=Ad, B=Bd, C=C, ldc_m=N, ldc_n=1, M=M, N=N, K=K, ksplit=4 if K > 500 else 1, part=part,
+          **a_kw, **b_kw)
+    torch.cuda.synchronize()
+    got = C.double().cpu()
+    bound = 2.0 ** -22 * K * (A.abs() @ B.abs())
+    assert torch.all((got - ref).abs() <= bound + 1e-30)
+
+
 def test_mfma_layout_identity_asymmetric(gpu):
     """A = I with an asymmetric B must reproduce B exactly (catches a transposed C write)."""
     n = 64
