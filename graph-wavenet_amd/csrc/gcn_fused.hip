@@ -50,9 +50,35 @@ __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int s
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
 
-// D'[c][w0+col] += sum_v buf[v][c] * G[v][w0+col]
+struct GBatch {
+  float v[KB];
+};
+
+// first K batch (32 nodes) of G's B-operand fragments; issued a phase ahead of its diffusion
+__device__ __forceinline__ GBatch g_first(const float* G, int ld, int nkb, int w0, int lane) {
+  const int half = lane >> 5, col = lane & 31;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, nkb * 32 * ld * 4, 0x00020000);
+  const int voff = (half * ld + w0 + col) * 4;
+  GBatch g;
+#pragma unroll
+  for (int j = 0; j < KB; ++j) g.v[j] = bload(rs, voff, j * 2 * ld * 4);
+  return g;
+}
+
+// W fragments for mlp_from_acc (A operand W[c'=col][off + crow(s, half)]); issued ahead
+__device__ __forceinline__ GBatch w_frags(const float* W, int ld_w, int off, int lane) {
+  const int half = lane >> 5, col = lane & 31;
+  const float* wp = W + (long)col * ld_w + off;
+  GBatch f;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) f.v[s] = wp[crow(s, half)];
+  return f;
+}
+
+// D'[c][w0+col] += sum_v buf[v][c] * G[v][w0+col];  g0 = g_first(G, ...) (consumed)
 __device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int ld, int nkb, int w0,
-                                          int lane, f32x16 acc) {
+                                          int lane, f32x16 acc, const GBatch& g0) {
   const int half = lane >> 5, col = lane & 31;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, nkb * 32 * ld * 4, 0x00020000);
@@ -60,7 +86,7 @@ __device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int 
   const int rowb = 2 * ld * 4;  // bytes between k-steps (2 nodes)
   float gq[KB];
 #pragma unroll
-  for (int j = 0; j < KB; ++j) gq[j] = bload(rs, voff, j * rowb);
+  for (int j = 0; j < KB; ++j) gq[j] = g0.v[j];
   for (int kb = 0; kb < nkb; ++kb) {
     float av[KB];
     const float* bp = buf + (32 * kb + half) * LDR + col;
@@ -78,16 +104,10 @@ __device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int 
   return acc;
 }
 
-// acc_out[c'][w] += sum_c W[c'][off + c] * D'[c][w]   with D' = the accumulator `d`
-__device__ __forceinline__ f32x16 mlp_from_acc(const float* W, int ld_w, int off, const f32x16& d,
-                                               int lane, f32x16 acc) {
-  const int half = lane >> 5, col = lane & 31;
-  const float* wp = W + (long)col * ld_w + off;
-  float wf[16];
+// acc_out[c'][w] += sum_c W[c'][off + c] * D'[c][w]   with D' = the accumulator `d`, wf = w_frags(off)
+__device__ __forceinline__ f32x16 mlp_from_acc(const GBatch& wf, const f32x16& d, f32x16 acc) {
 #pragma unroll
-  for (int s = 0; s < 16; ++s) wf[s] = wp[crow(s, half)];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s], d[s], acc, 0, 0, 0);
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wf.v[s], d[s], acc, 0, 0, 0);
   return acc;
 }
 
@@ -159,19 +179,25 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
   const long row0 = (long)blockIdx.x * n;
   const float* hs = a.h + row0 * a.ld_h;
 
+  // software pipeline: every G first batch / W fragment set is issued one phase before use
+  GBatch g0 = (a.nsup > 0) ? g_first(a.sup[0], a.ld_sup, nkb, w0, lane) : GBatch{};
   global_to_lds(hs, a.ld_h, n, np, xs);
   __syncthreads();
   f32x16 hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
   for (int k = 0; k < a.nsup; ++k) {
     const float* G = a.sup[k];
-    f32x16 d = diffuse(xs, G, a.ld_sup, nkb, w0, lane, zero16());
-    hacc = mlp_from_acc(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, d, lane, hacc);
+    GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
+    f32x16 d = diffuse(xs, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
+    g0 = g_first(G, a.ld_sup, nkb, w0, lane);  // hop 2 re-reads the same support
+    hacc = mlp_from_acc(wf, d, hacc);
+    wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
     __syncthreads();
     acc_to_lds(ys, d, w0, lane);
     __syncthreads();
     lds_to_global(ys, (float*)hs + (1 + 2 * k) * CH, a.ld_h, n);
-    d = diffuse(ys, G, a.ld_sup, nkb, w0, lane, zero16());
-    hacc = mlp_from_acc(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, d, lane, hacc);
+    d = diffuse(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
+    if (k + 1 < a.nsup) g0 = g_first(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
+    hacc = mlp_from_acc(wf, d, hacc);
     __syncthreads();
     acc_to_lds(ys, d, w0, lane);
     __syncthreads();
@@ -235,6 +261,7 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
   const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
   const long row0 = (long)blockIdx.x * n;
 
+  GBatch g0 = (a.nsup > 0) ? g_first(a.supT[0], a.ld_sup, nkb, w0, lane) : GBatch{};
   global_to_lds(a.dh + row0 * CH, CH, n, np, dhs);
   __syncthreads();
   f32x16 dx = mlpT_from_lds(a.w_mlp, a.ld_w, 0, dhs, w0, lane, zero16());
@@ -248,12 +275,14 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
     __syncthreads();
     if (k == a.adp_index) lds_to_global(buf, a.t2 + row0 * a.ld_t, a.ld_t, n);
     f32x16 t = mlpT_from_lds(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, w0, lane, zero16());
-    t = diffuse(buf, GT, a.ld_sup, nkb, w0, lane, t);  // dx1 = dP_x1 + A dP_x2
+    t = diffuse(buf, GT, a.ld_sup, nkb, w0, lane, t, g0);  // dx1 = dP_x1 + A dP_x2
+    g0 = g_first(GT, a.ld_sup, nkb, w0, lane);
     __syncthreads();
     acc_to_lds(buf, t, w0, lane);
     __syncthreads();
     if (k == a.adp_index) lds_to_global(buf, a.t1 + row0 * a.ld_t, a.ld_t, n);
-    dx = diffuse(buf, GT, a.ld_sup, nkb, w0, lane, dx);  // dxg += A dx1
+    dx = diffuse(buf, GT, a.ld_sup, nkb, w0, lane, dx, g0);  // dxg += A dx1
+    if (k + 1 < a.nsup) g0 = g_first(a.supT[k + 1], a.ld_sup, nkb, w0, lane);
   }
   __syncthreads();
   acc_to_lds(buf, dx, w0, lane);
