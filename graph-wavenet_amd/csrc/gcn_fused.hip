@@ -84,22 +84,45 @@ __device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int 
       __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, nkb * 32 * ld * 4, 0x00020000);
   const int voff = (half * ld + w0 + col) * 4;
   const int rowb = 2 * ld * 4;  // bytes between k-steps (2 nodes)
-  float gq[KB];
+  // Two register sets ga / gb (no write-after-read between a batch's MFMAs and the next batch's
+  // loads): the loads of batch b+1 issue at the top of batch b, 16 MFMAs ahead of their use.
+  // The loop body has no branch around a load, so hipcc keeps the waits counted (vmcnt(N)).
+  float ga[KB], gb[KB];
 #pragma unroll
-  for (int j = 0; j < KB; ++j) gq[j] = g0.v[j];
-  for (int kb = 0; kb < nkb; ++kb) {
-    float av[KB];
+  for (int j = 0; j < KB; ++j) ga[j] = g0.v[j];
+  auto lds_batch = [&](int kb, float* av) {
     const float* bp = buf + (32 * kb + half) * LDR + col;
 #pragma unroll
     for (int j = 0; j < KB; ++j) av[j] = bp[2 * j * LDR];
-    const bool more = kb + 1 < nkb;
-    const int nb = (kb + 1) * KB * rowb;
-    // rolling prefetch: slot j is refilled with batch kb+1 right after its MFMA consumed it
+  };
+  auto g_batch = [&](int kb, float* g) {
 #pragma unroll
-    for (int j = 0; j < KB; ++j) {
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], gq[j], acc, 0, 0, 0);
-      if (more) gq[j] = bload(rs, voff, nb + j * rowb);
-    }
+    for (int j = 0; j < KB; ++j) g[j] = bload(rs, voff, (kb * KB + j) * rowb);
+  };
+  auto mfma_batch = [&](const float* av, const float* g) {
+#pragma unroll
+    for (int j = 0; j < KB; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], g[j], acc, 0, 0, 0);
+  };
+  int kb = 0;
+  for (; kb + 2 < nkb; kb += 2) {
+    float av[KB];
+    g_batch(kb + 1, gb);
+    lds_batch(kb, av);
+    mfma_batch(av, ga);
+    g_batch(kb + 2, ga);
+    lds_batch(kb + 1, av);
+    mfma_batch(av, gb);
+  }
+  float av[KB];
+  if (kb + 1 < nkb) {  // two batches left
+    g_batch(kb + 1, gb);
+    lds_batch(kb, av);
+    mfma_batch(av, ga);
+    lds_batch(kb + 1, av);
+    mfma_batch(av, gb);
+  } else {             // one batch left
+    lds_batch(kb, av);
+    mfma_batch(av, ga);
   }
   return acc;
 }
@@ -186,17 +209,17 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
   f32x16 hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
   for (int k = 0; k < a.nsup; ++k) {
     const float* G = a.sup[k];
-    GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
     f32x16 d = diffuse(xs, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
     g0 = g_first(G, a.ld_sup, nkb, w0, lane);  // hop 2 re-reads the same support
+    GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
     hacc = mlp_from_acc(wf, d, hacc);
-    wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
     __syncthreads();
     acc_to_lds(ys, d, w0, lane);
     __syncthreads();
     lds_to_global(ys, (float*)hs + (1 + 2 * k) * CH, a.ld_h, n);
     d = diffuse(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
     if (k + 1 < a.nsup) g0 = g_first(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
+    wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
     hacc = mlp_from_acc(wf, d, hacc);
     __syncthreads();
     acc_to_lds(ys, d, w0, lane);

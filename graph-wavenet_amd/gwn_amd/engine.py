@@ -5,6 +5,8 @@ gradient (engine.py:46-51, util.py:527-538) -> hand-written backward -> clip_gra
 Adam (engine.py:52-55), all as libgwn launches on the current stream, followed by ONE device->host
 copy of (loss, mape, rmse) -- the reference does three ``.item()`` syncs (engine.py:56-58).
 """
+import os
+
 import torch
 
 from . import _lib, util
@@ -101,13 +103,17 @@ class trainer():
         self.state = None
         self._acts = {}
         self._host_metrics = torch.zeros(4, dtype=F32).pin_memory() if torch.cuda.is_available() else None
+        # HIP-graph replay of the fused training step (GWN_GRAPHS=0 disables): the ~240 launches
+        # of a step are captured once per (shape, hyper-parameter) key and replayed
+        self.use_graphs = os.environ.get("GWN_GRAPHS", "1") != "0"
+        self._graphs = {}
+        self._eager_runs = {}
 
     # ------------------------------------------------------------------------------------------
-    def _step(self, input, real_val, training):
-        """Fused step; returns the device metrics tensor [mae, mape, rmse]."""
+    def _phase_grads(self, input, real_val, training):
+        """pad -> forward -> masked loss (+ its gradient) -> backward -> flat gradient buffer."""
         model = self.model
-        model.train(training)
-        ex = model.executor()
+        ex = model._executor
         B, _, _, T = input.shape
         ts = ex.cfg.times(T + 1)  # engine.py:44 pads one step on the left before the forward
         key = (B, tuple(ts), training)
@@ -126,12 +132,71 @@ class trainer():
         if training:
             ex.backward(acts, dout)
             ex.unpack_grads(self.optimizer.grad_flat)
-            self._allreduce_grads()
-            clip = self.clip if self.clip is not None else _NO_CLIP
-            self.optimizer.apply(ex.layout.active, clip)
-            if model.dropout > 0:
-                _lib.call("gwn_increment_u64", ptr(ex.seed), 1, _lib.stream())
         return sc["metrics"]
+
+    def _phase_update(self):
+        """clip_grad_norm_(clip) + Adam on the flat buffers; advance the dropout counter."""
+        model = self.model
+        ex = model._executor
+        clip = self.clip if self.clip is not None else _NO_CLIP
+        self.optimizer.apply(ex.layout.active, clip)
+        if model.dropout > 0:
+            _lib.call("gwn_increment_u64", ptr(ex.seed), 1, _lib.stream())
+
+    def _distributed(self):
+        dist = torch.distributed
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+    def _step(self, input, real_val, training):
+        """Fused step; returns the device metrics tensor [mae, mape, rmse]."""
+        model = self.model
+        model.train(training)
+        model.executor()
+        if not training:
+            return self._phase_grads(input, real_val, False)
+        g = self.optimizer.param_groups[0]
+        key = (tuple(input.shape), tuple(real_val.shape), float(g["lr"]), tuple(g["betas"]), float(g["eps"]),
+               float(g["weight_decay"]), self.clip, float(model.dropout), model._flat.data_ptr())
+        if self.use_graphs and key in self._graphs:
+            return self._replay(key, input, real_val)
+        if self.use_graphs and self._eager_runs.get(key, 0) >= 1:
+            self._capture(key, input, real_val)
+            return self._replay(key, input, real_val)
+        self._eager_runs[key] = self._eager_runs.get(key, 0) + 1
+        m = self._phase_grads(input, real_val, True)
+        self._allreduce_grads()
+        self._phase_update()
+        return m
+
+    def _capture(self, key, input, real_val):
+        """Capture the step as one graph (single process) or two graphs around the gradient
+        all-reduce (data parallel: the collective stays eager)."""
+        sx = torch.empty_like(input).copy_(input)
+        sy = torch.empty_like(real_val).copy_(real_val)
+        torch.cuda.synchronize()
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            m = self._phase_grads(sx, sy, True)
+            if not self._distributed():
+                self._phase_update()
+        g2 = None
+        if self._distributed():
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                self._phase_update()
+        self._graphs[key] = (g1, g2, sx, sy, m)
+
+    def _replay(self, key, input, real_val):
+        g1, g2, sx, sy, m = self._graphs[key]
+        if sx.data_ptr() != input.data_ptr():
+            sx.copy_(input)
+        if sy.data_ptr() != real_val.data_ptr():
+            sy.copy_(real_val)
+        g1.replay()
+        if g2 is not None:
+            self._allreduce_grads()
+            g2.replay()
+        return m
 
     def _allreduce_grads(self):
         """Data parallel (one process per GPU): average the flat gradient over ranks with ONE

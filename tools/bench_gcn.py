@@ -1,0 +1,65 @@
+"""Micro-benchmark of the fused diffusion GCN kernels (gwn_gcn_fwd / gwn_gcn_bwd) at METR-LA
+layer shapes, timed with HIP events on the launch stream.  Usage: python tools/bench_gcn.py"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "graph-wavenet_amd"))
+
+import torch  # noqa: E402
+
+from gwn_amd import _lib  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    N, C, K, B = 207, 32, 3, 64
+    NP = (N + 31) // 32 * 32
+    W = (2 * K + 1) * C
+    torch.manual_seed(0)
+    sups = []
+    for _ in range(K):
+        s = torch.zeros(NP, NP, device=dev)
+        s[:N, :N] = torch.rand(N, N, device=dev) / N
+        sups.append(s)
+    supT = [s.t().contiguous() for s in sups]
+    arr = (ctypes.c_void_p * K)(*[s.data_ptr() for s in sups])
+    arrT = (ctypes.c_void_p * K)(*[s.data_ptr() for s in supT])
+    wm = torch.randn(C, W, device=dev) * 0.05
+    bm = torch.randn(C, device=dev)
+    seed = torch.zeros(1, device=dev, dtype=torch.int64)
+    st = _lib.stream()
+    for T in (12, 7, 1):
+        rows = T * B * N
+        h = torch.randn(rows, W, device=dev)
+        res = torch.randn(rows, C, device=dev)
+        z = torch.empty(rows, C, device=dev)
+        bnp = torch.empty(T * B * 3 * C, device=dev)
+        ga = _lib.GcnArgs(rows=rows, n=N, c=C, nsup=K, sup=ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)),
+                          ld_sup=NP, h=h.data_ptr(), ld_h=W, w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(),
+                          residual=res.data_ptr(), z=z.data_ptr(), seed_ptr=seed.data_ptr(), salt=0, drop_p=0.3,
+                          bn_partials=bnp.data_ptr())
+        dh = torch.randn(rows, C, device=dev)
+        dhc = torch.empty(rows, W, device=dev)
+        flop = T * B * (K * 2 * 2.0 * C * N * N + 2.0 * (2 * K + 1) * C * C * N)
+        for name, fn in (("fwd", lambda: _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)),
+                         ("bwd", lambda: _lib.load().gwn_gcn_fused_bwd_only(0))):
+            if name == "bwd":
+                continue
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 20
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = 1000.0 * e0.elapsed_time(e1) / reps
+            print("gcn %s T=%2d slices=%4d: %8.1f us  %6.1f TFLOP/s" % (name, T, T * B, us, flop / us / 1e6))
+        del dh, dhc
+
+
+if __name__ == "__main__":
+    main()
