@@ -183,6 +183,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, 
   };
 
   const int nkt = (kend > kbeg) ? (kend - kbeg + BK - 1) / BK : 0;
+  // ones column: the first column-tile's threads tid < BM also sum the staged A tile along k
+  const bool do_ones = p.ones_out != nullptr && blockIdx.y == 0;
+  float rsum = 0.0f;
   if (nkt > 0) {
     load(kbeg);
     store(0);
@@ -193,6 +196,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, 
     if (kt + 1 < nkt) load(kbeg + (kt + 1) * BK);
     const float* as = &As[buf][0];
     const float* bs = &Bs[buf][0];
+    if (do_ones && tid < BM) {
+#pragma unroll
+      for (int kk = 0; kk < BK; ++kk) rsum += as[kk * LDA + tid];
+    }
 #pragma unroll
     for (int kp = 0; kp < BK / 2; ++kp) {
       const int krow = 2 * kp + (lane >> 5);
@@ -211,48 +218,64 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, 
     __syncthreads();
   }
 
-  const unsigned long long seed = p.seed_ptr ? *p.seed_ptr : 0ull;
+  if (do_ones && tid < BM && m0 + tid < p.M) {
+    const float v = p.alpha * rsum;
+    if (p.ksplit > 1) p.part[(long)p.ksplit * p.M * p.N + (long)split * p.M + m0 + tid] = v;
+    else p.ones_out[m0 + tid] = v;
+  }
+  // epilogue: the mode branch is hoisted out of the (fully unrolled) accumulator walk
+  auto walk = [&](auto&& f) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + (wn * TN + j) * 32 + (lane & 31);
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + (wn * TN + j) * 32 + (lane & 31);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        float v = p.alpha * acc[i][j][r];
-        if (p.ksplit > 1) {
-          if (m < p.M && n < p.N) p.part[((long)split * p.M + m) * p.N + n] = v;
-        } else if (p.epi == EPI_GATE) {
-          // column n = 2c + g: g=0 filter (tanh), g=1 gate (sigmoid); partner lives in lane^1
-          v += (n < p.N) ? p.bias_n[n] : 0.0f;
-          const float other = __shfl_xor(v, 1);
-          if (((lane & 1) == 0) && m < p.M && n < p.N) {
-            const float f = tanhf(v), g = sigmoidf_(other);
-            const float xg = f * g;
-            const int c = n >> 1;
-            p.C[(long)m * p.ldc_m + c] = xg;
-            p.aux[(long)m * p.ld_aux + n] = f;
-            p.aux[(long)m * p.ld_aux + n + 1] = g;
-            if (p.aux2 && m >= p.aux2_row0) p.aux2[(long)(m - p.aux2_row0) * p.ld_aux2 + c] = xg;
-          }
-        } else if (m < p.M && n < p.N) {
-          epi_store(p, m, n, v, seed);
-        }
+        for (int r = 0; r < 16; ++r)
+          f(m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), n, p.alpha * acc[i][j][r]);
       }
-    }
+  };
+  if (p.ksplit > 1) {
+    float* part = p.part + (long)split * p.M * p.N;
+    walk([&](int m, int n, float v) {
+      if (m < p.M && n < p.N) part[(long)m * p.N + n] = v;
+    });
+  } else if (p.epi == EPI_GATE) {
+    // column n = 2c + g: g=0 filter (tanh), g=1 gate (sigmoid); partner lives in lane^1
+    walk([&](int m, int n, float v) {
+      v += (n < p.N) ? p.bias_n[n] : 0.0f;
+      const float other = __shfl_xor(v, 1);
+      if (((lane & 1) == 0) && m < p.M && n < p.N) {
+        const float f = tanhf(v), g = sigmoidf_(other);
+        const float xg = f * g;
+        const int c = n >> 1;
+        p.C[(long)m * p.ldc_m + c] = xg;
+        p.aux[(long)m * p.ld_aux + n] = f;
+        p.aux[(long)m * p.ld_aux + n + 1] = g;
+        if (p.aux2 && m >= p.aux2_row0) p.aux2[(long)(m - p.aux2_row0) * p.ld_aux2 + c] = xg;
+      }
+    });
+  } else {
+    const unsigned long long seed = p.seed_ptr ? *p.seed_ptr : 0ull;
+    walk([&](int m, int n, float v) {
+      if (m < p.M && n < p.N) epi_store(p, m, n, v, seed);
+    });
   }
 }
 
 // 8 outputs per block x 32 split lanes (lane l sums splits l, l+32, ...), then a fixed-order tree.
+// Outputs [M*N, M*N + M) are the ones column (partials stored after all [ksplit][M][N] tiles).
 __global__ void splitk_reduce_kernel(const GemmParams p) {
   __shared__ float sh[256];
-  const long total = (long)p.M * p.N;
+  const long mn = (long)p.M * p.N;
+  const long total = mn + (p.ones_out ? p.M : 0);
   const int ej = threadIdx.x & 7, lane = threadIdx.x >> 3;
   const long idx = blockIdx.x * 8L + ej;
   float v = 0.0f;
-  if (idx < total)
-    for (int s = lane; s < p.ksplit; s += 32) v += p.part[(long)s * total + idx];
+  if (idx < mn)
+    for (int s = lane; s < p.ksplit; s += 32) v += p.part[(long)s * mn + idx];
+  else if (idx < total)
+    for (int s = lane; s < p.ksplit; s += 32) v += p.part[(long)p.ksplit * mn + (long)s * p.M + (idx - mn)];
   sh[threadIdx.x] = v;
   __syncthreads();
 #pragma unroll
@@ -260,7 +283,9 @@ __global__ void splitk_reduce_kernel(const GemmParams p) {
     if (lane < w) sh[threadIdx.x] += sh[threadIdx.x + 8 * w];
     __syncthreads();
   }
-  if (lane == 0 && idx < total) {
+  if (lane == 0 && idx >= mn && idx < total) {
+    p.ones_out[idx - mn] = sh[ej];
+  } else if (lane == 0 && idx < mn) {
     const unsigned long long seed = p.seed_ptr ? *p.seed_ptr : 0ull;
     const int m = (int)(idx / p.N), n = (int)(idx - (long)m * p.N);
     epi_store(p, m, n, sh[ej], seed);
@@ -297,6 +322,7 @@ int gwn_gemm_launch(const GemmParams& pin, hipStream_t s) {
   GWN_REQUIRE(p.epi != EPI_GATE || (p.ksplit <= 1 && p.aux && p.bias_n && (p.N % 2) == 0),
               "gemm: gate epilogue needs aux, bias, even N and no split-K");
   GWN_REQUIRE(p.epi != EPI_MASKGRAD || p.mask, "gemm: mask-grad epilogue needs a mask");
+  GWN_REQUIRE(p.ones_out == nullptr || p.epi != EPI_GATE, "gemm: ones column is not combined with the gate epilogue");
   if (p.ksplit < 1) p.ksplit = 1;
   if (p.ksplit > 1) {
     GWN_REQUIRE(p.part != nullptr, "gemm: split-K needs a partial buffer");
@@ -329,7 +355,7 @@ int gwn_gemm_launch(const GemmParams& pin, hipStream_t s) {
   else if (p.M >= 128) rc = launch_cfg<2, 2, 2, 2>(p, akc, bkc, va, vb, s);               // 128 x 128
   else rc = launch_cfg<2, 2, 1, 1>(p, akc, bkc, va, vb, s);                               // 64 x 64
   if (rc != GWN_OK || p.ksplit <= 1) return rc;
-  const long total = (long)p.M * p.N;
+  const long total = (long)p.M * p.N + (p.ones_out ? p.M : 0);
   splitk_reduce_kernel<<<(unsigned)((total + 7) / 8), 256, 0, s>>>(p);
   GWN_CHECK_LAUNCH();
   return GWN_OK;

@@ -195,6 +195,36 @@ __global__ void colsum_partial_kernel(const float* a, long lda, const float* b, 
   }
 }
 
+// BatchNorm backward statistics in one pass: partial[blk][j] = sum dy, partial[blk][c + j] =
+// sum dy * xhat over the block's row chunk (c | 256)
+__global__ void bn_bwd_partial_kernel(const float* dy, const float* z, const float* mean, const float* rstd,
+                                      long rows, int c, float* partial) {
+  __shared__ float sh[2][256];
+  const long chunk = (rows + gridDim.x - 1) / gridDim.x;
+  const long r0 = blockIdx.x * chunk;
+  const long r1 = (r0 + chunk < rows) ? r0 + chunk : rows;
+  const int lanes = 256 / c;
+  const int col = threadIdx.x % c, rl = threadIdx.x / c;
+  float s0 = 0.0f, s1 = 0.0f;
+  if (rl < lanes) {
+    const float mu = mean[col], rs = rstd[col];
+    for (long r = r0 + rl; r < r1; r += lanes) {
+      const float g = dy[r * c + col];
+      s0 += g;
+      s1 += g * ((z[r * c + col] - mu) * rs);
+    }
+  }
+  sh[0][threadIdx.x] = (rl < lanes) ? s0 : 0.0f;
+  sh[1][threadIdx.x] = (rl < lanes) ? s1 : 0.0f;
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * c; t += 256) {
+    const int h = t / c, j = t - h * c;
+    float s = 0.0f;
+    for (int i = 0; i < lanes; ++i) s += sh[h][i * c + j];
+    partial[(long)blockIdx.x * 2 * c + t] = s;
+  }
+}
+
 // 8 columns per block x 32 partial lanes, then a fixed-order tree over the lanes.
 __global__ void colsum_final_kernel(const float* partial, int nparts, int ncol, float* out,
                                     int accumulate) {
@@ -318,11 +348,16 @@ __global__ void bn_bwd_apply_kernel(const float* dy, const float* z, long rows, 
                                     const float* gamma, const float* mean, const float* rstd,
                                     const float* sums, float* dres, int res_row0, float* dh,
                                     const unsigned long long* seed_ptr, unsigned long long salt,
-                                    float drop_p) {
+                                    float drop_p, float* dgamma, float* dbeta) {
   const long total = rows * c;
   const unsigned long long seed = seed_ptr ? *seed_ptr : 0ull;
   const float inv_n = 1.0f / (float)rows;
   const long zero_total = (long)res_row0 * c;
+  if (blockIdx.x == 0)
+    for (int j = threadIdx.x; j < c; j += blockDim.x) {
+      if (dbeta) dbeta[j] = sums[j];
+      if (dgamma) dgamma[j] = sums[c + j];
+    }
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total + zero_total;
        idx += (long)gridDim.x * blockDim.x) {
     if (idx >= total) {
@@ -574,7 +609,9 @@ int gwn_gemm(const gwn_gemm_desc* d, hipStream_t s) {
   return gwn_gemm_launch(*d, s);
 }
 
-long gwn_gemm_workspace_floats(int M, int N, int ksplit) { return (long)M * N * (ksplit > 1 ? ksplit : 0); }
+long gwn_gemm_workspace_floats(int M, int N, int ksplit) {
+  return ((long)M * N + M) * (ksplit > 1 ? ksplit : 0);  // + M: the optional ones column
+}
 
 // ---------------------------------------------------------------------------------------------
 int gwn_nconv(const float* A, int lda, int transpose_a, const float* x, long ldx, float* y, long ldy,
@@ -677,9 +714,7 @@ static int tcn_w_ksplit(int rows, int c) { return pick_ksplit(2 * c, 2 * c, rows
 
 long gwn_gated_tcn_bwd_workspace_floats(int t_in, int P, int c, int dilation) {
   const int rows = (t_in - dilation) * P;
-  const long wk = (long)tcn_w_ksplit(rows, c) * 4 * c * c;
-  const long cs = gwn_colsum_workspace_floats(rows, 2 * c);
-  return wk > cs ? wk : cs;
+  return gwn_gemm_workspace_floats(2 * c, 2 * c, tcn_w_ksplit(rows, c));
 }
 
 int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
@@ -689,17 +724,16 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
   gate_bwd_kernel<<<grid_for(rows * c), 256, 0, s>>>(a->dxg, a->ld_dxg, a->dskip, a->ld_dskip,
                                                      a->skip_row0, a->fg, rows, c, a->dfg);
   GWN_CHECK_LAUNCH();
-  // dW_fg[j][tap*c + ci] = sum_r dfg[r][j] * x[r + tap*d*P][ci]
+  // dW_fg[j][tap*c + ci] = sum_r dfg[r][j] * x[r + tap*d*P][ci];  db_fg[j] = sum_r dfg[r][j]
   gwn_gemm_desc d = gemm_zero();
   d.A = a->dfg; d.lda_m = 1; d.lda_k = 2 * c;
   d.B = a->x; d.ldb_k = c; d.ldb_n = 1; d.b_nin = c; d.b_no_stride = (long)a->dilation * P * c;
   d.C = a->dw_fg; d.ldc_m = 2 * c; d.ldc_n = 1;
+  d.ones_out = a->db_fg;
   d.M = 2 * c; d.N = 2 * c; d.K = (int)rows;
   d.ksplit = tcn_w_ksplit((int)rows, c);
   d.part = a->workspace;
   int rc = gwn_gemm_launch(d, s);
-  if (rc) return rc;
-  rc = gwn_colsum(a->dfg, (int)rows, 2 * c, 2 * c, a->db_fg, 0, a->workspace, s);
   if (rc) return rc;
   // dx[r'][ci] (+)= sum_tap sum_j dfg[r' - tap*d*P][j] * Wfg[j][tap*c + ci]
   d = gemm_zero();
@@ -746,29 +780,25 @@ static int gcn_w_ksplit(int rows, int c, int width) { return pick_ksplit(c, widt
 
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup) {
   const int width = (2 * nsup + 1) * c;
-  long w = (long)gcn_w_ksplit(rows, c, width) * c * width;
+  long w = gwn_gemm_workspace_floats(c, width, gcn_w_ksplit(rows, c, width));
   const long g = gwn_nconv_adj_grad_workspace_floats(n, c, rows / n);
-  const long cs = gwn_colsum_workspace_floats(rows, c);
-  if (g > w) w = g;
-  if (cs > w) w = cs;
-  return w;
+  return g > w ? g : w;
 }
 
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_bwd: rows must be slices*n");
   const int c = a->c, n = a->n, slices = a->rows / n;
   const int width = (2 * a->nsup + 1) * c;
-  // dW_mlp[j][k] = sum_r dh[r][j] h[r][k]
+  // dW_mlp[j][k] = sum_r dh[r][j] h[r][k];  db_mlp[j] = sum_r dh[r][j] (ones column)
   gwn_gemm_desc d = gemm_zero();
   d.A = a->dh; d.lda_m = 1; d.lda_k = c;
   d.B = a->h; d.ldb_k = a->ld_h; d.ldb_n = 1;
   d.C = a->dw_mlp; d.ldc_m = width; d.ldc_n = 1;
+  d.ones_out = a->db_mlp;
   d.M = c; d.N = width; d.K = a->rows;
   d.ksplit = gcn_w_ksplit(a->rows, c, width);
   d.part = a->workspace;
   int rc = gwn_gemm_launch(d, s);
-  if (rc) return rc;
-  rc = gwn_colsum(a->dh, a->rows, c, c, a->db_mlp, 0, a->workspace, s);
   if (rc) return rc;
   if (a->sup_t && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup)) {
     // fused: dxg -> dhcat piece 0; for the adaptive support dx1 -> piece 1, dx2 -> piece 2
@@ -864,24 +894,17 @@ int gwn_batchnorm_bwd(const float* dy, const float* z, int rows, int c, const fl
                       const float* save_mean, const float* save_rstd, float* dgamma, float* dbeta,
                       float* dres, int res_row0, float* dh, const unsigned long long* seed_ptr,
                       unsigned long long salt, float drop_p, float* ws, hipStream_t s) {
-  GWN_REQUIRE(rows > 0 && c > 0 && c <= 256, "batchnorm_bwd: bad shape");
+  GWN_REQUIRE(rows > 0 && c > 0 && c <= 256 && 256 % c == 0, "batchnorm_bwd: c must divide 256");
   float* part = ws;
   float* sums = ws + (long)RED_BLOCKS * 3 * c;  // [2][c]: sum dy, sum dy*xhat
-  colsum_partial_kernel<0><<<RED_BLOCKS, 256, 0, s>>>(dy, c, nullptr, 0, nullptr, nullptr, rows, c, part);
+  bn_bwd_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(dy, z, save_mean, save_rstd, rows, c, part);
   GWN_CHECK_LAUNCH();
-  colsum_final_kernel<<<(c + 7) / 8, 256, 0, s>>>(part, RED_BLOCKS, c, sums, 0);
+  colsum_final_kernel<<<(2 * c + 7) / 8, 256, 0, s>>>(part, RED_BLOCKS, 2 * c, sums, 0);
   GWN_CHECK_LAUNCH();
-  colsum_partial_kernel<1><<<RED_BLOCKS, 256, 0, s>>>(dy, c, z, c, save_mean, save_rstd, rows, c, part);
-  GWN_CHECK_LAUNCH();
-  colsum_final_kernel<<<(c + 7) / 8, 256, 0, s>>>(part, RED_BLOCKS, c, sums + c, 0);
-  GWN_CHECK_LAUNCH();
-  if (dbeta && hipMemcpyAsync(dbeta, sums, sizeof(float) * c, hipMemcpyDeviceToDevice, s) != hipSuccess)
-    return gwn_set_error(GWN_ERR_HIP, "batchnorm_bwd: dbeta copy");
-  if (dgamma && hipMemcpyAsync(dgamma, sums + c, sizeof(float) * c, hipMemcpyDeviceToDevice, s) != hipSuccess)
-    return gwn_set_error(GWN_ERR_HIP, "batchnorm_bwd: dgamma copy");
   const long total = (long)rows * c + (long)res_row0 * c;
   bn_bwd_apply_kernel<<<grid_for(total), 256, 0, s>>>(dy, z, rows, c, gamma, save_mean, save_rstd, sums,
-                                                      dres, res_row0, dh, seed_ptr, salt, drop_p);
+                                                      dres, res_row0, dh, seed_ptr, salt, drop_p, dgamma,
+                                                      dbeta);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

@@ -33,7 +33,7 @@ class GemmDesc(ctypes.Structure):
         ("aux", c_void_p), ("ld_aux", c_long),
         ("aux2", c_void_p), ("ld_aux2", c_long), ("aux2_row0", c_int),
         ("seed_ptr", c_void_p), ("seed_salt", c_u64), ("drop_p", c_float),
-        ("ksplit", c_int), ("kchunk", c_int), ("part", c_void_p),
+        ("ksplit", c_int), ("kchunk", c_int), ("part", c_void_p), ("ones_out", c_void_p),
     ]
 
 

@@ -150,7 +150,8 @@ class trainer():
     def _step(self, input, real_val, training):
         """Fused step; returns the device metrics tensor [mae, mape, rmse]."""
         model = self.model
-        model.train(training)
+        if model.training != training:
+            model.train(training)
         model.executor()
         if not training:
             return self._phase_grads(input, real_val, False)
@@ -250,15 +251,22 @@ class trainer():
         return v[0], v[1], v[2]
 
     def _expose_grads(self):
-        """Make ``p.grad`` views of the flat gradient buffer (as after the reference's step)."""
+        """Make ``p.grad`` views of the flat gradient buffer (as after the reference's step).
+        The (param, view) pairs are built once per (layout, gradient buffer)."""
         lay = self.model._executor.layout
-        active = set(lay.active)
-        for name, p in self.model.named_parameters():
-            if name in active:
-                off, shape = lay.flat_off[name]
-                g = self.optimizer.grad_flat[off:off + p.numel()].view(shape)
-                if p.grad is None or p.grad.data_ptr() != g.data_ptr():
-                    p.grad = g
+        gf = self.optimizer.grad_flat
+        key = (id(lay), gf.data_ptr())
+        if getattr(self, "_grad_views_key", None) != key:
+            active = set(lay.active)
+            views = []
+            for name, p in self.model.named_parameters():
+                if name in active:
+                    off, shape = lay.flat_off[name]
+                    views.append((p, gf[off:off + p.numel()].view(shape)))
+            self._grad_views, self._grad_views_key = views, key
+        for p, g in self._grad_views:
+            if p.grad is not g:
+                p.grad = g
 
     # ------------------------------------------------------------------------------------------
     # generic path for a user-supplied loss: the model is still one libgwn autograd node

@@ -422,18 +422,15 @@ class Executor:
         dout = dout.contiguous()
         lib.call("gwn_from_nchw", ptr(dout), B, O, N, tf, ptr(sc["dy"]), st)
         # end_conv_2
-        wgrad(sc["dy"], O, acts.e1, E, rows_f, self.gk("e2_w"), ws)
-        lib.call("gwn_colsum", ptr(sc["dy"]), rows_f, O, O, ptr(self.gk("e2_b")), 0, ptr(ws), st)
+        wgrad(sc["dy"], O, acts.e1, E, rows_f, self.gk("e2_w"), ws, self.gk("e2_b"))
         gemm(sc["dy"], O, 1, self.pk("e2_w"), E, 1, sc["de1"], E, 1, M=rows_f, N=E, K=O,
              epi=2, mask=acts.e1, ldmask=E)
         # end_conv_1
-        wgrad(sc["de1"], E, acts.skr, S, rows_f, self.gk("e1_w"), ws)
-        lib.call("gwn_colsum", ptr(sc["de1"]), rows_f, E, E, ptr(self.gk("e1_b")), 0, ptr(ws), st)
+        wgrad(sc["de1"], E, acts.skr, S, rows_f, self.gk("e1_w"), ws, self.gk("e1_b"))
         gemm(sc["de1"], E, 1, self.pk("e1_w"), S, 1, sc["dsk"], S, 1, M=rows_f, N=S, K=E,
              epi=2, mask=acts.skr, ldmask=S)
         # skip convs
-        wgrad(sc["dsk"], S, acts.skipcat, L * C, rows_f, self.gk("skip_w"), ws)
-        lib.call("gwn_colsum", ptr(sc["dsk"]), rows_f, S, S, ptr(self.gk("skip_bsum")), 0, ptr(ws), st)
+        wgrad(sc["dsk"], S, acts.skipcat, L * C, rows_f, self.gk("skip_w"), ws, self.gk("skip_bsum"))
         gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * C, 1, sc["dskipcat"], L * C, 1, M=rows_f, N=L * C, K=S)
         # layers in reverse
         dnext = None
@@ -475,8 +472,7 @@ class Executor:
             dnext = dx
         # start conv
         rows0 = ts[0] * P
-        wgrad(dnext, C, acts.xin, cfg.Cin, rows0, self.gk("start_w"), ws)
-        lib.call("gwn_colsum", ptr(dnext), rows0, C, C, ptr(self.gk("start_b")), 0, ptr(ws), st)
+        wgrad(dnext, C, acts.xin, cfg.Cin, rows0, self.gk("start_w"), ws, self.gk("start_b"))
         if cfg.use_gcn and cfg.adaptive:
             lib.call("gwn_adaptive_adj_bwd", ptr(self.pk("nv1")), ptr(self.pk("nv2")), ptr(acts.adp),
                      ptr(sc["dadp"]), N, 10, cfg.NP, ptr(self.gk("nv1")), ptr(self.gk("nv2")), ptr(ws), st)
@@ -494,7 +490,7 @@ def _ksplit(M, N, K):
 
 
 def gemm(A, lda_m, lda_k, B, ldb_k, ldb_n, Cout, ldc_m, ldc_n, M, N, K, bias=None, relu=0, epi=0,
-         mask=None, ldmask=0, C0=None, ldc0=0, beta=1.0, ksplit=1, part=None):
+         mask=None, ldmask=0, C0=None, ldc0=0, beta=1.0, ksplit=1, part=None, ones_out=None):
     d = _lib.GemmDesc()
     d.A, d.lda_m, d.lda_k = ptr(A), lda_m, lda_k
     d.B, d.ldb_k, d.ldb_n = ptr(B), ldb_k, ldb_n
@@ -510,10 +506,12 @@ def gemm(A, lda_m, lda_k, B, ldb_k, ldb_n, Cout, ldc_m, ldc_n, M, N, K, bias=Non
         d.C0, d.ldc0_m, d.ldc0_n = ptr(C0), ldc0, 1
     d.ksplit = ksplit
     d.part = ptr(part)
+    d.ones_out = ptr(ones_out)
     _lib.call("gwn_gemm", ctypes.byref(d), _lib.stream())
 
 
-def wgrad(dY, J, X, Kc, rows, out, ws):
-    """out[j][k] = sum_r dY[r][j] * X[r][k]   (1x1 conv weight gradient, split over rows)."""
+def wgrad(dY, J, X, Kc, rows, out, ws, bias_out=None):
+    """out[j][k] = sum_r dY[r][j] * X[r][k]   (1x1 conv weight gradient, split over rows);
+    bias_out[j] = sum_r dY[r][j] from the same launch (the GEMM's ones column)."""
     ks = _ksplit(J, Kc, rows)
-    gemm(dY, 1, J, X, Kc, 1, out, Kc, 1, M=J, N=Kc, K=rows, ksplit=ks, part=ws)
+    gemm(dY, 1, J, X, Kc, 1, out, Kc, 1, M=J, N=Kc, K=rows, ksplit=ks, part=ws, ones_out=bias_out)

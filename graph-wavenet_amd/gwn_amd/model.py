@@ -187,10 +187,13 @@ class gwnet(nn.Module):
                 m.num_batches_tracked = nbt[i]
         self._flat = flat
         self._nbt = nbt
+        self._params_cache = params
         self._flat_ptrs = tuple(p.data_ptr() for p in params)
 
     def _ensure_flat(self):
-        params = list(self.parameters())
+        # the Parameter objects are fixed at construction (the reference never re-registers
+        # them); only their storage can move (.to(), .data = ...), which the pointer check sees
+        params = self._params_cache
         ptrs = tuple(p.data_ptr() for p in params)
         if ptrs != self._flat_ptrs or params[0].device != self._flat.device:
             if any(p.dtype != F32 for p in params):

@@ -60,6 +60,10 @@ typedef struct gwn_gemm_desc {
   float* aux2; long ld_aux2; int aux2_row0;
   const unsigned long long* seed_ptr; unsigned long long seed_salt; float drop_p;
   int ksplit, kchunk; float* part;
+  /* optional: ones_out[m] = alpha * sum_k A(m,k) (B extended by a column of ones).  In a weight
+   * gradient dW = dY^T X this is the bias gradient sum_r dY[r][m], for free.  With split-K the
+   * partial buffer holds ksplit*(M*N + M) floats (gwn_gemm_workspace_floats covers it). */
+  float* ones_out;
 } gwn_gemm_desc;
 
 int gwn_gemm(const gwn_gemm_desc* desc, hipStream_t stream);

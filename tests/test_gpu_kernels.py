@@ -105,6 +105,23 @@ def test_gemm_splitk_bias_relu_residual(gpu):
     assert rel_err(C.cpu().numpy(), ref.cpu().numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K,ks", [(64, 224, 13248, 12), (32, 32, 700, 1), (300, 40, 2000, 4), (20, 96, 37, 1)])
+def test_gemm_ones_column_bias_grad(gpu, M, N, K, ks):
+    """Weight-gradient form dW = dY^T X with the bias gradient sum_r dY[r][m] from the ones column."""
+    from gwn_amd import _lib
+    torch.manual_seed(11)
+    dY = torch.randn(K, M, device=gpu)
+    X = torch.randn(K, N, device=gpu)
+    ws = torch.empty(max(1, _lib.load().gwn_gemm_workspace_floats(M, N, ks)), device=gpu)
+    dW = torch.empty(M, N, device=gpu)
+    db = torch.full((M,), float("nan"), device=gpu)
+    _gemm(A=dY, lda_m=1, lda_k=M, B=X, ldb_k=N, ldb_n=1, C=dW, ldc_m=N, ldc_n=1, M=M, N=N, K=K, ksplit=ks,
+          part=ws, ones_out=db, alpha=0.5)
+    torch.cuda.synchronize()
+    assert rel_err(dW.cpu().numpy(), 0.5 * (dY.double().t() @ X.double()).cpu().numpy()) < 1e-5
+    assert rel_err(db.cpu().numpy(), 0.5 * dY.double().sum(0).cpu().numpy()) < 1e-5
+
+
 def test_gemm_two_level_taps_and_slices(gpu):
     """Dilated two-tap rows (a_kin / a_row_shift / a_rows) and strided slices (b_nin / c_nin)."""
     P, T, Cc, d = 10, 6, 16, 2

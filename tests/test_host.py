@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
         assert s in _lib.EXPORTED, s
     assert lib.gwn_version() == 1
     assert isinstance(lib.gwn_last_error(), bytes)
-    assert ctypes.sizeof(_lib.GemmDesc) == 304
+    assert ctypes.sizeof(_lib.GemmDesc) == 312
 
 
 def _sup_tensors(g):
