@@ -46,8 +46,16 @@ struct FusedBwd {
 
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
+#ifndef GWN_EXP
+#define GWN_EXP 0  // kernel experiments (timing only, wrong results): 1 no G loads, 2 no x1/x2 stores,
+#endif             // 4 no mlp, 8 no epilogue
+
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+#if GWN_EXP & 1
+  return (float)(voff + soff) * 1e-9f;
+#else
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+#endif
 }
 
 struct GBatch {
@@ -93,7 +101,7 @@ __device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int 
   auto lds_batch = [&](int kb, float* av) {
     const float* bp = buf + (32 * kb + half) * LDR + col;
 #pragma unroll
-    for (int j = 0; j < KB; ++j) av[j] = bp[2 * j * LDR];
+    for (int j = 0; j < KB; ++j) av[j] = (GWN_EXP & 16) ? ga[j] * 0.5f : bp[2 * j * LDR];
   };
   auto g_batch = [&](int kb, float* g) {
 #pragma unroll
@@ -211,24 +219,34 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
     const float* G = a.sup[k];
     f32x16 d = diffuse(xs, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
     g0 = g_first(G, a.ld_sup, nkb, w0, lane);  // hop 2 re-reads the same support
-    GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
-    hacc = mlp_from_acc(wf, d, hacc);
-    __syncthreads();
+    if (!(GWN_EXP & 4)) {
+      GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
+      hacc = mlp_from_acc(wf, d, hacc);
+    }
+    if (!(GWN_EXP & 32)) __syncthreads();
     acc_to_lds(ys, d, w0, lane);
-    __syncthreads();
-    lds_to_global(ys, (float*)hs + (1 + 2 * k) * CH, a.ld_h, n);
+    if (!(GWN_EXP & 32)) __syncthreads();
+    if (!(GWN_EXP & 2)) lds_to_global(ys, (float*)hs + (1 + 2 * k) * CH, a.ld_h, n);
     d = diffuse(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
     if (k + 1 < a.nsup) g0 = g_first(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
-    wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
-    hacc = mlp_from_acc(wf, d, hacc);
-    __syncthreads();
+    if (!(GWN_EXP & 4)) {
+      GBatch wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
+      hacc = mlp_from_acc(wf, d, hacc);
+    } else {
+      hacc += d;
+    }
+    if (!(GWN_EXP & 32)) __syncthreads();
     acc_to_lds(ys, d, w0, lane);
-    __syncthreads();
-    lds_to_global(ys, (float*)hs + (2 + 2 * k) * CH, a.ld_h, n);
+    if (!(GWN_EXP & 32)) __syncthreads();
+    if (!(GWN_EXP & 2)) lds_to_global(ys, (float*)hs + (2 + 2 * k) * CH, a.ld_h, n);
   }
   __syncthreads();
   acc_to_lds(ys, hacc, w0, lane);
   __syncthreads();
+  if (GWN_EXP & 8) {
+    lds_to_global(ys, a.z + row0 * CH, CH, n);
+    return;
+  }
   // epilogue: bias, dropout (same counter hash as the GEMM epilogue: index m*32 + c), residual
   const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
   const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;

@@ -11,7 +11,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgwn.so")
+# GWN_LIB: alternative build of the same library (kernel experiments, tools/); default in-tree
+LIB_PATH = os.environ.get("GWN_LIB") or os.path.join(_HERE, "libgwn.so")
 
 c_int, c_long, c_float, c_void_p, c_u64 = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
                                           ctypes.c_void_p, ctypes.c_ulonglong)

@@ -1,5 +1,8 @@
-"""Micro-benchmark of the fused diffusion GCN kernels (gwn_gcn_fwd / gwn_gcn_bwd) at METR-LA
-layer shapes, timed with HIP events on the launch stream.  Usage: python tools/bench_gcn.py"""
+"""Micro-benchmark of the diffusion GCN layer (gwn_gcn_fwd / gwn_gcn_bwd through the C-ABI) at
+METR-LA layer shapes, timed with HIP events on the launch stream.  The backward includes the
+mlp weight gradient and the adaptive-support grams (separate kernels in a kernel trace).
+Usage: python tools/bench_gcn.py [--reps R] [--ts 12,7,1]"""
+import argparse
 import ctypes
 import os
 import sys
@@ -13,8 +16,13 @@ from gwn_amd import _lib  # noqa: E402
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--ts", default="12,7,1")
+    ap.add_argument("--nodes", type=int, default=207)
+    args = ap.parse_args()
     dev = torch.device("cuda:0")
-    N, C, K, B = 207, 32, 3, 64
+    N, C, K, B = args.nodes, 32, 3, 64
     NP = (N + 31) // 32 * 32
     W = (2 * K + 1) * C
     torch.manual_seed(0)
@@ -30,7 +38,8 @@ def main():
     bm = torch.randn(C, device=dev)
     seed = torch.zeros(1, device=dev, dtype=torch.int64)
     st = _lib.stream()
-    for T in (12, 7, 1):
+    lib = _lib.load()
+    for T in [int(t) for t in args.ts.split(",")]:
         rows = T * B * N
         h = torch.randn(rows, W, device=dev)
         res = torch.randn(rows, C, device=dev)
@@ -42,22 +51,29 @@ def main():
                           bn_partials=bnp.data_ptr())
         dh = torch.randn(rows, C, device=dev)
         dhc = torch.empty(rows, W, device=dev)
+        dwm = torch.empty(C, W, device=dev)
+        dbm = torch.empty(C, device=dev)
+        dadp = torch.zeros(NP, NP, device=dev)
+        ws = torch.empty(lib.gwn_gcn_bwd_workspace_floats(rows, N, C, K) + 16, device=dev)
+        gb = _lib.GcnBwdArgs(rows=rows, n=N, c=C, nsup=K, sup=ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)),
+                             ld_sup=NP, h=h.data_ptr(), ld_h=W, w_mlp=wm.data_ptr(), dh=dh.data_ptr(),
+                             dhcat=dhc.data_ptr(), ld_dhcat=W, dw_mlp=dwm.data_ptr(), db_mlp=dbm.data_ptr(),
+                             adp_index=K - 1, dadp=dadp.data_ptr(), accumulate_dadp=0, workspace=ws.data_ptr(),
+                             sup_t=ctypes.cast(arrT, ctypes.POINTER(ctypes.c_void_p)))
         flop = T * B * (K * 2 * 2.0 * C * N * N + 2.0 * (2 * K + 1) * C * C * N)
         for name, fn in (("fwd", lambda: _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)),
-                         ("bwd", lambda: _lib.load().gwn_gcn_fused_bwd_only(0))):
-            if name == "bwd":
-                continue
+                         ("bwd", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gb), st))):
             for _ in range(3):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            reps = 20
             e0.record()
-            for _ in range(reps):
+            for _ in range(args.reps):
                 fn()
             e1.record()
             torch.cuda.synchronize()
-            us = 1000.0 * e0.elapsed_time(e1) / reps
-            print("gcn %s T=%2d slices=%4d: %8.1f us  %6.1f TFLOP/s" % (name, T, T * B, us, flop / us / 1e6))
+            us = 1000.0 * e0.elapsed_time(e1) / args.reps
+            print("gcn %s T=%2d slices=%4d: %8.1f us  %6.1f TFLOP/s (fwd-equivalent flops)"
+                  % (name, T, T * B, us, flop / us / 1e6), flush=True)
         del dh, dhc
 
 
