@@ -44,6 +44,10 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
 int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT, float* dxg, long ld_dxg,
                              float* t1, float* t2, long ld_t, hipStream_t s);
 
+// Weight-stationary row GEMMs of the gated TCN (rowgemm.hip), c = 32
+int gwn_rowgemm_tcn_fwd(const gwn_tcn_args* a, hipStream_t s);
+int gwn_rowgemm_tcn_bwd_data(const gwn_tcn_bwd_args* a, hipStream_t s);
+
 // Deterministic counter-based dropout RNG (splitmix64 finaliser), identical in every kernel
 // that applies or differentiates the same mask.
 __host__ __device__ inline float gwn_uniform(unsigned long long seed, unsigned long long salt,

@@ -11,6 +11,8 @@ thread_local char g_err[512] = "";
 
 constexpr int RED_BLOCKS = 512;  // partial-reduction blocks (fixed -> fixed summation order)
 
+inline bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
+
 gwn_gemm_desc gemm_zero() {
   gwn_gemm_desc d;
   memset(&d, 0, sizeof(d));
@@ -697,6 +699,7 @@ int gwn_gated_tcn_fwd(const gwn_tcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->t_in > a->dilation && a->c > 0 && a->P > 0, "gated_tcn_fwd: bad shape");
   GWN_REQUIRE(a->c % 16 == 0, "gated_tcn_fwd: channels must be a multiple of 16");
   const int c = a->c, P = a->P, t_out = a->t_in - a->dilation;
+  if (c == 32 && aligned16(a->x) && aligned16(a->fg)) return gwn_rowgemm_tcn_fwd(a, s);
   gwn_gemm_desc d = gemm_zero();
   d.A = a->x; d.lda_m = c; d.lda_k = 1; d.a_kin = c; d.a_row_shift = a->dilation * P;
   d.a_rows = a->t_in * P;
@@ -736,6 +739,7 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
   int rc = gwn_gemm_launch(d, s);
   if (rc) return rc;
   // dx[r'][ci] (+)= sum_tap sum_j dfg[r' - tap*d*P][j] * Wfg[j][tap*c + ci]
+  if (c == 32 && aligned16(a->dfg) && aligned16(a->dx)) return gwn_rowgemm_tcn_bwd_data(a, s);
   d = gemm_zero();
   d.A = a->dfg; d.lda_m = 2 * c; d.lda_k = 1; d.a_kin = 2 * c; d.a_row_shift = -a->dilation * P;
   d.a_rows = (int)rows;
