@@ -1,0 +1,156 @@
+// Adaptive-support gradient ("gram"): the backward of nconv w.r.t. the support,
+//     dA[v][w] (+)= sum_p sum_s sum_c X_p[s*n + v][c] * T_p[s*n + w][c]      (p < npairs <= 2)
+// over all slices s of a layer (model.py:12-14 differentiated w.r.t. A; two pairs per layer for
+// order 2: (xg, dx1) and (x1, dx2)).  M = N = n (<= 224 here), K = slices * 32 per pair.
+//
+// One wave per (32x32 output tile, slice range).  The contraction is laid onto
+// v_mfma_f32_32x32x2_f32 PERMUTED: step j takes channel c = 16h + j in lane half h, so lane (i, h)
+// needs the 16 contiguous floats X[s*n + 32*vt + i][16h ..] (A) and T[s*n + 32*wt + i][16h ..]
+// (B) — four 16-B buffer loads each, nodes >= n reading zeros (out-of-range offset).  No LDS, no
+// barriers; the next slice's fragments are in flight while the current slice's MFMAs run.
+// Waves of one slice range are placed on one XCD (blocks round-robin over the 8 XCDs), so the
+// 7x re-reads of each row block hit that XCD's L2.  Partials [nsplit][npad][npad] are summed in
+// a fixed order by a second kernel (deterministic).
+#include "gwn_internal.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int OOR = 0x7ffffff0;
+constexpr int NXCD = 8;
+
+struct Gram {
+  const float* X[2]; const float* T[2]; int npairs;  // pair 1 used iff npairs == 2
+  long ldx, ldt;
+  int n, nt, slices, nsplit;  // nt = ceil(n / 32)
+  float* part;                // [nsplit][32 nt][32 nt]
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+template <int NP>
+__global__ __launch_bounds__(64) void gram_kernel(const Gram g) {
+  const int lane = threadIdx.x, half = lane >> 5, col = lane & 31;
+  const int ntile = g.nt * g.nt;
+  // XCD-aware placement: block b runs on XCD b % 8; keep every (tile, split) of one split on one XCD
+  const int b = blockIdx.x, xcd = b % NXCD, j = b / NXCD;
+  const int tile = j % ntile, split = (j / ntile) * NXCD + xcd;
+  if (split >= g.nsplit) return;
+  const int vt = tile / g.nt, wt = tile % g.nt;
+  const int s0 = (int)((long)g.slices * split / g.nsplit), s1 = (int)((long)g.slices * (split + 1) / g.nsplit);
+
+  __amdgpu_buffer_rsrc_t rx[NP], rt[NP];
+  const long rows = (long)g.slices * g.n;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    rx[p] = rsrc(g.X[p], rows * g.ldx * 4);
+    rt[p] = rsrc(g.T[p], rows * g.ldt * 4);
+  }
+  const int v = 32 * vt + col, w = 32 * wt + col;
+  auto load = [&](int s, float4* fa, float4* fb) {
+    const bool ok = s < s1;
+    const long rv = (long)s * g.n + v, rw = (long)s * g.n + w;
+    const int ox = (ok && v < g.n) ? (int)((rv * g.ldx + 16 * half) * 4) : OOR;
+    const int ot = (ok && w < g.n) ? (int)((rw * g.ldt + 16 * half) * 4) : OOR;
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        fa[4 * p + q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx[p], ox, 16 * q, 0));
+        fb[4 * p + q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt[p], ot, 16 * q, 0));
+      }
+  };
+
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  float4 fa[4 * NP], fb[4 * NP];
+  load(s0, fa, fb);
+  for (int s = s0; s < s1; ++s) {
+    float4 na[4 * NP], nb[4 * NP];
+    load(s + 1, na, nb);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4 * NP; ++q) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[q].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, fb[q].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, fb[q].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, fb[q].w, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4 * NP; ++q) { fa[q] = na[q]; fb[q] = nb[q]; }
+  }
+  // D[v][w]: col = lane&31 -> w, rows -> v
+  const int np = 32 * g.nt;
+  float* out = g.part + (long)split * np * np + (long)(32 * vt) * np + 32 * wt + col;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) out[(long)crow(r, half) * np] = acc[r];
+}
+
+// dA[v][w] (+)= sum_split part[split][v][w], fixed order
+__global__ void gram_reduce_kernel(const float* part, int nsplit, int n, int np, float* dA, int ld,
+                                   int accumulate) {
+  const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (idx >= (long)n * n) return;
+  const int v = (int)(idx / n), w = (int)(idx - (long)v * n);
+  const float* p = part + (long)v * np + w;
+  const long st = (long)np * np;
+  // eight independent chains (loads in flight together), merged in a fixed order
+  float a[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  int k = 0;
+  for (; k + 8 <= nsplit; k += 8)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += p[(k + u) * st];
+  for (; k < nsplit; ++k) a[k & 7] += p[k * st];
+  const float s = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  float* o = dA + (long)v * ld + w;
+  *o = accumulate ? *o + s : s;
+}
+
+int gram_nsplit(int n, int slices) {
+  const int nt = (n + 31) / 32;
+  // ~4096 waves over 256 CUs (3-4 per SIMD); a multiple of the XCD count; >= 1 slice per split
+  int ns = 4096 / (nt * nt);
+  ns = (ns / NXCD) * NXCD;
+  if (ns < NXCD) ns = NXCD;
+  if (ns > slices) ns = slices;
+  return ns < 1 ? 1 : ns;
+}
+
+}  // namespace
+
+long gwn_gram_workspace_floats(int n, int slices) {
+  const int np = 32 * ((n + 31) / 32);
+  return (long)gram_nsplit(n, slices) * np * np;
+}
+
+// dA (+)= sum over slices of X1^T T1 (+ X2^T T2); c = 32 channels per slice row
+int gwn_gram(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
+             int slices, float* dA, int ld_dA, int accumulate, float* ws, hipStream_t s) {
+  GWN_REQUIRE(n > 0 && slices > 0 && x1 && t1 && ws, "gram: bad arguments");
+  GWN_REQUIRE(((uintptr_t)x1 & 15) == 0 && ((uintptr_t)t1 & 15) == 0 && (ldx & 3) == 0 && (ldt & 3) == 0 &&
+                  (!x2 || (((uintptr_t)x2 & 15) == 0 && ((uintptr_t)t2 & 15) == 0)),
+              "gram: operands must be 16-B aligned with ld % 4 == 0");
+  GWN_REQUIRE((long)slices * n * (ldx > ldt ? ldx : ldt) * 4 < 0x7fff0000L, "gram: operand beyond a 2 GB buffer window");
+  Gram g = {};
+  g.X[0] = x1; g.T[0] = t1; g.X[1] = x2; g.T[1] = t2;
+  g.npairs = x2 ? 2 : 1;
+  g.ldx = ldx; g.ldt = ldt;
+  g.n = n; g.nt = (n + 31) / 32; g.slices = slices;
+  g.nsplit = gram_nsplit(n, slices);
+  g.part = ws;
+  const int per_split = g.nt * g.nt;
+  const int blocks = ((g.nsplit + NXCD - 1) / NXCD) * NXCD * per_split;
+  if (g.npairs == 2) gram_kernel<2><<<blocks, 64, 0, s>>>(g);
+  else gram_kernel<1><<<blocks, 64, 0, s>>>(g);
+  GWN_CHECK_LAUNCH();
+  const long outs = (long)n * n;
+  gram_reduce_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(ws, g.nsplit, n, 32 * g.nt, dA, ld_dA,
+                                                                     accumulate);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}

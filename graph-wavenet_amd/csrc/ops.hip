@@ -635,11 +635,19 @@ static int adj_grad_ksplit(int n, int c, int slices) {
 
 long gwn_nconv_adj_grad_workspace_floats(int n, int c, int slices) {
   const int ks = adj_grad_ksplit(n, c, slices);
-  return ks > 1 ? (long)ks * n * n : 0;
+  const long g = gwn_gram_workspace_floats(n, slices);
+  const long w = ks > 1 ? (long)ks * n * n : 0;
+  return g > w ? g : w;
+}
+
+static bool gram_eligible(const float* x, long ldx, const float* dy, long lddy, int c) {
+  return c == 32 && aligned16(x) && aligned16(dy) && (ldx & 3) == 0 && (lddy & 3) == 0;
 }
 
 int gwn_nconv_adj_grad(const float* x, long ldx, const float* dy, long lddy, int n, int c, int slices,
                        float* dA, int ld_dA, int accumulate, float* ws, hipStream_t s) {
+  if (gram_eligible(x, ldx, dy, lddy, c))
+    return gwn_gram(x, dy, nullptr, nullptr, ldx, lddy, n, slices, dA, ld_dA, accumulate, ws, s);
   gwn_gemm_desc d = gemm_zero();
   d.A = x; d.lda_m = ldx; d.lda_k = 1; d.a_kin = c; d.a_ko_stride = (long)n * ldx;
   d.B = dy; d.ldb_k = 1; d.ldb_n = lddy; d.b_kin = c; d.b_ko_stride = (long)n * lddy;
@@ -811,12 +819,17 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
     rc = gwn_gcn_fused_bwd_launch(a, a->sup_t, a->dhcat, a->ld_dhcat, t1, t2, a->ld_dhcat, s);
     if (rc) return rc;
     if (a->adp_index >= 0 && a->adp_index < a->nsup && a->dadp) {
+      // dA = sum xg (x) dx1 + sum x1 (x) dx2: one launch over both pairs
       const int k = a->adp_index;
+      const float* x1 = a->h + (1 + 2 * k) * c;
+      if (gram_eligible(a->h, a->ld_h, t1, a->ld_dhcat, c) && gram_eligible(x1, a->ld_h, t2, a->ld_dhcat, c))
+        return gwn_gram(a->h, t1, x1, t2, a->ld_h, a->ld_dhcat, n, slices, a->dadp, a->ld_sup,
+                        a->accumulate_dadp, a->workspace, s);
       rc = gwn_nconv_adj_grad(a->h, a->ld_h, t1, a->ld_dhcat, n, c, slices, a->dadp, a->ld_sup,
                               a->accumulate_dadp, a->workspace, s);
       if (rc) return rc;
-      rc = gwn_nconv_adj_grad(a->h + (1 + 2 * k) * c, a->ld_h, t2, a->ld_dhcat, n, c, slices, a->dadp,
-                              a->ld_sup, 1, a->workspace, s);
+      rc = gwn_nconv_adj_grad(x1, a->ld_h, t2, a->ld_dhcat, n, c, slices, a->dadp, a->ld_sup, 1,
+                              a->workspace, s);
     }
     return rc;
   }
