@@ -344,15 +344,23 @@ int gwn_gemm_launch(const GemmParams& pin, hipStream_t s) {
                  (akc ? m4(p.lda_m) : (p.lda_m == 1 && m4(p.lda_k) && m4(p.a_row_shift)));
   const int vb = al16(p.B) && b_tiled && m4(p.b_ko_stride) && m4(p.b_no_stride) && m4(p.b_kin) &&
                  (bkc ? m4(p.ldb_n) : (p.ldb_n == 1 && m4(p.ldb_k) && m4(p.b_nin)));
+  // tile choice: the largest tile that still gives >= 2 workgroups per CU (512), else the one with
+  // the most workgroups; thin dimensions get thin tiles
+  auto nblk = [&](int bm, int bn) { return (long)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * p.ksplit; };
+  constexpr long FILL = 512;
   int rc;
   if (p.M <= 32 && p.N <= 32) rc = launch_cfg<1, 1, 1, 1>(p, akc, bkc, va, vb, s);        // 32 x 32
   else if (p.M <= 32 && p.N <= 224) rc = launch_cfg<1, 7, 1, 1>(p, akc, bkc, va, vb, s);  // 32 x 224
-  else if (p.N <= 32) rc = launch_cfg<4, 1, 2, 1>(p, akc, bkc, va, vb, s);                // 256 x 32
+  else if (p.N <= 32)
+    rc = nblk(256, 32) >= FILL ? launch_cfg<4, 1, 2, 1>(p, akc, bkc, va, vb, s)          // 256 x 32
+                               : launch_cfg<1, 1, 1, 1>(p, akc, bkc, va, vb, s);         // 32 x 32
   else if (p.N <= 64 && p.M <= 64) rc = launch_cfg<2, 2, 1, 1>(p, akc, bkc, va, vb, s);   // 64 x 64
   else if (p.N <= 64 && p.M > 128 && p.M <= 224) rc = launch_cfg<7, 1, 1, 2>(p, akc, bkc, va, vb, s);  // 224 x 64
-  else if (p.N <= 64) rc = launch_cfg<4, 1, 1, 2>(p, akc, bkc, va, vb, s);                // 128 x 64
+  else if (p.N <= 64)
+    rc = nblk(128, 64) >= FILL ? launch_cfg<4, 1, 1, 2>(p, akc, bkc, va, vb, s)          // 128 x 64
+                               : launch_cfg<2, 2, 1, 1>(p, akc, bkc, va, vb, s);
   else if (p.M > 160 && p.M <= 224) rc = launch_cfg<7, 1, 1, 2>(p, akc, bkc, va, vb, s);
-  else if (p.M >= 128) rc = launch_cfg<2, 2, 2, 2>(p, akc, bkc, va, vb, s);               // 128 x 128
+  else if (p.M >= 128 && nblk(128, 128) >= FILL) rc = launch_cfg<2, 2, 2, 2>(p, akc, bkc, va, vb, s);  // 128 x 128
   else rc = launch_cfg<2, 2, 1, 1>(p, akc, bkc, va, vb, s);                               // 64 x 64
   if (rc != GWN_OK || p.ksplit <= 1) return rc;
   const long total = (long)p.M * p.N + (p.ones_out ? p.M : 0);

@@ -725,7 +725,9 @@ static int tcn_w_ksplit(int rows, int c) { return pick_ksplit(2 * c, 2 * c, rows
 
 long gwn_gated_tcn_bwd_workspace_floats(int t_in, int P, int c, int dilation) {
   const int rows = (t_in - dilation) * P;
-  return gwn_gemm_workspace_floats(2 * c, 2 * c, tcn_w_ksplit(rows, c));
+  const long g = gwn_gemm_workspace_floats(2 * c, 2 * c, tcn_w_ksplit(rows, c));
+  const long w = gwn_wgrad_workspace_floats(rows, 2 * c, 2 * c);
+  return g > w ? g : w;
 }
 
 int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
@@ -736,15 +738,21 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
                                                      a->skip_row0, a->fg, rows, c, a->dfg);
   GWN_CHECK_LAUNCH();
   // dW_fg[j][tap*c + ci] = sum_r dfg[r][j] * x[r + tap*d*P][ci];  db_fg[j] = sum_r dfg[r][j]
+  int rc;
   gwn_gemm_desc d = gemm_zero();
-  d.A = a->dfg; d.lda_m = 1; d.lda_k = 2 * c;
-  d.B = a->x; d.ldb_k = c; d.ldb_n = 1; d.b_nin = c; d.b_no_stride = (long)a->dilation * P * c;
-  d.C = a->dw_fg; d.ldc_m = 2 * c; d.ldc_n = 1;
-  d.ones_out = a->db_fg;
-  d.M = 2 * c; d.N = 2 * c; d.K = (int)rows;
-  d.ksplit = tcn_w_ksplit((int)rows, c);
-  d.part = a->workspace;
-  int rc = gwn_gemm_launch(d, s);
+  if (c % 32 == 0) {
+    rc = gwn_wgrad(a->dfg, 2 * c, 2 * c, a->x, c, (long)a->t_in * P, c, 2, (long)a->dilation * P, (int)rows,
+                   a->dw_fg, 2 * c, a->db_fg, a->workspace, s);
+  } else {
+    d.A = a->dfg; d.lda_m = 1; d.lda_k = 2 * c;
+    d.B = a->x; d.ldb_k = c; d.ldb_n = 1; d.b_nin = c; d.b_no_stride = (long)a->dilation * P * c;
+    d.C = a->dw_fg; d.ldc_m = 2 * c; d.ldc_n = 1;
+    d.ones_out = a->db_fg;
+    d.M = 2 * c; d.N = 2 * c; d.K = (int)rows;
+    d.ksplit = tcn_w_ksplit((int)rows, c);
+    d.part = a->workspace;
+    rc = gwn_gemm_launch(d, s);
+  }
   if (rc) return rc;
   // dx[r'][ci] (+)= sum_tap sum_j dfg[r' - tap*d*P][j] * Wfg[j][tap*c + ci]
   if (c == 32 && aligned16(a->dfg) && aligned16(a->dx)) return gwn_rowgemm_tcn_bwd_data(a, s);
@@ -794,6 +802,8 @@ long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup) {
   const int width = (2 * nsup + 1) * c;
   long w = gwn_gemm_workspace_floats(c, width, gcn_w_ksplit(rows, c, width));
   const long g = gwn_nconv_adj_grad_workspace_floats(n, c, rows / n);
+  const long v = gwn_wgrad_workspace_floats(rows, c, width);
+  if (v > w) w = v;
   return g > w ? g : w;
 }
 
@@ -801,16 +811,22 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_bwd: rows must be slices*n");
   const int c = a->c, n = a->n, slices = a->rows / n;
   const int width = (2 * a->nsup + 1) * c;
-  // dW_mlp[j][k] = sum_r dh[r][j] h[r][k];  db_mlp[j] = sum_r dh[r][j] (ones column)
+  // dW_mlp[j][k] = sum_r dh[r][j] h[r][k];  db_mlp[j] = sum_r dh[r][j]
   gwn_gemm_desc d = gemm_zero();
-  d.A = a->dh; d.lda_m = 1; d.lda_k = c;
-  d.B = a->h; d.ldb_k = a->ld_h; d.ldb_n = 1;
-  d.C = a->dw_mlp; d.ldc_m = width; d.ldc_n = 1;
-  d.ones_out = a->db_mlp;
-  d.M = c; d.N = width; d.K = a->rows;
-  d.ksplit = gcn_w_ksplit(a->rows, c, width);
-  d.part = a->workspace;
-  int rc = gwn_gemm_launch(d, s);
+  int rc;
+  if (c % 32 == 0 && width % 32 == 0) {
+    rc = gwn_wgrad(a->dh, c, c, a->h, a->ld_h, a->rows, width, 1, 0, a->rows, a->dw_mlp, width, a->db_mlp,
+                   a->workspace, s);
+  } else {
+    d.A = a->dh; d.lda_m = 1; d.lda_k = c;
+    d.B = a->h; d.ldb_k = a->ld_h; d.ldb_n = 1;
+    d.C = a->dw_mlp; d.ldc_m = width; d.ldc_n = 1;
+    d.ones_out = a->db_mlp;
+    d.M = c; d.N = width; d.K = a->rows;
+    d.ksplit = gcn_w_ksplit(a->rows, c, width);
+    d.part = a->workspace;
+    rc = gwn_gemm_launch(d, s);
+  }
   if (rc) return rc;
   if (a->sup_t && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup)) {
     // fused: dxg -> dhcat piece 0; for the adaptive support dx1 -> piece 1, dx2 -> piece 2

@@ -1,0 +1,151 @@
+// Weight (+ bias) gradients of the channels-last 1x1 / dilated convolutions:
+//     dW[j][k] = sum_r dY[r][j] * X[r + tap(k)*shift][col(k)],    db[j] = sum_r dY[r][j]
+// with j < J (32 or 64), k < Kc = ntaps * Kt, tap(k) = k / Kt, col(k) = k % Kt, r < R (all
+// positions: ~10^5 rows).  Used for the gcn mlp (J = 32, Kc = 224, X = the concat buffer h) and the
+// gated TCN (J = 64, Kc = 2 taps x 32).  Memory-bound: every input byte is read once from HBM.
+//
+// A wave owns one 32x32 output tile for its whole life; a workgroup holds all (J/32)*(Kc/32) tiles
+// and walks one contiguous row range, so the partial of a workgroup is the full dW.  An MFMA
+// k-step covers two rows: lane (i, h) loads dY[r + h][32*jt + i] (A operand) and
+// X[r + h (+shift)][32*kt + i] (B operand) — each wave-load instruction is two 128-B row
+// segments.  No LDS, no barriers; 16 k-steps of loads are in flight ahead of the MFMAs.  The
+// bias gradient rides along on the kt == 0 waves (VALU sums of the A fragments).  Workgroup
+// partials [nblk][J*Kc + J] are summed in a fixed order by the reduce kernel (deterministic).
+#include "gwn_internal.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int OOR = 0x7ffffff0;
+constexpr int D = 16;  // k-steps (row pairs) per batch
+
+struct Wgrad {
+  const float* dY; long ldy; int J;
+  const float* X; long ldx; long x_rows; int Kt, ntaps; long shift;
+  int R, nblk;
+  float* part;  // [nblk][J*Kc + J]
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+__global__ __launch_bounds__(1024) void wgrad_kernel(const Wgrad g) {
+  const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar) tile
+  const int Kc = g.ntaps * g.Kt, nkt = Kc / 32;
+  const int jt = wave / nkt, kt = wave % nkt;
+  const int tap = (32 * kt) / g.Kt, xc = 32 * kt - tap * g.Kt;
+  const int r0 = (int)((long)g.R * blockIdx.x / g.nblk), r1 = (int)((long)g.R * (blockIdx.x + 1) / g.nblk);
+
+  // buffer windows end at this workgroup's last row: rows >= r1 read zeros with no per-lane
+  // predicate (a predicated offset would be compiled into branches around the loads)
+  const long xshift = (long)tap * g.shift;
+  const __amdgpu_buffer_rsrc_t ry = rsrc(g.dY, (long)r1 * g.ldy * 4);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(g.X, (r1 + xshift) * g.ldx * 4);
+  auto load = [&](int r, float* a, float* b) {
+    const int oy = (int)(((long)(r + half) * g.ldy + 32 * jt + col) * 4);
+    const int ox = (int)((((long)(r + half) + xshift) * g.ldx + xc + col) * 4);
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+      a[s] = bld(ry, oy + (int)(2 * s * g.ldy * 4));
+      b[s] = bld(rx, ox + (int)(2 * s * g.ldx * 4));
+    }
+  };
+
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+  float bsum = 0.0f;
+  float a[D], b[D];
+  load(r0, a, b);
+  for (int r = r0; r < r1; r += 2 * D) {
+    float an[D], bn[D];
+    load(r + 2 * D, an, bn);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+      bsum += a[s];
+    }
+#pragma unroll
+    for (int s = 0; s < D; ++s) { a[s] = an[s]; b[s] = bn[s]; }
+  }
+  // D[j][k]: col = lane&31 -> k, rows -> j
+  const int stride = g.J * Kc + g.J;
+  float* out = g.part + (long)blockIdx.x * stride;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) out[(32 * jt + crow(i, half)) * Kc + 32 * kt + col] = acc[i];
+  if (kt == 0) {
+    // lane (i, h) summed rows of parity h for j = 32 jt + i: add the two halves
+    const float other = __shfl_xor(bsum, 32);
+    if (half == 0) out[g.J * Kc + 32 * jt + col] = bsum + other;
+  }
+}
+
+// dW[j][k] (ld_w) and db[j] from the workgroup partials: 8 outputs per workgroup x 32 lanes over
+// the partials (lane l sums partials l, l+32, ...), then a fixed-order tree
+__global__ void wgrad_reduce_kernel(const float* part, int nblk, int J, int Kc, float* dW, long ld_w, float* db) {
+  __shared__ float sh[256];
+  const int stride = J * Kc + J;
+  const int ej = threadIdx.x & 7, l = threadIdx.x >> 3;
+  const int idx = blockIdx.x * 8 + ej;
+  float v = 0.0f;
+  if (idx < stride)
+    for (int b = l; b < nblk; b += 32) v += part[(long)b * stride + idx];
+  sh[threadIdx.x] = v;
+  __syncthreads();
+#pragma unroll
+  for (int w = 16; w > 0; w >>= 1) {
+    if (l < w) sh[threadIdx.x] += sh[threadIdx.x + 8 * w];
+    __syncthreads();
+  }
+  if (l != 0 || idx >= stride) return;
+  if (idx < J * Kc) dW[(long)(idx / Kc) * ld_w + idx % Kc] = sh[ej];
+  else if (db) db[idx - J * Kc] = sh[ej];
+}
+
+int wgrad_nblk(int R, int waves_per_blk) {
+  // a whole number of workgroups per CU (256 CUs), 12-16 waves per CU; >= 256 rows per workgroup
+  int per_cu = 16 / waves_per_blk;
+  if (per_cu < 1) per_cu = 1;
+  int nb = 256 * per_cu;
+  const int byrows = R / 256;
+  if (nb > byrows) nb = byrows;
+  return nb < 1 ? 1 : nb;
+}
+
+}  // namespace
+
+long gwn_wgrad_workspace_floats(int R, int J, int Kc) {
+  if (J < 32 || Kc < 32 || J % 32 || Kc % 32 || R <= 0) return 0;  // not eligible: no workspace
+  return (long)wgrad_nblk(R, (J / 32) * (Kc / 32)) * (J * Kc + J);
+}
+
+// dW[j][k] = sum_r dY[r][j] X[r + (k / Kt) * shift][k % Kt]; db[j] = sum_r dY[r][j] (db may be NULL)
+int gwn_wgrad(const float* dY, long ldy, int J, const float* X, long ldx, long x_rows, int Kt, int ntaps,
+              long shift, int R, float* dW, long ld_w, float* db, float* ws, hipStream_t s) {
+  const int Kc = Kt * ntaps;
+  GWN_REQUIRE(J % 32 == 0 && Kt % 32 == 0 && R > 0 && ws, "wgrad: J and Kt must be multiples of 32");
+  const int wpb = (J / 32) * (Kc / 32);
+  GWN_REQUIRE(wpb <= 16, "wgrad: at most 16 output tiles");
+  GWN_REQUIRE((long)R * ldy * 4 < 0x7fff0000L && x_rows * ldx * 4 < 0x7fff0000L,
+              "wgrad: operand beyond a 2 GB buffer window");
+  GWN_REQUIRE(x_rows >= (long)R + (ntaps - 1) * shift, "wgrad: X rows do not cover the taps");
+  Wgrad g = {};
+  g.dY = dY; g.ldy = ldy; g.J = J;
+  g.X = X; g.ldx = ldx; g.x_rows = x_rows; g.Kt = Kt; g.ntaps = ntaps; g.shift = shift;
+  g.R = R; g.nblk = wgrad_nblk(R, wpb);
+  g.part = ws;
+  wgrad_kernel<<<g.nblk, 64 * wpb, 0, s>>>(g);
+  GWN_CHECK_LAUNCH();
+  const int outs = J * Kc + J;
+  wgrad_reduce_kernel<<<(outs + 7) / 8, 256, 0, s>>>(ws, g.nblk, J, Kc, dW, ld_w, db);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
