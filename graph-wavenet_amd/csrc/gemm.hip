@@ -263,24 +263,34 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, 
   }
 }
 
-// 8 outputs per block x 32 split lanes (lane l sums splits l, l+32, ...), then a fixed-order tree.
+// 32 consecutive outputs per block x 8 split lanes (lane l sums splits l, l+8, ...; each wave-load
+// covers two 128-B segments), then a fixed-order tree over the 8 lanes.
 // Outputs [M*N, M*N + M) are the ones column (partials stored after all [ksplit][M][N] tiles).
 __global__ void splitk_reduce_kernel(const GemmParams p) {
   __shared__ float sh[256];
   const long mn = (long)p.M * p.N;
   const long total = mn + (p.ones_out ? p.M : 0);
-  const int ej = threadIdx.x & 7, lane = threadIdx.x >> 3;
-  const long idx = blockIdx.x * 8L + ej;
-  float v = 0.0f;
-  if (idx < mn)
-    for (int s = lane; s < p.ksplit; s += 32) v += p.part[(long)s * mn + idx];
-  else if (idx < total)
-    for (int s = lane; s < p.ksplit; s += 32) v += p.part[(long)p.ksplit * mn + (long)s * p.M + (idx - mn)];
-  sh[threadIdx.x] = v;
+  const int ej = threadIdx.x & 31, lane = threadIdx.x >> 5;
+  const long idx = blockIdx.x * 32L + ej;
+  // four independent chains per lane keep four loads in flight; merged in a fixed order
+  float v0 = 0.0f, v1 = 0.0f, v2 = 0.0f, v3 = 0.0f;
+  if (idx < total) {
+    const float* q = idx < mn ? p.part + idx : p.part + (long)p.ksplit * mn + (idx - mn);
+    const long st = idx < mn ? mn : p.M;
+    int s = lane;
+    for (; s + 24 < p.ksplit; s += 32) {
+      v0 += q[(long)s * st];
+      v1 += q[(long)(s + 8) * st];
+      v2 += q[(long)(s + 16) * st];
+      v3 += q[(long)(s + 24) * st];
+    }
+    for (; s < p.ksplit; s += 8) v0 += q[(long)s * st];
+  }
+  sh[threadIdx.x] = (v0 + v1) + (v2 + v3);
   __syncthreads();
 #pragma unroll
-  for (int w = 16; w > 0; w >>= 1) {
-    if (lane < w) sh[threadIdx.x] += sh[threadIdx.x + 8 * w];
+  for (int w = 4; w > 0; w >>= 1) {
+    if (lane < w) sh[threadIdx.x] += sh[threadIdx.x + 32 * w];
     __syncthreads();
   }
   if (lane == 0 && idx >= mn && idx < total) {
@@ -364,7 +374,7 @@ int gwn_gemm_launch(const GemmParams& pin, hipStream_t s) {
   else rc = launch_cfg<2, 2, 1, 1>(p, akc, bkc, va, vb, s);                               // 64 x 64
   if (rc != GWN_OK || p.ksplit <= 1) return rc;
   const long total = (long)p.M * p.N + (p.ones_out ? p.M : 0);
-  splitk_reduce_kernel<<<(unsigned)((total + 7) / 8), 256, 0, s>>>(p);
+  splitk_reduce_kernel<<<(unsigned)((total + 31) / 32), 256, 0, s>>>(p);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

@@ -88,21 +88,32 @@ __global__ __launch_bounds__(1024) void wgrad_kernel(const Wgrad g) {
   }
 }
 
-// dW[j][k] (ld_w) and db[j] from the workgroup partials: 8 outputs per workgroup x 32 lanes over
-// the partials (lane l sums partials l, l+32, ...), then a fixed-order tree
+// dW[j][k] (ld_w) and db[j] from the workgroup partials: 32 consecutive outputs per workgroup x 8
+// partial lanes (lane l sums partials l, l+8, ...; every wave-load is two 128-B segments), then a
+// fixed-order tree over the 8 lanes
 __global__ void wgrad_reduce_kernel(const float* part, int nblk, int J, int Kc, float* dW, long ld_w, float* db) {
   __shared__ float sh[256];
   const int stride = J * Kc + J;
-  const int ej = threadIdx.x & 7, l = threadIdx.x >> 3;
-  const int idx = blockIdx.x * 8 + ej;
-  float v = 0.0f;
-  if (idx < stride)
-    for (int b = l; b < nblk; b += 32) v += part[(long)b * stride + idx];
-  sh[threadIdx.x] = v;
+  const int ej = threadIdx.x & 31, l = threadIdx.x >> 5;
+  const int idx = blockIdx.x * 32 + ej;
+  // four independent chains per lane keep four loads in flight; merged in a fixed order
+  float v0 = 0.0f, v1 = 0.0f, v2 = 0.0f, v3 = 0.0f;
+  if (idx < stride) {
+    const float* p = part + idx;
+    int b = l;
+    for (; b + 24 < nblk; b += 32) {
+      v0 += p[(long)b * stride];
+      v1 += p[(long)(b + 8) * stride];
+      v2 += p[(long)(b + 16) * stride];
+      v3 += p[(long)(b + 24) * stride];
+    }
+    for (; b < nblk; b += 8) v0 += p[(long)b * stride];
+  }
+  sh[threadIdx.x] = (v0 + v1) + (v2 + v3);
   __syncthreads();
 #pragma unroll
-  for (int w = 16; w > 0; w >>= 1) {
-    if (l < w) sh[threadIdx.x] += sh[threadIdx.x + 8 * w];
+  for (int w = 4; w > 0; w >>= 1) {
+    if (l < w) sh[threadIdx.x] += sh[threadIdx.x + 32 * w];
     __syncthreads();
   }
   if (l != 0 || idx >= stride) return;
@@ -145,7 +156,7 @@ int gwn_wgrad(const float* dY, long ldy, int J, const float* X, long ldx, long x
   wgrad_kernel<<<g.nblk, 64 * wpb, 0, s>>>(g);
   GWN_CHECK_LAUNCH();
   const int outs = J * Kc + J;
-  wgrad_reduce_kernel<<<(outs + 7) / 8, 256, 0, s>>>(ws, g.nblk, J, Kc, dW, ld_w, db);
+  wgrad_reduce_kernel<<<(outs + 31) / 32, 256, 0, s>>>(ws, g.nblk, J, Kc, dW, ld_w, db);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

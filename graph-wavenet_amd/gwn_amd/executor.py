@@ -300,6 +300,7 @@ class Executor:
         for (M_, N_, K_) in ((cfg.O, cfg.E, tf * P), (cfg.E, cfg.S, tf * P), (cfg.S, L * C, tf * P),
                              (C, cfg.Cin, ts[0] * P)):
             need.append(lib.gwn_gemm_workspace_floats(M_, N_, _ksplit(M_, N_, K_)))
+        need.append(lib.gwn_gemm_workspace_floats(tf * P, cfg.O, _ksplit_thin(tf * P, cfg.O, cfg.E)))
         s["ws"] = e(int(max(need)) + 16)
         self._scratch[key] = s
         return s
@@ -402,7 +403,8 @@ class Executor:
         gemm(acts.skr, cfg.S, 1, self.pk("e1_w"), 1, cfg.S, acts.e1, cfg.E, 1,
              M=rows_f, N=cfg.E, K=cfg.S, bias=self.pk("e1_b"), relu=1)
         gemm(acts.e1, cfg.E, 1, self.pk("e2_w"), 1, cfg.E, acts.y, cfg.O, 1,
-             M=rows_f, N=cfg.O, K=cfg.E, bias=self.pk("e2_b"))
+             M=rows_f, N=cfg.O, K=cfg.E, bias=self.pk("e2_b"),
+             ksplit=_ksplit_thin(rows_f, cfg.O, cfg.E), part=ws)
         out = torch.empty(B, cfg.O, N, tf, device=self.device, dtype=F32)
         lib.call("gwn_to_nchw", ptr(acts.y), B, cfg.O, N, tf, ptr(out), st)
         return out, acts
@@ -480,6 +482,15 @@ class Executor:
     def unpack_grads(self, gflat):
         _lib.call("gwn_gather", ptr(self.gpacked), ptr(self.uidx), ptr(gflat), self.layout.flat_total,
                   _lib.stream())
+
+
+def _ksplit_thin(M, N, K):
+    """Split-K for a thin output (N <= 32, e.g. end_conv_2: 12 columns) with a long K: the
+    256 x 32 tiles alone give too few workgroups to fill the chip."""
+    blocks = (M + 255) // 256
+    if N > 32 or K < 256 or blocks >= 512:
+        return 1
+    return max(1, min(512 // blocks, K // 64))
 
 
 def _ksplit(M, N, K):
