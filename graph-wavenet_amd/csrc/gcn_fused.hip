@@ -176,6 +176,17 @@ __device__ __forceinline__ void acc_to_lds(float* buf, const f32x16& d, int w0, 
   for (int r = 0; r < 16; ++r) bp[crow(r, half)] = d[r];
 }
 
+// Tile D'[c][w] straight from the accumulator to rows w of dst: each store instruction writes
+// 2 channels of 32 rows; the 16 instructions of a wave cover its 32 full 128-B row segments, which
+// L2 merges before write-back.  No LDS round trip and no barrier.
+__device__ __forceinline__ void acc_to_global(float* dst, long ld, const f32x16& d, int w0, int lane, int n) {
+  const int half = lane >> 5, col = lane & 31;
+  if (w0 + col >= n) return;
+  float* p = dst + (long)(w0 + col) * ld;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) p[crow(r, half)] = d[r];
+}
+
 __device__ __forceinline__ void lds_to_global(const float* buf, float* dst, long ld, int n) {
   for (int e = threadIdx.x; e < n * CH; e += blockDim.x) {
     const int w = e >> 5, c = e & 31;
@@ -223,10 +234,11 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
       hacc = mlp_from_acc(wf, d, hacc);
     }
+    // ys is free once every wave finished the previous support's hop 2
     if (!(GWN_EXP & 32)) __syncthreads();
     acc_to_lds(ys, d, w0, lane);
+    if (!(GWN_EXP & 2)) acc_to_global((float*)hs + (1 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
     if (!(GWN_EXP & 32)) __syncthreads();
-    if (!(GWN_EXP & 2)) lds_to_global(ys, (float*)hs + (1 + 2 * k) * CH, a.ld_h, n);
     d = diffuse(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
     if (k + 1 < a.nsup) g0 = g_first(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
     if (!(GWN_EXP & 4)) {
@@ -235,10 +247,8 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
     } else {
       hacc += d;
     }
-    if (!(GWN_EXP & 32)) __syncthreads();
-    acc_to_lds(ys, d, w0, lane);
-    if (!(GWN_EXP & 32)) __syncthreads();
-    if (!(GWN_EXP & 2)) lds_to_global(ys, (float*)hs + (2 + 2 * k) * CH, a.ld_h, n);
+    // x2 only goes to h (the backward's dW_mlp): straight from the accumulator
+    if (!(GWN_EXP & 2)) acc_to_global((float*)hs + (2 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
   }
   __syncthreads();
   acc_to_lds(ys, hacc, w0, lane);
@@ -312,23 +322,20 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
       const f32x16 u = mlpT_from_lds(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, w0, lane, zero16());
       __syncthreads();
       acc_to_lds(buf, u, w0, lane);
+      if (k == a.adp_index) acc_to_global(a.t2 + row0 * a.ld_t, a.ld_t, u, w0, lane, n);
     }
     __syncthreads();
-    if (k == a.adp_index) lds_to_global(buf, a.t2 + row0 * a.ld_t, a.ld_t, n);
     f32x16 t = mlpT_from_lds(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, w0, lane, zero16());
     t = diffuse(buf, GT, a.ld_sup, nkb, w0, lane, t, g0);  // dx1 = dP_x1 + A dP_x2
     g0 = g_first(GT, a.ld_sup, nkb, w0, lane);
     __syncthreads();
     acc_to_lds(buf, t, w0, lane);
+    if (k == a.adp_index) acc_to_global(a.t1 + row0 * a.ld_t, a.ld_t, t, w0, lane, n);
     __syncthreads();
-    if (k == a.adp_index) lds_to_global(buf, a.t1 + row0 * a.ld_t, a.ld_t, n);
     dx = diffuse(buf, GT, a.ld_sup, nkb, w0, lane, dx, g0);  // dxg += A dx1
     if (k + 1 < a.nsup) g0 = g_first(a.supT[k + 1], a.ld_sup, nkb, w0, lane);
   }
-  __syncthreads();
-  acc_to_lds(buf, dx, w0, lane);
-  __syncthreads();
-  lds_to_global(buf, a.dxg + row0 * a.ld_dxg, a.ld_dxg, n);
+  acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
 }
 
 // dst (padded [np][ld_dst], zero outside n x n) = src or src^T
