@@ -48,16 +48,6 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
 int gwn_rowgemm_tcn_fwd(const gwn_tcn_args* a, hipStream_t s);
 int gwn_rowgemm_tcn_bwd_data(const gwn_tcn_bwd_args* a, hipStream_t s);
 
-// Adaptive-support gradient over slices, c = 32 (gram.hip): dA (+)= sum_s X1_s^T T1_s (+ X2_s^T T2_s)
-long gwn_gram_workspace_floats(int n, int slices);
-int gwn_gram(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
-             int slices, float* dA, int ld_dA, int accumulate, float* ws, hipStream_t s);
-
-// Weight + bias gradients over rows, J and Kt multiples of 32 (wgrad.hip)
-long gwn_wgrad_workspace_floats(int R, int J, int Kc);
-int gwn_wgrad(const float* dY, long ldy, int J, const float* X, long ldx, long x_rows, int Kt, int ntaps,
-              long shift, int R, float* dW, long ld_w, float* db, float* ws, hipStream_t s);
-
 // Deterministic counter-based dropout RNG (splitmix64 finaliser), identical in every kernel
 // that applies or differentiates the same mask.
 __host__ __device__ inline float gwn_uniform(unsigned long long seed, unsigned long long salt,

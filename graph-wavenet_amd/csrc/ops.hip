@@ -738,9 +738,11 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
                                                      a->skip_row0, a->fg, rows, c, a->dfg);
   GWN_CHECK_LAUNCH();
   // dW_fg[j][tap*c + ci] = sum_r dfg[r][j] * x[r + tap*d*P][ci];  db_fg[j] = sum_r dfg[r][j]
-  int rc;
+  int rc = GWN_OK;
   gwn_gemm_desc d = gemm_zero();
-  if (c % 32 == 0) {
+  if (a->skip_weight_grads) {
+    // caller computes dW_fg / db_fg itself (gwn_wgrad)
+  } else if (c % 32 == 0) {
     rc = gwn_wgrad(a->dfg, 2 * c, 2 * c, a->x, c, (long)a->t_in * P, c, 2, (long)a->dilation * P, (int)rows,
                    a->dw_fg, 2 * c, a->db_fg, a->workspace, s);
   } else {
@@ -813,8 +815,10 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   const int width = (2 * a->nsup + 1) * c;
   // dW_mlp[j][k] = sum_r dh[r][j] h[r][k];  db_mlp[j] = sum_r dh[r][j]
   gwn_gemm_desc d = gemm_zero();
-  int rc;
-  if (c % 32 == 0 && width % 32 == 0) {
+  int rc = GWN_OK;
+  const bool wgrads = !a->skip_weight_grads;  // else the caller runs gwn_wgrad / gwn_gram itself
+  if (!wgrads) {
+  } else if (c % 32 == 0 && width % 32 == 0) {
     rc = gwn_wgrad(a->dh, c, c, a->h, a->ld_h, a->rows, width, 1, 0, a->rows, a->dw_mlp, width, a->db_mlp,
                    a->workspace, s);
   } else {
@@ -834,7 +838,7 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
     float* t2 = a->dhcat + 2 * c;
     rc = gwn_gcn_fused_bwd_launch(a, a->sup_t, a->dhcat, a->ld_dhcat, t1, t2, a->ld_dhcat, s);
     if (rc) return rc;
-    if (a->adp_index >= 0 && a->adp_index < a->nsup && a->dadp) {
+    if (wgrads && a->adp_index >= 0 && a->adp_index < a->nsup && a->dadp) {
       // dA = sum xg (x) dx1 + sum x1 (x) dx2: one launch over both pairs
       const int k = a->adp_index;
       const float* x1 = a->h + (1 + 2 * k) * c;
@@ -864,7 +868,7 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
     rc = gwn_nconv(a->sup[k], a->ld_sup, 0, t2, a->ld_dhcat, t1, a->ld_dhcat, t1, a->ld_dhcat, n, c,
                    slices, s);
     if (rc) return rc;
-    if (k == a->adp_index && a->dadp) {
+    if (wgrads && k == a->adp_index && a->dadp) {
       // dA = sum xg (x) dx1  +  sum x1 (x) dx2
       rc = gwn_nconv_adj_grad(a->h, a->ld_h, t1, a->ld_dhcat, n, c, slices, a->dadp, a->ld_sup,
                               a->accumulate_dadp, a->workspace, s);

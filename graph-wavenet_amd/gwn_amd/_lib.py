@@ -58,6 +58,7 @@ class TcnBwdArgs(ctypes.Structure):
         ("dw_fg", c_void_p), ("db_fg", c_void_p),
         ("dx", c_void_p), ("accumulate_dx", c_int),
         ("workspace", c_void_p),
+        ("skip_weight_grads", c_int),
     ]
 
 
@@ -86,6 +87,7 @@ class GcnBwdArgs(ctypes.Structure):
         ("adp_index", c_int), ("dadp", c_void_p), ("accumulate_dadp", c_int),
         ("workspace", c_void_p),
         ("sup_t", ctypes.POINTER(c_void_p)),
+        ("skip_weight_grads", c_int),
     ]
 
 
@@ -111,6 +113,12 @@ _SIGS = [
     ("gwn_gcn_fwd", c_int, [ctypes.POINTER(GcnArgs), c_void_p]),
     ("gwn_gcn_bwd", c_int, [ctypes.POINTER(GcnBwdArgs), c_void_p]),
     ("gwn_gcn_bwd_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
+    ("gwn_wgrad", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,
+                          c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
+    ("gwn_wgrad_workspace_floats", c_long, [c_int, c_int, c_int]),
+    ("gwn_gram", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_int,
+                         c_int, c_void_p, c_void_p]),
+    ("gwn_gram_workspace_floats", c_long, [c_int, c_int]),
     ("gwn_batchnorm_fwd", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                   c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gwn_batchnorm_workspace_floats", c_long, [c_int, c_int]),

@@ -14,6 +14,7 @@ After the layers: SKR = relu(SKIPCAT Wskip^T + sum_i b_i) (only the last T_f ste
 skip term reach the output, model.py:216-222, 238), E1 = relu(end_conv_1), Y = end_conv_2.
 """
 import ctypes
+import os
 from collections import OrderedDict
 
 import torch
@@ -282,6 +283,10 @@ class Executor:
             "dfg": e(maxrows, 2 * C),
             "dh": e(maxrows, C),
             "dhc": e(maxrows, cfg.W),
+            # second-parity buffers for the side-stream weight gradients (backward overlap)
+            "dfg2": e(maxrows, 2 * C),
+            "dh2": e(maxrows, C),
+            "dhc2": e(maxrows, cfg.W),
             "dadp": torch.zeros(cfg.NP, cfg.NP, device=self.device, dtype=F32),
             "metrics": e(4),
             "bnpart": e(ts[0] * B * 3 * C),  # per-slice BN partials of one layer
@@ -302,6 +307,10 @@ class Executor:
             need.append(lib.gwn_gemm_workspace_floats(M_, N_, _ksplit(M_, N_, K_)))
         need.append(lib.gwn_gemm_workspace_floats(tf * P, cfg.O, _ksplit_thin(tf * P, cfg.O, cfg.E)))
         s["ws"] = e(int(max(need)) + 16)
+        side_need = [lib.gwn_wgrad_workspace_floats(maxrows, C, cfg.W),
+                     lib.gwn_wgrad_workspace_floats(maxrows, 2 * C, 2 * C),
+                     lib.gwn_gram_workspace_floats(N, maxrows // N)]
+        s["ws_side"] = e(int(max(side_need)) + 16)
         self._scratch[key] = s
         return s
 
@@ -434,50 +443,113 @@ class Executor:
         # skip convs
         wgrad(sc["dsk"], S, acts.skipcat, L * C, rows_f, self.gk("skip_w"), ws, self.gk("skip_bsum"))
         gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * C, 1, sc["dskipcat"], L * C, 1, M=rows_f, N=L * C, K=S)
-        # layers in reverse
+        # layers in reverse.  With the fused data path (C = 32) the weight / adjacency gradients
+        # (gwn_wgrad, gwn_gram: off the critical path) run on a second stream, overlapping the next
+        # layers' data path; the buffers they read (dh, dhcat, dfg) alternate by layer parity and a
+        # layer reuses its parity's buffers only after the side stream finished the layer + 2.
+        overlap = self._overlap_ok(acts)
+        main = torch.cuda.current_stream()
+        side = self._side_stream() if overlap else None
+        side_done = {}
         dnext = None
         bufs = [sc["dxa"], sc["dxb"]]
         first_adp = True
+        adp_index = cfg.nsup - 1 if (cfg.use_gcn and cfg.adaptive) else -1
         for i in range(L - 1, -1, -1):
             d = cfg.dilations[i]
             rows = ts[i + 1] * P
             dx = bufs[i % 2]
+            par = "" if (i % 2 == 0 or not overlap) else "2"
+            dh, dhc, dfg = sc["dh" + par], sc["dhc" + par], sc["dfg" + par]
+            if overlap and (i + 2) in side_done:
+                main.wait_event(side_done[i + 2])
             dxg, ld_dxg, acc = None, 0, 0
             if dnext is not None:
                 lib.call("gwn_batchnorm_bwd", ptr(dnext), ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
                          ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(self.gk("bn_g%d" % i)),
-                         ptr(self.gk("bn_b%d" % i)), ptr(dx), d * P, ptr(sc["dh"]), ptr(self.seed), i,
+                         ptr(self.gk("bn_b%d" % i)), ptr(dx), d * P, ptr(dh), ptr(self.seed), i,
                          float(self.dropout) if (acts.training and cfg.use_gcn) else 0.0, ptr(ws), st)
-                adp_index = cfg.nsup - 1 if (cfg.use_gcn and cfg.adaptive) else -1
                 gb = _lib.GcnBwdArgs(rows=rows, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
                                      sup=ctypes.cast(acts.sup_arr, ctypes.POINTER(ctypes.c_void_p)),
                                      ld_sup=cfg.NP,
                                      h=ptr(acts.H[i]), ld_h=cfg.W, w_mlp=ptr(self.pk("mlp_w%d" % i)),
-                                     dh=ptr(sc["dh"]), dhcat=ptr(sc["dhc"]), ld_dhcat=cfg.W,
+                                     dh=ptr(dh), dhcat=ptr(dhc), ld_dhcat=cfg.W,
                                      dw_mlp=ptr(self.gk("mlp_w%d" % i)), db_mlp=ptr(self.gk("mlp_b%d" % i)),
                                      adp_index=adp_index, dadp=ptr(sc["dadp"]),
                                      accumulate_dadp=0 if first_adp else 1, workspace=ptr(ws),
                                      sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
-                                     if acts.supT_arr is not None else None)
+                                     if acts.supT_arr is not None else None,
+                                     skip_weight_grads=1 if overlap else 0)
                 lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)
+                if overlap:
+                    self._side_gcn_grads(main, side, acts, i, rows, dh, dhc, adp_index, first_adp, sc)
                 if adp_index >= 0:
                     first_adp = False
-                dxg, ld_dxg, acc = sc["dhc"], cfg.W, 1
+                dxg, ld_dxg, acc = dhc, cfg.W, 1
             tb = _lib.TcnBwdArgs(x=ptr(acts.X[i]), t_in=ts[i], P=P, c=C, dilation=d,
                                  w_fg=ptr(self.pk("fg_w%d" % i)), fg=ptr(acts.FG[i]),
                                  dxg=ptr(dxg), ld_dxg=ld_dxg,
                                  dskip=sc["dskipcat"].data_ptr() + 4 * i * C, ld_dskip=L * C,
-                                 skip_row0=(ts[i + 1] - tf) * P, dfg=ptr(sc["dfg"]),
+                                 skip_row0=(ts[i + 1] - tf) * P, dfg=ptr(dfg),
                                  dw_fg=ptr(self.gk("fg_w%d" % i)), db_fg=ptr(self.gk("fg_b%d" % i)),
-                                 dx=ptr(dx), accumulate_dx=acc, workspace=ptr(ws))
+                                 dx=ptr(dx), accumulate_dx=acc, workspace=ptr(ws),
+                                 skip_weight_grads=1 if overlap else 0)
             lib.call("gwn_gated_tcn_bwd", ctypes.byref(tb), st)
+            if overlap:
+                side_done[i] = self._side_tcn_grads(main, side, acts, i, rows, dfg, sc)
             dnext = dx
+        if overlap:
+            main.wait_event(side_done[0])  # dadp and every side-stream weight gradient are complete
         # start conv
         rows0 = ts[0] * P
         wgrad(dnext, C, acts.xin, cfg.Cin, rows0, self.gk("start_w"), ws, self.gk("start_b"))
         if cfg.use_gcn and cfg.adaptive:
             lib.call("gwn_adaptive_adj_bwd", ptr(self.pk("nv1")), ptr(self.pk("nv2")), ptr(acts.adp),
                      ptr(sc["dadp"]), N, 10, cfg.NP, ptr(self.gk("nv1")), ptr(self.gk("nv2")), ptr(ws), st)
+
+    # ---------------------------------------------------------------------------------------
+    def _overlap_ok(self, acts):
+        cfg = self.cfg
+        return (os.environ.get("GWN_OVERLAP", "1") != "0" and cfg.C == 32 and cfg.W % 32 == 0
+                and acts.supT_arr is not None)
+
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
+    def _side_gcn_grads(self, main, side, acts, i, rows, dh, dhc, adp_index, first_adp, sc):
+        """dW_mlp / db_mlp (gwn_wgrad) and the adaptive-support gradient (gwn_gram) of layer i on
+        the side stream, after the main stream's gcn data path of layer i."""
+        cfg = self.cfg
+        C, W = cfg.C, cfg.W
+        ev = torch.cuda.Event()
+        ev.record(main)
+        side.wait_event(ev)
+        sst, wss = side.cuda_stream, sc["ws_side"]
+        _lib.call("gwn_wgrad", ptr(dh), C, C, ptr(acts.H[i]), W, rows, W, 1, 0, rows,
+                  ptr(self.gk("mlp_w%d" % i)), W, ptr(self.gk("mlp_b%d" % i)), ptr(wss), sst)
+        if adp_index >= 0:
+            h = acts.H[i].data_ptr()
+            t = dhc.data_ptr()
+            _lib.call("gwn_gram", h, t + 4 * C, h + 4 * (1 + 2 * adp_index) * C, t + 4 * 2 * C, W, W, cfg.N,
+                      rows // cfg.N, ptr(sc["dadp"]), cfg.NP, 0 if first_adp else 1, ptr(wss), sst)
+
+    def _side_tcn_grads(self, main, side, acts, i, rows, dfg, sc):
+        """dW_fg / db_fg of layer i (gwn_wgrad over both taps) on the side stream; returns the
+        event that marks the end of layer i's side work."""
+        cfg = self.cfg
+        C = cfg.C
+        P = acts.P
+        ev = torch.cuda.Event()
+        ev.record(main)
+        side.wait_event(ev)
+        _lib.call("gwn_wgrad", ptr(dfg), 2 * C, 2 * C, ptr(acts.X[i]), C, acts.ts[i] * P, C, 2,
+                  cfg.dilations[i] * P, rows, ptr(self.gk("fg_w%d" % i)), 2 * C, ptr(self.gk("fg_b%d" % i)),
+                  ptr(sc["ws_side"]), side.cuda_stream)
+        done = torch.cuda.Event()
+        done.record(side)
+        return done
 
     def unpack_grads(self, gflat):
         _lib.call("gwn_gather", ptr(self.gpacked), ptr(self.uidx), ptr(gflat), self.layout.flat_total,

@@ -142,6 +142,9 @@ typedef struct gwn_tcn_bwd_args {
   float* dw_fg; float* db_fg;
   float* dx; int accumulate_dx;
   float* workspace;
+  /* 1 = data path only (dfg, dx); dW_fg / db_fg are left to a gwn_wgrad call of the caller
+   * (e.g. on a second stream) */
+  int skip_weight_grads;
 } gwn_tcn_bwd_args;
 int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t stream);
 long gwn_gated_tcn_bwd_workspace_floats(int t_in, int P, int c, int dilation);
@@ -194,9 +197,31 @@ typedef struct gwn_gcn_bwd_args {
   /* optional transposed supports (gwn_transpose) enabling the fused backward (c == 32,
    * n <= 512); NULL = generic path */
   const float* const* sup_t;
+  /* 1 = data path only (dhcat); dW_mlp / db_mlp / dadp are left to gwn_wgrad / gwn_gram calls of
+   * the caller (e.g. on a second stream) */
+  int skip_weight_grads;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);
+
+/* ---------------------------------------------------------------------------------------------
+ * Weight + bias gradients of a channels-last 1x1 / dilated conv, the row reduction
+ *   dW[j][k] = sum_{r<R} dY[r][j] * X[r + (k / Kt) * shift][k % Kt]   (j < J, k < Kt * ntaps)
+ *   db[j]    = sum_{r<R} dY[r][j]                                      (db may be NULL)
+ * J and Kt multiples of 32, (J/32)*(Kt*ntaps/32) <= 16; X has x_rows >= R + (ntaps-1)*shift rows.
+ * gcn mlp: J = c, X = h, Kt = (2K+1)c, ntaps = 1.  gated TCN: J = 2c, X = x, Kt = c, ntaps = 2,
+ * shift = dilation*P.  Deterministic (fixed-order partial sums).
+ * ------------------------------------------------------------------------------------------- */
+int gwn_wgrad(const float* dY, long ldy, int J, const float* X, long ldx, long x_rows, int Kt, int ntaps,
+              long shift, int R, float* dW, long ld_w, float* db, float* workspace, hipStream_t stream);
+long gwn_wgrad_workspace_floats(int R, int J, int Kc);
+
+/* Adjacency gradient of order-2 diffusion over all slices (c = 32 channels per row):
+ *   dA[v][w] (+)= sum_s sum_c X1[s*n + v][c] T1[s*n + w][c]  (+ same for X2, T2 when non-NULL)
+ * i.e. both pairs (xg, dx1) and (x1, dx2) of gcn.forward's adaptive support in one launch. */
+int gwn_gram(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
+             int slices, float* dA, int ld_dA, int accumulate, float* workspace, hipStream_t stream);
+long gwn_gram_workspace_floats(int n, int slices);
 
 /* ---------------------------------------------------------------------------------------------
  * BatchNorm2d (model.py:236, bn = nn.BatchNorm2d(c) model.py:152) over the rows of z [rows][c].
