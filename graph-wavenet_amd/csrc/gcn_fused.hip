@@ -426,6 +426,17 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   return GWN_OK;
 }
 
+// diagnostics: resident workgroups per CU of the fused kernels for n nodes (HIP occupancy API)
+extern "C" int gwn_fused_occupancy(int n, int backward) {
+  const int nwt = (n + 31) / 32;
+  const size_t lds = fused_lds_bytes(n);
+  int blocks = -1;
+  hipError_t e;
+  if (backward) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_fused_kernel<512>, 64 * nwt, lds);
+  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_fused_kernel<512>, 64 * nwt, lds);
+  return e == hipSuccess ? blocks : -(int)e;
+}
+
 extern "C" int gwn_transpose(const float* src, int n, int ld_src, float* dst, int ld_dst, hipStream_t s) {
   GWN_REQUIRE(n > 0, "transpose: bad shape");
   dim3 grid((n + 31) / 32, (n + 31) / 32);

@@ -17,7 +17,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-constexpr int OOR = 0x7ffffff0;
 constexpr int D = 16;  // k-steps (row pairs) per batch
 
 struct Wgrad {

@@ -241,6 +241,8 @@ int gwn_batchnorm_fwd_partials(const float* z, int rows, int c, const float* par
                                float* save_mean, float* save_rstd, hipStream_t stream);
 /* dst[j][i] = src[i][j] for an n x n matrix (supports for the fused backward) */
 int gwn_transpose(const float* src, int n, int ld_src, float* dst, int ld_dst, hipStream_t stream);
+/* diagnostics: resident workgroups per CU of the fused gcn kernel (forward, or backward != 0) */
+int gwn_fused_occupancy(int n, int backward);
 /* dst [np][ld_dst] = src (or src^T if transpose) inside [n][n], zero elsewhere (np >= n) */
 int gwn_pad_square(const float* src, int n, int ld_src, float* dst, int np, int ld_dst, int transpose,
                    hipStream_t stream);
