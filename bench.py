@@ -146,7 +146,7 @@ def measure_dominant(eng, dev, rounds=5):
     st = _lib.stream()
     launches = [acts.gcn_args[i] for i in sorted(acts.gcn_args)]
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in launches]
-    total_ms, total_flop, count = 0.0, 0.0, 0
+    total_ms, total_flop, total_bytes, count = 0.0, 0.0, 0.0, 0
     for _ in range(rounds):
         for ga, (e0, e1) in zip(launches, evs):
             e0.record()
@@ -157,13 +157,23 @@ def measure_dominant(eng, dev, rounds=5):
             slices = ga.rows // N
             total_ms += e0.elapsed_time(e1)
             total_flop += slices * (K * 2 * 2.0 * C * N * N + 2.0 * (2 * K + 1) * C * C * N)
+            # compulsory bytes: xg + residual in, 2K hop outputs + z out
+            total_bytes += slices * N * C * 4.0 * (2 + 2 * K + 1)
             count += 1
     avg_us = 1000.0 * total_ms / count
     achieved = total_flop / (total_ms / 1000.0) / 1e12
+    # HBM bytes per launch from the committed PMC passes of this kernel (tools/pmc_dominant.py:
+    # separate FETCH_SIZE / WRITE_SIZE rocprofv3 runs of this bench, gfx950 FETCH correction)
+    traffic, pmc = None, os.path.join(ROOT, "profiles", "r01", "pmc_gcn_fwd_fused.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("traffic_bytes_per_launch")
     return {"kernel": "gcn_fwd_fused_kernel<512> (fused diffusion GCN forward, 8 launches/step)",
             "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+            "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "traffic_source": "profiles/r01/pmc_gcn_fwd_fused.json" if traffic else None,
             "avg_launch_us": round(avg_us, 3), "flop_per_launch_avg": round(total_flop / count, 1),
+            "algorithmic_bytes_per_launch": round(total_bytes / count),
             "launches_timed": count}
 
 
