@@ -124,6 +124,7 @@ _SIGS = [
     ("gwn_batchnorm_workspace_floats", c_long, [c_int, c_int]),
     ("gwn_batchnorm_fwd_partials", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("gwn_fused_occupancy", c_int, [c_int, c_int]),
     ("gwn_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     ("gwn_pad_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
     ("gwn_batchnorm_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
