@@ -42,6 +42,12 @@ struct FusedBwd {
   float* dxg; long ld_dxg;
   float* t1; float* t2; long ld_t; int adp_index;
   int n;
+  // optional BatchNorm-backward prologue (dh computed from the BN output gradient)
+  const float* bn_dy; const float* bn_z; const float* bn_gamma; const float* bn_mean; const float* bn_rstd;
+  const float* bn_sums; float* bn_dgamma; float* bn_dbeta; float* dres; float* dh_out;
+  const unsigned long long* seed_ptr; unsigned long long salt; float drop_p; float inv_rows;
+  // optional gate-backward epilogue (dfg instead of dxg)
+  const float* fg; const float* dskip; long ld_dskip; long skip_row0; float* dfg;
 };
 
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
@@ -313,7 +319,38 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
   const long row0 = (long)blockIdx.x * n;
 
   GBatch g0 = (a.nsup > 0) ? g_first(a.supT[0], a.ld_sup, nkb, w0, lane) : GBatch{};
-  global_to_lds(a.dh + row0 * CH, CH, n, np, dhs);
+  if (a.bn_dy) {
+    // BatchNorm backward of this layer's output (same arithmetic as bn_bwd_apply_kernel, ops.hip):
+    //   dz = gamma*rstd*(dy - k1 - xhat*k2) -> residual gradient dres; dropout'(dz) -> dh (LDS + HBM)
+    if (blockIdx.x == 0 && threadIdx.x < CH) {
+      if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
+      if (a.bn_dgamma) a.bn_dgamma[threadIdx.x] = a.bn_sums[CH + threadIdx.x];
+    }
+    const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
+    const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+    const int c = threadIdx.x & 31;  // blockDim.x is a multiple of 32: c is fixed per thread
+    const float mu = a.bn_mean[c], rs = a.bn_rstd[c];
+    const float k1 = a.bn_sums[c] * a.inv_rows, k2 = a.bn_sums[CH + c] * a.inv_rows;
+    for (int e = threadIdx.x; e < np * CH; e += blockDim.x) {
+      const int w = e >> 5;
+      float v = 0.0f;
+      if (w < n) {
+        const long idx = (row0 + w) * CH + c;
+        const float xhat = (a.bn_z[idx] - mu) * rs;
+        const float dz = a.bn_gamma[c] * rs * (a.bn_dy[idx] - k1 - xhat * k2);
+        a.dres[idx] = dz;
+        v = dz;
+        if (a.drop_p > 0.0f) {
+          const float u = gwn_uniform(seed, a.salt, (unsigned long long)idx);
+          v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
+        }
+        a.dh_out[idx] = v;
+      }
+      dhs[w * LDR + c] = v;
+    }
+  } else {
+    global_to_lds(a.dh + row0 * CH, CH, n, np, dhs);
+  }
   __syncthreads();
   f32x16 dx = mlpT_from_lds(a.w_mlp, a.ld_w, 0, dhs, w0, lane, zero16());
   for (int k = 0; k < a.nsup; ++k) {
@@ -335,7 +372,27 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
     dx = diffuse(buf, GT, a.ld_sup, nkb, w0, lane, dx, g0);  // dxg += A dx1
     if (k + 1 < a.nsup) g0 = g_first(a.supT[k + 1], a.ld_sup, nkb, w0, lane);
   }
-  acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
+  if (!a.dfg) {
+    acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
+    return;
+  }
+  // gate backward (gate_bwd_kernel, ops.hip): g = dxg (+ dskip) -> dfg through the saved
+  // (tanh f, sigmoid s) pairs, staged through LDS so the fg / dfg rows move as coalesced float2s
+  __syncthreads();  // every wave finished reading buf
+  acc_to_lds(buf, dx, w0, lane);
+  __syncthreads();
+  for (int e = threadIdx.x; e < n * CH; e += blockDim.x) {
+    const int w = e >> 5, c = e & 31;
+    const long m = row0 + w;
+    float g = buf[w * LDR + c];
+    if (a.dskip && m >= a.skip_row0) g += a.dskip[(m - a.skip_row0) * a.ld_dskip + c];
+    const float2 fs = *(const float2*)(a.fg + m * 2 * CH + 2 * c);
+    const float f = fs.x, sg = fs.y;
+    float2 o;
+    o.x = g * sg * (1.0f - f * f);
+    o.y = g * f * sg * (1.0f - sg);
+    *(float2*)(a.dfg + m * 2 * CH + 2 * c) = o;
+  }
 }
 
 // dst (padded [np][ld_dst], zero outside n x n) = src or src^T
@@ -413,6 +470,17 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   a.dxg = dxg; a.ld_dxg = ld_dxg;
   a.t1 = t1; a.t2 = t2; a.ld_t = ld_t; a.adp_index = g->adp_index;
   a.n = g->n;
+  a.bn_dy = g->bn_dy; a.bn_z = g->bn_z; a.bn_gamma = g->bn_gamma; a.bn_mean = g->bn_mean;
+  a.bn_rstd = g->bn_rstd; a.bn_sums = g->bn_sums; a.bn_dgamma = g->bn_dgamma; a.bn_dbeta = g->bn_dbeta;
+  a.dres = g->dres; a.dh_out = g->dh_out;
+  a.seed_ptr = g->seed_ptr; a.salt = g->salt; a.drop_p = g->drop_p; a.inv_rows = 1.0f / (float)g->rows;
+  a.fg = g->fg; a.dskip = g->dskip; a.ld_dskip = g->ld_dskip; a.skip_row0 = g->skip_row0; a.dfg = g->dfg;
+  if (a.bn_dy)
+    GWN_REQUIRE(a.bn_z && a.bn_gamma && a.bn_mean && a.bn_rstd && a.bn_sums && a.dres && a.dh_out,
+                "gcn_bwd (fused): BN prologue needs bn_z, gamma, mean, rstd, sums, dres and dh_out");
+  else
+    GWN_REQUIRE(a.dh != nullptr, "gcn_bwd (fused): dh is required without the BN prologue");
+  if (a.dfg) GWN_REQUIRE(a.fg != nullptr, "gcn_bwd (fused): the gate epilogue needs fg");
   static bool attr_set = false;
   if (!attr_set) {
     ensure_lds_attr(gcn_bwd_fused_kernel<512>);

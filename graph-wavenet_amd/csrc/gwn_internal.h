@@ -47,6 +47,8 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
 // Weight-stationary row GEMMs of the gated TCN (rowgemm.hip), c = 32
 int gwn_rowgemm_tcn_fwd(const gwn_tcn_args* a, hipStream_t s);
 int gwn_rowgemm_tcn_bwd_data(const gwn_tcn_bwd_args* a, hipStream_t s);
+int gwn_rowgemm_tcn_bwd_nparts(const gwn_tcn_bwd_args* a);
+constexpr int GWN_ROWGEMM_MAX_PARTS = 2048;  // waves of one rowgemm launch (8 per CU)
 
 // Deterministic counter-based dropout RNG (splitmix64 finaliser), identical in every kernel
 // that applies or differentiates the same mask.

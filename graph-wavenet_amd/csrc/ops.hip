@@ -606,6 +606,16 @@ extern "C" {
 int gwn_version(void) { return 1; }
 const char* gwn_last_error(void) { return g_err; }
 
+long gwn_abi_sizeof(const char* name) {
+  if (!name) return -1;
+  if (!strcmp(name, "gwn_gemm_desc")) return (long)sizeof(gwn_gemm_desc);
+  if (!strcmp(name, "gwn_tcn_args")) return (long)sizeof(gwn_tcn_args);
+  if (!strcmp(name, "gwn_tcn_bwd_args")) return (long)sizeof(gwn_tcn_bwd_args);
+  if (!strcmp(name, "gwn_gcn_args")) return (long)sizeof(gwn_gcn_args);
+  if (!strcmp(name, "gwn_gcn_bwd_args")) return (long)sizeof(gwn_gcn_bwd_args);
+  return -1;
+}
+
 int gwn_gemm(const gwn_gemm_desc* d, hipStream_t s) {
   GWN_REQUIRE(d != nullptr, "gemm: null descriptor");
   return gwn_gemm_launch(*d, s);
@@ -727,16 +737,24 @@ long gwn_gated_tcn_bwd_workspace_floats(int t_in, int P, int c, int dilation) {
   const int rows = (t_in - dilation) * P;
   const long g = gwn_gemm_workspace_floats(2 * c, 2 * c, tcn_w_ksplit(rows, c));
   const long w = gwn_wgrad_workspace_floats(rows, 2 * c, 2 * c);
-  return g > w ? g : w;
+  long m = g > w ? g : w;
+  // BN statistics partials of the fused rowgemm epilogue, or of the generic fallback pass
+  const long b = (long)(GWN_ROWGEMM_MAX_PARTS > RED_BLOCKS ? GWN_ROWGEMM_MAX_PARTS : RED_BLOCKS) * 2 * c;
+  return m > b ? m : b;
 }
 
 int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->t_in > a->dilation && a->c % 16 == 0, "gated_tcn_bwd: bad shape");
   const int c = a->c, P = a->P, t_out = a->t_in - a->dilation;
   const long rows = (long)t_out * P;
-  gate_bwd_kernel<<<grid_for(rows * c), 256, 0, s>>>(a->dxg, a->ld_dxg, a->dskip, a->ld_dskip,
-                                                     a->skip_row0, a->fg, rows, c, a->dfg);
-  GWN_CHECK_LAUNCH();
+  GWN_REQUIRE(a->acc_row0 >= 0 && a->acc_row0 <= (long)a->t_in * P, "gated_tcn_bwd: bad acc_row0");
+  if (a->bn_sums) GWN_REQUIRE(a->bn_z && a->bn_mean && a->bn_rstd && c <= 256 && 256 % c == 0,
+                              "gated_tcn_bwd: BN statistics need bn_z, bn_mean, bn_rstd");
+  if (!a->dfg_ready) {
+    gate_bwd_kernel<<<grid_for(rows * c), 256, 0, s>>>(a->dxg, a->ld_dxg, a->dskip, a->ld_dskip,
+                                                       a->skip_row0, a->fg, rows, c, a->dfg);
+    GWN_CHECK_LAUNCH();
+  }
   // dW_fg[j][tap*c + ci] = sum_r dfg[r][j] * x[r + tap*d*P][ci];  db_fg[j] = sum_r dfg[r][j]
   int rc = GWN_OK;
   gwn_gemm_desc d = gemm_zero();
@@ -757,7 +775,18 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
   }
   if (rc) return rc;
   // dx[r'][ci] (+)= sum_tap sum_j dfg[r' - tap*d*P][j] * Wfg[j][tap*c + ci]
-  if (c == 32 && aligned16(a->dfg) && aligned16(a->dx)) return gwn_rowgemm_tcn_bwd_data(a, s);
+  if (c == 32 && aligned16(a->dfg) && aligned16(a->dx)) {
+    rc = gwn_rowgemm_tcn_bwd_data(a, s);
+    if (rc || !a->bn_sums) return rc;
+    colsum_final_kernel<<<(2 * c + 7) / 8, 256, 0, s>>>(a->workspace, gwn_rowgemm_tcn_bwd_nparts(a), 2 * c,
+                                                        a->bn_sums, 0);
+    GWN_CHECK_LAUNCH();
+    return GWN_OK;
+  }
+  if (a->accumulate_dx && a->acc_row0 > 0) {
+    if (hipMemsetAsync(a->dx, 0, (size_t)a->acc_row0 * c * sizeof(float), s) != hipSuccess)
+      return gwn_set_error(GWN_ERR_HIP, "gated_tcn_bwd: memset failed");
+  }
   d = gemm_zero();
   d.A = a->dfg; d.lda_m = 2 * c; d.lda_k = 1; d.a_kin = 2 * c; d.a_row_shift = -a->dilation * P;
   d.a_rows = (int)rows;
@@ -765,7 +794,15 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
   d.C = a->dx; d.ldc_m = c; d.ldc_n = 1;
   if (a->accumulate_dx) { d.C0 = a->dx; d.ldc0_m = c; d.ldc0_n = 1; d.beta = 1.0f; }
   d.M = a->t_in * P; d.N = c; d.K = 4 * c;
-  return gwn_gemm_launch(d, s);
+  rc = gwn_gemm_launch(d, s);
+  if (rc || !a->bn_sums) return rc;
+  const long rows_in = (long)a->t_in * P;
+  bn_bwd_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(a->dx, a->bn_z, a->bn_mean, a->bn_rstd, rows_in, c,
+                                                   a->workspace);
+  GWN_CHECK_LAUNCH();
+  colsum_final_kernel<<<(2 * c + 7) / 8, 256, 0, s>>>(a->workspace, RED_BLOCKS, 2 * c, a->bn_sums, 0);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -813,16 +850,28 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_bwd: rows must be slices*n");
   const int c = a->c, n = a->n, slices = a->rows / n;
   const int width = (2 * a->nsup + 1) * c;
+  const bool fused = a->sup_t && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup);
+  GWN_REQUIRE(fused || (!a->bn_dy && !a->dfg), "gcn_bwd: the BN / gate fusions need the fused path "
+                                               "(sup_t given, c == 32, n <= 512)");
+  const float* dh = a->bn_dy ? a->dh_out : a->dh;
+  const bool wgrads = !a->skip_weight_grads;  // else the caller runs gwn_wgrad / gwn_gram itself
+  int rc = GWN_OK;
+  if (fused) {
+    // fused: dxg -> dhcat piece 0 (or dfg through the gate epilogue); for the adaptive support
+    // dx1 -> piece 1, dx2 -> piece 2
+    float* t1 = a->dhcat + c;
+    float* t2 = a->dhcat + 2 * c;
+    rc = gwn_gcn_fused_bwd_launch(a, a->sup_t, a->dhcat, a->ld_dhcat, t1, t2, a->ld_dhcat, s);
+    if (rc) return rc;
+  }
   // dW_mlp[j][k] = sum_r dh[r][j] h[r][k];  db_mlp[j] = sum_r dh[r][j]
   gwn_gemm_desc d = gemm_zero();
-  int rc = GWN_OK;
-  const bool wgrads = !a->skip_weight_grads;  // else the caller runs gwn_wgrad / gwn_gram itself
   if (!wgrads) {
   } else if (c % 32 == 0 && width % 32 == 0) {
-    rc = gwn_wgrad(a->dh, c, c, a->h, a->ld_h, a->rows, width, 1, 0, a->rows, a->dw_mlp, width, a->db_mlp,
+    rc = gwn_wgrad(dh, c, c, a->h, a->ld_h, a->rows, width, 1, 0, a->rows, a->dw_mlp, width, a->db_mlp,
                    a->workspace, s);
   } else {
-    d.A = a->dh; d.lda_m = 1; d.lda_k = c;
+    d.A = dh; d.lda_m = 1; d.lda_k = c;
     d.B = a->h; d.ldb_k = a->ld_h; d.ldb_n = 1;
     d.C = a->dw_mlp; d.ldc_m = width; d.ldc_n = 1;
     d.ones_out = a->db_mlp;
@@ -832,12 +881,9 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
     rc = gwn_gemm_launch(d, s);
   }
   if (rc) return rc;
-  if (a->sup_t && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup)) {
-    // fused: dxg -> dhcat piece 0; for the adaptive support dx1 -> piece 1, dx2 -> piece 2
+  if (fused) {
     float* t1 = a->dhcat + c;
     float* t2 = a->dhcat + 2 * c;
-    rc = gwn_gcn_fused_bwd_launch(a, a->sup_t, a->dhcat, a->ld_dhcat, t1, t2, a->ld_dhcat, s);
-    if (rc) return rc;
     if (wgrads && a->adp_index >= 0 && a->adp_index < a->nsup && a->dadp) {
       // dA = sum xg (x) dx1 + sum x1 (x) dx2: one launch over both pairs
       const int k = a->adp_index;

@@ -25,6 +25,9 @@ struct RowGemm {
   float* aux; long ld_aux;                                       // GATE: aux[m][n] = tanh f / sigmoid g
   float* aux2; long ld_aux2; int aux2_row0;                      // GATE: skip copy of xg for m >= row0
   int M, ntiles;                                                 // N = 32 * ntiles
+  long acc_row0;                                                 // STORE + accumulate: rows < acc_row0 not accumulated
+  const float* bn_z; const float* bn_mean; const float* bn_rstd; // BNSTAT: per-wave partials of sum C and
+  float* bn_part;                                                //   sum C*xhat(bn_z), [wave][2][32]
 };
 
 // Branch-free gate nonlinearities on v_exp_f32 / v_rcp_f32: absolute error ~1e-7 (a few ulp of
@@ -53,7 +56,7 @@ __device__ __forceinline__ float ld32(__amdgpu_buffer_rsrc_t r, int off) {
 // g = cols 2c+1 (tile 1) — so every lane owns channel c = col of both and writes full rows:
 // xg[m][c] = tanh(f) * sigmoid(g) (128 B per row) and fg[m][2c .. 2c+1] = (tanh f, sigmoid g).
 // STORE: ntiles waves share a chunk, one 32-column tile each.
-template <int KH, bool GATE>
+template <int KH, bool GATE, bool BNSTAT>
 __global__ __launch_bounds__(256) void rowgemm_kernel(const RowGemm p) {
   constexpr int NQ = KH / 4;  // float4 per lane per chunk
   constexpr int NT = GATE ? 2 : 1;
@@ -116,15 +119,26 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(const RowGemm p) {
     bn[0] = 0.0f;
   }
   if (wave >= nwaves) return;  // after the block-wide staging barrier
+  // BNSTAT (N = 32: channel n = col): running sums of the final C and C*xhat over this wave's rows
+  const __amdgpu_buffer_rsrc_t rz = rsrc(BNSTAT ? p.bn_z : p.C, BNSTAT ? (long)p.M * 32 * 4 : 0);
+  const float bmu = BNSTAT ? p.bn_mean[col] : 0.0f, brs = BNSTAT ? p.bn_rstd[col] : 0.0f;
+  float bs0 = 0.0f, bs1 = 0.0f;
   for (; chunk < nchunks; chunk += nwaves) {
     const long m0 = (long)chunk * 32;
     // C0 of this chunk first, then the next chunk's A: the epilogue waits only for the former
-    float c0[16];
+    float c0[16], zz[16];
     if (!GATE && p.accumulate) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const long m = m0 + crow(r, half);
-        c0[r] = ld32(rc, m < p.M ? (int)((m * p.ldc + n) * 4) : OOR);
+        c0[r] = ld32(rc, (m < p.M && m >= p.acc_row0) ? (int)((m * p.ldc + n) * 4) : OOR);
+      }
+    }
+    if (BNSTAT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long m = m0 + crow(r, half);
+        zz[r] = ld32(rz, m < p.M ? (int)((m * 32 + n) * 4) : OOR);
       }
     }
     float4 an[NQ];
@@ -161,14 +175,35 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(const RowGemm p) {
         float v = acc[0][r];
         if (p.accumulate) v += c0[r];
         st32(rc, ok ? (int)((m * p.ldc + n) * 4) : OOR, v);
+        if (BNSTAT && ok) {
+          bs0 += v;
+          bs1 += v * ((zz[r] - bmu) * brs);
+        }
       }
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) a[q] = an[q];
   }
+  if (BNSTAT) {
+    // lane halves hold disjoint rows of the same channel: fold half 1 onto half 0 (fixed order)
+    bs0 += __shfl_xor(bs0, 32);
+    bs1 += __shfl_xor(bs1, 32);
+    if (half == 0) {
+      p.bn_part[(long)gw * 64 + col] = bs0;
+      p.bn_part[(long)gw * 64 + 32 + col] = bs1;
+    }
+  }
 }
 
-template <int KH, bool GATE>
+inline int rowgemm_grid(int M, int ntiles, bool gate) {
+  const int nchunks = (M + 31) / 32;
+  int waves = nchunks * (gate ? 1 : ntiles);
+  const int cap = 256 * 8;
+  if (waves > cap) waves = cap;
+  return (waves + 3) / 4;  // 4 | 4*grid, so every tile gets grid*4/ntiles waves
+}
+
+template <int KH, bool GATE, bool BNSTAT = false>
 int launch(const RowGemm& p, hipStream_t s) {
   GWN_REQUIRE((long)p.a_rows * p.lda * 4 < 0x7fff0000L && (long)p.M * p.ldc * 4 < 0x7fff0000L &&
                   (long)p.M * p.ld_aux * 4 < 0x7fff0000L && (long)p.M * p.ld_aux2 * 4 < 0x7fff0000L,
@@ -177,12 +212,11 @@ int launch(const RowGemm& p, hipStream_t s) {
   // 8 waves per CU (2 per SIMD at ~200 VGPRs), grid-stride over the chunks; the wave count is
   // a multiple of ntiles so every tile gets the same number of waves
   GWN_REQUIRE(p.ntiles == 1 || p.ntiles == 2 || p.ntiles == 4, "rowgemm: N must be 32, 64 or 128");
-  int waves = nchunks * (GATE ? 1 : p.ntiles);
-  const int cap = 256 * 8;
-  if (waves > cap) waves = cap;
-  const int grid = (waves + 3) / 4;  // 4 | 4*grid, so every tile gets grid*4/ntiles waves
+  GWN_REQUIRE(!BNSTAT || (p.ntiles == 1 && p.ldc == 32), "rowgemm: BN statistics need N = ldc = 32");
+  (void)nchunks;
+  const int grid = rowgemm_grid(p.M, p.ntiles, GATE);
   const size_t lds = GATE ? (size_t)64 * (2 * KH + 4) * sizeof(float) : 0;
-  rowgemm_kernel<KH, GATE><<<grid, 256, lds, s>>>(p);
+  rowgemm_kernel<KH, GATE, BNSTAT><<<grid, 256, lds, s>>>(p);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -215,7 +249,14 @@ int gwn_rowgemm_tcn_bwd_data(const gwn_tcn_bwd_args* a, hipStream_t s) {
   p.A = a->dfg; p.lda = 2 * c; p.a_rows = t_out * P; p.shift = -(long)a->dilation * P; p.a_tap = 0;
   // B(k = tap*2c + j, n = ci) = w_fg[j][tap*c + ci]
   p.B = a->w_fg; p.ldb_k = 2 * c; p.ldb_tap = c; p.ldb_n = 1;
-  p.C = a->dx; p.ldc = c; p.accumulate = a->accumulate_dx;
+  p.C = a->dx; p.ldc = c; p.accumulate = a->accumulate_dx; p.acc_row0 = a->acc_row0;
   p.M = a->t_in * P; p.ntiles = 1;
+  if (a->bn_sums) {
+    p.bn_z = a->bn_z; p.bn_mean = a->bn_mean; p.bn_rstd = a->bn_rstd; p.bn_part = a->workspace;
+    return launch<64, false, true>(p, s);
+  }
   return launch<64, false>(p, s);
 }
+
+// partial count of gwn_rowgemm_tcn_bwd_data's BN statistics ([n][2][32] in the workspace)
+int gwn_rowgemm_tcn_bwd_nparts(const gwn_tcn_bwd_args* a) { return 4 * rowgemm_grid(a->t_in * a->P, 1, false); }

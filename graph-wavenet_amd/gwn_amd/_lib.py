@@ -59,6 +59,8 @@ class TcnBwdArgs(ctypes.Structure):
         ("dx", c_void_p), ("accumulate_dx", c_int),
         ("workspace", c_void_p),
         ("skip_weight_grads", c_int),
+        ("dfg_ready", c_int), ("acc_row0", c_long),
+        ("bn_z", c_void_p), ("bn_mean", c_void_p), ("bn_rstd", c_void_p), ("bn_sums", c_void_p),
     ]
 
 
@@ -88,13 +90,24 @@ class GcnBwdArgs(ctypes.Structure):
         ("workspace", c_void_p),
         ("sup_t", ctypes.POINTER(c_void_p)),
         ("skip_weight_grads", c_int),
+        ("bn_dy", c_void_p), ("bn_z", c_void_p), ("bn_gamma", c_void_p), ("bn_mean", c_void_p),
+        ("bn_rstd", c_void_p), ("bn_sums", c_void_p), ("bn_dgamma", c_void_p), ("bn_dbeta", c_void_p),
+        ("dres", c_void_p), ("dh_out", c_void_p),
+        ("seed_ptr", c_void_p), ("salt", c_u64), ("drop_p", c_float),
+        ("fg", c_void_p), ("dskip", c_void_p), ("ld_dskip", c_long), ("skip_row0", c_int),
+        ("dfg", c_void_p),
     ]
+
+# ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time
+_STRUCTS = {"gwn_gemm_desc": GemmDesc, "gwn_tcn_args": TcnArgs, "gwn_tcn_bwd_args": TcnBwdArgs,
+            "gwn_gcn_args": GcnArgs, "gwn_gcn_bwd_args": GcnBwdArgs}
 
 
 # (name, restype, argtypes) of every exported entry point declared in include/gwn.h
 _SIGS = [
     ("gwn_version", c_int, []),
     ("gwn_last_error", ctypes.c_char_p, []),
+    ("gwn_abi_sizeof", c_long, [ctypes.c_char_p]),
     ("gwn_gemm", c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     ("gwn_gemm_workspace_floats", c_long, [c_int, c_int, c_int]),
     ("gwn_nconv", c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,
@@ -166,6 +179,10 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        for cname, st in _STRUCTS.items():
+            if lib.gwn_abi_sizeof(cname.encode()) != ctypes.sizeof(st):
+                raise GwnError("libgwn.so ABI mismatch: sizeof(%s) = %d, ctypes mirror %d (stale build?)"
+                               % (cname, lib.gwn_abi_sizeof(cname.encode()), ctypes.sizeof(st)))
         _lib = lib
     return _lib
 

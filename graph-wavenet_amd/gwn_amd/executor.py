@@ -289,6 +289,7 @@ class Executor:
             "dhc2": e(maxrows, cfg.W),
             "dadp": torch.zeros(cfg.NP, cfg.NP, device=self.device, dtype=F32),
             "metrics": e(4),
+            "bnsums": e(2 * C),  # BN-backward statistics handed from a layer's TCN backward to the next
             "bnpart": e(ts[0] * B * 3 * C),  # per-slice BN partials of one layer
         }
         lib = _lib.load()
@@ -448,6 +449,9 @@ class Executor:
         # layers' data path; the buffers they read (dh, dhcat, dfg) alternate by layer parity and a
         # layer reuses its parity's buffers only after the side stream finished the layer + 2.
         overlap = self._overlap_ok(acts)
+        # fused layer backward: BN backward in the gcn_bwd prologue, gate backward in its epilogue,
+        # the next BN's statistics in the TCN input-gradient epilogue (3 launches fewer per layer)
+        fuse = overlap and cfg.use_gcn and os.environ.get("GWN_FUSE_BWD", "1") != "0"
         main = torch.cuda.current_stream()
         side = self._side_stream() if overlap else None
         side_done = {}
@@ -464,11 +468,13 @@ class Executor:
             if overlap and (i + 2) in side_done:
                 main.wait_event(side_done[i + 2])
             dxg, ld_dxg, acc = None, 0, 0
+            drop = float(self.dropout) if (acts.training and cfg.use_gcn) else 0.0
             if dnext is not None:
-                lib.call("gwn_batchnorm_bwd", ptr(dnext), ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
-                         ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(self.gk("bn_g%d" % i)),
-                         ptr(self.gk("bn_b%d" % i)), ptr(dx), d * P, ptr(dh), ptr(self.seed), i,
-                         float(self.dropout) if (acts.training and cfg.use_gcn) else 0.0, ptr(ws), st)
+                if not fuse:
+                    lib.call("gwn_batchnorm_bwd", ptr(dnext), ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
+                             ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(self.gk("bn_g%d" % i)),
+                             ptr(self.gk("bn_b%d" % i)), ptr(dx), d * P, ptr(dh), ptr(self.seed), i,
+                             drop, ptr(ws), st)
                 gb = _lib.GcnBwdArgs(rows=rows, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
                                      sup=ctypes.cast(acts.sup_arr, ctypes.POINTER(ctypes.c_void_p)),
                                      ld_sup=cfg.NP,
@@ -480,6 +486,15 @@ class Executor:
                                      sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
                                      if acts.supT_arr is not None else None,
                                      skip_weight_grads=1 if overlap else 0)
+                if fuse:
+                    gb.dh = None
+                    gb.bn_dy, gb.bn_z = ptr(dnext), ptr(acts.Z[i])
+                    gb.bn_gamma, gb.bn_mean, gb.bn_rstd = ptr(self.pk("bn_g%d" % i)), ptr(acts.mean[i]), ptr(acts.rstd[i])
+                    gb.bn_sums, gb.bn_dgamma, gb.bn_dbeta = ptr(sc["bnsums"]), ptr(self.gk("bn_g%d" % i)), ptr(self.gk("bn_b%d" % i))
+                    gb.dres, gb.dh_out = dx.data_ptr() + 4 * d * P * C, ptr(dh)
+                    gb.seed_ptr, gb.salt, gb.drop_p = ptr(self.seed), i, drop
+                    gb.fg, gb.dskip, gb.ld_dskip = ptr(acts.FG[i]), sc["dskipcat"].data_ptr() + 4 * i * C, L * C
+                    gb.skip_row0, gb.dfg = (ts[i + 1] - tf) * P, ptr(dfg)
                 lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)
                 if overlap:
                     self._side_gcn_grads(main, side, acts, i, rows, dh, dhc, adp_index, first_adp, sc)
@@ -494,6 +509,12 @@ class Executor:
                                  dw_fg=ptr(self.gk("fg_w%d" % i)), db_fg=ptr(self.gk("fg_b%d" % i)),
                                  dx=ptr(dx), accumulate_dx=acc, workspace=ptr(ws),
                                  skip_weight_grads=1 if overlap else 0)
+            if fuse:
+                if dnext is not None:
+                    tb.dfg_ready, tb.acc_row0 = 1, d * P
+                if i >= 1:  # statistics of bn[i-1], whose output gradient is this dx
+                    tb.bn_z, tb.bn_mean, tb.bn_rstd = ptr(acts.Z[i - 1]), ptr(acts.mean[i - 1]), ptr(acts.rstd[i - 1])
+                    tb.bn_sums = ptr(sc["bnsums"])
             lib.call("gwn_gated_tcn_bwd", ctypes.byref(tb), st)
             if overlap:
                 side_done[i] = self._side_tcn_grads(main, side, acts, i, rows, dfg, sc)

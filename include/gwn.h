@@ -31,6 +31,10 @@ extern "C" {
 
 int gwn_version(void);
 const char* gwn_last_error(void);
+/* sizeof of the argument structs below, for bindings that mirror them (ctypes, cgo):
+ * "gwn_gemm_desc", "gwn_tcn_args", "gwn_tcn_bwd_args", "gwn_gcn_args", "gwn_gcn_bwd_args";
+ * -1 for an unknown name */
+long gwn_abi_sizeof(const char* struct_name);
 
 /* ---------------------------------------------------------------------------------------------
  * Generic fp32 MFMA GEMM:  C(m,n) = epi(alpha * sum_k A(m,k) * B(k,n)).
@@ -145,6 +149,17 @@ typedef struct gwn_tcn_bwd_args {
   /* 1 = data path only (dfg, dx); dW_fg / db_fg are left to a gwn_wgrad call of the caller
    * (e.g. on a second stream) */
   int skip_weight_grads;
+  /* --- optional fusions of the c == 32 row-GEMM path (zero / NULL = off) ---
+   * dfg_ready: dfg already holds the gate gradient (gwn_gcn_bwd's fused epilogue wrote it); the
+   *   element-wise gate backward is skipped and dxg / dskip are ignored.
+   * acc_row0: with accumulate_dx, dx rows < acc_row0 are overwritten rather than accumulated
+   *   (their residual part is zero, so nobody has to clear them first).
+   * bn_z / bn_mean / bn_rstd / bn_sums: BatchNorm-backward statistics of the layer below over the
+   *   FINAL dx (which is that BatchNorm's output gradient), from the same launch:
+   *   bn_sums[j] = sum_r dx[r][j],  bn_sums[c + j] = sum_r dx[r][j] * (bn_z[r][j] - mean[j]) * rstd[j]
+   *   (fixed-order partials in the workspace, then an in-order merge). */
+  int dfg_ready; long acc_row0;
+  const float* bn_z; const float* bn_mean; const float* bn_rstd; float* bn_sums;
 } gwn_tcn_bwd_args;
 int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t stream);
 long gwn_gated_tcn_bwd_workspace_floats(int t_in, int P, int c, int dilation);
@@ -200,6 +215,23 @@ typedef struct gwn_gcn_bwd_args {
   /* 1 = data path only (dhcat); dW_mlp / db_mlp / dadp are left to gwn_wgrad / gwn_gram calls of
    * the caller (e.g. on a second stream) */
   int skip_weight_grads;
+  /* --- optional fusions of the fused path (sup_t given, c == 32, n <= 512; NULL = off) ---
+   * BatchNorm backward prologue (replaces gwn_batchnorm_bwd for this layer): with bn_dy != NULL,
+   * dh is not read but computed per slice from the BN output gradient bn_dy [rows][c], the BN
+   * input bn_z [rows][c], its saved mean / rstd, gamma and bn_sums [2c] (sum dy, sum dy*xhat,
+   * e.g. gwn_gated_tcn_bwd's bn_sums):
+   *   dz = gamma*rstd*(dy - sums[j]/rows - xhat*sums[c+j]/rows),  dres[r][j] = dz,
+   *   dh_out[r][j] = dropout'(dz) (mask hash(seed, salt, r*c + j) >= drop_p, scale 1/(1-p)),
+   *   bn_dbeta = sums[0..c), bn_dgamma = sums[c..2c)           (identical to gwn_batchnorm_bwd) */
+  const float* bn_dy; const float* bn_z; const float* bn_gamma; const float* bn_mean;
+  const float* bn_rstd; const float* bn_sums; float* bn_dgamma; float* bn_dbeta;
+  float* dres; float* dh_out;
+  const unsigned long long* seed_ptr; unsigned long long salt; float drop_p;
+  /* gate backward epilogue (replaces the element-wise part of gwn_gated_tcn_bwd): with dfg != NULL
+   * the input gradient dxg is not stored to dhcat piece 0; instead, with g = dxg + dskip (dskip
+   * [rows - skip_row0][ld_dskip] for rows >= skip_row0, NULL = none) and fg = (tanh f, sigmoid s)
+   * interleaved [rows][2c]:  dfg[r][2j] = g*s*(1 - f^2),  dfg[r][2j+1] = g*f*s*(1 - s). */
+  const float* fg; const float* dskip; long ld_dskip; int skip_row0; float* dfg;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);

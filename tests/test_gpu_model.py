@@ -306,3 +306,38 @@ def test_trainer_step_is_deterministic(gpu):
         res.append((mets, eng.model._flat.clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.3])
+def test_fused_layer_backward_matches_unfused(gpu, monkeypatch, dropout):
+    """The fused layer backward (BN backward in the gcn_bwd prologue, gate backward in its
+    epilogue, BN statistics in the TCN input-gradient epilogue) against the separate-kernel
+    schedule (GWN_FUSE_BWD=0) on the same inputs and dropout masks: only the summation order of
+    the BN statistics differs."""
+    from gwn_amd import synthetic, util
+    from gwn_amd.engine import trainer
+    adj = synthetic.random_sensor_graph(207, seed=0)
+    sups = [torch.tensor(a, device=gpu) for a in synthetic.double_transition(adj)]
+    x, y = synthetic.synthetic_batch(8, 207, 12, seed=4)
+    grads = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("GWN_FUSE_BWD", fuse)
+        monkeypatch.setenv("GWN_GRAPHS", "0")
+        torch.manual_seed(999)
+        eng = trainer(util.StandardScaler(54.4, 19.5), 2, 12, 207, 32, dropout, 0.0, 0.0, gpu, sups, True, True,
+                      None, 4, 2)
+        eng.clip = None
+        eng.model.executor().seed.fill_(77)
+        eng.train(torch.tensor(x, device=gpu), torch.tensor(y, device=gpu))
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.detach().clone() for n, p in eng.model.named_parameters() if p.grad is not None})
+    assert set(grads[0]) == set(grads[1])
+    scale = max(float(v.abs().max()) for v in grads[1].values())
+    for k in grads[0]:
+        a, b = grads[0][k].double(), grads[1][k].double()
+        if _bn_cancelled(k) and dropout == 0.0:
+            assert float((a - b).abs().max()) <= 1e-5 * scale, k
+        elif b.norm() > 0:
+            assert float((a - b).norm() / b.norm()) <= 1e-5, k
+        else:
+            assert float(a.abs().max()) <= 1e-6, k
