@@ -25,6 +25,7 @@ namespace {
 constexpr int CH = 32;   // channels (one MFMA tile)
 constexpr int LDR = 33;  // LDS row stride (floats): conflict-free row and column reads
 constexpr int KB = 16;   // k-steps (32 nodes) per batch of the K loop
+constexpr int EPT = 16;  // epilogue elements per thread: np*32 / (64*np/32) = 16 for every n
 
 struct FusedFwd {
   const float* h; long ld_h;
@@ -266,17 +267,32 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
   // epilogue: bias, dropout (same counter hash as the GEMM epilogue: index m*32 + c), residual
   const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
   const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
-  for (int e = threadIdx.x; e < n * CH; e += blockDim.x) {
-    const int w = e >> 5, c = e & 31;
-    const long m = row0 + w;
-    float v = ys[w * LDR + c] + a.b_mlp[c];
-    if (a.drop_p > 0.0f) {
-      const float u = gwn_uniform(seed, a.salt, (unsigned long long)m * CH + c);
-      v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
+  {
+    // EPT elements per thread (np*32 = 16*blockDim): all residual loads are issued before the
+    // first store (the compiler cannot reorder loads across possibly aliasing stores itself)
+    const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
+    const float bias = a.b_mlp[c];
+    float res[EPT];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int w = min(wb + i * ws, n - 1);
+      res[i] = a.residual[(row0 + w) * CH + c];
     }
-    v += a.residual[m * CH + c];
-    a.z[m * CH + c] = v;
-    ys[w * LDR + c] = v;
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int w = wb + i * ws;
+      if (w < n) {
+        const long m = row0 + w;
+        float v = ys[w * LDR + c] + bias;
+        if (a.drop_p > 0.0f) {
+          const float u = gwn_uniform(seed, a.salt, (unsigned long long)m * CH + c);
+          v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
+        }
+        v += res[i];
+        a.z[m * CH + c] = v;
+        ys[w * LDR + c] = v;
+      }
+    }
   }
   if (a.bn_part == nullptr) return;
   __syncthreads();
@@ -328,16 +344,24 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
     }
     const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
     const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
-    const int c = threadIdx.x & 31;  // blockDim.x is a multiple of 32: c is fixed per thread
-    const float mu = a.bn_mean[c], rs = a.bn_rstd[c];
+    const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
+    const float mu = a.bn_mean[c], rs = a.bn_rstd[c], gm = a.bn_gamma[c];
     const float k1 = a.bn_sums[c] * a.inv_rows, k2 = a.bn_sums[CH + c] * a.inv_rows;
-    for (int e = threadIdx.x; e < np * CH; e += blockDim.x) {
-      const int w = e >> 5;
+    float dy[EPT], zv[EPT];  // all loads before the first store (see the forward epilogue)
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const long idx = (row0 + min(wb + i * ws, n - 1)) * CH + c;
+      dy[i] = a.bn_dy[idx];
+      zv[i] = a.bn_z[idx];
+    }
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int w = wb + i * ws;  // < np
       float v = 0.0f;
       if (w < n) {
         const long idx = (row0 + w) * CH + c;
-        const float xhat = (a.bn_z[idx] - mu) * rs;
-        const float dz = a.bn_gamma[c] * rs * (a.bn_dy[idx] - k1 - xhat * k2);
+        const float xhat = (zv[i] - mu) * rs;
+        const float dz = gm * rs * (dy[i] - k1 - xhat * k2);
         a.dres[idx] = dz;
         v = dz;
         if (a.drop_p > 0.0f) {
@@ -381,17 +405,27 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
   __syncthreads();  // every wave finished reading buf
   acc_to_lds(buf, dx, w0, lane);
   __syncthreads();
-  for (int e = threadIdx.x; e < n * CH; e += blockDim.x) {
-    const int w = e >> 5, c = e & 31;
-    const long m = row0 + w;
-    float g = buf[w * LDR + c];
-    if (a.dskip && m >= a.skip_row0) g += a.dskip[(m - a.skip_row0) * a.ld_dskip + c];
-    const float2 fs = *(const float2*)(a.fg + m * 2 * CH + 2 * c);
-    const float f = fs.x, sg = fs.y;
-    float2 o;
-    o.x = g * sg * (1.0f - f * f);
-    o.y = g * f * sg * (1.0f - sg);
-    *(float2*)(a.dfg + m * 2 * CH + 2 * c) = o;
+  const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
+  float2 fs[EPT];
+  float dsk[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const long m = row0 + min(wb + i * ws, n - 1);
+    fs[i] = *(const float2*)(a.fg + m * 2 * CH + 2 * c);
+    dsk[i] = (a.dskip && m >= a.skip_row0) ? a.dskip[(m - a.skip_row0) * a.ld_dskip + c] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int w = wb + i * ws;
+    if (w < n) {
+      const long m = row0 + w;
+      const float g = buf[w * LDR + c] + dsk[i];
+      const float f = fs[i].x, sg = fs[i].y;
+      float2 o;
+      o.x = g * sg * (1.0f - f * f);
+      o.y = g * f * sg * (1.0f - sg);
+      *(float2*)(a.dfg + m * 2 * CH + 2 * c) = o;
+    }
   }
 }
 

@@ -227,23 +227,27 @@ __global__ void bn_bwd_partial_kernel(const float* dy, const float* z, const flo
   }
 }
 
-// 8 columns per block x 32 partial lanes, then a fixed-order tree over the lanes.
-__global__ void colsum_final_kernel(const float* partial, int nparts, int ncol, float* out,
-                                    int accumulate) {
+// Many partials (e.g. one per wave of a rowgemm launch): one block per column, 256 lanes each
+// summing a strided subset, then a fixed-order tree.
+__global__ void colsum_final_wide_kernel(const float* partial, int nparts, int ncol, float* out,
+                                         int accumulate) {
   __shared__ float sh[256];
-  const int cj = threadIdx.x & 7, lane = threadIdx.x >> 3;
-  const int j = blockIdx.x * 8 + cj;
-  float s = 0.0f;
-  if (j < ncol)
-    for (int i = lane; i < nparts; i += 32) s += partial[(long)i * ncol + j];
-  sh[threadIdx.x] = s;
+  const int j = blockIdx.x;
+  float s0 = 0.0f, s1 = 0.0f;
+  int i = threadIdx.x;
+  for (; i + 256 < nparts; i += 512) {
+    s0 += partial[(long)i * ncol + j];
+    s1 += partial[(long)(i + 256) * ncol + j];
+  }
+  if (i < nparts) s0 += partial[(long)i * ncol + j];
+  sh[threadIdx.x] = s0 + s1;
   __syncthreads();
 #pragma unroll
-  for (int w = 16; w > 0; w >>= 1) {
-    if (lane < w) sh[threadIdx.x] += sh[threadIdx.x + 8 * w];
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
     __syncthreads();
   }
-  if (lane == 0 && j < ncol) out[j] = accumulate ? out[j] + sh[cj] : sh[cj];
+  if (threadIdx.x == 0) out[j] = accumulate ? out[j] + sh[0] : sh[0];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -778,8 +782,8 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
   if (c == 32 && aligned16(a->dfg) && aligned16(a->dx)) {
     rc = gwn_rowgemm_tcn_bwd_data(a, s);
     if (rc || !a->bn_sums) return rc;
-    colsum_final_kernel<<<(2 * c + 7) / 8, 256, 0, s>>>(a->workspace, gwn_rowgemm_tcn_bwd_nparts(a), 2 * c,
-                                                        a->bn_sums, 0);
+    colsum_final_wide_kernel<<<2 * c, 256, 0, s>>>(a->workspace, gwn_rowgemm_tcn_bwd_nparts(a), 2 * c,
+                                                   a->bn_sums, 0);
     GWN_CHECK_LAUNCH();
     return GWN_OK;
   }
@@ -800,7 +804,7 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
   bn_bwd_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(a->dx, a->bn_z, a->bn_mean, a->bn_rstd, rows_in, c,
                                                    a->workspace);
   GWN_CHECK_LAUNCH();
-  colsum_final_kernel<<<(2 * c + 7) / 8, 256, 0, s>>>(a->workspace, RED_BLOCKS, 2 * c, a->bn_sums, 0);
+  colsum_final_wide_kernel<<<2 * c, 256, 0, s>>>(a->workspace, RED_BLOCKS, 2 * c, a->bn_sums, 0);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -982,7 +986,7 @@ int gwn_batchnorm_bwd(const float* dy, const float* z, int rows, int c, const fl
   float* sums = ws + (long)RED_BLOCKS * 3 * c;  // [2][c]: sum dy, sum dy*xhat
   bn_bwd_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(dy, z, save_mean, save_rstd, rows, c, part);
   GWN_CHECK_LAUNCH();
-  colsum_final_kernel<<<(2 * c + 7) / 8, 256, 0, s>>>(part, RED_BLOCKS, 2 * c, sums, 0);
+  colsum_final_wide_kernel<<<2 * c, 256, 0, s>>>(part, RED_BLOCKS, 2 * c, sums, 0);
   GWN_CHECK_LAUNCH();
   const long total = (long)rows * c + (long)res_row0 * c;
   bn_bwd_apply_kernel<<<grid_for(total), 256, 0, s>>>(dy, z, rows, c, gamma, save_mean, save_rstd, sums,
@@ -1002,7 +1006,7 @@ int gwn_colsum(const float* dy, int rows, int ncol, long ld, float* out, int acc
   GWN_REQUIRE(rows > 0 && ncol > 0, "colsum: bad shape");
   colsum_partial_kernel<0><<<RED_BLOCKS, 256, 0, s>>>(dy, ld, nullptr, 0, nullptr, nullptr, rows, ncol, ws);
   GWN_CHECK_LAUNCH();
-  colsum_final_kernel<<<(ncol + 7) / 8, 256, 0, s>>>(ws, RED_BLOCKS, ncol, out, accumulate);
+  colsum_final_wide_kernel<<<ncol, 256, 0, s>>>(ws, RED_BLOCKS, ncol, out, accumulate);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

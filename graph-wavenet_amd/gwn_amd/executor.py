@@ -311,6 +311,8 @@ class Executor:
         side_need = [lib.gwn_wgrad_workspace_floats(maxrows, C, cfg.W),
                      lib.gwn_wgrad_workspace_floats(maxrows, 2 * C, 2 * C),
                      lib.gwn_gram_workspace_floats(N, maxrows // N)]
+        for (M_, N_, K_) in ((cfg.O, cfg.E, tf * P), (cfg.E, cfg.S, tf * P), (cfg.S, L * C, tf * P)):
+            side_need.append(lib.gwn_gemm_workspace_floats(M_, N_, _ksplit(M_, N_, K_)))
         s["ws_side"] = e(int(max(side_need)) + 16)
         self._scratch[key] = s
         return s
@@ -433,27 +435,39 @@ class Executor:
         lib = _lib
         dout = dout.contiguous()
         lib.call("gwn_from_nchw", ptr(dout), B, O, N, tf, ptr(sc["dy"]), st)
-        # end_conv_2
-        wgrad(sc["dy"], O, acts.e1, E, rows_f, self.gk("e2_w"), ws, self.gk("e2_b"))
-        gemm(sc["dy"], O, 1, self.pk("e2_w"), E, 1, sc["de1"], E, 1, M=rows_f, N=E, K=O,
-             epi=2, mask=acts.e1, ldmask=E)
-        # end_conv_1
-        wgrad(sc["de1"], E, acts.skr, S, rows_f, self.gk("e1_w"), ws, self.gk("e1_b"))
-        gemm(sc["de1"], E, 1, self.pk("e1_w"), S, 1, sc["dsk"], S, 1, M=rows_f, N=S, K=E,
-             epi=2, mask=acts.skr, ldmask=S)
-        # skip convs
-        wgrad(sc["dsk"], S, acts.skipcat, L * C, rows_f, self.gk("skip_w"), ws, self.gk("skip_bsum"))
-        gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * C, 1, sc["dskipcat"], L * C, 1, M=rows_f, N=L * C, K=S)
-        # layers in reverse.  With the fused data path (C = 32) the weight / adjacency gradients
-        # (gwn_wgrad, gwn_gram: off the critical path) run on a second stream, overlapping the next
-        # layers' data path; the buffers they read (dh, dhcat, dfg) alternate by layer parity and a
-        # layer reuses its parity's buffers only after the side stream finished the layer + 2.
+        # Weight / adjacency gradients (head wgrads, gwn_wgrad, gwn_gram: off the critical path)
+        # run on a second stream when the fused data path is on (C = 32), overlapping the input
+        # gradients that follow; in the layers the buffers they read (dh, dhcat, dfg) alternate by
+        # layer parity and a layer reuses its parity's buffers only after the side stream finished
+        # the layer + 2.
         overlap = self._overlap_ok(acts)
         # fused layer backward: BN backward in the gcn_bwd prologue, gate backward in its epilogue,
         # the next BN's statistics in the TCN input-gradient epilogue (3 launches fewer per layer)
-        fuse = overlap and cfg.use_gcn and os.environ.get("GWN_FUSE_BWD", "1") != "0"
+        fuse = self._fuse_ok(acts)
         main = torch.cuda.current_stream()
         side = self._side_stream() if overlap else None
+
+        def head_wgrad(dY, J, X, Kc, w, b):
+            if not overlap:
+                wgrad(dY, J, X, Kc, rows_f, w, ws, b)
+                return
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                wgrad(dY, J, X, Kc, rows_f, w, sc["ws_side"], b)
+
+        # end_conv_2
+        head_wgrad(sc["dy"], O, acts.e1, E, self.gk("e2_w"), self.gk("e2_b"))
+        gemm(sc["dy"], O, 1, self.pk("e2_w"), E, 1, sc["de1"], E, 1, M=rows_f, N=E, K=O,
+             epi=2, mask=acts.e1, ldmask=E)
+        # end_conv_1
+        head_wgrad(sc["de1"], E, acts.skr, S, self.gk("e1_w"), self.gk("e1_b"))
+        gemm(sc["de1"], E, 1, self.pk("e1_w"), S, 1, sc["dsk"], S, 1, M=rows_f, N=S, K=E,
+             epi=2, mask=acts.skr, ldmask=S)
+        # skip convs
+        head_wgrad(sc["dsk"], S, acts.skipcat, L * C, self.gk("skip_w"), self.gk("skip_bsum"))
+        gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * C, 1, sc["dskipcat"], L * C, 1, M=rows_f, N=L * C, K=S)
         side_done = {}
         dnext = None
         bufs = [sc["dxa"], sc["dxb"]]
@@ -533,6 +547,11 @@ class Executor:
         cfg = self.cfg
         return (os.environ.get("GWN_OVERLAP", "1") != "0" and cfg.C == 32 and cfg.W % 32 == 0
                 and acts.supT_arr is not None)
+
+    def _fuse_ok(self, acts):
+        cfg = self.cfg
+        return (os.environ.get("GWN_FUSE_BWD", "1") != "0" and cfg.use_gcn and cfg.C == 32
+                and cfg.W % 32 == 0 and cfg.N <= 512 and acts.supT_arr is not None)
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:

@@ -61,8 +61,24 @@ def main():
                              adp_index=K - 1, dadp=dadp.data_ptr(), accumulate_dadp=0, workspace=ws.data_ptr(),
                              sup_t=ctypes.cast(arrT, ctypes.POINTER(ctypes.c_void_p)))
         flop = T * B * (K * 2 * 2.0 * C * N * N + 2.0 * (2 * K + 1) * C * C * N)
+        # data path only, plain and with the BN-backward prologue + gate-backward epilogue
+        gd = _lib.GcnBwdArgs.from_buffer_copy(gb)
+        gd.skip_weight_grads = 1
+        gf = _lib.GcnBwdArgs.from_buffer_copy(gd)
+        zb, dres, dho = torch.randn(rows, C, device=dev), torch.empty(rows, C, device=dev), torch.empty(rows, C, device=dev)
+        gam, mu, rs, sums = (torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev), torch.rand(C, device=dev) + 0.5,
+                             torch.randn(2 * C, device=dev))
+        dgam, dbet = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        fgb, dskb, dfgb = torch.rand(rows, 2 * C, device=dev), torch.randn(rows, 8 * C, device=dev), torch.empty(rows, 2 * C, device=dev)
+        gf.bn_dy, gf.bn_z, gf.bn_gamma, gf.bn_mean, gf.bn_rstd, gf.bn_sums = (dh.data_ptr(), zb.data_ptr(), gam.data_ptr(),
+                                                                              mu.data_ptr(), rs.data_ptr(), sums.data_ptr())
+        gf.bn_dgamma, gf.bn_dbeta, gf.dres, gf.dh_out = dgam.data_ptr(), dbet.data_ptr(), dres.data_ptr(), dho.data_ptr()
+        gf.seed_ptr, gf.salt, gf.drop_p = seed.data_ptr(), 3, 0.3
+        gf.fg, gf.dskip, gf.ld_dskip, gf.skip_row0, gf.dfg = fgb.data_ptr(), dskb.data_ptr(), 8 * C, 0, dfgb.data_ptr()
         for name, fn in (("fwd", lambda: _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)),
-                         ("bwd", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gb), st))):
+                         ("bwd", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)),
+                         ("bwd-data", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gd), st)),
+                         ("bwd-data+bn+gate", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gf), st))):
             for _ in range(3):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -72,7 +88,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             us = 1000.0 * e0.elapsed_time(e1) / args.reps
-            print("gcn %s T=%2d slices=%4d: %8.1f us  %6.1f TFLOP/s (fwd-equivalent flops)"
+            print("gcn %-16s T=%2d slices=%4d: %8.1f us  %6.1f TFLOP/s (fwd-equivalent flops)"
                   % (name, T, T * B, us, flop / us / 1e6), flush=True)
         del dh, dhc
 
