@@ -109,6 +109,8 @@ _SIGS = [
     ("gwn_last_error", ctypes.c_char_p, []),
     ("gwn_abi_sizeof", c_long, [ctypes.c_char_p]),
     ("gwn_gemm", c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
+    ("gwn_gemm_nt", c_int, [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int,
+                            c_void_p, c_int, c_void_p, c_long, c_void_p]),
     ("gwn_gemm_workspace_floats", c_long, [c_int, c_int, c_int]),
     ("gwn_nconv", c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,
                           c_int, c_int, c_int, c_void_p]),

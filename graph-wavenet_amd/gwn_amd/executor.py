@@ -52,7 +52,10 @@ class PackedLayout:
             segs[name] = (len(pidx), numel)
 
         def gather_seg(name, src_index):
-            # src_index: LongTensor of flat indices, in packed order
+            # src_index: LongTensor of flat indices, in packed order.  Segments start 16-B aligned
+            # (the row-tile GEMMs load weights as float4).
+            while len(pidx) % 4:
+                pidx.append(0)
             segs[name] = (len(pidx), src_index.numel())
             pidx.extend(src_index.tolist())
 
@@ -131,6 +134,10 @@ class PackedLayout:
         map_grad("end_conv_2.weight", seg_index("e2_w", (O, E, 1, 1)))
         gather_seg("e2_b", flat_range("end_conv_2.bias"))
         map_grad("end_conv_2.bias", seg_index("e2_b", (O,)))
+        # transposed copies of the head weights for the input gradients (NT GEMMs, no grads)
+        gather_seg("skip_wT", sk.reshape(S, L * C).t().contiguous().reshape(-1))
+        gather_seg("e1_wT", flat_range("end_conv_1.weight").reshape(E, S).t().contiguous().reshape(-1))
+        gather_seg("e2_wT", flat_range("end_conv_2.weight").reshape(O, E).t().contiguous().reshape(-1))
         self.zero_slot = len(pidx)
         pidx.append(0)
         self.total = len(pidx)
@@ -410,13 +417,21 @@ class Executor:
                          ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(ws), st)
         rows_f = tf * P
         # skip sum (relu'd) -> end_conv_1 (+relu) -> end_conv_2
-        gemm(acts.skipcat, L * C, 1, self.pk("skip_w"), 1, L * C, acts.skr, cfg.S, 1,
-             M=rows_f, N=cfg.S, K=L * C, bias=self.pk("skip_bsum"), relu=1)
-        gemm(acts.skr, cfg.S, 1, self.pk("e1_w"), 1, cfg.S, acts.e1, cfg.E, 1,
-             M=rows_f, N=cfg.E, K=cfg.S, bias=self.pk("e1_b"), relu=1)
-        gemm(acts.e1, cfg.E, 1, self.pk("e2_w"), 1, cfg.E, acts.y, cfg.O, 1,
-             M=rows_f, N=cfg.O, K=cfg.E, bias=self.pk("e2_b"),
-             ksplit=_ksplit_thin(rows_f, cfg.O, cfg.E), part=ws)
+        if self._head_nt():
+            gemm_nt(acts.skipcat, L * C, self.pk("skip_w"), L * C, acts.skr, cfg.S, rows_f, cfg.S, L * C,
+                    bias=self.pk("skip_bsum"), relu=1)
+            gemm_nt(acts.skr, cfg.S, self.pk("e1_w"), cfg.S, acts.e1, cfg.E, rows_f, cfg.E, cfg.S,
+                    bias=self.pk("e1_b"), relu=1)
+            gemm_nt(acts.e1, cfg.E, self.pk("e2_w"), cfg.E, acts.y, cfg.O, rows_f, cfg.O, cfg.E,
+                    bias=self.pk("e2_b"))
+        else:
+            gemm(acts.skipcat, L * C, 1, self.pk("skip_w"), 1, L * C, acts.skr, cfg.S, 1,
+                 M=rows_f, N=cfg.S, K=L * C, bias=self.pk("skip_bsum"), relu=1)
+            gemm(acts.skr, cfg.S, 1, self.pk("e1_w"), 1, cfg.S, acts.e1, cfg.E, 1,
+                 M=rows_f, N=cfg.E, K=cfg.S, bias=self.pk("e1_b"), relu=1)
+            gemm(acts.e1, cfg.E, 1, self.pk("e2_w"), 1, cfg.E, acts.y, cfg.O, 1,
+                 M=rows_f, N=cfg.O, K=cfg.E, bias=self.pk("e2_b"),
+                 ksplit=_ksplit_thin(rows_f, cfg.O, cfg.E), part=ws)
         out = torch.empty(B, cfg.O, N, tf, device=self.device, dtype=F32)
         lib.call("gwn_to_nchw", ptr(acts.y), B, cfg.O, N, tf, ptr(out), st)
         return out, acts
@@ -457,17 +472,27 @@ class Executor:
             with torch.cuda.stream(side):
                 wgrad(dY, J, X, Kc, rows_f, w, sc["ws_side"], b)
 
+        nt = self._head_nt()
         # end_conv_2
         head_wgrad(sc["dy"], O, acts.e1, E, self.gk("e2_w"), self.gk("e2_b"))
-        gemm(sc["dy"], O, 1, self.pk("e2_w"), E, 1, sc["de1"], E, 1, M=rows_f, N=E, K=O,
-             epi=2, mask=acts.e1, ldmask=E)
+        if nt:
+            gemm_nt(sc["dy"], O, self.pk("e2_wT"), O, sc["de1"], E, rows_f, E, O, mask=acts.e1, ldmask=E)
+        else:
+            gemm(sc["dy"], O, 1, self.pk("e2_w"), E, 1, sc["de1"], E, 1, M=rows_f, N=E, K=O,
+                 epi=2, mask=acts.e1, ldmask=E)
         # end_conv_1
         head_wgrad(sc["de1"], E, acts.skr, S, self.gk("e1_w"), self.gk("e1_b"))
-        gemm(sc["de1"], E, 1, self.pk("e1_w"), S, 1, sc["dsk"], S, 1, M=rows_f, N=S, K=E,
-             epi=2, mask=acts.skr, ldmask=S)
+        if nt:
+            gemm_nt(sc["de1"], E, self.pk("e1_wT"), E, sc["dsk"], S, rows_f, S, E, mask=acts.skr, ldmask=S)
+        else:
+            gemm(sc["de1"], E, 1, self.pk("e1_w"), S, 1, sc["dsk"], S, 1, M=rows_f, N=S, K=E,
+                 epi=2, mask=acts.skr, ldmask=S)
         # skip convs
         head_wgrad(sc["dsk"], S, acts.skipcat, L * C, self.gk("skip_w"), self.gk("skip_bsum"))
-        gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * C, 1, sc["dskipcat"], L * C, 1, M=rows_f, N=L * C, K=S)
+        if nt:
+            gemm_nt(sc["dsk"], S, self.pk("skip_wT"), S, sc["dskipcat"], L * C, rows_f, L * C, S)
+        else:
+            gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * C, 1, sc["dskipcat"], L * C, 1, M=rows_f, N=L * C, K=S)
         side_done = {}
         dnext = None
         bufs = [sc["dxa"], sc["dxb"]]
@@ -547,6 +572,12 @@ class Executor:
         cfg = self.cfg
         return (os.environ.get("GWN_OVERLAP", "1") != "0" and cfg.C == 32 and cfg.W % 32 == 0
                 and acts.supT_arr is not None)
+
+    def _head_nt(self):
+        """Row-tile NT GEMMs for the head (K dims / leading dims multiples of 4)."""
+        cfg = self.cfg
+        return (os.environ.get("GWN_HEAD_NT", "1") != "0"
+                and all(v % 4 == 0 for v in (cfg.O, cfg.S, cfg.E, cfg.L * cfg.C)))
 
     def _fuse_ok(self, acts):
         cfg = self.cfg
@@ -631,6 +662,12 @@ def gemm(A, lda_m, lda_k, B, ldb_k, ldb_n, Cout, ldc_m, ldc_n, M, N, K, bias=Non
     d.part = ptr(part)
     d.ones_out = ptr(ones_out)
     _lib.call("gwn_gemm", ctypes.byref(d), _lib.stream())
+
+
+def gemm_nt(A, lda, B, ldb, Cout, ldc, M, N, K, bias=None, relu=0, mask=None, ldmask=0):
+    """Cout[m][n] = epi(sum_k A[m][k] B[n][k])  (gwn_gemm_nt)."""
+    _lib.call("gwn_gemm_nt", ptr(A), lda, ptr(B), ldb, ptr(Cout), ldc, M, N, K, ptr(bias), relu, ptr(mask),
+              ldmask, _lib.stream())
 
 
 def wgrad(dY, J, X, Kc, rows, out, ws, bias_out=None):

@@ -73,6 +73,14 @@ typedef struct gwn_gemm_desc {
 int gwn_gemm(const gwn_gemm_desc* desc, hipStream_t stream);
 long gwn_gemm_workspace_floats(int M, int N, int ksplit);
 
+/* Row-tile "NT" GEMM for 1x1 convs over channels-last rows (the output head, model.py:216-222,
+ * 238-240, and with a transposed weight their input gradients):
+ *   C[m][n] = epi( sum_k A[m][k] * B[n][k] ),  epi: + bias[n] (NULL = none), relu (0/1), then
+ *   mask: v = (mask[m][ldmask] > 0) ? v : 0 (NULL = none; the relu backward).
+ * A [M][lda], B [N][ldb] K-contiguous, K / lda / ldb multiples of 4, A and B 16-B aligned. */
+int gwn_gemm_nt(const float* A, long lda, const float* B, long ldb, float* C, long ldc, int M, int N, int K,
+                const float* bias, int relu, const float* mask, long ldmask, hipStream_t stream);
+
 /* ---------------------------------------------------------------------------------------------
  * nconv (model.py:12-14): einsum('ncvl,vw->ncwl', x, A), i.e. for every slice s
  *   y_s[w][c] = sum_v A[v][w] * x_s[v][c]            (transpose_a = 1, the forward)

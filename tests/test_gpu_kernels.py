@@ -287,3 +287,34 @@ def test_masked_loss_and_grad(gpu):
     np.testing.assert_allclose(m[:3], [mae.item(), mape.item(), rmse.item()], rtol=2e-5)
     assert rel_err(dout.cpu().numpy(), oc.grad.numpy()) < 1e-5
     del real_t
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 12, 512), (1000, 12, 512), (1000, 512, 12), (777, 256, 256),
+                                   (13248, 512, 256), (300, 200, 36), (129, 64, 4)])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu", "mask"])
+def test_gemm_nt(gpu, M, N, K, epi):
+    """gwn_gemm_nt (head convs and their input gradients) vs fp64: C = epi(A B^T), ragged tiles,
+    K < one LDS tile, N < one MFMA tile; columns of C beyond N untouched."""
+    from gwn_amd import _lib
+    torch.manual_seed(M + 3 * N + 7 * K)
+    A = torch.randn(M, K, dtype=torch.float64)
+    Bm = torch.randn(N, K, dtype=torch.float64)
+    bias = torch.randn(N, dtype=torch.float64)
+    mask = torch.randn(M, N, dtype=torch.float64)
+    ref = A @ Bm.t()
+    if epi == "bias_relu":
+        ref = torch.clamp(ref + bias, min=0.0)
+    elif epi == "mask":
+        ref = torch.where(mask > 0, ref, torch.zeros_like(ref))
+    ldc = N + 4
+    Cd = torch.full((M, ldc), 7.0, device=gpu)
+    Ad, Bd = A.float().to(gpu), Bm.float().to(gpu)
+    bd, md = bias.float().to(gpu), mask.float().to(gpu)
+    _lib.call("gwn_gemm_nt", Ad.data_ptr(), K, Bd.data_ptr(), K, Cd.data_ptr(), ldc, M, N, K,
+              bd.data_ptr() if epi == "bias_relu" else None, 1 if epi == "bias_relu" else 0,
+              md.data_ptr() if epi == "mask" else None, N, _lib.stream())
+    torch.cuda.synchronize()
+    got = Cd.cpu().double()
+    assert torch.all(got[:, N:] == 7.0)
+    scale = float(ref.abs().max()) + 1e-30
+    assert float((got[:, :N] - ref).abs().max()) / scale <= 2e-6
