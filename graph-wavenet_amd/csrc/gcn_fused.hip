@@ -2,8 +2,8 @@
 // and its backward, for C = 32 channels and N <= 512 nodes.
 //
 // One workgroup = one slice (a (t, b) pair: N nodes x 32 channels, contiguous rows of the
-// channels-last activation).  Wave w owns node tile [32w, 32w+32).  All products run on
-// v_mfma_f32_32x32x2_f32 in the transposed orientation
+// channels-last activation).  All products run on v_mfma_f32_32x32x2_f32 in the transposed
+// orientation
 //     D'[c][w] = sum_v X[v][c] * G[v][w]            (M = channel, N = node, K = node)
 // so that
 //   * the A operand X[v][c] is an LDS row read (conflict-free, rows padded to 33 floats),
@@ -13,6 +13,14 @@
 //     of the next product that contracts over channels (the 1x1 mlp): no lane shuffles.
 // The node features never leave LDS between hops; only the pieces needed by the backward
 // (x1, x2 per support) and the layer output are written to HBM, as full coalesced rows.
+//
+// Two wave layouts of the same schedule:
+//   * n <= 256 ("4-wave", default): 256 threads = one wave per SIMD; wave v owns the node tiles
+//     {v, v + 4}.  Every LDS A value feeds two MFMAs, every wave runs two independent accumulator
+//     chains, and the W fragments of the mlp are loaded once for both tiles.  A tile slot beyond
+//     the last node tile (e.g. tile 7 for n <= 224) is computed on finite don't-care columns and
+//     never stored, so the four waves run the same instruction stream (no divergent barriers).
+//   * otherwise ("tile-wave"): one wave per 32-node tile (up to 16 waves, n <= 512).
 //
 // Contract on the supports: [np][ld] with np = 32*ceil(n/32) <= ld, ZERO outside [n][n]
 // (the executor keeps padded copies), so the K loop runs whole 32-node batches unguarded.
@@ -25,7 +33,9 @@ namespace {
 constexpr int CH = 32;   // channels (one MFMA tile)
 constexpr int LDR = 33;  // LDS row stride (floats): conflict-free row and column reads
 constexpr int KB = 16;   // k-steps (32 nodes) per batch of the K loop
-constexpr int EPT = 16;  // epilogue elements per thread: np*32 / (64*np/32) = 16 for every n
+constexpr int EPT = 16;  // tile-wave epilogue elements per thread: np*32 / (64*np/32) = 16 for every n
+constexpr int EPT4 = 32; // 4-wave epilogue elements per thread: covers np <= 256 with 256 threads
+constexpr int TPW = 2;   // node tiles per wave in the 4-wave layout
 
 struct FusedFwd {
   const float* h; long ld_h;
@@ -34,6 +44,9 @@ struct FusedFwd {
   const float* residual; float* z; float* bn_part;
   const unsigned long long* seed_ptr; unsigned long long salt; float drop_p;
   int n;
+  int store_pieces;  // 0: hop outputs not written to h (inference: no backward follows)
+  // eval BatchNorm folded into the epilogue (running statistics): x_out = bn(z); z not written
+  const float* bn_rm; const float* bn_rv; const float* bn_g; const float* bn_b; float bn_eps; float* x_out;
 };
 
 struct FusedBwd {
@@ -54,8 +67,8 @@ struct FusedBwd {
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
 #ifndef GWN_EXP
-#define GWN_EXP 0  // kernel experiments (timing only, wrong results): 1 no G loads, 2 no x1/x2 stores,
-#endif             // 4 no mlp, 8 no epilogue
+#define GWN_EXP 0  // kernel experiments (timing only, wrong results): 1 no G loads
+#endif
 
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
 #if GWN_EXP & 1
@@ -108,7 +121,7 @@ __device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int 
   auto lds_batch = [&](int kb, float* av) {
     const float* bp = buf + (32 * kb + half) * LDR + col;
 #pragma unroll
-    for (int j = 0; j < KB; ++j) av[j] = (GWN_EXP & 16) ? ga[j] * 0.5f : bp[2 * j * LDR];
+    for (int j = 0; j < KB; ++j) av[j] = bp[2 * j * LDR];
   };
   auto g_batch = [&](int kb, float* g) {
 #pragma unroll
@@ -194,13 +207,6 @@ __device__ __forceinline__ void acc_to_global(float* dst, long ld, const f32x16&
   for (int r = 0; r < 16; ++r) p[crow(r, half)] = d[r];
 }
 
-__device__ __forceinline__ void lds_to_global(const float* buf, float* dst, long ld, int n) {
-  for (int e = threadIdx.x; e < n * CH; e += blockDim.x) {
-    const int w = e >> 5, c = e & 31;
-    dst[(long)w * ld + c] = buf[w * LDR + c];
-  }
-}
-
 __device__ __forceinline__ void global_to_lds(const float* src, long ld, int n, int np, float* buf) {
   for (int e = threadIdx.x; e < np * CH; e += blockDim.x) {
     const int w = e >> 5, c = e & 31;
@@ -214,6 +220,157 @@ __device__ __forceinline__ f32x16 zero16() {
   for (int r = 0; r < 16; ++r) z[r] = 0.0f;
   return z;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Shared prologue / epilogue bodies (NEPT rows-per-thread bound: wb + i*ws covers np rows)
+
+// forward epilogue on the mlp output in ys: bias, dropout (same counter hash as the GEMM
+// epilogue: index m*32 + c), residual -> z (+ per-slice BN partials), or -> bn(z) in eval mode
+template <int NEPT>
+__device__ __forceinline__ void fwd_epilogue(const FusedFwd& a, float* ys, float* red0, float* red1, long row0,
+                                             int n) {
+  const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
+  const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
+  const float bias = a.b_mlp[c];
+  float bmu = 0.0f, brs = 1.0f, bg = 1.0f, bb = 0.0f;
+  if (a.x_out) {  // eval BatchNorm, the arithmetic of bn_apply_kernel (ops.hip)
+    bmu = a.bn_rm[c];
+    brs = 1.0f / sqrtf(a.bn_rv[c] + a.bn_eps);
+    bg = a.bn_g[c];
+    bb = a.bn_b[c];
+  }
+  // all residual loads are issued before the first store (the compiler cannot reorder loads
+  // across possibly aliasing stores itself)
+  float res[NEPT];
+#pragma unroll
+  for (int i = 0; i < NEPT; ++i) {
+    const int w = min(wb + i * ws, n - 1);
+    res[i] = a.residual[(row0 + w) * CH + c];
+  }
+#pragma unroll
+  for (int i = 0; i < NEPT; ++i) {
+    const int w = wb + i * ws;
+    if (w < n) {
+      const long m = row0 + w;
+      float v = ys[w * LDR + c] + bias;
+      if (a.drop_p > 0.0f) {
+        const float u = gwn_uniform(seed, a.salt, (unsigned long long)m * CH + c);
+        v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
+      }
+      v += res[i];
+      if (a.x_out) {
+        a.x_out[m * CH + c] = (v - bmu) * brs * bg + bb;
+      } else {
+        a.z[m * CH + c] = v;
+        ys[w * LDR + c] = v;
+      }
+    }
+  }
+  if (a.bn_part == nullptr || a.x_out) return;
+  __syncthreads();
+  // per-slice BN partials (count, mean, M2) per channel, fixed order
+  const int ngroups = blockDim.x >> 5;
+  const int g = threadIdx.x >> 5;
+  float s = 0.0f;
+  for (int w = g; w < n; w += ngroups) s += ys[w * LDR + c];
+  red0[threadIdx.x] = s;
+  __syncthreads();
+  float mean = 0.0f;
+  for (int i = 0; i < ngroups; ++i) mean += red0[i * 32 + c];
+  mean /= (float)n;
+  float q = 0.0f;
+  for (int w = g; w < n; w += ngroups) {
+    const float dlt = ys[w * LDR + c] - mean;
+    q += dlt * dlt;
+  }
+  red1[threadIdx.x] = q;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float m2 = 0.0f;
+    for (int i = 0; i < ngroups; ++i) m2 += red1[i * 32 + c];
+    float* pp = a.bn_part + (long)blockIdx.x * 3 * CH;
+    pp[c] = (float)n;
+    pp[CH + c] = mean;
+    pp[2 * CH + c] = m2;
+  }
+}
+
+// backward prologue: dh of the slice into LDS (rows >= n zero), either loaded or computed by the
+// BatchNorm backward of this layer's output (same arithmetic as bn_bwd_apply_kernel, ops.hip):
+//   dz = gamma*rstd*(dy - k1 - xhat*k2) -> residual gradient dres; dropout'(dz) -> dh (LDS + HBM)
+template <int NEPT>
+__device__ __forceinline__ void bwd_prologue(const FusedBwd& a, float* dhs, long row0, int n, int np) {
+  if (!a.bn_dy) {
+    global_to_lds(a.dh + row0 * CH, CH, n, np, dhs);
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < CH) {
+    if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
+    if (a.bn_dgamma) a.bn_dgamma[threadIdx.x] = a.bn_sums[CH + threadIdx.x];
+  }
+  const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
+  const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
+  const float mu = a.bn_mean[c], rs = a.bn_rstd[c], gm = a.bn_gamma[c];
+  const float k1 = a.bn_sums[c] * a.inv_rows, k2 = a.bn_sums[CH + c] * a.inv_rows;
+  float dy[NEPT], zv[NEPT];  // all loads before the first store (see fwd_epilogue)
+#pragma unroll
+  for (int i = 0; i < NEPT; ++i) {
+    const long idx = (row0 + min(wb + i * ws, n - 1)) * CH + c;
+    dy[i] = a.bn_dy[idx];
+    zv[i] = a.bn_z[idx];
+  }
+#pragma unroll
+  for (int i = 0; i < NEPT; ++i) {
+    const int w = wb + i * ws;
+    float v = 0.0f;
+    if (w < n) {
+      const long idx = (row0 + w) * CH + c;
+      const float xhat = (zv[i] - mu) * rs;
+      const float dz = gm * rs * (dy[i] - k1 - xhat * k2);
+      a.dres[idx] = dz;
+      v = dz;
+      if (a.drop_p > 0.0f) {
+        const float u = gwn_uniform(seed, a.salt, (unsigned long long)idx);
+        v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
+      }
+      a.dh_out[idx] = v;
+    }
+    if (w < np) dhs[w * LDR + c] = v;
+  }
+}
+
+// gate backward (gate_bwd_kernel, ops.hip) on dxg staged in buf: g = dxg (+ dskip) -> dfg through
+// the saved (tanh f, sigmoid s) pairs; the fg / dfg rows move as coalesced float2s
+template <int NEPT>
+__device__ __forceinline__ void bwd_gate_epilogue(const FusedBwd& a, const float* buf, long row0, int n) {
+  const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
+  float2 fs[NEPT];
+  float dsk[NEPT];
+#pragma unroll
+  for (int i = 0; i < NEPT; ++i) {
+    const long m = row0 + min(wb + i * ws, n - 1);
+    fs[i] = *(const float2*)(a.fg + m * 2 * CH + 2 * c);
+    dsk[i] = (a.dskip && m >= a.skip_row0) ? a.dskip[(m - a.skip_row0) * a.ld_dskip + c] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < NEPT; ++i) {
+    const int w = wb + i * ws;
+    if (w < n) {
+      const long m = row0 + w;
+      const float g = buf[w * LDR + c] + dsk[i];
+      const float f = fs[i].x, sg = fs[i].y;
+      float2 o;
+      o.x = g * sg * (1.0f - f * f);
+      o.y = g * f * sg * (1.0f - sg);
+      *(float2*)(a.dfg + m * 2 * CH + 2 * c) = o;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// tile-wave layout: one wave per 32-node tile
 
 template <int MAXT>
 __global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
@@ -237,90 +394,27 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
     const float* G = a.sup[k];
     f32x16 d = diffuse(xs, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
     g0 = g_first(G, a.ld_sup, nkb, w0, lane);  // hop 2 re-reads the same support
-    if (!(GWN_EXP & 4)) {
+    {
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
       hacc = mlp_from_acc(wf, d, hacc);
     }
-    // ys is free once every wave finished the previous support's hop 2
-    if (!(GWN_EXP & 32)) __syncthreads();
+    __syncthreads();  // ys is free once every wave finished the previous support's hop 2
     acc_to_lds(ys, d, w0, lane);
-    if (!(GWN_EXP & 2)) acc_to_global((float*)hs + (1 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
-    if (!(GWN_EXP & 32)) __syncthreads();
+    if (a.store_pieces) acc_to_global((float*)hs + (1 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
+    __syncthreads();
     d = diffuse(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
     if (k + 1 < a.nsup) g0 = g_first(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
-    if (!(GWN_EXP & 4)) {
+    {
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
       hacc = mlp_from_acc(wf, d, hacc);
-    } else {
-      hacc += d;
     }
     // x2 only goes to h (the backward's dW_mlp): straight from the accumulator
-    if (!(GWN_EXP & 2)) acc_to_global((float*)hs + (2 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
+    if (a.store_pieces) acc_to_global((float*)hs + (2 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
   }
   __syncthreads();
   acc_to_lds(ys, hacc, w0, lane);
   __syncthreads();
-  if (GWN_EXP & 8) {
-    lds_to_global(ys, a.z + row0 * CH, CH, n);
-    return;
-  }
-  // epilogue: bias, dropout (same counter hash as the GEMM epilogue: index m*32 + c), residual
-  const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
-  const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
-  {
-    // EPT elements per thread (np*32 = 16*blockDim): all residual loads are issued before the
-    // first store (the compiler cannot reorder loads across possibly aliasing stores itself)
-    const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
-    const float bias = a.b_mlp[c];
-    float res[EPT];
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-      const int w = min(wb + i * ws, n - 1);
-      res[i] = a.residual[(row0 + w) * CH + c];
-    }
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-      const int w = wb + i * ws;
-      if (w < n) {
-        const long m = row0 + w;
-        float v = ys[w * LDR + c] + bias;
-        if (a.drop_p > 0.0f) {
-          const float u = gwn_uniform(seed, a.salt, (unsigned long long)m * CH + c);
-          v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
-        }
-        v += res[i];
-        a.z[m * CH + c] = v;
-        ys[w * LDR + c] = v;
-      }
-    }
-  }
-  if (a.bn_part == nullptr) return;
-  __syncthreads();
-  // per-slice BN partials (count, mean, M2) per channel, fixed order
-  const int ngroups = blockDim.x >> 5;
-  const int c = threadIdx.x & 31, g = threadIdx.x >> 5;
-  float s = 0.0f;
-  for (int w = g; w < n; w += ngroups) s += ys[w * LDR + c];
-  red[0][threadIdx.x] = s;
-  __syncthreads();
-  float mean = 0.0f;
-  for (int i = 0; i < ngroups; ++i) mean += red[0][i * 32 + c];
-  mean /= (float)n;
-  float q = 0.0f;
-  for (int w = g; w < n; w += ngroups) {
-    const float dlt = ys[w * LDR + c] - mean;
-    q += dlt * dlt;
-  }
-  red[1][threadIdx.x] = q;
-  __syncthreads();
-  if (threadIdx.x < 32) {
-    float m2 = 0.0f;
-    for (int i = 0; i < ngroups; ++i) m2 += red[1][i * 32 + c];
-    float* pp = a.bn_part + (long)blockIdx.x * 3 * CH;
-    pp[c] = (float)n;
-    pp[CH + c] = mean;
-    pp[2 * CH + c] = m2;
-  }
+  fwd_epilogue<EPT>(a, ys, red[0], red[1], row0, n);
 }
 
 template <int MAXT>
@@ -335,46 +429,7 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
   const long row0 = (long)blockIdx.x * n;
 
   GBatch g0 = (a.nsup > 0) ? g_first(a.supT[0], a.ld_sup, nkb, w0, lane) : GBatch{};
-  if (a.bn_dy) {
-    // BatchNorm backward of this layer's output (same arithmetic as bn_bwd_apply_kernel, ops.hip):
-    //   dz = gamma*rstd*(dy - k1 - xhat*k2) -> residual gradient dres; dropout'(dz) -> dh (LDS + HBM)
-    if (blockIdx.x == 0 && threadIdx.x < CH) {
-      if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
-      if (a.bn_dgamma) a.bn_dgamma[threadIdx.x] = a.bn_sums[CH + threadIdx.x];
-    }
-    const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
-    const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
-    const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
-    const float mu = a.bn_mean[c], rs = a.bn_rstd[c], gm = a.bn_gamma[c];
-    const float k1 = a.bn_sums[c] * a.inv_rows, k2 = a.bn_sums[CH + c] * a.inv_rows;
-    float dy[EPT], zv[EPT];  // all loads before the first store (see the forward epilogue)
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-      const long idx = (row0 + min(wb + i * ws, n - 1)) * CH + c;
-      dy[i] = a.bn_dy[idx];
-      zv[i] = a.bn_z[idx];
-    }
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-      const int w = wb + i * ws;  // < np
-      float v = 0.0f;
-      if (w < n) {
-        const long idx = (row0 + w) * CH + c;
-        const float xhat = (zv[i] - mu) * rs;
-        const float dz = gm * rs * (dy[i] - k1 - xhat * k2);
-        a.dres[idx] = dz;
-        v = dz;
-        if (a.drop_p > 0.0f) {
-          const float u = gwn_uniform(seed, a.salt, (unsigned long long)idx);
-          v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
-        }
-        a.dh_out[idx] = v;
-      }
-      dhs[w * LDR + c] = v;
-    }
-  } else {
-    global_to_lds(a.dh + row0 * CH, CH, n, np, dhs);
-  }
+  bwd_prologue<EPT>(a, dhs, row0, n, np);
   __syncthreads();
   f32x16 dx = mlpT_from_lds(a.w_mlp, a.ld_w, 0, dhs, w0, lane, zero16());
   for (int k = 0; k < a.nsup; ++k) {
@@ -400,33 +455,256 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
     acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
     return;
   }
-  // gate backward (gate_bwd_kernel, ops.hip): g = dxg (+ dskip) -> dfg through the saved
-  // (tanh f, sigmoid s) pairs, staged through LDS so the fg / dfg rows move as coalesced float2s
   __syncthreads();  // every wave finished reading buf
   acc_to_lds(buf, dx, w0, lane);
   __syncthreads();
-  const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
-  float2 fs[EPT];
-  float dsk[EPT];
+  bwd_gate_epilogue<EPT>(a, buf, row0, n);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 4-wave layout (n <= 256): wave v owns node tiles {v, v + 4}
+
+struct GBatch2 {
+  float v[TPW][KB];
+};
+
+__device__ __forceinline__ GBatch2 g_first2(const float* G, int ld, int nkb, const int* w0, int lane) {
+  GBatch2 g;
 #pragma unroll
-  for (int i = 0; i < EPT; ++i) {
-    const long m = row0 + min(wb + i * ws, n - 1);
-    fs[i] = *(const float2*)(a.fg + m * 2 * CH + 2 * c);
-    dsk[i] = (a.dskip && m >= a.skip_row0) ? a.dskip[(m - a.skip_row0) * a.ld_dskip + c] : 0.0f;
+  for (int i = 0; i < TPW; ++i) {
+    const GBatch b = g_first(G, ld, nkb, w0[i], lane);
+#pragma unroll
+    for (int j = 0; j < KB; ++j) g.v[i][j] = b.v[j];
   }
+  return g;
+}
+
+// acc[i] += D' of tile i (diffuse() for TPW tiles sharing every A operand); g0 = g_first2(G, ...)
+__device__ __forceinline__ void diffuse2(const float* buf, const float* G, int ld, int nkb, const int* w0,
+                                         int lane, f32x16* acc, const GBatch2& g0) {
+  const int half = lane >> 5, col = lane & 31;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, nkb * 32 * ld * 4, 0x00020000);
+  int voff[TPW];
 #pragma unroll
-  for (int i = 0; i < EPT; ++i) {
-    const int w = wb + i * ws;
-    if (w < n) {
-      const long m = row0 + w;
-      const float g = buf[w * LDR + c] + dsk[i];
-      const float f = fs[i].x, sg = fs[i].y;
-      float2 o;
-      o.x = g * sg * (1.0f - f * f);
-      o.y = g * f * sg * (1.0f - sg);
-      *(float2*)(a.dfg + m * 2 * CH + 2 * c) = o;
+  for (int i = 0; i < TPW; ++i) voff[i] = (half * ld + w0[i] + col) * 4;
+  const int rowb = 2 * ld * 4;
+  float ga[TPW][KB], gb[TPW][KB];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+#pragma unroll
+    for (int j = 0; j < KB; ++j) ga[i][j] = g0.v[i][j];
+  auto lds_batch = [&](int kb, float* av) {
+    const float* bp = buf + (32 * kb + half) * LDR + col;
+#pragma unroll
+    for (int j = 0; j < KB; ++j) av[j] = bp[2 * j * LDR];
+  };
+  auto g_batch = [&](int kb, float (*g)[KB]) {
+#pragma unroll
+    for (int i = 0; i < TPW; ++i)
+#pragma unroll
+      for (int j = 0; j < KB; ++j) g[i][j] = bload(rs, voff[i], (kb * KB + j) * rowb);
+  };
+  auto mfma_batch = [&](const float* av, float (*g)[KB]) {
+#pragma unroll
+    for (int j = 0; j < KB; ++j)
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], g[i][j], acc[i], 0, 0, 0);
+  };
+  int kb = 0;
+  for (; kb + 2 < nkb; kb += 2) {
+    float av[KB];
+    g_batch(kb + 1, gb);
+    lds_batch(kb, av);
+    mfma_batch(av, ga);
+    g_batch(kb + 2, ga);
+    lds_batch(kb + 1, av);
+    mfma_batch(av, gb);
+  }
+  float av[KB];
+  if (kb + 1 < nkb) {
+    g_batch(kb + 1, gb);
+    lds_batch(kb, av);
+    mfma_batch(av, ga);
+    lds_batch(kb + 1, av);
+    mfma_batch(av, gb);
+  } else {
+    lds_batch(kb, av);
+    mfma_batch(av, ga);
+  }
+}
+
+__device__ __forceinline__ void mlp_from_lds2(const float* W, int ld_w, int off, const float* buf, const int* w0,
+                                              int lane, f32x16* acc) {
+  const int half = lane >> 5, col = lane & 31;
+  const float* wp = W + (long)col * ld_w + off;
+  float wf[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) wf[s] = wp[2 * s + half];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const float* bp = buf + (w0[i] + col) * LDR;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s], bp[2 * s + half], acc[i], 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void mlpT_from_lds2(const float* W, int ld_w, int off, const float* buf, const int* w0,
+                                               int lane, f32x16* acc) {
+  const int half = lane >> 5, col = lane & 31;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, CH * ld_w * 4, 0x00020000);
+  const int voff = (half * ld_w + off + col) * 4;
+  float wf[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) wf[s] = bload(rs, voff, 2 * s * ld_w * 4);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const float* bp = buf + (w0[i] + col) * LDR;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s], bp[2 * s + half], acc[i], 0, 0, 0);
+  }
+}
+
+// launch bounds (256 threads, >= 2 waves per SIMD): <= 256 VGPRs, two workgroups per CU
+__global__ __launch_bounds__(256, 2) void gcn_fwd_fused4_kernel(const FusedFwd a) {
+  extern __shared__ float lds[];
+  __shared__ float red[2][256];
+  const int n = a.n;
+  const int nkb = (n + 31) >> 5;
+  const int np = nkb * 32;
+  float* xs = lds;
+  float* ys = lds + np * LDR;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long row0 = (long)blockIdx.x * n;
+  const float* hs = a.h + row0 * a.ld_h;
+  int w0[TPW];
+  bool tv[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    w0[i] = 32 * (wv + 4 * i);
+    tv[i] = wv + 4 * i < nkb;
+  }
+
+  GBatch2 g0 = (a.nsup > 0) ? g_first2(a.sup[0], a.ld_sup, nkb, w0, lane) : GBatch2{};
+  global_to_lds(hs, a.ld_h, n, np, xs);
+  __syncthreads();
+  f32x16 hacc[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) hacc[i] = zero16();
+  mlp_from_lds2(a.w_mlp, a.ld_w, 0, xs, w0, lane, hacc);
+  for (int k = 0; k < a.nsup; ++k) {
+    const float* G = a.sup[k];
+    f32x16 d[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) d[i] = zero16();
+    diffuse2(xs, G, a.ld_sup, nkb, w0, lane, d, g0);
+    g0 = g_first2(G, a.ld_sup, nkb, w0, lane);  // hop 2 re-reads the same support
+    {
+      const GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) hacc[i] = mlp_from_acc(wf, d[i], hacc[i]);
+    }
+    __syncthreads();  // ys is free once every wave finished the previous support's hop 2
+#pragma unroll
+    for (int i = 0; i < TPW; ++i)
+      if (tv[i]) acc_to_lds(ys, d[i], w0[i], lane);
+    if (a.store_pieces) {
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) acc_to_global((float*)hs + (1 + 2 * k) * CH, a.ld_h, d[i], w0[i], lane, n);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) d[i] = zero16();
+    diffuse2(ys, G, a.ld_sup, nkb, w0, lane, d, g0);
+    if (k + 1 < a.nsup) g0 = g_first2(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
+    {
+      const GBatch wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) hacc[i] = mlp_from_acc(wf, d[i], hacc[i]);
+    }
+    if (a.store_pieces) {
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) acc_to_global((float*)hs + (2 + 2 * k) * CH, a.ld_h, d[i], w0[i], lane, n);
     }
   }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+    if (tv[i]) acc_to_lds(ys, hacc[i], w0[i], lane);
+  __syncthreads();
+  fwd_epilogue<EPT4>(a, ys, red[0], red[1], row0, n);
+}
+
+__global__ __launch_bounds__(256, 2) void gcn_bwd_fused4_kernel(const FusedBwd a) {
+  extern __shared__ float lds[];
+  const int n = a.n;
+  const int nkb = (n + 31) >> 5;
+  const int np = nkb * 32;
+  float* dhs = lds;
+  float* buf = lds + np * LDR;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long row0 = (long)blockIdx.x * n;
+  int w0[TPW];
+  bool tv[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    w0[i] = 32 * (wv + 4 * i);
+    tv[i] = wv + 4 * i < nkb;
+  }
+
+  GBatch2 g0 = (a.nsup > 0) ? g_first2(a.supT[0], a.ld_sup, nkb, w0, lane) : GBatch2{};
+  bwd_prologue<EPT4>(a, dhs, row0, n, np);
+  __syncthreads();
+  f32x16 dx[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) dx[i] = zero16();
+  mlpT_from_lds2(a.w_mlp, a.ld_w, 0, dhs, w0, lane, dx);
+  for (int k = 0; k < a.nsup; ++k) {
+    const float* GT = a.supT[k];
+    {
+      f32x16 u[TPW];
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) u[i] = zero16();
+      mlpT_from_lds2(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, w0, lane, u);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < TPW; ++i)
+        if (tv[i]) acc_to_lds(buf, u[i], w0[i], lane);
+      if (k == a.adp_index) {
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) acc_to_global(a.t2 + row0 * a.ld_t, a.ld_t, u[i], w0[i], lane, n);
+      }
+    }
+    __syncthreads();
+    f32x16 t[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) t[i] = zero16();
+    mlpT_from_lds2(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, w0, lane, t);
+    diffuse2(buf, GT, a.ld_sup, nkb, w0, lane, t, g0);  // dx1 = dP_x1 + A dP_x2
+    g0 = g_first2(GT, a.ld_sup, nkb, w0, lane);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TPW; ++i)
+      if (tv[i]) acc_to_lds(buf, t[i], w0[i], lane);
+    if (k == a.adp_index) {
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) acc_to_global(a.t1 + row0 * a.ld_t, a.ld_t, t[i], w0[i], lane, n);
+    }
+    __syncthreads();
+    diffuse2(buf, GT, a.ld_sup, nkb, w0, lane, dx, g0);  // dxg += A dx1
+    if (k + 1 < a.nsup) g0 = g_first2(a.supT[k + 1], a.ld_sup, nkb, w0, lane);
+  }
+  if (!a.dfg) {
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx[i], w0[i], lane, n);
+    return;
+  }
+  __syncthreads();  // every wave finished reading buf
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+    if (tv[i]) acc_to_lds(buf, dx[i], w0[i], lane);
+  __syncthreads();
+  bwd_gate_epilogue<EPT4>(a, buf, row0, n);
 }
 
 // dst (padded [np][ld_dst], zero outside n x n) = src or src^T
@@ -462,6 +740,9 @@ void ensure_lds_attr(K kern) {
                             (int)fused_lds_bytes(512));
 }
 
+// layout: 0 = auto (4-wave when n <= 256), 1 = tile-wave, 2 = 4-wave
+bool use_4wave(int layout, int nwt) { return nwt <= 8 && layout != 1; }
+
 }  // namespace
 
 bool gwn_gcn_fused_eligible(int c, int n, int nsup, int ld_sup) {
@@ -471,6 +752,8 @@ bool gwn_gcn_fused_eligible(int c, int n, int nsup, int ld_sup) {
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
   const int nwt = (g->n + 31) / 32;
   GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_fwd (fused): supports must be padded to 32*ceil(n/32)");
+  GWN_REQUIRE(g->layout >= 0 && g->layout <= 2 && !(g->layout == 2 && nwt > 8),
+              "gcn_fwd (fused): layout 2 (4-wave) needs n <= 256");
   FusedFwd a;
   a.h = g->h; a.ld_h = g->ld_h;
   for (int k = 0; k < 8; ++k) a.sup[k] = (k < g->nsup) ? g->sup[k] : nullptr;
@@ -479,15 +762,26 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.residual = g->residual; a.z = g->z; a.bn_part = bn_part;
   a.seed_ptr = g->seed_ptr; a.salt = g->salt; a.drop_p = g->drop_p;
   a.n = g->n;
+  a.store_pieces = g->no_pieces ? 0 : 1;
+  a.bn_rm = g->bn_running_mean; a.bn_rv = g->bn_running_var; a.bn_g = g->bn_weight; a.bn_b = g->bn_bias;
+  a.bn_eps = g->bn_eps; a.x_out = g->bn_out;
+  if (a.x_out)
+    GWN_REQUIRE(a.bn_rm && a.bn_rv && a.bn_g && a.bn_b && !bn_part,
+                "gcn_fwd (fused): eval BatchNorm needs running mean / var, weight, bias (and no BN partials)");
+  else
+    GWN_REQUIRE(a.z != nullptr, "gcn_fwd (fused): z is required");
   const size_t lds = fused_lds_bytes(g->n);
   static bool attr_set = false;
   if (!attr_set) {
     ensure_lds_attr(gcn_fwd_fused_kernel<512>);
     ensure_lds_attr(gcn_fwd_fused_kernel<1024>);
+    ensure_lds_attr(gcn_fwd_fused4_kernel);
     attr_set = true;
   }
-  if (nwt <= 8) gcn_fwd_fused_kernel<512><<<g->rows / g->n, 64 * nwt, lds, s>>>(a);
-  else gcn_fwd_fused_kernel<1024><<<g->rows / g->n, 64 * nwt, lds, s>>>(a);
+  const int slices = g->rows / g->n;
+  if (use_4wave(g->layout, nwt)) gcn_fwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
+  else if (nwt <= 8) gcn_fwd_fused_kernel<512><<<slices, 64 * nwt, lds, s>>>(a);
+  else gcn_fwd_fused_kernel<1024><<<slices, 64 * nwt, lds, s>>>(a);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -496,6 +790,8 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
                              float* t1, float* t2, long ld_t, hipStream_t s) {
   const int nwt = (g->n + 31) / 32;
   GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_bwd (fused): supports must be padded to 32*ceil(n/32)");
+  GWN_REQUIRE(g->layout >= 0 && g->layout <= 2 && !(g->layout == 2 && nwt > 8),
+              "gcn_bwd (fused): layout 2 (4-wave) needs n <= 256");
   FusedBwd a;
   a.dh = g->dh;
   for (int k = 0; k < 8; ++k) a.supT[k] = (k < g->nsup) ? supT[k] : nullptr;
@@ -519,23 +815,33 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   if (!attr_set) {
     ensure_lds_attr(gcn_bwd_fused_kernel<512>);
     ensure_lds_attr(gcn_bwd_fused_kernel<1024>);
+    ensure_lds_attr(gcn_bwd_fused4_kernel);
     attr_set = true;
   }
   const size_t lds = fused_lds_bytes(g->n);
-  if (nwt <= 8) gcn_bwd_fused_kernel<512><<<g->rows / g->n, 64 * nwt, lds, s>>>(a);
-  else gcn_bwd_fused_kernel<1024><<<g->rows / g->n, 64 * nwt, lds, s>>>(a);
+  const int slices = g->rows / g->n;
+  if (use_4wave(g->layout, nwt)) gcn_bwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
+  else if (nwt <= 8) gcn_bwd_fused_kernel<512><<<slices, 64 * nwt, lds, s>>>(a);
+  else gcn_bwd_fused_kernel<1024><<<slices, 64 * nwt, lds, s>>>(a);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
 
-// diagnostics: resident workgroups per CU of the fused kernels for n nodes (HIP occupancy API)
+// diagnostics: resident workgroups per CU of the fused kernels for n nodes (HIP occupancy API),
+// for the layout the launchers pick by default
 extern "C" int gwn_fused_occupancy(int n, int backward) {
   const int nwt = (n + 31) / 32;
   const size_t lds = fused_lds_bytes(n);
   int blocks = -1;
   hipError_t e;
-  if (backward) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_fused_kernel<512>, 64 * nwt, lds);
-  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_fused_kernel<512>, 64 * nwt, lds);
+  if (use_4wave(0, nwt)) {
+    if (backward) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_fused4_kernel, 256, lds);
+    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_fused4_kernel, 256, lds);
+  } else if (backward) {
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_fused_kernel<1024>, 64 * nwt, lds);
+  } else {
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_fused_kernel<1024>, 64 * nwt, lds);
+  }
   return e == hipSuccess ? blocks : -(int)e;
 }
 

@@ -722,6 +722,7 @@ int gwn_gated_tcn_fwd(const gwn_tcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a->c % 16 == 0, "gated_tcn_fwd: channels must be a multiple of 16");
   const int c = a->c, P = a->P, t_out = a->t_in - a->dilation;
   if (c == 32 && aligned16(a->x) && aligned16(a->fg)) return gwn_rowgemm_tcn_fwd(a, s);
+  GWN_REQUIRE(a->fg != nullptr, "gated_tcn_fwd: fg may only be NULL on the c == 32 path");
   gwn_gemm_desc d = gemm_zero();
   d.A = a->x; d.lda_m = c; d.lda_k = 1; d.a_kin = c; d.a_row_shift = a->dilation * P;
   d.a_rows = a->t_in * P;
@@ -814,6 +815,7 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_fwd: rows must be slices*n");
   const int c = a->c, n = a->n, slices = a->rows / n;
   if (gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup)) return gwn_gcn_fused_fwd_launch(a, a->bn_partials, s);
+  GWN_REQUIRE(!a->no_pieces && !a->bn_out, "gcn_fwd: no_pieces / bn_out need the fused path (c == 32, n <= 512)");
   const int width = (2 * a->nsup + 1) * c;
   for (int k = 0; k < a->nsup; ++k) {
     float* x1 = a->h + (1 + 2 * k) * c;

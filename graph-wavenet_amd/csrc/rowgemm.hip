@@ -235,7 +235,7 @@ int gwn_rowgemm_tcn_fwd(const gwn_tcn_args* a, hipStream_t s) {
   p.B = a->w_fg; p.ldb_k = 1; p.ldb_tap = c; p.ldb_n = 2 * c;
   p.C = a->xg; p.ldc = a->ld_xg;
   p.bias = a->b_fg;
-  p.aux = a->fg; p.ld_aux = 2 * c;
+  p.aux = a->fg; p.ld_aux = a->fg ? 2 * c : 0;  // no fg: an empty window drops the stores
   p.aux2 = a->skipcat; p.ld_aux2 = a->ld_skip; p.aux2_row0 = a->skip_row0;
   p.M = t_out * P; p.ntiles = 2;
   return launch<32, true>(p, s);

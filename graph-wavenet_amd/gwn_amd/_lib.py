@@ -74,6 +74,10 @@ class GcnArgs(ctypes.Structure):
         ("z", c_void_p),
         ("seed_ptr", c_void_p), ("salt", c_u64), ("drop_p", c_float),
         ("bn_partials", c_void_p),
+        ("no_pieces", c_int),
+        ("bn_running_mean", c_void_p), ("bn_running_var", c_void_p), ("bn_weight", c_void_p),
+        ("bn_bias", c_void_p), ("bn_eps", c_float), ("bn_out", c_void_p),
+        ("layout", c_int),
     ]
 
 
@@ -96,6 +100,7 @@ class GcnBwdArgs(ctypes.Structure):
         ("seed_ptr", c_void_p), ("salt", c_u64), ("drop_p", c_float),
         ("fg", c_void_p), ("dskip", c_void_p), ("ld_dskip", c_long), ("skip_row0", c_int),
         ("dfg", c_void_p),
+        ("layout", c_int),
     ]
 
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time

@@ -139,6 +139,8 @@ typedef struct gwn_tcn_args {
   float* fg;
   float* skipcat; long ld_skip; int skip_row0;
 } gwn_tcn_args;
+/* fg may be NULL when no backward follows (inference; c == 32 row-GEMM path): the (tanh, sigmoid)
+ * pairs are then not stored. */
 int gwn_gated_tcn_fwd(const gwn_tcn_args* a, hipStream_t stream);
 
 /* Backward: dxg [rows][ld_dxg] (NULL = zero) (+ dskip [rows-skip_row0][ld_dskip] for rows >= skip_row0) ->
@@ -194,6 +196,18 @@ typedef struct gwn_gcn_args {
    * fused path (c == 32, n <= 512) for gwn_batchnorm_fwd_partials; NULL = not wanted.  When the
    * generic path runs instead, they are computed from z by a separate pass. */
   float* bn_partials;
+  /* --- optional (zero / NULL = off), fused path only ---
+   * no_pieces: the hop outputs (pieces 1..2K of h) are not stored: an inference forward that no
+   *   backward follows; h then only needs piece 0 (ld_h may be c).
+   * eval BatchNorm (model.py:236 with the module in eval mode) folded into the epilogue: with
+   *   bn_out != NULL, bn_out[r][j] = (z - running_mean[j]) / sqrt(running_var[j] + bn_eps) *
+   *   weight[j] + bias[j] is written instead of z (z may be NULL, bn_partials must be NULL).
+   * layout: wave layout of the fused kernels, 0 = auto (4-wave for n <= 256), 1 = one wave per
+   *   32-node tile, 2 = 4-wave (n <= 256). */
+  int no_pieces;
+  const float* bn_running_mean; const float* bn_running_var; const float* bn_weight; const float* bn_bias;
+  float bn_eps; float* bn_out;
+  int layout;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -240,6 +254,8 @@ typedef struct gwn_gcn_bwd_args {
    * [rows - skip_row0][ld_dskip] for rows >= skip_row0, NULL = none) and fg = (tanh f, sigmoid s)
    * interleaved [rows][2c]:  dfg[r][2j] = g*s*(1 - f^2),  dfg[r][2j+1] = g*f*s*(1 - s). */
   const float* fg; const float* dskip; long ld_dskip; int skip_row0; float* dfg;
+  /* wave layout of the fused kernel, as gwn_gcn_args.layout */
+  int layout;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);

@@ -318,3 +318,78 @@ def test_gemm_nt(gpu, M, N, K, epi):
     assert torch.all(got[:, N:] == 7.0)
     scale = float(ref.abs().max()) + 1e-30
     assert float((got[:, :N] - ref).abs().max()) / scale <= 2e-6
+
+
+@pytest.mark.parametrize("n", [16, 96, 207, 256])
+def test_gcn_fused_layouts_agree(gpu, n):
+    """The 4-wave layout (default for n <= 256) and the one-wave-per-tile layout of the fused
+    gcn forward / backward against each other and against fp64 (model.py:41-55): hop pieces,
+    z, BN partials, dxg and the adaptive-support pieces t1 / t2."""
+    import ctypes
+    from gwn_amd import _lib
+    torch.manual_seed(n)
+    C, K, S = 32, 3, 5
+    NP = (n + 31) // 32 * 32
+    W = (2 * K + 1) * C
+    rows = S * n
+    sups = []
+    for _ in range(K):
+        s = torch.zeros(NP, NP, device=gpu)
+        s[:n, :n] = torch.rand(n, n, device=gpu) / n
+        sups.append(s)
+    supT = [s.t().contiguous() for s in sups]
+    arr = (ctypes.c_void_p * K)(*[s.data_ptr() for s in sups])
+    arrT = (ctypes.c_void_p * K)(*[s.data_ptr() for s in supT])
+    wm = torch.randn(C, W, device=gpu) * 0.1
+    bm = torch.randn(C, device=gpu)
+    res = torch.randn(rows, C, device=gpu)
+    xg = torch.randn(rows, C, device=gpu)
+    dh = torch.randn(rows, C, device=gpu)
+    seed = torch.zeros(1, device=gpu, dtype=torch.int64)
+    outs = []
+    for layout in (1, 0):
+        h = torch.zeros(rows, W, device=gpu)
+        h[:, :C] = xg
+        z = torch.empty(rows, C, device=gpu)
+        bnp = torch.empty(S * 3 * C, device=gpu)
+        ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)),
+                          ld_sup=NP, h=h.data_ptr(), ld_h=W, w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(),
+                          residual=res.data_ptr(), z=z.data_ptr(), seed_ptr=seed.data_ptr(), salt=0, drop_p=0.0,
+                          bn_partials=bnp.data_ptr(), layout=layout)
+        _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
+        dhc = torch.zeros(rows, W, device=gpu)
+        gb = _lib.GcnBwdArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)),
+                             ld_sup=NP, h=h.data_ptr(), ld_h=W, w_mlp=wm.data_ptr(), dh=dh.data_ptr(),
+                             dhcat=dhc.data_ptr(), ld_dhcat=W, adp_index=K - 1, accumulate_dadp=0,
+                             sup_t=ctypes.cast(arrT, ctypes.POINTER(ctypes.c_void_p)), skip_weight_grads=1,
+                             layout=layout)
+        _lib.call("gwn_gcn_bwd", ctypes.byref(gb), _lib.stream())
+        torch.cuda.synchronize()
+        outs.append((h.clone(), z.clone(), bnp.clone(), dhc.clone()))
+    # fp64 truth
+    X = xg.double().cpu().view(S, n, C)
+    A = [s[:n, :n].double().cpu() for s in sups]
+    pieces = [X]
+    for a in A:
+        x1 = torch.einsum("svc,vw->swc", X, a)
+        x2 = torch.einsum("svc,vw->swc", x1, a)
+        pieces += [x1, x2]
+    H = torch.cat(pieces, dim=2).reshape(rows, W)
+    Z = H @ wm.double().cpu().t() + bm.double().cpu() + res.double().cpu()
+    D = dh.double().cpu().view(S, n, C)
+    dP = (dh.double().cpu() @ wm.double().cpu()).view(S, n, W)
+    dxg = dP[:, :, :C].clone()
+    for k, a in enumerate(A):
+        dx2 = dP[:, :, (2 + 2 * k) * C:(3 + 2 * k) * C]
+        dx1 = dP[:, :, (1 + 2 * k) * C:(2 + 2 * k) * C] + torch.einsum("swc,vw->svc", dx2, a)
+        dxg = dxg + torch.einsum("swc,vw->svc", dx1, a)
+    del D
+    for h, z, bnp, dhc in outs:
+        assert rel_err(h.cpu().numpy(), H.numpy()) <= 2e-6
+        assert rel_err(z.cpu().numpy(), Z.numpy()) <= 2e-6
+        assert rel_err(dhc[:, :C].cpu().numpy(), dxg.reshape(rows, C).numpy()) <= 2e-6
+        means = bnp.view(S, 3, C)[:, 1].cpu().double()
+        assert rel_err(means.numpy(), Z.view(S, n, C).mean(1).numpy()) <= 1e-5
+    # the two layouts: same products in the same k order per tile -> identical up to fma rounding
+    for a_, b_ in zip(outs[0], outs[1]):
+        assert rel_err(a_.cpu().numpy(), b_.cpu().numpy()) <= 1e-6

@@ -75,10 +75,20 @@ def main():
         gf.bn_dgamma, gf.bn_dbeta, gf.dres, gf.dh_out = dgam.data_ptr(), dbet.data_ptr(), dres.data_ptr(), dho.data_ptr()
         gf.seed_ptr, gf.salt, gf.drop_p = seed.data_ptr(), 3, 0.3
         gf.fg, gf.dskip, gf.ld_dskip, gf.skip_row0, gf.dfg = fgb.data_ptr(), dskb.data_ptr(), 8 * C, 0, dfgb.data_ptr()
-        for name, fn in (("fwd", lambda: _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)),
-                         ("bwd", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)),
-                         ("bwd-data", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gd), st)),
-                         ("bwd-data+bn+gate", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gf), st))):
+        variants = []
+        for lay in (0, 1):
+            tag = "" if lay == 0 else " L1"
+            ga_l = _lib.GcnArgs.from_buffer_copy(ga)
+            ga_l.layout = lay
+            gd_l = _lib.GcnBwdArgs.from_buffer_copy(gd)
+            gd_l.layout = lay
+            gf_l = _lib.GcnBwdArgs.from_buffer_copy(gf)
+            gf_l.layout = lay
+            variants += [("fwd" + tag, lambda a=ga_l: _lib.call("gwn_gcn_fwd", ctypes.byref(a), st)),
+                         ("bwd-data" + tag, lambda a=gd_l: _lib.call("gwn_gcn_bwd", ctypes.byref(a), st)),
+                         ("bwd-data+bn+gate" + tag, lambda a=gf_l: _lib.call("gwn_gcn_bwd", ctypes.byref(a), st))]
+        variants.append(("bwd (+wgrad, gram)", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)))
+        for name, fn in variants:
             for _ in range(3):
                 fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -88,7 +98,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             us = 1000.0 * e0.elapsed_time(e1) / args.reps
-            print("gcn %-16s T=%2d slices=%4d: %8.1f us  %6.1f TFLOP/s (fwd-equivalent flops)"
+            print("gcn %-20s T=%2d slices=%4d: %8.1f us  %6.1f TFLOP/s (fwd-equivalent flops)"
                   % (name, T, T * B, us, flop / us / 1e6), flush=True)
         del dh, dhc
 
