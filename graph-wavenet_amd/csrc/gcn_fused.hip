@@ -15,12 +15,13 @@
 // (x1, x2 per support) and the layer output are written to HBM, as full coalesced rows.
 //
 // Two wave layouts of the same schedule:
-//   * n <= 256 ("4-wave", default): 256 threads = one wave per SIMD; wave v owns the node tiles
+//   * 225 <= n <= 256 ("4-wave"; selectable for any n <= 256): 256 threads = one wave per SIMD; wave v owns the node tiles
 //     {v, v + 4}.  Every LDS A value feeds two MFMAs, every wave runs two independent accumulator
 //     chains, and the W fragments of the mlp are loaded once for both tiles.  A tile slot beyond
 //     the last node tile (e.g. tile 7 for n <= 224) is computed on finite don't-care columns and
 //     never stored, so the four waves run the same instruction stream (no divergent barriers).
-//   * otherwise ("tile-wave"): one wave per 32-node tile (up to 16 waves, n <= 512).
+//   * otherwise ("tile-wave"): one wave per 32-node tile (up to 16 waves, n <= 512).  At n = 207
+//     (7 tiles) it beats the 4-wave layout by 10-23 % (tools/bench_gcn.py, round 1).
 //
 // Contract on the supports: [np][ld] with np = 32*ceil(n/32) <= ld, ZERO outside [n][n]
 // (the executor keeps padded copies), so the K loop runs whole 32-node batches unguarded.
@@ -740,8 +741,10 @@ void ensure_lds_attr(K kern) {
                             (int)fused_lds_bytes(512));
 }
 
-// layout: 0 = auto (4-wave when n <= 256), 1 = tile-wave, 2 = 4-wave
-bool use_4wave(int layout, int nwt) { return nwt <= 8 && layout != 1; }
+// layout: 0 = auto, 1 = tile-wave, 2 = 4-wave.  Auto picks the tile-wave layout: measured at
+// METR-LA shape (n = 207, 7 tiles) the 4-wave kernel is 10-23 % slower (fewer waves to hide the
+// operand latency, plus the dead 8th tile slot); it is only auto-selected when all 8 slots are real.
+bool use_4wave(int layout, int nwt) { return layout == 2 || (layout == 0 && nwt == 8); }
 
 }  // namespace
 

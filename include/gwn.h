@@ -202,8 +202,8 @@ typedef struct gwn_gcn_args {
    * eval BatchNorm (model.py:236 with the module in eval mode) folded into the epilogue: with
    *   bn_out != NULL, bn_out[r][j] = (z - running_mean[j]) / sqrt(running_var[j] + bn_eps) *
    *   weight[j] + bias[j] is written instead of z (z may be NULL, bn_partials must be NULL).
-   * layout: wave layout of the fused kernels, 0 = auto (4-wave for n <= 256), 1 = one wave per
-   *   32-node tile, 2 = 4-wave (n <= 256). */
+   * layout: wave layout of the fused kernels, 0 = auto (4-wave only when n fills 8 node tiles,
+   *   225..256), 1 = one wave per 32-node tile, 2 = 4-wave (n <= 256). */
   int no_pieces;
   const float* bn_running_mean; const float* bn_running_var; const float* bn_weight; const float* bn_bias;
   float bn_eps; float* bn_out;
