@@ -164,6 +164,12 @@ _SIGS = [
     ("gwn_from_nchw", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("gwn_sum_vectors", c_int, [c_void_p, c_int, c_int, c_long, c_void_p, c_void_p]),
     ("gwn_increment_u64", c_int, [c_void_p, c_u64, c_void_p]),
+    ("gwn_horizon_metrics", c_int, [c_void_p, c_long, c_long, c_long, c_void_p, c_long, c_long, c_long, c_int,
+                                    c_int, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    ("gwn_horizon_metrics_workspace_floats", c_long, [c_int]),
+    ("gwn_gather_rows", c_int, [c_void_p, c_long, c_void_p, c_int, c_void_p, c_void_p]),
+    ("gwn_window_batch", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                 c_int, ctypes.c_double, ctypes.c_double, c_int, c_void_p, c_void_p, c_void_p]),
 ]
 
 EXPORTED = [s[0] for s in _SIGS]

@@ -134,6 +134,19 @@ class trainer():
             ex.unpack_grads(self.optimizer.grad_flat)
         return sc["metrics"]
 
+    def _eval_lean(self, input, real_val):
+        """engine.py:119-130 on the lean inference schedule: pad 1, eval forward (no saved state),
+        the three masked metrics from one HIP reduction (no gradient)."""
+        model = self.model
+        ex = model._executor
+        out, bf = ex.infer(model._flat, model._fixed_supports(), input, model._bn_bufs(), lead_pad=1)
+        B = input.shape[0]
+        rs = real_val.stride()
+        _lib.call("gwn_masked_loss", ptr(out), ptr(real_val), rs[0], rs[1], rs[2], B, ex.cfg.O, ex.cfg.N,
+                  out.shape[3], float(self.scaler.mean), float(self.scaler.std), ptr(bf["metrics"]), None,
+                  ptr(bf["ws"]), _lib.stream())
+        return bf["metrics"]
+
     def _phase_update(self):
         """clip_grad_norm_(clip) + Adam on the flat buffers; advance the dropout counter."""
         model = self.model
@@ -152,8 +165,10 @@ class trainer():
         model = self.model
         if model.training != training:
             model.train(training)
-        model.executor()
+        ex = model.executor()
         if not training:
+            if ex.infer_ok():
+                return self._eval_lean(input, real_val)
             return self._phase_grads(input, real_val, False)
         g = self.optimizer.param_groups[0]
         key = (tuple(input.shape), tuple(real_val.shape), float(g["lr"]), tuple(g["betas"]), float(g["eps"]),

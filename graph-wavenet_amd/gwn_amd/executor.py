@@ -241,6 +241,11 @@ class Acts:
         self.training = training
 
 
+class _HeadBufs:
+    def __init__(self, skipcat, skr, e1, y):
+        self.skipcat, self.skr, self.e1, self.y = skipcat, skr, e1, y
+
+
 class Executor:
     def __init__(self, model):
         self.cfg = Config(model)
@@ -416,7 +421,16 @@ class Executor:
                          ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps, 0,
                          ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(ws), st)
         rows_f = tf * P
-        # skip sum (relu'd) -> end_conv_1 (+relu) -> end_conv_2
+        self._head_fwd(acts.skipcat, acts.skr, acts.e1, acts.y, rows_f, ws)
+        out = torch.empty(B, cfg.O, N, tf, device=self.device, dtype=F32)
+        lib.call("gwn_to_nchw", ptr(acts.y), B, cfg.O, N, tf, ptr(out), st)
+        return out, acts
+
+    def _head_fwd(self, skipcat, skr, e1, y, rows_f, ws):
+        """skip sum (relu'd) -> end_conv_1 (+relu) -> end_conv_2 (model.py:216-222, 238-240)."""
+        cfg = self.cfg
+        L, C = cfg.L, cfg.C
+        acts = _HeadBufs(skipcat, skr, e1, y)
         if self._head_nt():
             gemm_nt(acts.skipcat, L * C, self.pk("skip_w"), L * C, acts.skr, cfg.S, rows_f, cfg.S, L * C,
                     bias=self.pk("skip_bsum"), relu=1)
@@ -432,9 +446,92 @@ class Executor:
             gemm(acts.e1, cfg.E, 1, self.pk("e2_w"), 1, cfg.E, acts.y, cfg.O, 1,
                  M=rows_f, N=cfg.O, K=cfg.E, bias=self.pk("e2_b"),
                  ksplit=_ksplit_thin(rows_f, cfg.O, cfg.E), part=ws)
+
+    # ---------------------------------------------------------------------------------------
+    def infer_ok(self):
+        """The lean inference schedule needs the fused GCN path and the NT head GEMMs."""
+        cfg = self.cfg
+        return (os.environ.get("GWN_LEAN_EVAL", "1") != "0" and cfg.C == 32 and cfg.N <= 512
+                and cfg.nsup <= 8 and self._head_nt())
+
+    def _infer_bufs(self, B, ts):
+        key = ("infer", B, tuple(ts))
+        b = self._scratch.get(key)
+        if b is not None:
+            return b
+        cfg = self.cfg
+        C, L, P = cfg.C, cfg.L, B * cfg.N
+        tf = ts[-1]
+        e = lambda *s_: torch.empty(*s_, device=self.device, dtype=F32)  # noqa: E731
+        maxrows = max(ts[i + 1] for i in range(L)) * P
+        b = {"x0": e(ts[0] * P, C), "xa": e(maxrows, C), "xb": e(maxrows, C), "xg": e(maxrows, C),
+             "skipcat": e(tf * P, L * C), "skr": e(tf * P, cfg.S), "e1": e(tf * P, cfg.E), "y": e(tf * P, cfg.O),
+             "adp": torch.zeros(cfg.NP, cfg.NP, device=self.device, dtype=F32) if cfg.adaptive else None,
+             "metrics": e(4),
+             "ws": e(_lib.load().gwn_masked_loss_workspace_floats(B, cfg.O, cfg.N, tf) + 16)}
+        self._scratch[key] = b
+        return b
+
+    def infer(self, flat, fixed_sups, x, bn_bufs, lead_pad=0):
+        """Eval-mode forward when no backward follows (model.py:175-241 with the module in eval
+        mode under torch.no_grad, as in train.py:385-386 / test.py:65-66): the schedule of
+        forward() minus the state a backward needs -- no (tanh, sigmoid) pairs, no hop pieces in
+        HBM, BatchNorm with running statistics folded into the fused GCN epilogue (no z), the
+        layer activations in two ping-pong buffers.  Returns (out [B, O, N, T_f], buffers)."""
+        cfg = self.cfg
+        C, N, L = cfg.C, cfg.N, cfg.L
+        if x.dim() != 4:
+            raise RuntimeError("gwnet: expected a 4-D input [B, C, N, T], got %d-D" % x.dim())
+        B, cin, n, t_in = x.shape
+        if n != N or cin != cfg.Cin:
+            raise RuntimeError("gwnet: expected input [B, %d, %d, T], got %s" % (cfg.Cin, N, tuple(x.shape)))
+        if x.dtype != F32 or not x.is_cuda:
+            raise RuntimeError("gwnet (gwn_amd): input must be a float32 CUDA/HIP tensor")
+        ts = cfg.times(t_in + lead_pad)
+        if ts[-1] < 1:
+            raise RuntimeError("gwnet: input too short for the receptive field")
+        st = _lib.stream()
+        self.pack_params(flat)
+        P = B * N
+        tf = ts[-1]
+        bf = self._infer_bufs(B, ts)
+        sups = list(fixed_sups) if cfg.use_gcn else []
+        if cfg.use_gcn and cfg.adaptive:
+            _lib.call("gwn_adaptive_adj_fwd", ptr(self.pk("nv1")), ptr(self.pk("nv2")), N, 10, ptr(bf["adp"]),
+                      cfg.NP, st)
+            sups.append(bf["adp"])
+        sup_arr = (ctypes.c_void_p * max(len(sups), 1))(*[s_.data_ptr() for s_ in sups])
+        sx = x.stride()
+        _lib.call("gwn_start_conv_fwd", ptr(x), sx[0], sx[1], sx[2], sx[3], B, cin, N, t_in, ts[0],
+                  ptr(self.pk("start_w")), ptr(self.pk("start_b")), C, ptr(bf["x0"]), None, st)
+        xcur = bf["x0"]
+        for i in range(L):
+            d = cfg.dilations[i]
+            ta = _lib.TcnArgs(x=ptr(xcur), t_in=ts[i], P=P, c=C, dilation=d,
+                              w_fg=ptr(self.pk("fg_w%d" % i)), b_fg=ptr(self.pk("fg_b%d" % i)),
+                              xg=ptr(bf["xg"]), ld_xg=C, fg=None,
+                              skipcat=bf["skipcat"].data_ptr() + 4 * i * C, ld_skip=L * C,
+                              skip_row0=(ts[i + 1] - tf) * P)
+            _lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), st)
+            if i == L - 1:
+                break  # the last gcn / bn output never reaches the output
+            xnext = bf["xa"] if xcur is not bf["xa"] else bf["xb"]
+            rm, rv, _, eps = bn_bufs[i]
+            ga = _lib.GcnArgs(rows=ts[i + 1] * P, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
+                              sup=ctypes.cast(sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=cfg.NP,
+                              h=ptr(bf["xg"]), ld_h=C,
+                              w_mlp=ptr(self.pk("mlp_w%d" % i)), b_mlp=ptr(self.pk("mlp_b%d" % i)),
+                              residual=xcur.data_ptr() + 4 * d * P * C, z=None,
+                              seed_ptr=ptr(self.seed), salt=i, drop_p=0.0, bn_partials=None,
+                              no_pieces=1, bn_running_mean=ptr(rm), bn_running_var=ptr(rv),
+                              bn_weight=ptr(self.pk("bn_g%d" % i)), bn_bias=ptr(self.pk("bn_b%d" % i)),
+                              bn_eps=eps, bn_out=ptr(xnext))
+            _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
+            xcur = xnext
+        self._head_fwd(bf["skipcat"], bf["skr"], bf["e1"], bf["y"], tf * P, None)
         out = torch.empty(B, cfg.O, N, tf, device=self.device, dtype=F32)
-        lib.call("gwn_to_nchw", ptr(acts.y), B, cfg.O, N, tf, ptr(out), st)
-        return out, acts
+        _lib.call("gwn_to_nchw", ptr(bf["y"]), B, cfg.O, N, tf, ptr(out), st)
+        return out, bf
 
     # ---------------------------------------------------------------------------------------
     def backward(self, acts, dout):

@@ -139,6 +139,10 @@ def load_dataset_metr(dataset_dir, batch_size, valid_batch_size=None, test_batch
     return data
 
 
+# test.py:56 calls ``util.load_dataset``; the reference's util only defines the METR-LA loader
+load_dataset = load_dataset_metr
+
+
 def _mask(labels, null_val):
     if np.isnan(null_val):
         mask = ~torch.isnan(labels)

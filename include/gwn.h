@@ -353,6 +353,30 @@ int gwn_sum_vectors(const float* x, int count, int len, long stride, float* out,
 /* (*counter) += inc  on the device (dropout seed / step bookkeeping inside graphs) */
 int gwn_increment_u64(unsigned long long* counter, unsigned long long inc, hipStream_t stream);
 
+
+/* ---------------------------------------------------------------------------------------------
+ * Evaluation and data ingestion (infer.hip)
+ *
+ * util.metric(scaler.inverse_transform(yhat[:, :, h]), real[:, :, h]) for every horizon h
+ * (train.py:392-400, test.py:76-85; util.py:510-559 with null_val 0): out[h] = (mae, mape, rmse).
+ * yhat / real are [S][N][H] addressed by element strides (s, h, n); pred = yhat * std + mean.
+ * Workspace: gwn_horizon_metrics_workspace_floats(H) floats.  Fixed-order reductions. */
+int gwn_horizon_metrics(const float* yhat, long ps, long ph, long pn, const float* real, long rs, long rh,
+                        long rn, int S, int H, int N, float mean, float std, float* out, float* workspace,
+                        hipStream_t stream);
+long gwn_horizon_metrics_workspace_floats(int H);
+/* dst[i][:] = src[idx[i]][:] for i < count, rows of row_floats floats (a shuffled mini-batch from
+ * an HBM-resident sample array, util.py:36-51) */
+int gwn_gather_rows(const float* src, long row_floats, const long long* idx, int count, float* dst,
+                    hipStream_t stream);
+/* Mini-batch of sliding windows (generate_training_data.py:28-49) straight from the raw series
+ * [T][N] (fp64): for b < B, x[b][l][n] = (series[t + xoff[l]][n] (- mean) / std if scale_x,
+ * computed in fp64), tod[t'] and dow[t'] appended as channels when non-NULL; y[b][l][n] the same
+ * with yoff and no scaling; t = t_last[b].  x, y fp32 [B][LX or LY][N][cin]. */
+int gwn_window_batch(const double* series, const double* tod, const double* dow, int N,
+                     const long long* t_last, int B, const int* xoff, int LX, const int* yoff, int LY,
+                     double mean, double std, int scale_x, float* x, float* y, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
