@@ -78,6 +78,9 @@ class GcnArgs(ctypes.Structure):
         ("bn_running_mean", c_void_p), ("bn_running_var", c_void_p), ("bn_weight", c_void_p),
         ("bn_bias", c_void_p), ("bn_eps", c_float), ("bn_out", c_void_p),
         ("layout", c_int),
+        ("split_planes", c_int),
+        ("sup_split", c_void_p), ("sup_split_stride", c_long), ("ld_split", c_int),
+        ("w_split", c_void_p),
     ]
 
 
@@ -131,6 +134,11 @@ _SIGS = [
     ("gwn_gated_tcn_bwd", c_int, [ctypes.POINTER(TcnBwdArgs), c_void_p]),
     ("gwn_gated_tcn_bwd_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
     ("gwn_gcn_fwd", c_int, [ctypes.POINTER(GcnArgs), c_void_p]),
+    ("gwn_gcn_split_supported", c_int, [c_int, c_int, c_int]),
+    ("gwn_split_support_elems", c_long, [c_int, c_int]),
+    ("gwn_split_supports", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_long, c_int, c_void_p]),
+    ("gwn_split_mlp_elems", c_long, [c_int, c_int]),
+    ("gwn_split_mlp_weights", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p]),
     ("gwn_gcn_bwd", c_int, [ctypes.POINTER(GcnBwdArgs), c_void_p]),
     ("gwn_gcn_bwd_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
     ("gwn_wgrad", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,

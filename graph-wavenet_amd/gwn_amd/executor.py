@@ -268,6 +268,46 @@ class Executor:
         self.seed.fill_(int(torch.randint(0, 2 ** 62, (1,)).item()))
         self._scratch = {}
 
+    # ---------------------------------------------------------------------------------------
+    def split_planes(self):
+        """bf16 pieces per operand of the split-MFMA gcn forward (GWN_SPLIT: 3 = fp32 accuracy,
+        0 = the f32-MFMA kernel, the default: at METR-LA shape the split kernel holds one
+        workgroup per CU (101 KB of LDS planes) and measured 223 vs 213 us per T=12 launch,
+        tools/bench_gcn.py).  0 when the shape has no split instantiation."""
+        cfg = self.cfg
+        planes = int(os.environ.get("GWN_SPLIT", "0"))
+        if planes == 0 or not cfg.use_gcn or cfg.nsup < 1:
+            return 0
+        return planes if _lib.load().gwn_gcn_split_supported(cfg.C, cfg.N, planes) else 0
+
+    def split_operands(self, sup_arr, nsup, planes):
+        """bf16 piece planes of the supports (transposed) and of every layer's mlp weights, for
+        the split path of gwn_gcn_fwd; rebuilt each forward (adp and the weights change)."""
+        cfg = self.cfg
+        lib = _lib.load()
+        st = _lib.stream()
+        sup_el = lib.gwn_split_support_elems(cfg.N, planes)
+        w_el = (lib.gwn_split_mlp_elems(nsup, planes) + 7) // 8 * 8
+        key = ("split", planes, nsup)
+        b = self._scratch.get(key)
+        if b is None:
+            b = {"sup": torch.empty(nsup * sup_el, device=self.device, dtype=torch.int16),
+                 "w": torch.empty(cfg.L * w_el, device=self.device, dtype=torch.int16)}
+            self._scratch[key] = b
+        _lib.call("gwn_split_supports", ctypes.cast(sup_arr, ctypes.c_void_p), nsup, cfg.N, cfg.NP, planes,
+                  ptr(b["sup"]), sup_el, cfg.NP, st)
+        w_arr = (ctypes.c_void_p * cfg.L)(*[self.pk("mlp_w%d" % i).data_ptr() for i in range(cfg.L)])
+        _lib.call("gwn_split_mlp_weights", ctypes.cast(w_arr, ctypes.c_void_p), cfg.L, nsup, planes, ptr(b["w"]),
+                  w_el, st)
+        return {"planes": planes, "sup": b["sup"].data_ptr(), "sup_stride": sup_el, "w": b["w"].data_ptr(),
+                "w_stride_bytes": 2 * w_el}
+
+    def split_fields(self, sp, i):
+        if sp is None:
+            return {}
+        return dict(split_planes=sp["planes"], sup_split=sp["sup"], sup_split_stride=sp["sup_stride"],
+                    ld_split=self.cfg.NP, w_split=sp["w"] + i * sp["w_stride_bytes"])
+
     def pk(self, name, buf=None):
         return self.layout.view(self.packed if buf is None else buf, name)
 
@@ -390,6 +430,8 @@ class Executor:
                  ptr(self.pk("start_w")), ptr(self.pk("start_b")), C, ptr(acts.X[0]), ptr(acts.xin), st)
         scr = self.scratch(B, ts)
         ws, bnpart = scr["ws"], scr["bnpart"]
+        planes = self.split_planes()
+        sp = self.split_operands(sup_arr, len(sups), planes) if planes else None
         for i in range(L):
             d = cfg.dilations[i]
             rows = ts[i + 1] * P
@@ -408,7 +450,7 @@ class Executor:
                               w_mlp=ptr(self.pk("mlp_w%d" % i)), b_mlp=ptr(self.pk("mlp_b%d" % i)),
                               residual=acts.X[i].data_ptr() + 4 * d * P * C, z=ptr(acts.Z[i]),
                               seed_ptr=ptr(self.seed), salt=i, drop_p=drop,
-                              bn_partials=ptr(bnpart) if training else None)
+                              bn_partials=ptr(bnpart) if training else None, **self.split_fields(sp, i))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
             rm, rv, mom, eps = bn_bufs[i]
@@ -501,6 +543,8 @@ class Executor:
                       cfg.NP, st)
             sups.append(bf["adp"])
         sup_arr = (ctypes.c_void_p * max(len(sups), 1))(*[s_.data_ptr() for s_ in sups])
+        planes = self.split_planes()
+        sp = self.split_operands(sup_arr, len(sups), planes) if planes else None
         sx = x.stride()
         _lib.call("gwn_start_conv_fwd", ptr(x), sx[0], sx[1], sx[2], sx[3], B, cin, N, t_in, ts[0],
                   ptr(self.pk("start_w")), ptr(self.pk("start_b")), C, ptr(bf["x0"]), None, st)
@@ -525,7 +569,7 @@ class Executor:
                               seed_ptr=ptr(self.seed), salt=i, drop_p=0.0, bn_partials=None,
                               no_pieces=1, bn_running_mean=ptr(rm), bn_running_var=ptr(rv),
                               bn_weight=ptr(self.pk("bn_g%d" % i)), bn_bias=ptr(self.pk("bn_b%d" % i)),
-                              bn_eps=eps, bn_out=ptr(xnext))
+                              bn_eps=eps, bn_out=ptr(xnext), **self.split_fields(sp, i))
             _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             xcur = xnext
         self._head_fwd(bf["skipcat"], bf["skr"], bf["e1"], bf["y"], tf * P, None)

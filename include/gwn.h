@@ -208,6 +208,15 @@ typedef struct gwn_gcn_args {
   const float* bn_running_mean; const float* bn_running_var; const float* bn_weight; const float* bn_bias;
   float bn_eps; float* bn_out;
   int layout;
+  /* split-bf16 path (split_planes = 2 or 3, 0 = off): every product on v_mfma_f32_32x32x16_bf16
+   * over bf16 pieces of the fp32 operands (3 pieces / 6 piece products = fp32 accuracy; 2 pieces
+   * ~1e-5 relative, measurements only).  Needs c == 32, nsup >= 1, 32*ceil(n/32) in {32, 224, 352}
+   * (2 pieces: 224 only), sup_split = gwn_split_supports output (support k at
+   * sup_split + k*sup_split_stride elements, rows ld_split), w_split = gwn_split_mlp_weights
+   * output for this layer.  The fp32 supports `sup` are not read on this path. */
+  int split_planes;
+  const void* sup_split; long sup_split_stride; int ld_split;
+  const void* w_split;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -215,6 +224,22 @@ typedef struct gwn_gcn_args {
  * must be [np][ld_sup] and ZERO outside [n][n] (gwn_pad_square makes such copies).
  * Otherwise: 2K nconv GEMMs + one mlp GEMM. */
 int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t stream);
+
+/* bf16 piece planes for the split path of gwn_gcn_fwd.
+ * gwn_split_supports: for each of the nsup padded supports sup[k] ([np][ld_sup], zero outside
+ *   [n][n], np = 32*ceil(n/32)) writes `planes` bf16 planes of sup[k]^T, [np][ld_dst] each, at
+ *   dst + k*sup_stride_elems (>= planes*np*ld_dst).  gwn_split_support_elems(n, planes) = the
+ *   elements of one support at ld_dst = np.
+ * gwn_split_mlp_weights: for each of nlayers gcn mlp weights w[l] ([32][(2*nsup+1)*32], the
+ *   reference's gconv.l.mlp.mlp.weight) writes the pieces in the kernel's input order at
+ *   dst + l*layer_stride_elems (>= gwn_split_mlp_elems(nsup, planes)).  Element type: bf16. */
+int gwn_gcn_split_supported(int c, int n, int planes); /* 1 if the split path takes (c, n, planes) */
+long gwn_split_support_elems(int n, int planes);
+int gwn_split_supports(const float* const* sup, int nsup, int n, int ld_sup, int planes, void* dst,
+                       long sup_stride_elems, int ld_dst, hipStream_t stream);
+long gwn_split_mlp_elems(int nsup, int planes);
+int gwn_split_mlp_weights(const float* const* w, int nlayers, int nsup, int planes, void* dst,
+                          long layer_stride_elems, hipStream_t stream);
 
 /* Backward of gwn_gcn_fwd given dh (gradient w.r.t. the dropout output, i.e. dz with the
  * dropout mask and scale already applied).  Produces dW_mlp [c][(2K+1)c], db_mlp [c], the

@@ -393,3 +393,92 @@ def test_gcn_fused_layouts_agree(gpu, n):
     # the two layouts: same products in the same k order per tile -> identical up to fma rounding
     for a_, b_ in zip(outs[0], outs[1]):
         assert rel_err(a_.cpu().numpy(), b_.cpu().numpy()) <= 1e-6
+
+
+@pytest.mark.parametrize("n,planes", [(16, 3), (207, 3), (325, 3), (207, 2)])
+def test_gcn_split_forward(gpu, n, planes):
+    """Split-bf16 MFMA forward of the fused gcn (bf16 pieces of every fp32 operand, 6 piece
+    products for 3 pieces) against fp64 (model.py:41-55 + residual model.py:234): hop pieces, z and
+    BN partials at the fp32 path's tolerance for 3 pieces; the 2-piece variant (~1e-5) at 1e-4.
+    Also: the eval-BN / no-pieces form and the dropout mask equal the f32 kernel's."""
+    import ctypes
+    from gwn_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(n + planes)
+    C, K, S = 32, 3, 6
+    NP = (n + 31) // 32 * 32
+    W = (2 * K + 1) * C
+    rows = S * n
+    assert lib.gwn_gcn_split_supported(C, n, planes) == 1
+    sups = []
+    for k in range(K):
+        s = torch.zeros(NP, NP, device=gpu)
+        a = torch.rand(n, n, device=gpu) * (torch.rand(n, n, device=gpu) < (0.05 if k < 2 else 1.0))
+        a = a + torch.eye(n, device=gpu)
+        s[:n, :n] = a / a.sum(1, keepdim=True)
+        sups.append(s)
+    arr = (ctypes.c_void_p * K)(*[s.data_ptr() for s in sups])
+    sup_el = lib.gwn_split_support_elems(n, planes)
+    ssup = torch.full((K * sup_el,), 12345, device=gpu, dtype=torch.int16)
+    _lib.call("gwn_split_supports", ctypes.cast(arr, ctypes.c_void_p), K, n, NP, planes, ssup.data_ptr(), sup_el, NP,
+              _lib.stream())
+    wm = torch.randn(C, W, device=gpu) * 0.1
+    w_el = lib.gwn_split_mlp_elems(K, planes)
+    sw = torch.empty(w_el, device=gpu, dtype=torch.int16)
+    warr = (ctypes.c_void_p * 1)(wm.data_ptr())
+    _lib.call("gwn_split_mlp_weights", ctypes.cast(warr, ctypes.c_void_p), 1, K, planes, sw.data_ptr(), w_el,
+              _lib.stream())
+    bm = torch.randn(C, device=gpu)
+    res = torch.randn(rows, C, device=gpu)
+    xg = torch.randn(rows, C, device=gpu)
+    seed = torch.full((1,), 99, device=gpu, dtype=torch.int64)
+
+    def run(split, drop=0.0, eval_bn=None):
+        h = torch.zeros(rows, W, device=gpu)
+        h[:, :C] = xg
+        z = torch.full((rows, C), 7.0, device=gpu)
+        bnp = torch.empty(S * 3 * C, device=gpu)
+        kw = {}
+        if split:
+            kw = dict(split_planes=planes, sup_split=ssup.data_ptr(), sup_split_stride=sup_el, ld_split=NP,
+                      w_split=sw.data_ptr())
+        if eval_bn is not None:
+            rm, rv, g_, b_, xo = eval_bn
+            kw.update(no_pieces=1, bn_running_mean=rm.data_ptr(), bn_running_var=rv.data_ptr(),
+                      bn_weight=g_.data_ptr(), bn_bias=b_.data_ptr(), bn_eps=1e-5, bn_out=xo.data_ptr())
+        ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)),
+                          ld_sup=NP, h=h.data_ptr(), ld_h=W, w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(),
+                          residual=res.data_ptr(), z=None if eval_bn is not None else z.data_ptr(),
+                          seed_ptr=seed.data_ptr(), salt=3, drop_p=drop,
+                          bn_partials=None if eval_bn is not None else bnp.data_ptr(), **kw)
+        _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
+        torch.cuda.synchronize()
+        return h, z, bnp
+
+    h, z, bnp = run(True)
+    X = xg.double().cpu().view(S, n, C)
+    pieces = [X]
+    for s in sups:
+        a = s[:n, :n].double().cpu()
+        x1 = torch.einsum("svc,vw->swc", X, a)
+        x2 = torch.einsum("svc,vw->swc", x1, a)
+        pieces += [x1, x2]
+    H = torch.cat(pieces, dim=2).reshape(rows, W)
+    Z = H @ wm.double().cpu().t() + bm.double().cpu() + res.double().cpu()
+    tol = 2e-6 if planes == 3 else 1e-4
+    assert rel_err(h.cpu().numpy(), H.numpy()) <= tol
+    assert rel_err(z.cpu().numpy(), Z.numpy()) <= tol
+    means = bnp.view(S, 3, C)[:, 1].cpu().double()
+    assert rel_err(means.numpy(), Z.view(S, n, C).mean(1).numpy()) <= max(tol, 1e-5)
+    # dropout: the same counter-hash mask as the f32 kernel
+    _, zs, _ = run(True, drop=0.3)
+    _, zf, _ = run(False, drop=0.3)
+    assert torch.equal(zs == res, zf == res)
+    assert rel_err(zs.cpu().numpy(), zf.cpu().numpy()) <= 10 * tol
+    # eval BatchNorm folded into the epilogue, no hop pieces stored
+    rm, rv = torch.randn(C, device=gpu), torch.rand(C, device=gpu) + 0.5
+    g_, b_ = torch.randn(C, device=gpu), torch.randn(C, device=gpu)
+    xo = torch.empty(rows, C, device=gpu)
+    run(True, eval_bn=(rm, rv, g_, b_, xo))
+    ref = (Z - rm.double().cpu()) / torch.sqrt(rv.double().cpu() + 1e-5) * g_.double().cpu() + b_.double().cpu()
+    assert rel_err(xo.cpu().numpy(), ref.numpy()) <= 10 * tol

@@ -341,3 +341,35 @@ def test_fused_layer_backward_matches_unfused(gpu, monkeypatch, dropout):
             assert float((a - b).norm() / b.norm()) <= 1e-5, k
         else:
             assert float(a.abs().max()) <= 1e-6, k
+
+
+def test_split_forward_matches_f32_forward(gpu, monkeypatch):
+    """A training step with the split-bf16 gcn forward (GWN_SPLIT=3) against the f32-MFMA
+    forward (GWN_SPLIT=0, the default) on the same inputs and dropout masks: loss and every
+    gradient agree to fp32 rounding."""
+    from gwn_amd import synthetic, util
+    from gwn_amd.engine import trainer
+    adj = synthetic.random_sensor_graph(207, seed=0)
+    sups = [torch.tensor(a, device=gpu) for a in synthetic.double_transition(adj)]
+    x, y = synthetic.synthetic_batch(8, 207, 12, seed=5)
+    grads, losses = [], []
+    for split in ("3", "0"):
+        monkeypatch.setenv("GWN_SPLIT", split)
+        monkeypatch.setenv("GWN_GRAPHS", "0")
+        torch.manual_seed(999)
+        eng = trainer(util.StandardScaler(54.4, 19.5), 2, 12, 207, 32, 0.3, 0.0, 0.0, gpu, sups, True, True,
+                      None, 4, 2)
+        eng.clip = None
+        eng.model.executor().seed.fill_(78)
+        losses.append(eng.train(torch.tensor(x, device=gpu), torch.tensor(y, device=gpu))[0])
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.detach().clone() for n, p in eng.model.named_parameters() if p.grad is not None})
+    assert abs(losses[0] - losses[1]) <= 1e-5 * abs(losses[1])
+    assert set(grads[0]) == set(grads[1])
+    scale = max(float(v.abs().max()) for v in grads[1].values())
+    for k in grads[0]:
+        a, b = grads[0][k].double(), grads[1][k].double()
+        if b.norm() > 1e-3 * scale:
+            assert float((a - b).norm() / b.norm()) <= 2e-5, k
+        else:
+            assert float((a - b).abs().max()) <= 1e-5 * scale, k

@@ -88,6 +88,23 @@ def main():
                          ("bwd-data" + tag, lambda a=gd_l: _lib.call("gwn_gcn_bwd", ctypes.byref(a), st)),
                          ("bwd-data+bn+gate" + tag, lambda a=gf_l: _lib.call("gwn_gcn_bwd", ctypes.byref(a), st))]
         variants.append(("bwd (+wgrad, gram)", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)))
+        for planes in (3, 2):
+            if not lib.gwn_gcn_split_supported(C, N, planes):
+                continue
+            sup_el = lib.gwn_split_support_elems(N, planes)
+            w_el = (lib.gwn_split_mlp_elems(K, planes) + 7) // 8 * 8
+            ssup = torch.empty(K * sup_el, device=dev, dtype=torch.int16)
+            sw = torch.empty(w_el, device=dev, dtype=torch.int16)
+            warr = (ctypes.c_void_p * 1)(wm.data_ptr())
+            _lib.call("gwn_split_supports", ctypes.cast(arr, ctypes.c_void_p), K, N, NP, planes, ssup.data_ptr(),
+                      sup_el, NP, st)
+            _lib.call("gwn_split_mlp_weights", ctypes.cast(warr, ctypes.c_void_p), 1, K, planes, sw.data_ptr(),
+                      w_el, st)
+            ga_s = _lib.GcnArgs.from_buffer_copy(ga)
+            ga_s.split_planes, ga_s.sup_split, ga_s.sup_split_stride = planes, ssup.data_ptr(), sup_el
+            ga_s.ld_split, ga_s.w_split = NP, sw.data_ptr()
+            variants.append(("fwd split%d" % planes,
+                             lambda a=ga_s, keep=(ssup, sw): _lib.call("gwn_gcn_fwd", ctypes.byref(a), st)))
         for name, fn in variants:
             for _ in range(3):
                 fn()
