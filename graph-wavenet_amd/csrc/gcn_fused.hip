@@ -79,6 +79,10 @@ __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int s
 #endif
 }
 
+// the last 32-node K batch holds at most 16 real nodes: its upper 8 k-steps (2 nodes each) only
+// multiply zero rows of the padded support and are skipped (n = 207: nodes 192..206)
+__host__ __device__ constexpr bool half_last_batch(int n) { return n - 32 * ((n + 31) / 32 - 1) <= 16; }
+
 struct GBatch {
   float v[KB];
 };
@@ -106,6 +110,7 @@ __device__ __forceinline__ GBatch w_frags(const float* W, int ld_w, int off, int
 }
 
 // D'[c][w0+col] += sum_v buf[v][c] * G[v][w0+col];  g0 = g_first(G, ...) (consumed)
+template <bool HL>
 __device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int ld, int nkb, int w0,
                                           int lane, f32x16 acc, const GBatch& g0) {
   const int half = lane >> 5, col = lane & 31;
@@ -138,6 +143,22 @@ __device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int 
 #pragma unroll
     for (int j = 0; j < KB; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], g[j], acc, 0, 0, 0);
   };
+  // k-step j of a batch covers nodes 32 kb + 2 j + {0, 1}: when the last batch holds at most 16
+  // real nodes (n = 207: nodes 192..206) its upper 8 k-steps multiply zero rows and are skipped
+  // (HL = half_last_batch(n), a kernel template flag; 7 % of the diffusion MFMAs at n = 207)
+  auto last_batch = [&](int kb, const float* g) {
+    const float* bp = buf + (32 * kb + half) * LDR + col;
+    float av[KB];
+    if (HL) {
+#pragma unroll
+      for (int j = 0; j < KB / 2; ++j) av[j] = bp[2 * j * LDR];
+#pragma unroll
+      for (int j = 0; j < KB / 2; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], g[j], acc, 0, 0, 0);
+    } else {
+      lds_batch(kb, av);
+      mfma_batch(av, g);
+    }
+  };
   int kb = 0;
   for (; kb + 2 < nkb; kb += 2) {
     float av[KB];
@@ -148,16 +169,14 @@ __device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int 
     lds_batch(kb + 1, av);
     mfma_batch(av, gb);
   }
-  float av[KB];
   if (kb + 1 < nkb) {  // two batches left
+    float av[KB];
     g_batch(kb + 1, gb);
     lds_batch(kb, av);
     mfma_batch(av, ga);
-    lds_batch(kb + 1, av);
-    mfma_batch(av, gb);
+    last_batch(kb + 1, gb);
   } else {             // one batch left
-    lds_batch(kb, av);
-    mfma_batch(av, ga);
+    last_batch(kb, ga);
   }
   return acc;
 }
@@ -379,8 +398,8 @@ __device__ __forceinline__ void bwd_gate_epilogue(const FusedBwd& a, const float
 // ---------------------------------------------------------------------------------------------
 // tile-wave layout: one wave per 32-node tile
 
-template <int MAXT>
-__global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
+template <int MAXT, bool HL>
+__global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a) {
   extern __shared__ float lds[];
   __shared__ float red[2][MAXT];
   const int n = a.n;
@@ -399,7 +418,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
   f32x16 hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
   for (int k = 0; k < a.nsup; ++k) {
     const float* G = a.sup[k];
-    f32x16 d = diffuse(xs, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
+    f32x16 d = diffuse<HL>(xs, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
     g0 = g_first(G, a.ld_sup, nkb, w0, lane);  // hop 2 re-reads the same support
     {
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
@@ -409,7 +428,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
     acc_to_lds(ys, d, w0, lane);
     if (a.store_pieces) acc_to_global((float*)hs + (1 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
     __syncthreads();
-    d = diffuse(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
+    d = diffuse<HL>(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
     if (k + 1 < a.nsup) g0 = g_first(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
     {
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
@@ -424,8 +443,8 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_fused_kernel(const FusedFwd a) {
   fwd_epilogue<EPT>(a, ys, red[0], red[1], row0, n);
 }
 
-template <int MAXT>
-__global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
+template <int MAXT, bool HL>
+__global__ __launch_bounds__(MAXT, 4) void gcn_bwd_fused_kernel(const FusedBwd a) {
   extern __shared__ float lds[];
   const int n = a.n;
   const int nkb = (int)(blockDim.x >> 6);
@@ -449,13 +468,13 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_fused_kernel(const FusedBwd a) {
     }
     __syncthreads();
     f32x16 t = mlpT_from_lds(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, w0, lane, zero16());
-    t = diffuse(buf, GT, a.ld_sup, nkb, w0, lane, t, g0);  // dx1 = dP_x1 + A dP_x2
+    t = diffuse<HL>(buf, GT, a.ld_sup, nkb, w0, lane, t, g0);  // dx1 = dP_x1 + A dP_x2
     g0 = g_first(GT, a.ld_sup, nkb, w0, lane);
     __syncthreads();
     acc_to_lds(buf, t, w0, lane);
     if (k == a.adp_index) acc_to_global(a.t1 + row0 * a.ld_t, a.ld_t, t, w0, lane, n);
     __syncthreads();
-    dx = diffuse(buf, GT, a.ld_sup, nkb, w0, lane, dx, g0);  // dxg += A dx1
+    dx = diffuse<HL>(buf, GT, a.ld_sup, nkb, w0, lane, dx, g0);  // dxg += A dx1
     if (k + 1 < a.nsup) g0 = g_first(a.supT[k + 1], a.ld_sup, nkb, w0, lane);
   }
   if (!a.dfg) {
@@ -790,15 +809,22 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   const size_t lds = fused_lds_bytes(g->n);
   static bool attr_set = false;
   if (!attr_set) {
-    ensure_lds_attr(gcn_fwd_fused_kernel<512>);
-    ensure_lds_attr(gcn_fwd_fused_kernel<1024>);
+    ensure_lds_attr(gcn_fwd_fused_kernel<512, false>);
+    ensure_lds_attr(gcn_fwd_fused_kernel<512, true>);
+    ensure_lds_attr(gcn_fwd_fused_kernel<1024, false>);
+    ensure_lds_attr(gcn_fwd_fused_kernel<1024, true>);
     ensure_lds_attr(gcn_fwd_fused4_kernel);
     attr_set = true;
   }
   const int slices = g->rows / g->n;
   if (use_4wave(g->layout, nwt)) gcn_fwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
-  else if (nwt <= 8) gcn_fwd_fused_kernel<512><<<slices, 64 * nwt, lds, s>>>(a);
-  else gcn_fwd_fused_kernel<1024><<<slices, 64 * nwt, lds, s>>>(a);
+  else if (half_last_batch(g->n)) {
+    if (nwt <= 8) gcn_fwd_fused_kernel<512, true><<<slices, 64 * nwt, lds, s>>>(a);
+    else gcn_fwd_fused_kernel<1024, true><<<slices, 64 * nwt, lds, s>>>(a);
+  } else {
+    if (nwt <= 8) gcn_fwd_fused_kernel<512, false><<<slices, 64 * nwt, lds, s>>>(a);
+    else gcn_fwd_fused_kernel<1024, false><<<slices, 64 * nwt, lds, s>>>(a);
+  }
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -830,16 +856,23 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   if (a.dfg) GWN_REQUIRE(a.fg != nullptr, "gcn_bwd (fused): the gate epilogue needs fg");
   static bool attr_set = false;
   if (!attr_set) {
-    ensure_lds_attr(gcn_bwd_fused_kernel<512>);
-    ensure_lds_attr(gcn_bwd_fused_kernel<1024>);
+    ensure_lds_attr(gcn_bwd_fused_kernel<512, false>);
+    ensure_lds_attr(gcn_bwd_fused_kernel<512, true>);
+    ensure_lds_attr(gcn_bwd_fused_kernel<1024, false>);
+    ensure_lds_attr(gcn_bwd_fused_kernel<1024, true>);
     ensure_lds_attr(gcn_bwd_fused4_kernel);
     attr_set = true;
   }
   const size_t lds = fused_lds_bytes(g->n);
   const int slices = g->rows / g->n;
   if (use_4wave(g->layout, nwt)) gcn_bwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
-  else if (nwt <= 8) gcn_bwd_fused_kernel<512><<<slices, 64 * nwt, lds, s>>>(a);
-  else gcn_bwd_fused_kernel<1024><<<slices, 64 * nwt, lds, s>>>(a);
+  else if (half_last_batch(g->n)) {
+    if (nwt <= 8) gcn_bwd_fused_kernel<512, true><<<slices, 64 * nwt, lds, s>>>(a);
+    else gcn_bwd_fused_kernel<1024, true><<<slices, 64 * nwt, lds, s>>>(a);
+  } else {
+    if (nwt <= 8) gcn_bwd_fused_kernel<512, false><<<slices, 64 * nwt, lds, s>>>(a);
+    else gcn_bwd_fused_kernel<1024, false><<<slices, 64 * nwt, lds, s>>>(a);
+  }
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -855,9 +888,9 @@ extern "C" int gwn_fused_occupancy(int n, int backward) {
     if (backward) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_fused4_kernel, 256, lds);
     else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_fused4_kernel, 256, lds);
   } else if (backward) {
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_fused_kernel<1024>, 64 * nwt, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_fused_kernel<1024, false>, 64 * nwt, lds);
   } else {
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_fused_kernel<1024>, 64 * nwt, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_fused_kernel<1024, false>, 64 * nwt, lds);
   }
   return e == hipSuccess ? blocks : -(int)e;
 }
