@@ -131,7 +131,7 @@ def main():
 
 
 def measure_dominant(eng, dev, rounds=5):
-    """The dominant kernel is the fused diffusion graph convolution gcn_fwd_fused_kernel<512>
+    """The dominant kernel is the fused diffusion graph convolution gcn_fwd_fused_kernel<512, true>
     (gwn_gcn_fwd: 3 supports x 2 hops of 'ncvl,vw->ncwl' + the 224->32 mlp + residual + dropout
     + BN partials, one launch per layer, 8 per step).  Replay exactly the last training step's 8
     launches (same arguments and buffers; the replay is idempotent) with HIP events on the
@@ -168,7 +168,7 @@ def measure_dominant(eng, dev, rounds=5):
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get("traffic_bytes_per_launch")
-    return {"kernel": "gcn_fwd_fused_kernel<512> (fused diffusion GCN forward, 8 launches/step)",
+    return {"kernel": "gcn_fwd_fused_kernel<512, true> (fused diffusion GCN forward, 8 launches/step)",
             "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "traffic_source": "profiles/r01/pmc_gcn_fwd_fused.json" if traffic else None,
