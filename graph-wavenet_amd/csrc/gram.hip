@@ -3,11 +3,16 @@
 // over all slices s of a layer (model.py:12-14 differentiated w.r.t. A; two pairs per layer for
 // order 2: (xg, dx1) and (x1, dx2)).  M = N = n (<= 224 here), K = slices * 32 per pair.
 //
-// One wave per (32x32 output tile, slice range).  The contraction is laid onto
-// v_mfma_f32_32x32x2_f32 PERMUTED: step j takes channel c = 16h + j in lane half h, so lane (i, h)
-// needs the 16 contiguous floats X[s*n + 32*vt + i][16h ..] (A) and T[s*n + 32*wt + i][16h ..]
-// (B) — four 16-B buffer loads each, nodes >= n reading zeros (out-of-range offset).  No LDS, no
-// barriers; the next slice's fragments are in flight while the current slice's MFMAs run.
+// One wave per (32x64 output block = one row tile x two column tiles, slice range).  The
+// contraction is laid onto v_mfma_f32_32x32x2_f32 PERMUTED: step j takes channel c = 16h + j in
+// lane half h, so lane (i, h) needs the 16 contiguous floats X[s*n + 32*vt + i][16h ..] (A) and
+// T[s*n + 32*wt + i][16h ..] (B) — four 16-B buffer loads each, nodes >= n reading zeros
+// (out-of-range offset).  Each A fragment feeds two accumulator chains (0.375 loads per MFMA
+// instead of 1).  The K loop walks (slice, pair) steps with the next step's 12 fragments in flight
+// while the current step's 32 MFMAs run (pairs unrolled: scalar buffer resources).  No LDS, no
+// barriers.  Measured (tools/bench_gcn.py under rocprofv3, T=12, 768 slices): 72 us against 78 us
+// for one 32x32 tile per wave; a whole slice in flight (200 VGPRs) or 4096 waves were slower.
+// Still ~55 TFLOP/s: each 16-B fragment load touches 32 rows (32 cache lines per instruction).
 // Waves of one slice range are placed on one XCD (blocks round-robin over the 8 XCDs), so the
 // 7x re-reads of each row block hit that XCD's L2.  Partials [nsplit][npad][npad] are summed in
 // a fixed order by a second kernel (deterministic).
@@ -19,6 +24,9 @@ namespace {
 
 constexpr int OOR = 0x7ffffff0;
 constexpr int NXCD = 8;
+#ifndef GRAM_WAVES
+#define GRAM_WAVES 2560  // target wave count of a gram launch
+#endif
 
 struct Gram {
   const float* X[2]; const float* T[2]; int npairs;  // pair 1 used iff npairs == 2
@@ -35,12 +43,14 @@ __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >
 template <int NP>
 __global__ __launch_bounds__(64) void gram_kernel(const Gram g) {
   const int lane = threadIdx.x, half = lane >> 5, col = lane & 31;
-  const int ntile = g.nt * g.nt;
-  // XCD-aware placement: block b runs on XCD b % 8; keep every (tile, split) of one split on one XCD
+  const int ntp = (g.nt + 1) / 2;  // column tile pairs
+  const int per_split = g.nt * ntp;
+  // XCD-aware placement: block b runs on XCD b % 8; keep every block of one split on one XCD
   const int b = blockIdx.x, xcd = b % NXCD, j = b / NXCD;
-  const int tile = j % ntile, split = (j / ntile) * NXCD + xcd;
+  const int blk = j % per_split, split = (j / per_split) * NXCD + xcd;
   if (split >= g.nsplit) return;
-  const int vt = tile / g.nt, wt = tile % g.nt;
+  const int vt = blk / ntp, wt0 = 2 * (blk % ntp);
+  const bool two = wt0 + 1 < g.nt;  // wave-uniform: the last pair of an odd tile count has one tile
   const int s0 = (int)((long)g.slices * split / g.nsplit), s1 = (int)((long)g.slices * (split + 1) / g.nsplit);
 
   __amdgpu_buffer_rsrc_t rx[NP], rt[NP];
@@ -50,45 +60,67 @@ __global__ __launch_bounds__(64) void gram_kernel(const Gram g) {
     rx[p] = rsrc(g.X[p], rows * g.ldx * 4);
     rt[p] = rsrc(g.T[p], rows * g.ldt * 4);
   }
-  const int v = 32 * vt + col, w = 32 * wt + col;
-  auto load = [&](int s, float4* fa, float4* fb) {
+  const int v = 32 * vt + col, w0 = 32 * wt0 + col, w1 = w0 + 32;
+  // fragments of (slice s, pair p); p must be a compile-time constant after unrolling so the buffer
+  // resource stays scalar (a run-time select makes it a per-lane value: waterfall loops per load).
+  // Past the last slice every offset is out of range (zeros).
+  auto load = [&](int s, int p, float4* fa, float4* fb) {
     const bool ok = s < s1;
-    const long rv = (long)s * g.n + v, rw = (long)s * g.n + w;
-    const int ox = (ok && v < g.n) ? (int)((rv * g.ldx + 16 * half) * 4) : OOR;
-    const int ot = (ok && w < g.n) ? (int)((rw * g.ldt + 16 * half) * 4) : OOR;
+    const long base = (long)s * g.n;
+    const int ox = (ok && v < g.n) ? (int)(((base + v) * g.ldx + 16 * half) * 4) : OOR;
+    const int o0 = (ok && w0 < g.n) ? (int)(((base + w0) * g.ldt + 16 * half) * 4) : OOR;
+    const int o1 = (ok && two && w1 < g.n) ? (int)(((base + w1) * g.ldt + 16 * half) * 4) : OOR;
 #pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        fa[4 * p + q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx[p], ox, 16 * q, 0));
-        fb[4 * p + q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt[p], ot, 16 * q, 0));
-      }
+    for (int q = 0; q < 4; ++q) {
+      fa[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx[p], ox, 16 * q, 0));
+      fb[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt[p], o0, 16 * q, 0));
+      fb[4 + q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt[p], o1, 16 * q, 0));
+    }
   };
 
-  f32x16 acc;
+  f32x16 acc0, acc1;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-  float4 fa[4 * NP], fb[4 * NP];
-  load(s0, fa, fb);
+  for (int r = 0; r < 16; ++r) {
+    acc0[r] = 0.0f;
+    acc1[r] = 0.0f;
+  }
+  float4 fa[4], fb[8];
+  load(s0, 0, fa, fb);
   for (int s = s0; s < s1; ++s) {
-    float4 na[4 * NP], nb[4 * NP];
-    load(s + 1, na, nb);
-    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int q = 0; q < 4 * NP; ++q) {
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[q].x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, fb[q].y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, fb[q].z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, fb[q].w, acc, 0, 0, 0);
+    for (int p = 0; p < NP; ++p) {
+      float4 na[4], nb[8];
+      if (p + 1 < NP) load(s, p + 1, na, nb);
+      else load(s + 1, 0, na, nb);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[q].x, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[4 + q].x, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, fb[q].y, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, fb[4 + q].y, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, fb[q].z, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, fb[4 + q].z, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, fb[q].w, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, fb[4 + q].w, acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        fa[q] = na[q];
+        fb[q] = nb[q];
+        fb[4 + q] = nb[4 + q];
+      }
     }
-#pragma unroll
-    for (int q = 0; q < 4 * NP; ++q) { fa[q] = na[q]; fb[q] = nb[q]; }
   }
   // D[v][w]: col = lane&31 -> w, rows -> v
   const int np = 32 * g.nt;
-  float* out = g.part + (long)split * np * np + (long)(32 * vt) * np + 32 * wt + col;
+  float* out = g.part + (long)split * np * np + (long)(32 * vt) * np + 32 * wt0 + col;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) out[(long)crow(r, half) * np] = acc[r];
+  for (int r = 0; r < 16; ++r) out[(long)crow(r, half) * np] = acc0[r];
+  if (two) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[(long)crow(r, half) * np + 32] = acc1[r];
+  }
 }
 
 // dA[v][w] (+)= sum_split part[split][v][w], fixed order
@@ -113,8 +145,9 @@ __global__ void gram_reduce_kernel(const float* part, int nsplit, int n, int np,
 
 int gram_nsplit(int n, int slices) {
   const int nt = (n + 31) / 32;
-  // ~4096 waves over 256 CUs (3-4 per SIMD); a multiple of the XCD count; >= 1 slice per split
-  int ns = 4096 / (nt * nt);
+  // ~2.5k waves over 256 CUs (2-3 per SIMD, each with two accumulator chains); a multiple of the
+  // XCD count; >= 1 slice per split.  More splits cost partial-sum traffic (splits x np^2 floats).
+  int ns = GRAM_WAVES / (nt * ((nt + 1) / 2));
   ns = (ns / NXCD) * NXCD;
   if (ns < NXCD) ns = NXCD;
   if (ns > slices) ns = slices;
@@ -143,7 +176,7 @@ int gwn_gram(const float* x1, const float* t1, const float* x2, const float* t2,
   g.n = n; g.nt = (n + 31) / 32; g.slices = slices;
   g.nsplit = gram_nsplit(n, slices);
   g.part = ws;
-  const int per_split = g.nt * g.nt;
+  const int per_split = g.nt * ((g.nt + 1) / 2);
   const int blocks = ((g.nsplit + NXCD - 1) / NXCD) * NXCD * per_split;
   if (g.npairs == 2) gram_kernel<2><<<blocks, 64, 0, s>>>(g);
   else gram_kernel<1><<<blocks, 64, 0, s>>>(g);

@@ -482,3 +482,44 @@ def test_gcn_split_forward(gpu, n, planes):
     run(True, eval_bn=(rm, rv, g_, b_, xo))
     ref = (Z - rm.double().cpu()) / torch.sqrt(rv.double().cpu() + 1e-5) * g_.double().cpu() + b_.double().cpu()
     assert rel_err(xo.cpu().numpy(), ref.numpy()) <= 10 * tol
+
+
+@pytest.mark.parametrize("n,slices,pairs,ld", [(207, 50, 2, 32), (16, 3, 1, 32), (325, 7, 2, 40), (33, 1, 2, 224),
+                                               (207, 768, 2, 32)])
+@pytest.mark.parametrize("accumulate", [0, 1])
+def test_gram_vs_fp64(gpu, n, slices, pairs, ld, accumulate):
+    """gwn_gram (the adaptive-support gradient, the backward of model.py:13 w.r.t. A over all slices of
+    a layer, both hop pairs) against an fp64 einsum: odd tile counts (n = 207: 7 tiles, 325: 11), a
+    single tile, one slice, padded row strides, accumulation into dA.  Bound: an fp32 FMA chain over
+    K = slices*32*pairs terms, |err| <= 2^-22 K sum|x||t|."""
+    from gwn_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(n + slices)
+    X = [torch.randn(slices * n, ld, dtype=torch.float64) for _ in range(pairs)]
+    T = [torch.randn(slices * n, ld, dtype=torch.float64) for _ in range(pairs)]
+    ref = torch.zeros(n, n, dtype=torch.float64)
+    absb = torch.zeros(n, n, dtype=torch.float64)
+    for p in range(pairs):
+        xs = X[p][:, :32].reshape(slices, n, 32)
+        ts = T[p][:, :32].reshape(slices, n, 32)
+        ref += torch.einsum("svc,swc->vw", xs, ts)
+        absb += torch.einsum("svc,swc->vw", xs.abs(), ts.abs())
+    ldA = n + 3
+    init = torch.randn(n, ldA, dtype=torch.float64)
+    dA = init.float().to(gpu)
+    if accumulate:
+        ref = ref + init[:, :n].float().double()
+        absb = absb + init[:, :n].abs()
+    Xd = [x.float().to(gpu) for x in X]
+    Td = [t.float().to(gpu) for t in T]
+    ws = torch.empty(lib.gwn_gram_workspace_floats(n, slices) + 16, device=gpu)
+    x2 = Xd[1].data_ptr() if pairs == 2 else None
+    t2 = Td[1].data_ptr() if pairs == 2 else None
+    _lib.call("gwn_gram", Xd[0].data_ptr(), Td[0].data_ptr(), x2, t2, ld, ld, n, slices, dA.data_ptr(), ldA,
+              accumulate, ws.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    got = dA.double().cpu()[:, :n]
+    bound = 2.0 ** -22 * (slices * 32 * pairs + 8) * absb
+    assert torch.all((got - ref).abs() <= bound + 1e-30), float(((got - ref).abs() / (bound + 1e-30)).max())
+    # columns beyond n untouched
+    assert torch.equal(dA.cpu()[:, n:], init.float()[:, n:])

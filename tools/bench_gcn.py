@@ -88,6 +88,11 @@ def main():
                          ("bwd-data" + tag, lambda a=gd_l: _lib.call("gwn_gcn_bwd", ctypes.byref(a), st)),
                          ("bwd-data+bn+gate" + tag, lambda a=gf_l: _lib.call("gwn_gcn_bwd", ctypes.byref(a), st))]
         variants.append(("bwd (+wgrad, gram)", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)))
+        gx = [torch.randn(rows, C, device=dev) for _ in range(4)]
+        gws = torch.empty(lib.gwn_gram_workspace_floats(N, T * B) + 16, device=dev)
+        variants.append(("gram (2 pairs)", lambda gx=gx, gws=gws: _lib.call(
+            "gwn_gram", gx[0].data_ptr(), gx[1].data_ptr(), gx[2].data_ptr(), gx[3].data_ptr(), C, C, N, T * B,
+            dadp.data_ptr(), NP, 0, gws.data_ptr(), st)))
         for planes in (3, 2):
             if not lib.gwn_gcn_split_supported(C, N, planes):
                 continue
