@@ -68,7 +68,10 @@ struct FusedBwd {
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
 #ifndef GWN_EXP
-#define GWN_EXP 0  // kernel experiments (timing only, wrong results): 1 no G loads, 2 no LDS A reads
+// kernel experiments (timing only; 1-16 give wrong results): 1 no G loads, 2 no LDS A reads,
+// 4 no W loads, 16 no phase barriers (forward); 32 = forward hop pieces stored straight from the
+// accumulators instead of as whole rows through LDS (correct, 2 % slower at T = 12)
+#define GWN_EXP 0
 #endif
 
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
@@ -105,7 +108,13 @@ __device__ __forceinline__ GBatch w_frags(const float* W, int ld_w, int off, int
   const float* wp = W + (long)col * ld_w + off;
   GBatch f;
 #pragma unroll
-  for (int s = 0; s < 16; ++s) f.v[s] = wp[crow(s, half)];
+  for (int s = 0; s < 16; ++s) {
+#if GWN_EXP & 4
+    f.v[s] = (float)(off + s) * 1e-6f + (float)lane * 1e-9f;
+#else
+    f.v[s] = wp[crow(s, half)];
+#endif
+  }
   return f;
 }
 
@@ -225,12 +234,32 @@ __device__ __forceinline__ void acc_to_lds(float* buf, const f32x16& d, int w0, 
 // Tile D'[c][w] straight from the accumulator to rows w of dst: each store instruction writes
 // 2 channels of 32 rows; the 16 instructions of a wave cover its 32 full 128-B row segments, which
 // L2 merges before write-back.  No LDS round trip and no barrier.
+// A lane's 16 accumulator rows are 4 runs of 4 consecutive channels (crow(4g..4g+3, half) =
+// 8g + 4h + 0..3), so with a 16-B aligned row base they go out as 4 dwordx4 stores: a quarter of
+// the write requests of 16 dword stores (measured: the scalar form cost 20 % of the forward at
+// T = 12, where every CU streams hop pieces out at once).
 __device__ __forceinline__ void acc_to_global(float* dst, long ld, const f32x16& d, int w0, int lane, int n) {
   const int half = lane >> 5, col = lane & 31;
   if (w0 + col >= n) return;
   float* p = dst + (long)(w0 + col) * ld;
+  if ((((uintptr_t)dst & 15) | (ld & 3)) == 0) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) p[crow(r, half)] = d[r];
+    for (int g = 0; g < 4; ++g)
+      *(float4*)(p + crow(4 * g, half)) = make_float4(d[4 * g], d[4 * g + 1], d[4 * g + 2], d[4 * g + 3]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) p[crow(r, half)] = d[r];
+  }
+}
+
+// Rows [0, n) of an LDS image (row stride LDR) to dst [n][ld] as whole 128-B rows: 8 lanes per
+// row, one 16-B store each (dst 16-B aligned, ld % 4 == 0; checked by the caller).
+__device__ __forceinline__ void lds_rows_to_global(const float* buf, float* dst, long ld, int n) {
+  for (int e = threadIdx.x; e < n * 8; e += blockDim.x) {
+    const int w = e >> 3, q = e & 7;
+    const float* b = buf + w * LDR + 4 * q;
+    *(float4*)(dst + (long)w * ld + 4 * q) = make_float4(b[0], b[1], b[2], b[3]);
+  }
 }
 
 __device__ __forceinline__ void global_to_lds(const float* src, long ld, int n, int np, float* buf) {
@@ -411,6 +440,9 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
   const long row0 = (long)blockIdx.x * n;
   const float* hs = a.h + row0 * a.ld_h;
 
+  // hop pieces leave as whole rows through LDS when h allows 16-B stores (GWN_EXP & 32: from the
+  // accumulators, 4 x 16 B per lane over 32 rows)
+  const bool rows_out = !(GWN_EXP & 32) && ((((uintptr_t)a.h) & 15) | (a.ld_h & 3)) == 0;
   // software pipeline: every G first batch / W fragment set is issued one phase before use
   GBatch g0 = (a.nsup > 0) ? g_first(a.sup[0], a.ld_sup, nkb, w0, lane) : GBatch{};
   global_to_lds(hs, a.ld_h, n, np, xs);
@@ -424,18 +456,32 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
       hacc = mlp_from_acc(wf, d, hacc);
     }
+#if !(GWN_EXP & 16)
     __syncthreads();  // ys is free once every wave finished the previous support's hop 2
+#endif
     acc_to_lds(ys, d, w0, lane);
-    if (a.store_pieces) acc_to_global((float*)hs + (1 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
+    if (a.store_pieces && !rows_out) acc_to_global((float*)hs + (1 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
+#if !(GWN_EXP & 16)
     __syncthreads();
+#endif
+    if (a.store_pieces && rows_out) lds_rows_to_global(ys, (float*)hs + (1 + 2 * k) * CH, a.ld_h, n);
     d = diffuse<HL>(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
     if (k + 1 < a.nsup) g0 = g_first(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
     {
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
       hacc = mlp_from_acc(wf, d, hacc);
     }
-    // x2 only goes to h (the backward's dW_mlp): straight from the accumulator
-    if (a.store_pieces) acc_to_global((float*)hs + (2 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
+    // x2 only goes to h (the backward's dW_mlp)
+    if (a.store_pieces) {
+      if (rows_out) {  // staged through ys (free once every wave finished hop 2) as whole rows
+        __syncthreads();
+        acc_to_lds(ys, d, w0, lane);
+        __syncthreads();
+        lds_rows_to_global(ys, (float*)hs + (2 + 2 * k) * CH, a.ld_h, n);
+      } else {
+        acc_to_global((float*)hs + (2 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
+      }
+    }
   }
   __syncthreads();
   acc_to_lds(ys, hacc, w0, lane);

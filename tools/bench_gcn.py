@@ -88,6 +88,9 @@ def main():
                          ("bwd-data" + tag, lambda a=gd_l: _lib.call("gwn_gcn_bwd", ctypes.byref(a), st)),
                          ("bwd-data+bn+gate" + tag, lambda a=gf_l: _lib.call("gwn_gcn_bwd", ctypes.byref(a), st))]
         variants.append(("bwd (+wgrad, gram)", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)))
+        ga_np = _lib.GcnArgs.from_buffer_copy(ga)
+        ga_np.no_pieces = 1
+        variants.append(("fwd no pieces", lambda a=ga_np: _lib.call("gwn_gcn_fwd", ctypes.byref(a), st)))
         gx = [torch.randn(rows, C, device=dev) for _ in range(4)]
         gws = torch.empty(lib.gwn_gram_workspace_floats(N, T * B) + 16, device=dev)
         variants.append(("gram (2 pairs)", lambda gx=gx, gws=gws: _lib.call(
