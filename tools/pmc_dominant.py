@@ -27,7 +27,7 @@ def main():
     f_kib = sum(fetch) / len(fetch)
     w_kib = sum(write) / len(write)
     res = {
-        "kernel": KERNEL + "<512>",
+        "kernel": KERNEL + "<512, true>",
         "dispatches": [len(fetch), len(write)],
         "fetch_kib_avg": round(f_kib, 1),
         "write_kib_avg": round(w_kib, 1),
