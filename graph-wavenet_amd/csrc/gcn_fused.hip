@@ -70,7 +70,7 @@ __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >
 #ifndef GWN_EXP
 // kernel experiments (timing only; 1-16 give wrong results): 1 no G loads, 2 no LDS A reads,
 // 4 no W loads, 16 no phase barriers (forward); 32 = forward hop pieces stored straight from the
-// accumulators instead of as whole rows through LDS (correct, 2 % slower at T = 12)
+// accumulators by the compute waves instead of by a store wave through LDS (correct, slower)
 #define GWN_EXP 0
 #endif
 
@@ -252,16 +252,6 @@ __device__ __forceinline__ void acc_to_global(float* dst, long ld, const f32x16&
   }
 }
 
-// Rows [0, n) of an LDS image (row stride LDR) to dst [n][ld] as whole 128-B rows: 8 lanes per
-// row, one 16-B store each (dst 16-B aligned, ld % 4 == 0; checked by the caller).
-__device__ __forceinline__ void lds_rows_to_global(const float* buf, float* dst, long ld, int n) {
-  for (int e = threadIdx.x; e < n * 8; e += blockDim.x) {
-    const int w = e >> 3, q = e & 7;
-    const float* b = buf + w * LDR + 4 * q;
-    *(float4*)(dst + (long)w * ld + 4 * q) = make_float4(b[0], b[1], b[2], b[3]);
-  }
-}
-
 __device__ __forceinline__ void global_to_lds(const float* src, long ld, int n, int np, float* buf) {
   for (int e = threadIdx.x; e < np * CH; e += blockDim.x) {
     const int w = e >> 5, c = e & 31;
@@ -427,64 +417,84 @@ __device__ __forceinline__ void bwd_gate_epilogue(const FusedBwd& a, const float
 // ---------------------------------------------------------------------------------------------
 // tile-wave layout: one wave per 32-node tile
 
+// With one wave more than node tiles (blockDim = 64 * (nkb + 1), the launcher's choice whenever the
+// hop pieces are stored), the last wave is a store wave: it copies each hop piece from the LDS
+// image to h as whole 128-B rows while the compute waves run the next diffusion.  gfx950 counts
+// stores in vmcnt, in order with loads, so a compute wave that stored a piece would wait for those
+// writes to complete at its next G-fragment wait; the store wave takes them off that path (and
+// lands on the SIMD that hosts one compute wave, 2,2,2,1 -> 2,2,2,2).
 template <int MAXT, bool HL>
 __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a) {
   extern __shared__ float lds[];
   __shared__ float red[2][MAXT];
   const int n = a.n;
-  const int nkb = (int)(blockDim.x >> 6);
+  const int nkb = (n + 31) >> 5;
   const int np = nkb * 32;
   float* xs = lds;
   float* ys = lds + np * LDR;
-  const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, w0 = wave * 32;
+  const bool compute = wave < nkb;
+  const bool store_wave = (int)(blockDim.x >> 6) > nkb;  // block-uniform
   const long row0 = (long)blockIdx.x * n;
-  const float* hs = a.h + row0 * a.ld_h;
+  const long ldh = a.ld_h, pstride = CH;  // piece p of row w at hs + w*ldh + p*pstride
+  const float* hs = a.h + row0 * ldh;
+  // hop pieces: by the store wave (whole rows through LDS), else straight from the accumulators
+  auto piece_rows = [&](int piece) {  // store wave only
+    const float* src = ys;
+    float* dst = (float*)hs + piece * pstride;
+    for (int e = lane; e < n * 8; e += 64) {
+      const int w = e >> 3, q = e & 7;
+      const float* b = src + w * LDR + 4 * q;
+      // write-once data the backward reads after the whole forward: non-temporal
+      typedef float f32x4_t __attribute__((ext_vector_type(4)));
+      const f32x4_t v = {b[0], b[1], b[2], b[3]};
+      __builtin_nontemporal_store(v, (f32x4_t*)(dst + (long)w * ldh + 4 * q));
+    }
+  };
 
-  // hop pieces leave as whole rows through LDS when h allows 16-B stores (GWN_EXP & 32: from the
-  // accumulators, 4 x 16 B per lane over 32 rows)
-  const bool rows_out = !(GWN_EXP & 32) && ((((uintptr_t)a.h) & 15) | (a.ld_h & 3)) == 0;
   // software pipeline: every G first batch / W fragment set is issued one phase before use
-  GBatch g0 = (a.nsup > 0) ? g_first(a.sup[0], a.ld_sup, nkb, w0, lane) : GBatch{};
-  global_to_lds(hs, a.ld_h, n, np, xs);
+  GBatch g0 = (a.nsup > 0 && compute) ? g_first(a.sup[0], a.ld_sup, nkb, w0, lane) : GBatch{};
+  global_to_lds(hs, ldh, n, np, xs);
   __syncthreads();
-  f32x16 hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
+  f32x16 hacc = zero16();
+  if (compute) hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
   for (int k = 0; k < a.nsup; ++k) {
     const float* G = a.sup[k];
-    f32x16 d = diffuse<HL>(xs, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
-    g0 = g_first(G, a.ld_sup, nkb, w0, lane);  // hop 2 re-reads the same support
-    {
+    f32x16 d = zero16();
+    if (compute) {
+      d = diffuse<HL>(xs, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
+      g0 = g_first(G, a.ld_sup, nkb, w0, lane);  // hop 2 re-reads the same support
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
       hacc = mlp_from_acc(wf, d, hacc);
     }
 #if !(GWN_EXP & 16)
-    __syncthreads();  // ys is free once every wave finished the previous support's hop 2
+    __syncthreads();  // ys is free: every wave finished the previous support's hop 2 (and its store)
 #endif
-    acc_to_lds(ys, d, w0, lane);
-    if (a.store_pieces && !rows_out) acc_to_global((float*)hs + (1 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
+    if (compute) {
+      acc_to_lds(ys, d, w0, lane);
+      if (a.store_pieces && !store_wave) acc_to_global((float*)hs + (1 + 2 * k) * pstride, ldh, d, w0, lane, n);
+    }
 #if !(GWN_EXP & 16)
     __syncthreads();
 #endif
-    if (a.store_pieces && rows_out) lds_rows_to_global(ys, (float*)hs + (1 + 2 * k) * CH, a.ld_h, n);
-    d = diffuse<HL>(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
-    if (k + 1 < a.nsup) g0 = g_first(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
-    {
+    if (compute) {
+      d = diffuse<HL>(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
+      if (k + 1 < a.nsup) g0 = g_first(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
       hacc = mlp_from_acc(wf, d, hacc);
+      if (a.store_pieces && !store_wave) acc_to_global((float*)hs + (2 + 2 * k) * pstride, ldh, d, w0, lane, n);
+    } else if (a.store_pieces) {
+      piece_rows(1 + 2 * k);  // x1 (in ys) while the compute waves run hop 2
     }
-    // x2 only goes to h (the backward's dW_mlp)
-    if (a.store_pieces) {
-      if (rows_out) {  // staged through ys (free once every wave finished hop 2) as whole rows
-        __syncthreads();
-        acc_to_lds(ys, d, w0, lane);
-        __syncthreads();
-        lds_rows_to_global(ys, (float*)hs + (2 + 2 * k) * CH, a.ld_h, n);
-      } else {
-        acc_to_global((float*)hs + (2 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
-      }
+    if (a.store_pieces && store_wave) {  // x2 through ys as well
+      __syncthreads();
+      if (compute) acc_to_lds(ys, d, w0, lane);
+      __syncthreads();
+      if (!compute) piece_rows(2 + 2 * k);  // while the compute waves run the next hop 1
     }
   }
   __syncthreads();
-  acc_to_lds(ys, hacc, w0, lane);
+  if (compute) acc_to_lds(ys, hacc, w0, lane);
   __syncthreads();
   fwd_epilogue<EPT>(a, ys, red[0], red[1], row0, n);
 }
@@ -864,12 +874,17 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   }
   const int slices = g->rows / g->n;
   if (use_4wave(g->layout, nwt)) gcn_fwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
-  else if (half_last_batch(g->n)) {
-    if (nwt <= 8) gcn_fwd_fused_kernel<512, true><<<slices, 64 * nwt, lds, s>>>(a);
-    else gcn_fwd_fused_kernel<1024, true><<<slices, 64 * nwt, lds, s>>>(a);
-  } else {
-    if (nwt <= 8) gcn_fwd_fused_kernel<512, false><<<slices, 64 * nwt, lds, s>>>(a);
-    else gcn_fwd_fused_kernel<1024, false><<<slices, 64 * nwt, lds, s>>>(a);
+  else {
+    // + one store wave when hop pieces are stored through LDS rows (h 16-B aligned, ld % 4 == 0)
+    const bool rows_ok = !(GWN_EXP & 32) && ((((uintptr_t)a.h) & 15) | (a.ld_h & 3)) == 0;
+    const int waves = nwt + ((a.store_pieces && rows_ok && nwt < 16) ? 1 : 0);
+    if (half_last_batch(g->n)) {
+      if (waves <= 8) gcn_fwd_fused_kernel<512, true><<<slices, 64 * waves, lds, s>>>(a);
+      else gcn_fwd_fused_kernel<1024, true><<<slices, 64 * waves, lds, s>>>(a);
+    } else {
+      if (waves <= 8) gcn_fwd_fused_kernel<512, false><<<slices, 64 * waves, lds, s>>>(a);
+      else gcn_fwd_fused_kernel<1024, false><<<slices, 64 * waves, lds, s>>>(a);
+    }
   }
   GWN_CHECK_LAUNCH();
   return GWN_OK;
@@ -936,7 +951,9 @@ extern "C" int gwn_fused_occupancy(int n, int backward) {
   } else if (backward) {
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_fused_kernel<1024, false>, 64 * nwt, lds);
   } else {
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_fused_kernel<1024, false>, 64 * nwt, lds);
+    // training forward: the compute waves plus the store wave
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_fused_kernel<1024, false>,
+                                                     64 * (nwt < 16 ? nwt + 1 : nwt), lds);
   }
   return e == hipSuccess ? blocks : -(int)e;
 }
