@@ -70,7 +70,9 @@ __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >
 #ifndef GWN_EXP
 // kernel experiments (timing only; 1-16 give wrong results): 1 no G loads, 2 no LDS A reads,
 // 4 no W loads, 16 no phase barriers (forward); 32 = forward hop pieces stored straight from the
-// accumulators by the compute waves instead of by a store wave through LDS (correct, slower)
+// accumulators by the compute waves instead of by a store wave through LDS (correct, slower);
+// 256 = clock diagnostic (per-workgroup cycles / real-time ticks after the BN partials,
+// tools/clock_gcn.py)
 #define GWN_EXP 0
 #endif
 
@@ -452,6 +454,10 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
     }
   };
 
+#if GWN_EXP & 256
+  // clock diagnostic: shader cycles and 100 MHz real-time ticks over the workgroup's life
+  const unsigned long long t_cyc0 = __builtin_amdgcn_s_memtime(), t_real0 = __builtin_amdgcn_s_memrealtime();
+#endif
   // software pipeline: every G first batch / W fragment set is issued one phase before use
   GBatch g0 = (a.nsup > 0 && compute) ? g_first(a.sup[0], a.ld_sup, nkb, w0, lane) : GBatch{};
   global_to_lds(hs, ldh, n, np, xs);
@@ -497,6 +503,18 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
   if (compute) acc_to_lds(ys, hacc, w0, lane);
   __syncthreads();
   fwd_epilogue<EPT>(a, ys, red[0], red[1], row0, n);
+#if GWN_EXP & 256
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    // past the per-slice BN partials: [slices][3][32] floats, then 4 floats per workgroup
+    float* dg = a.bn_part + (long)gridDim.x * 3 * CH + 4 * blockIdx.x;
+    dg[0] = (float)(c1 - t_cyc0);
+    dg[1] = (float)(r1 - t_real0);
+    dg[2] = (float)(t_real0 & 0xffffffull);  // start tick (low 24 bits)
+    dg[3] = (float)__smid();
+  }
+#endif
 }
 
 template <int MAXT, bool HL>
