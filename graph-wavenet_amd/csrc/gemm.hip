@@ -18,7 +18,7 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf
 
 // Shared epilogue for EPI_STORE / EPI_MASKGRAD (also used by the split-K reduction).
 __device__ __forceinline__ void epi_store(const GemmParams& p, int m, int n, float v,
-                                          unsigned long long seed) {
+                                          unsigned long long seed, long cofs = 0) {
   if (p.epi == EPI_MASKGRAD) {
     v = (p.mask[(long)m * p.ldmask_m + n] > 0.0f) ? v : 0.0f;
   } else {
@@ -30,8 +30,8 @@ __device__ __forceinline__ void epi_store(const GemmParams& p, int m, int n, flo
     }
   }
   const int no = n / p.c_nin, ni = n - no * p.c_nin;  // C0 shares the column map of C
-  if (p.C0) v += p.beta * p.C0[(long)m * p.ldc0_m + (long)ni * p.ldc0_n + (long)no * p.c0_no_stride];
-  p.C[(long)m * p.ldc_m + (long)ni * p.ldc_n + (long)no * p.c_no_stride] = v;
+  if (p.C0) v += p.beta * p.C0[cofs + (long)m * p.ldc0_m + (long)ni * p.ldc0_n + (long)no * p.c0_no_stride];
+  p.C[cofs + (long)m * p.ldc_m + (long)ni * p.ldc_n + (long)no * p.c_no_stride] = v;
 }
 
 // Operands are staged as "quads": 4 consecutive elements along the operand's contiguous
@@ -54,7 +54,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int split = blockIdx.z;
+  // blockIdx.z: the split-K index, or the batch index of a batched launch (ksplit == 1 then)
+  const bool batched = p.batch > 1;
+  const int split = batched ? 0 : (int)blockIdx.z;
+  const long bz = batched ? (long)blockIdx.z : 0;
+  const float* __restrict__ Ap = p.A + bz * p.a_bstride;
+  const float* __restrict__ Bp = p.B + bz * p.b_bstride;
+  const long cofs = bz * p.c_bstride;
   const int kbeg = split * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
 
@@ -77,14 +83,14 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, 
     const int ki = k - ko * p.a_kin;
     const int srow = m + ko * p.a_row_shift;
     if (srow < 0 || srow >= p.a_rows) return 0.0f;
-    return p.A[(long)srow * p.lda_m + (long)ki * p.lda_k + (long)ko * p.a_ko_stride];
+    return Ap[(long)srow * p.lda_m + (long)ki * p.lda_k + (long)ko * p.a_ko_stride];
   };
   auto b_elem = [&](int k, int n, int kb0) -> float {
     if (n >= p.N || k >= kend) return 0.0f;
     const int kb = b_tiled ? kb0 : (int)((unsigned)k / (unsigned)p.b_kin);
     const int kj = k - kb * p.b_kin;
     const int no = (unsigned)n / (unsigned)p.b_nin, ni = n - no * p.b_nin;
-    return p.B[(long)kj * p.ldb_k + (long)kb * p.b_ko_stride + (long)ni * p.ldb_n + (long)no * p.b_no_stride];
+    return Bp[(long)kj * p.ldb_k + (long)kb * p.b_ko_stride + (long)ni * p.ldb_n + (long)no * p.b_no_stride];
   };
 
   auto load = [&](int k0) {
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, 
           const int m = m0 + q / (BK / 4), k = k0 + (q % (BK / 4)) * 4;
           const int srow = m + ko0 * p.a_row_shift;
           if (vec_a && m < p.M && k + 3 < kend && srow >= 0 && srow < p.a_rows) {
-            v = *(const float4*)(p.A + (long)srow * p.lda_m + (k - ko0 * p.a_kin) + (long)ko0 * p.a_ko_stride);
+            v = *(const float4*)(Ap + (long)srow * p.lda_m + (k - ko0 * p.a_kin) + (long)ko0 * p.a_ko_stride);
           } else {
             v.x = a_elem(m, k, ko0); v.y = a_elem(m, k + 1, ko0);
             v.z = a_elem(m, k + 2, ko0); v.w = a_elem(m, k + 3, ko0);
@@ -109,7 +115,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, 
           const int k = k0 + q / (BM / 4), m = m0 + (q % (BM / 4)) * 4;
           const int srow = m + ko0 * p.a_row_shift;
           if (vec_a && k < kend && m + 3 < p.M && srow >= 0 && srow + 3 < p.a_rows) {
-            v = *(const float4*)(p.A + srow + (long)(k - ko0 * p.a_kin) * p.lda_k + (long)ko0 * p.a_ko_stride);
+            v = *(const float4*)(Ap + srow + (long)(k - ko0 * p.a_kin) * p.lda_k + (long)ko0 * p.a_ko_stride);
           } else {
             v.x = a_elem(m, k, ko0); v.y = a_elem(m + 1, k, ko0);
             v.z = a_elem(m + 2, k, ko0); v.w = a_elem(m + 3, k, ko0);
@@ -128,7 +134,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, 
           const int n = n0 + q / (BK / 4), k = k0 + (q % (BK / 4)) * 4;
           if (vec_b && n < p.N && k + 3 < kend) {
             const int no = (unsigned)n / (unsigned)p.b_nin, ni = n - no * p.b_nin;
-            v = *(const float4*)(p.B + (k - kb0 * p.b_kin) + (long)kb0 * p.b_ko_stride + (long)ni * p.ldb_n +
+            v = *(const float4*)(Bp + (k - kb0 * p.b_kin) + (long)kb0 * p.b_ko_stride + (long)ni * p.ldb_n +
                                  (long)no * p.b_no_stride);
           } else {
             v.x = b_elem(k, n, kb0); v.y = b_elem(k + 1, n, kb0);
@@ -138,7 +144,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, 
           const int k = k0 + q / (BN / 4), n = n0 + (q % (BN / 4)) * 4;
           if (vec_b && k < kend && n + 3 < p.N) {
             const int no = (unsigned)n / (unsigned)p.b_nin, ni = n - no * p.b_nin;
-            v = *(const float4*)(p.B + (long)(k - kb0 * p.b_kin) * p.ldb_k + (long)kb0 * p.b_ko_stride + ni +
+            v = *(const float4*)(Bp + (long)(k - kb0 * p.b_kin) * p.ldb_k + (long)kb0 * p.b_ko_stride + ni +
                                  (long)no * p.b_no_stride);
           } else {
             v.x = b_elem(k, n, kb0); v.y = b_elem(k, n + 1, kb0);
@@ -258,7 +264,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p, 
   } else {
     const unsigned long long seed = p.seed_ptr ? *p.seed_ptr : 0ull;
     walk([&](int m, int n, float v) {
-      if (m < p.M && n < p.N) epi_store(p, m, n, v, seed);
+      if (m < p.M && n < p.N) epi_store(p, m, n, v, seed, cofs);
     });
   }
 }
@@ -305,7 +311,7 @@ __global__ void splitk_reduce_kernel(const GemmParams p) {
 template <int WM, int WN, int TM, int TN>
 int launch_cfg(const GemmParams& p, bool akc, bool bkc, int va, int vb, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.ksplit);
+  dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.batch > 1 ? p.batch : p.ksplit);
   dim3 block(64 * WM * WN);
   if (akc && bkc) gemm_kernel<WM, WN, TM, TN, true, true><<<grid, block, 0, s>>>(p, va, vb);
   else if (akc) gemm_kernel<WM, WN, TM, TN, true, false><<<grid, block, 0, s>>>(p, va, vb);
@@ -334,6 +340,9 @@ int gwn_gemm_launch(const GemmParams& pin, hipStream_t s) {
   GWN_REQUIRE(p.epi != EPI_MASKGRAD || p.mask, "gemm: mask-grad epilogue needs a mask");
   GWN_REQUIRE(p.ones_out == nullptr || p.epi != EPI_GATE, "gemm: ones column is not combined with the gate epilogue");
   if (p.ksplit < 1) p.ksplit = 1;
+  if (p.batch > 1)
+    GWN_REQUIRE(p.ksplit == 1 && p.epi == EPI_STORE && !p.ones_out && !p.mask && !p.aux && p.batch <= 65535,
+                "gemm: a batched launch needs ksplit 1, the store epilogue, no ones column / mask / aux");
   if (p.ksplit > 1) {
     GWN_REQUIRE(p.part != nullptr, "gemm: split-K needs a partial buffer");
     int chunk = (p.K + p.ksplit - 1) / p.ksplit;
@@ -350,13 +359,16 @@ int gwn_gemm_launch(const GemmParams& pin, hipStream_t s) {
   const bool b_tiled = (p.b_kin % BK == 0) || (p.b_kin >= p.K);
   // 16-B quads are legal when the quad never straddles an index block and every stride that
   // moves between quads is a multiple of 4 floats
-  const int va = al16(p.A) && a_tiled && m4(p.a_ko_stride) && m4(p.a_kin) &&
+  const bool bat = p.batch > 1;
+  const int va = al16(p.A) && (!bat || m4(p.a_bstride)) && a_tiled && m4(p.a_ko_stride) && m4(p.a_kin) &&
                  (akc ? m4(p.lda_m) : (p.lda_m == 1 && m4(p.lda_k) && m4(p.a_row_shift)));
-  const int vb = al16(p.B) && b_tiled && m4(p.b_ko_stride) && m4(p.b_no_stride) && m4(p.b_kin) &&
+  const int vb = al16(p.B) && (!bat || m4(p.b_bstride)) && b_tiled && m4(p.b_ko_stride) && m4(p.b_no_stride) && m4(p.b_kin) &&
                  (bkc ? m4(p.ldb_n) : (p.ldb_n == 1 && m4(p.ldb_k) && m4(p.b_nin)));
   // tile choice: the largest tile that still gives >= 2 workgroups per CU (512), else the one with
   // the most workgroups; thin dimensions get thin tiles
-  auto nblk = [&](int bm, int bn) { return (long)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * p.ksplit; };
+  auto nblk = [&](int bm, int bn) {
+    return (long)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * (p.batch > 1 ? p.batch : p.ksplit);
+  };
   constexpr long FILL = 512;
   int rc;
   if (p.M <= 32 && p.N <= 32) rc = launch_cfg<1, 1, 1, 1>(p, akc, bkc, va, vb, s);        // 32 x 32

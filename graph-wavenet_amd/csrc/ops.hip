@@ -643,6 +643,34 @@ int gwn_nconv(const float* A, int lda, int transpose_a, const float* x, long ldx
   return gwn_gemm_launch(d, s);
 }
 
+int gwn_nconv2(const float* A, int lda, long a_bstride, int transpose_a, const float* x, long ldx, float* y,
+               long ldy, int n, int c, int slices, int batch, hipStream_t s) {
+  GWN_REQUIRE(n > 0 && c > 0 && slices > 0 && batch > 0 && A && x && y, "nconv2: bad shape");
+  gwn_gemm_desc d = gemm_zero();
+  d.A = A;
+  if (transpose_a) { d.lda_m = 1; d.lda_k = lda; } else { d.lda_m = lda; d.lda_k = 1; }
+  d.B = x; d.ldb_k = ldx; d.ldb_n = 1; d.b_nin = c; d.b_no_stride = (long)n * ldx;
+  d.C = y; d.ldc_m = ldy; d.ldc_n = 1; d.c_nin = c; d.c_no_stride = (long)n * ldy;
+  d.M = n; d.N = c * slices; d.K = n;
+  d.batch = batch; d.a_bstride = a_bstride;
+  d.b_bstride = (long)slices * n * ldx; d.c_bstride = (long)slices * n * ldy;
+  return gwn_gemm_launch(d, s);
+}
+
+int gwn_nconv2_adj_grad(const float* x, long ldx, const float* dy, long lddy, int n, int c, int slices, int batch,
+                        float* dA, int ld_dA, long dA_bstride, int accumulate, hipStream_t s) {
+  GWN_REQUIRE(n > 0 && c > 0 && slices > 0 && batch > 0 && x && dy && dA, "nconv2_adj_grad: bad shape");
+  gwn_gemm_desc d = gemm_zero();
+  d.A = x; d.lda_m = ldx; d.lda_k = 1; d.a_kin = c; d.a_ko_stride = (long)n * ldx;
+  d.B = dy; d.ldb_k = 1; d.ldb_n = lddy; d.b_kin = c; d.b_ko_stride = (long)n * lddy;
+  d.C = dA; d.ldc_m = ld_dA; d.ldc_n = 1;
+  if (accumulate) { d.C0 = dA; d.ldc0_m = ld_dA; d.ldc0_n = 1; d.beta = 1.0f; }
+  d.M = n; d.N = n; d.K = c * slices;
+  d.batch = batch; d.a_bstride = (long)slices * n * ldx; d.b_bstride = (long)slices * n * lddy;
+  d.c_bstride = dA_bstride;
+  return gwn_gemm_launch(d, s);
+}
+
 static int adj_grad_ksplit(int n, int c, int slices) {
   return pick_ksplit(n, n, c * slices);
 }

@@ -35,6 +35,7 @@ class GemmDesc(ctypes.Structure):
         ("aux2", c_void_p), ("ld_aux2", c_long), ("aux2_row0", c_int),
         ("seed_ptr", c_void_p), ("seed_salt", c_u64), ("drop_p", c_float),
         ("ksplit", c_int), ("kchunk", c_int), ("part", c_void_p), ("ones_out", c_void_p),
+        ("batch", c_int), ("a_bstride", c_long), ("b_bstride", c_long), ("c_bstride", c_long),
     ]
 
 
@@ -133,6 +134,10 @@ _SIGS = [
     ("gwn_gated_tcn_fwd", c_int, [ctypes.POINTER(TcnArgs), c_void_p]),
     ("gwn_gated_tcn_bwd", c_int, [ctypes.POINTER(TcnBwdArgs), c_void_p]),
     ("gwn_gated_tcn_bwd_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
+    ("gwn_nconv2", c_int, [c_void_p, c_int, c_long, c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int,
+                           c_int, c_void_p]),
+    ("gwn_nconv2_adj_grad", c_int, [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                    c_long, c_int, c_void_p]),
     ("gwn_gcn_fwd", c_int, [ctypes.POINTER(GcnArgs), c_void_p]),
     ("gwn_gcn_split_supported", c_int, [c_int, c_int, c_int]),
     ("gwn_split_support_elems", c_long, [c_int, c_int]),

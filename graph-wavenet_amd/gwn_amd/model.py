@@ -59,6 +59,47 @@ class _NconvFn(torch.autograd.Function):
         return dx, dA
 
 
+class nconv2(nn.Module):
+    """``einsum('ncvl,nvw->ncwl')`` (reference model.py:16-22): diffusion with one support per
+    sample (the per-sample-graph variant's operator), one batched MFMA GEMM launch per call."""
+
+    def forward(self, x, A):
+        return _Nconv2Fn.apply(x, A)
+
+
+class _Nconv2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, A):
+        _require_device(x, A)
+        B, C, N, T = x.shape
+        if tuple(A.shape) != (B, N, N):
+            raise RuntimeError("nconv2: supports must be [B, N, N] = [%d, %d, %d], got %s" % (B, N, N, tuple(A.shape)))
+        x = x.contiguous()
+        A = A.contiguous()
+        y = torch.empty_like(x)
+        # NCHW: sample b holds C slices of [N][T] (rows = nodes, "channels" = time steps)
+        _lib.call("gwn_nconv2", A.data_ptr(), N, N * N, 1, x.data_ptr(), T, y.data_ptr(), T, N, T, C, B,
+                  _lib.stream())
+        ctx.save_for_backward(x, A)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, A = ctx.saved_tensors
+        dy = dy.contiguous()
+        B, C, N, T = x.shape
+        dx = dA = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _lib.call("gwn_nconv2", A.data_ptr(), N, N * N, 0, dy.data_ptr(), T, dx.data_ptr(), T, N, T, C, B,
+                      _lib.stream())
+        if ctx.needs_input_grad[1]:
+            dA = torch.empty_like(A)
+            _lib.call("gwn_nconv2_adj_grad", x.data_ptr(), T, dy.data_ptr(), T, N, T, C, B, dA.data_ptr(), N, N * N,
+                      0, _lib.stream())
+        return dx, dA
+
+
 class linear(nn.Module):
     """1x1 convolution container (reference model.py:24-30); holds ``mlp`` for state_dict parity."""
 

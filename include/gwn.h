@@ -68,6 +68,10 @@ typedef struct gwn_gemm_desc {
    * gradient dW = dY^T X this is the bias gradient sum_r dY[r][m], for free.  With split-K the
    * partial buffer holds ksplit*(M*N + M) floats (gwn_gemm_workspace_floats covers it). */
   float* ones_out;
+  /* optional batch (batch <= 1 = none): blockIdx.z walks `batch` independent GEMMs whose A, B, C
+   * (and C0) start a_bstride, b_bstride, c_bstride floats apart.  Needs ksplit == 1, epi 0, no
+   * ones_out / mask (the per-sample nconv2, model.py:20-22). */
+  int batch; long a_bstride, b_bstride, c_bstride;
 } gwn_gemm_desc;
 
 int gwn_gemm(const gwn_gemm_desc* desc, hipStream_t stream);
@@ -98,6 +102,18 @@ int gwn_nconv_adj_grad(const float* x, long ldx, const float* dy, long lddy, int
                        int slices, float* dA, int ld_dA, int accumulate, float* workspace,
                        hipStream_t stream);
 long gwn_nconv_adj_grad_workspace_floats(int n, int c, int slices);
+
+/* Per-sample diffusion nconv2 (model.py:16-22): einsum('ncvl,nvw->ncwl', x, A) with one support
+ * per batch element b: A_b = A + b*a_bstride ([n][lda]); x / y hold `batch` groups of `slices`
+ * slices (n rows of c floats each, row stride ldx / ldy), group b at b*slices*n rows.  One launch.
+ *   y_s[w][:] = sum_v A_b[v][w] x_s[v][:]   (transpose_a = 1, the forward)
+ *   y_s[v][:] = sum_w A_b[v][w] x_s[w][:]   (transpose_a = 0, its input gradient) */
+int gwn_nconv2(const float* A, int lda, long a_bstride, int transpose_a, const float* x, long ldx, float* y,
+               long ldy, int n, int c, int slices, int batch, hipStream_t stream);
+/* Its support gradient: dA_b[v][w] (+)= sum_{s in group b} sum_c x_s[v][c] dy_s[w][c]; dA_b at
+ * dA + b*dA_bstride ([n][ld_dA]).  One launch, no workspace. */
+int gwn_nconv2_adj_grad(const float* x, long ldx, const float* dy, long lddy, int n, int c, int slices,
+                        int batch, float* dA, int ld_dA, long dA_bstride, int accumulate, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Adaptive adjacency (model.py:185-188): adp = softmax(relu(E1 @ E2), dim=1), E1 [n][d],

@@ -7,6 +7,7 @@ never imports it.
 It restates, with plain torch-CPU tensor algebra written independently of the reference source,
 the arithmetic of:
   * nconv               reference model.py:12-14     ('ncvl,vw->ncwl')
+  * nconv2 / gcn2       reference model.py:16-22, 57-80  (per-sample supports 'ncvl,nvw->ncwl')
   * gcn                 reference model.py:41-55     (K supports x order 2, concat, 1x1, dropout)
   * gwnet.forward       reference model.py:175-241   (pad, start conv, 8 gated/dilated layers,
                                                       skip, residual, BN, head)
@@ -79,6 +80,26 @@ def diffuse(x, a):
     b, c, n, t = x.shape
     xt = x.permute(0, 1, 3, 2).reshape(b * c * t, n)
     return (xt @ a).reshape(b, c, t, n).permute(0, 1, 3, 2)
+
+
+def diffuse_per_sample(x, a):
+    """y[b,c,w,t] = sum_v x[b,c,v,t] a[b,v,w]   (nconv2: one support per sample, model.py:16-22)."""
+    b, c, n, t = x.shape
+    xt = x.permute(0, 1, 3, 2).reshape(b, c * t, n)
+    return torch.bmm(xt, a).reshape(b, c, t, n).permute(0, 1, 3, 2)
+
+
+def gcn2(x, supports, w, bias, order=2):
+    """gcn2.forward (model.py:64-80) in eval mode: per-sample supports [B,N,N], piece-major concat
+    [x, A1 x, A1^2 x, A2 x, ...], then the 1x1 conv."""
+    out = [x]
+    for a in supports:
+        x1 = diffuse_per_sample(x, a)
+        out.append(x1)
+        for _ in range(2, order + 1):
+            x1 = diffuse_per_sample(x1, a)
+            out.append(x1)
+    return pointwise(torch.cat(out, dim=1), w, bias)
 
 
 def pointwise(x, w, bias=None):

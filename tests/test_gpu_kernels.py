@@ -523,3 +523,45 @@ def test_gram_vs_fp64(gpu, n, slices, pairs, ld, accumulate):
     assert torch.all((got - ref).abs() <= bound + 1e-30), float(((got - ref).abs() / (bound + 1e-30)).max())
     # columns beyond n untouched
     assert torch.equal(dA.cpu()[:, n:], init.float()[:, n:])
+
+
+def test_nconv2_vs_reference_golden(gpu):
+    """nconv2 (model.py:16-22, per-sample supports) on the batched MFMA GEMM against the reference's
+    own output and fp64 autograd gradients (tests/golden/make_golden_nconv2.py).  fp32 MFMA chain
+    over K = N = 37 terms: max-rel 1e-5."""
+    from gwn_amd.model import nconv2
+    g = load_golden("g9_nconv2_n37.npz")
+    x = torch.tensor(g["x"], dtype=torch.float32, device=gpu, requires_grad=True)
+    A = torch.tensor(g["A"], dtype=torch.float32, device=gpu, requires_grad=True)
+    y = nconv2()(x, A)
+    (y * torch.tensor(g["g"], dtype=torch.float32, device=gpu)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(y.detach().cpu().numpy(), g["y"]) < 1e-5
+    assert rel_err(x.grad.cpu().numpy(), g["dx"]) < 1e-5
+    assert rel_err(A.grad.cpu().numpy(), g["dA"]) < 1e-5
+
+
+@pytest.mark.parametrize("B,C,N,T", [(1, 1, 1, 1), (2, 3, 33, 7), (64, 32, 207, 12), (5, 2, 325, 13)])
+def test_nconv2_vs_fp64(gpu, B, C, N, T):
+    """nconv2 forward and both gradients against an fp64 einsum at METR-LA / PEMS-BAY shapes and
+    ragged edges (16-B quad loads off when strides are not multiples of 4).  Bound: fp32 FMA chain,
+    |err| <= 2^-22 K sum|a||b| per element."""
+    from gwn_amd.model import nconv2
+    torch.manual_seed(B * 1000 + N)
+    x = torch.randn(B, C, N, T, dtype=torch.float64)
+    A = torch.rand(B, N, N, dtype=torch.float64) / N
+    gy = torch.randn(B, C, N, T, dtype=torch.float64)
+    ref = torch.einsum("ncvl,nvw->ncwl", x, A)
+    dx_ref = torch.einsum("ncwl,nvw->ncvl", gy, A)
+    dA_ref = torch.einsum("ncvl,ncwl->nvw", x, gy)
+    xd = x.float().to(gpu).requires_grad_(True)
+    Ad = A.float().to(gpu).requires_grad_(True)
+    y = nconv2()(xd, Ad)
+    y.backward(gy.float().to(gpu))
+    torch.cuda.synchronize()
+    b_y = 2.0 ** -22 * N * torch.einsum("ncvl,nvw->ncwl", x.abs(), A.abs()) + 1e-30
+    b_dx = 2.0 ** -22 * N * torch.einsum("ncwl,nvw->ncvl", gy.abs(), A.abs()) + 1e-30
+    b_dA = 2.0 ** -22 * C * T * torch.einsum("ncvl,ncwl->nvw", x.abs(), gy.abs()) + 1e-30
+    for got, want, bound in ((y.detach(), ref, b_y), (xd.grad, dx_ref, b_dx), (Ad.grad, dA_ref, b_dA)):
+        err = (got.double().cpu() - want).abs()
+        assert torch.all(err <= bound), float((err / bound).max())
