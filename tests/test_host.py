@@ -27,7 +27,11 @@ def test_library_exports_every_declared_symbol():
         assert s in _lib.EXPORTED, s
     assert lib.gwn_version() == 1
     assert isinstance(lib.gwn_last_error(), bytes)
-    assert ctypes.sizeof(_lib.GemmDesc) == 312
+    # every ctypes mirror has the size of the C struct it mirrors (the library reports them)
+    for name, mirror in (("gwn_gemm_desc", _lib.GemmDesc), ("gwn_tcn_args", _lib.TcnArgs),
+                         ("gwn_tcn_bwd_args", _lib.TcnBwdArgs), ("gwn_gcn_args", _lib.GcnArgs),
+                         ("gwn_gcn_bwd_args", _lib.GcnBwdArgs)):
+        assert lib.gwn_abi_sizeof(name.encode()) == ctypes.sizeof(mirror), name
 
 
 def _sup_tensors(g):
