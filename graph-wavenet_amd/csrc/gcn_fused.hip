@@ -48,6 +48,7 @@ struct FusedFwd {
   int store_pieces;  // 0: hop outputs not written to h (inference: no backward follows)
   // eval BatchNorm folded into the epilogue (running statistics): x_out = bn(z); z not written
   const float* bn_rm; const float* bn_rv; const float* bn_g; const float* bn_b; float bn_eps; float* x_out;
+  long sup_bstride; int sup_batch;  // per-sample supports (sup_batch > 1): sample b = slice % sup_batch
 };
 
 struct FusedBwd {
@@ -63,7 +64,14 @@ struct FusedBwd {
   const unsigned long long* seed_ptr; unsigned long long salt; float drop_p; float inv_rows;
   // optional gate-backward epilogue (dfg instead of dxg)
   const float* fg; const float* dskip; long ld_dskip; long skip_row0; float* dfg;
+  long sup_bstride; int sup_batch;  // per-sample supports, as FusedFwd
 };
+
+// support k of this workgroup's slice (per-sample supports: sample = slice % sup_batch)
+template <typename Args>
+__device__ __forceinline__ const float* slice_sup(const Args& a, const float* base) {
+  return a.sup_batch > 1 ? base + (long)(blockIdx.x % a.sup_batch) * a.sup_bstride : base;
+}
 
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
@@ -459,13 +467,13 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
   const unsigned long long t_cyc0 = __builtin_amdgcn_s_memtime(), t_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
   // software pipeline: every G first batch / W fragment set is issued one phase before use
-  GBatch g0 = (a.nsup > 0 && compute) ? g_first(a.sup[0], a.ld_sup, nkb, w0, lane) : GBatch{};
+  GBatch g0 = (a.nsup > 0 && compute) ? g_first(slice_sup(a, a.sup[0]), a.ld_sup, nkb, w0, lane) : GBatch{};
   global_to_lds(hs, ldh, n, np, xs);
   __syncthreads();
   f32x16 hacc = zero16();
   if (compute) hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
   for (int k = 0; k < a.nsup; ++k) {
-    const float* G = a.sup[k];
+    const float* G = slice_sup(a, a.sup[k]);
     f32x16 d = zero16();
     if (compute) {
       d = diffuse<HL>(xs, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
@@ -485,7 +493,7 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
 #endif
     if (compute) {
       d = diffuse<HL>(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
-      if (k + 1 < a.nsup) g0 = g_first(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
+      if (k + 1 < a.nsup) g0 = g_first(slice_sup(a, a.sup[k + 1]), a.ld_sup, nkb, w0, lane);
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
       hacc = mlp_from_acc(wf, d, hacc);
       if (a.store_pieces && !store_wave) acc_to_global((float*)hs + (2 + 2 * k) * pstride, ldh, d, w0, lane, n);
@@ -528,12 +536,12 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_bwd_fused_kernel(const FusedBwd a
   const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
   const long row0 = (long)blockIdx.x * n;
 
-  GBatch g0 = (a.nsup > 0) ? g_first(a.supT[0], a.ld_sup, nkb, w0, lane) : GBatch{};
+  GBatch g0 = (a.nsup > 0) ? g_first(slice_sup(a, a.supT[0]), a.ld_sup, nkb, w0, lane) : GBatch{};
   bwd_prologue<EPT>(a, dhs, row0, n, np);
   __syncthreads();
   f32x16 dx = mlpT_from_lds(a.w_mlp, a.ld_w, 0, dhs, w0, lane, zero16());
   for (int k = 0; k < a.nsup; ++k) {
-    const float* GT = a.supT[k];
+    const float* GT = slice_sup(a, a.supT[k]);
     {
       const f32x16 u = mlpT_from_lds(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, w0, lane, zero16());
       __syncthreads();
@@ -549,7 +557,7 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_bwd_fused_kernel(const FusedBwd a
     if (k == a.adp_index) acc_to_global(a.t1 + row0 * a.ld_t, a.ld_t, t, w0, lane, n);
     __syncthreads();
     dx = diffuse<HL>(buf, GT, a.ld_sup, nkb, w0, lane, dx, g0);  // dxg += A dx1
-    if (k + 1 < a.nsup) g0 = g_first(a.supT[k + 1], a.ld_sup, nkb, w0, lane);
+    if (k + 1 < a.nsup) g0 = g_first(slice_sup(a, a.supT[k + 1]), a.ld_sup, nkb, w0, lane);
   }
   if (!a.dfg) {
     acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
@@ -685,7 +693,7 @@ __global__ __launch_bounds__(256, 2) void gcn_fwd_fused4_kernel(const FusedFwd a
     tv[i] = wv + 4 * i < nkb;
   }
 
-  GBatch2 g0 = (a.nsup > 0) ? g_first2(a.sup[0], a.ld_sup, nkb, w0, lane) : GBatch2{};
+  GBatch2 g0 = (a.nsup > 0) ? g_first2(slice_sup(a, a.sup[0]), a.ld_sup, nkb, w0, lane) : GBatch2{};
   global_to_lds(hs, a.ld_h, n, np, xs);
   __syncthreads();
   f32x16 hacc[TPW];
@@ -693,7 +701,7 @@ __global__ __launch_bounds__(256, 2) void gcn_fwd_fused4_kernel(const FusedFwd a
   for (int i = 0; i < TPW; ++i) hacc[i] = zero16();
   mlp_from_lds2(a.w_mlp, a.ld_w, 0, xs, w0, lane, hacc);
   for (int k = 0; k < a.nsup; ++k) {
-    const float* G = a.sup[k];
+    const float* G = slice_sup(a, a.sup[k]);
     f32x16 d[TPW];
 #pragma unroll
     for (int i = 0; i < TPW; ++i) d[i] = zero16();
@@ -716,7 +724,7 @@ __global__ __launch_bounds__(256, 2) void gcn_fwd_fused4_kernel(const FusedFwd a
 #pragma unroll
     for (int i = 0; i < TPW; ++i) d[i] = zero16();
     diffuse2(ys, G, a.ld_sup, nkb, w0, lane, d, g0);
-    if (k + 1 < a.nsup) g0 = g_first2(a.sup[k + 1], a.ld_sup, nkb, w0, lane);
+    if (k + 1 < a.nsup) g0 = g_first2(slice_sup(a, a.sup[k + 1]), a.ld_sup, nkb, w0, lane);
     {
       const GBatch wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
 #pragma unroll
@@ -752,7 +760,7 @@ __global__ __launch_bounds__(256, 2) void gcn_bwd_fused4_kernel(const FusedBwd a
     tv[i] = wv + 4 * i < nkb;
   }
 
-  GBatch2 g0 = (a.nsup > 0) ? g_first2(a.supT[0], a.ld_sup, nkb, w0, lane) : GBatch2{};
+  GBatch2 g0 = (a.nsup > 0) ? g_first2(slice_sup(a, a.supT[0]), a.ld_sup, nkb, w0, lane) : GBatch2{};
   bwd_prologue<EPT4>(a, dhs, row0, n, np);
   __syncthreads();
   f32x16 dx[TPW];
@@ -760,7 +768,7 @@ __global__ __launch_bounds__(256, 2) void gcn_bwd_fused4_kernel(const FusedBwd a
   for (int i = 0; i < TPW; ++i) dx[i] = zero16();
   mlpT_from_lds2(a.w_mlp, a.ld_w, 0, dhs, w0, lane, dx);
   for (int k = 0; k < a.nsup; ++k) {
-    const float* GT = a.supT[k];
+    const float* GT = slice_sup(a, a.supT[k]);
     {
       f32x16 u[TPW];
 #pragma unroll
@@ -792,7 +800,7 @@ __global__ __launch_bounds__(256, 2) void gcn_bwd_fused4_kernel(const FusedBwd a
     }
     __syncthreads();
     diffuse2(buf, GT, a.ld_sup, nkb, w0, lane, dx, g0);  // dxg += A dx1
-    if (k + 1 < a.nsup) g0 = g_first2(a.supT[k + 1], a.ld_sup, nkb, w0, lane);
+    if (k + 1 < a.nsup) g0 = g_first2(slice_sup(a, a.supT[k + 1]), a.ld_sup, nkb, w0, lane);
   }
   if (!a.dfg) {
 #pragma unroll
@@ -870,6 +878,10 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.store_pieces = g->no_pieces ? 0 : 1;
   a.bn_rm = g->bn_running_mean; a.bn_rv = g->bn_running_var; a.bn_g = g->bn_weight; a.bn_b = g->bn_bias;
   a.bn_eps = g->bn_eps; a.x_out = g->bn_out;
+  a.sup_bstride = g->sup_bstride; a.sup_batch = g->sup_batch;
+  if (a.sup_batch > 1)
+    GWN_REQUIRE(!g->split_planes && (g->rows / g->n) % a.sup_batch == 0,
+                "gcn_fwd (per-sample supports): slices must be a multiple of sup_batch, no split path");
   if (a.x_out)
     GWN_REQUIRE(a.bn_rm && a.bn_rv && a.bn_g && a.bn_b && !bn_part,
                 "gcn_fwd (fused): eval BatchNorm needs running mean / var, weight, bias (and no BN partials)");
@@ -927,6 +939,10 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   a.dres = g->dres; a.dh_out = g->dh_out;
   a.seed_ptr = g->seed_ptr; a.salt = g->salt; a.drop_p = g->drop_p; a.inv_rows = 1.0f / (float)g->rows;
   a.fg = g->fg; a.dskip = g->dskip; a.ld_dskip = g->ld_dskip; a.skip_row0 = g->skip_row0; a.dfg = g->dfg;
+  a.sup_bstride = g->sup_bstride; a.sup_batch = g->sup_batch;
+  if (a.sup_batch > 1)
+    GWN_REQUIRE((g->rows / g->n) % a.sup_batch == 0 && g->adp_index < 0,
+                "gcn_bwd (per-sample supports): slices must be a multiple of sup_batch, adp_index -1");
   if (a.bn_dy)
     GWN_REQUIRE(a.bn_z && a.bn_gamma && a.bn_mean && a.bn_rstd && a.bn_sums && a.dres && a.dh_out,
                 "gcn_bwd (fused): BN prologue needs bn_z, gamma, mean, rstd, sums, dres and dh_out");

@@ -843,6 +843,7 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_fwd: rows must be slices*n");
   const int c = a->c, n = a->n, slices = a->rows / n;
   if (gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup)) return gwn_gcn_fused_fwd_launch(a, a->bn_partials, s);
+  GWN_REQUIRE(a->sup_batch <= 1, "gcn_fwd: per-sample supports need the fused path (c == 32, n <= 512)");
   GWN_REQUIRE(!a->no_pieces && !a->bn_out, "gcn_fwd: no_pieces / bn_out need the fused path (c == 32, n <= 512)");
   const int width = (2 * a->nsup + 1) * c;
   for (int k = 0; k < a->nsup; ++k) {
@@ -885,8 +886,9 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   const int c = a->c, n = a->n, slices = a->rows / n;
   const int width = (2 * a->nsup + 1) * c;
   const bool fused = a->sup_t && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup);
-  GWN_REQUIRE(fused || (!a->bn_dy && !a->dfg), "gcn_bwd: the BN / gate fusions need the fused path "
-                                               "(sup_t given, c == 32, n <= 512)");
+  GWN_REQUIRE(fused || (!a->bn_dy && !a->dfg && a->sup_batch <= 1),
+              "gcn_bwd: the BN / gate fusions and per-sample supports need the fused path "
+              "(sup_t given, c == 32, n <= 512)");
   const float* dh = a->bn_dy ? a->dh_out : a->dh;
   const bool wgrads = !a->skip_weight_grads;  // else the caller runs gwn_wgrad / gwn_gram itself
   int rc = GWN_OK;

@@ -82,6 +82,7 @@ class GcnArgs(ctypes.Structure):
         ("split_planes", c_int),
         ("sup_split", c_void_p), ("sup_split_stride", c_long), ("ld_split", c_int),
         ("w_split", c_void_p),
+        ("sup_bstride", c_long), ("sup_batch", c_int),
     ]
 
 
@@ -105,6 +106,7 @@ class GcnBwdArgs(ctypes.Structure):
         ("fg", c_void_p), ("dskip", c_void_p), ("ld_dskip", c_long), ("skip_row0", c_int),
         ("dfg", c_void_p),
         ("layout", c_int),
+        ("sup_bstride", c_long), ("sup_batch", c_int),
     ]
 
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time

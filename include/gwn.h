@@ -233,6 +233,10 @@ typedef struct gwn_gcn_args {
   int split_planes;
   const void* sup_split; long sup_split_stride; int ld_split;
   const void* w_split;
+  /* per-sample supports (the per-sample-graph variant, gcn2 model.py:57-80; sup_batch <= 1 = shared):
+   * slice s = t*sup_batch + b diffuses with support k at sup[k] + b*sup_bstride (floats), same
+   * padded [np][ld_sup] layout.  Fused path only (c == 32, n <= 512), f32 MFMA (split_planes 0). */
+  long sup_bstride; int sup_batch;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -297,6 +301,9 @@ typedef struct gwn_gcn_bwd_args {
   const float* fg; const float* dskip; long ld_dskip; int skip_row0; float* dfg;
   /* wave layout of the fused kernel, as gwn_gcn_args.layout */
   int layout;
+  /* per-sample supports, as gwn_gcn_args (sup and sup_t alike); needs the fused path and
+   * adp_index = -1 (the per-sample variant's supports are inputs: no adjacency gradient) */
+  long sup_bstride; int sup_batch;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);

@@ -565,3 +565,65 @@ def test_nconv2_vs_fp64(gpu, B, C, N, T):
     for got, want, bound in ((y.detach(), ref, b_y), (xd.grad, dx_ref, b_dx), (Ad.grad, dA_ref, b_dA)):
         err = (got.double().cpu() - want).abs()
         assert torch.all(err <= bound), float((err / bound).max())
+
+
+@pytest.mark.parametrize("n,layout", [(16, 0), (207, 0), (207, 1), (96, 2)])
+def test_gcn_fused_per_sample_supports(gpu, n, layout):
+    """Fused gcn forward / backward with one support set per sample (gcn2, model.py:57-80: the
+    per-sample-graph variant's 'ncvl,nvw->ncwl' diffusions): slice s = t*Bs + b diffuses with
+    sample b's supports.  Against fp64: hop pieces, z, dxg; tile-wave and 4-wave layouts."""
+    import ctypes
+    from gwn_amd import _lib
+    torch.manual_seed(n + layout)
+    C, K, Bs, T = 32, 2, 3, 2
+    S = T * Bs
+    NP = (n + 31) // 32 * 32
+    W = (2 * K + 1) * C
+    rows = S * n
+    sup = torch.zeros(K, Bs, NP, NP, device=gpu)
+    sup[:, :, :n, :n] = torch.rand(K, Bs, n, n, device=gpu) / n
+    supT = sup.transpose(2, 3).contiguous()
+    arr = (ctypes.c_void_p * K)(*[sup[k].data_ptr() for k in range(K)])
+    arrT = (ctypes.c_void_p * K)(*[supT[k].data_ptr() for k in range(K)])
+    wm = torch.randn(C, W, device=gpu) * 0.1
+    bm = torch.randn(C, device=gpu)
+    res = torch.randn(rows, C, device=gpu)
+    xg = torch.randn(rows, C, device=gpu)
+    dh = torch.randn(rows, C, device=gpu)
+    seed = torch.zeros(1, device=gpu, dtype=torch.int64)
+    h = torch.zeros(rows, W, device=gpu)
+    h[:, :C] = xg
+    z = torch.empty(rows, C, device=gpu)
+    ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)),
+                      ld_sup=NP, h=h.data_ptr(), ld_h=W, w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(),
+                      residual=res.data_ptr(), z=z.data_ptr(), seed_ptr=seed.data_ptr(), salt=0, drop_p=0.0,
+                      layout=layout, sup_bstride=NP * NP, sup_batch=Bs)
+    _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
+    dhc = torch.zeros(rows, W, device=gpu)
+    gb = _lib.GcnBwdArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)),
+                         ld_sup=NP, h=h.data_ptr(), ld_h=W, w_mlp=wm.data_ptr(), dh=dh.data_ptr(),
+                         dhcat=dhc.data_ptr(), ld_dhcat=W, adp_index=-1, accumulate_dadp=0,
+                         sup_t=ctypes.cast(arrT, ctypes.POINTER(ctypes.c_void_p)), skip_weight_grads=1,
+                         layout=layout, sup_bstride=NP * NP, sup_batch=Bs)
+    _lib.call("gwn_gcn_bwd", ctypes.byref(gb), _lib.stream())
+    torch.cuda.synchronize()
+    # fp64 truth, slice s -> sample s % Bs
+    X = xg.double().cpu().view(S, n, C)
+    A = sup[:, :, :n, :n].double().cpu()                        # [K][Bs][n][n]
+    Aslice = A[:, torch.arange(S) % Bs]                          # [K][S][n][n]
+    pieces = [X]
+    for k in range(K):
+        x1 = torch.einsum("svc,svw->swc", X, Aslice[k])
+        x2 = torch.einsum("svc,svw->swc", x1, Aslice[k])
+        pieces += [x1, x2]
+    H = torch.cat(pieces, dim=2).reshape(rows, W)
+    Z = H @ wm.double().cpu().t() + bm.double().cpu() + res.double().cpu()
+    dP = (dh.double().cpu() @ wm.double().cpu()).view(S, n, W)
+    dxg = dP[:, :, :C].clone()
+    for k in range(K):
+        dx2 = dP[:, :, (2 + 2 * k) * C:(3 + 2 * k) * C]
+        dx1 = dP[:, :, (1 + 2 * k) * C:(2 + 2 * k) * C] + torch.einsum("swc,svw->svc", dx2, Aslice[k])
+        dxg = dxg + torch.einsum("swc,svw->svc", dx1, Aslice[k])
+    assert rel_err(h.cpu().numpy(), H.numpy()) <= 2e-6
+    assert rel_err(z.cpu().numpy(), Z.numpy()) <= 2e-6
+    assert rel_err(dhc[:, :C].cpu().numpy(), dxg.reshape(rows, C).numpy()) <= 2e-6
