@@ -627,3 +627,19 @@ def test_gcn_fused_per_sample_supports(gpu, n, layout):
     assert rel_err(h.cpu().numpy(), H.numpy()) <= 2e-6
     assert rel_err(z.cpu().numpy(), Z.numpy()) <= 2e-6
     assert rel_err(dhc[:, :C].cpu().numpy(), dxg.reshape(rows, C).numpy()) <= 2e-6
+
+
+def test_nconv2_errors_and_strided_input(gpu):
+    """nconv2 raises like the reference on a support batch that does not match x (einsum shape
+    error), refuses CPU tensors (no fallback), and accepts non-contiguous x (a transpose view)."""
+    from gwn_amd.model import nconv2
+    x = torch.randn(2, 3, 16, 5, device=gpu)
+    with pytest.raises(RuntimeError):
+        nconv2()(x, torch.rand(3, 16, 16, device=gpu))
+    with pytest.raises(RuntimeError):
+        nconv2()(x.cpu(), torch.rand(2, 16, 16))
+    A = torch.rand(2, 16, 16, device=gpu)
+    xt = torch.randn(2, 3, 5, 16, device=gpu).transpose(2, 3)  # [2, 3, 16, 5], non-contiguous
+    y = nconv2()(xt, A)
+    ref = torch.einsum("ncvl,nvw->ncwl", xt.double().cpu(), A.double().cpu())
+    assert rel_err(y.cpu().numpy(), ref.numpy()) < 1e-5
