@@ -18,6 +18,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 namespace {
 
 constexpr int D = 16;  // k-steps (row pairs) per batch
+#ifndef WGRAD_WAVES_PER_CU
+#define WGRAD_WAVES_PER_CU 8  // target resident waves per CU (whole workgroups); 8 beat 16 and 32 (fewer
+                              // partials to write and reduce: mlp dW 37 vs 41 us at T=12, +1 % per step)
+#endif
 
 struct Wgrad {
   const float* dY; long ldy; int J;
@@ -121,8 +125,8 @@ __global__ void wgrad_reduce_kernel(const float* part, int nblk, int J, int Kc, 
 }
 
 int wgrad_nblk(int R, int waves_per_blk) {
-  // a whole number of workgroups per CU (256 CUs), 12-16 waves per CU; >= 256 rows per workgroup
-  int per_cu = 16 / waves_per_blk;
+  // a whole number of workgroups per CU (256 CUs), ~WGRAD_WAVES_PER_CU waves per CU; >= 256 rows per workgroup
+  int per_cu = WGRAD_WAVES_PER_CU / waves_per_blk;
   if (per_cu < 1) per_cu = 1;
   int nb = 256 * per_cu;
   const int byrows = R / 256;

@@ -91,6 +91,10 @@ def main():
         ga_np = _lib.GcnArgs.from_buffer_copy(ga)
         ga_np.no_pieces = 1
         variants.append(("fwd no pieces", lambda a=ga_np: _lib.call("gwn_gcn_fwd", ctypes.byref(a), st)))
+        wws = torch.empty(lib.gwn_wgrad_workspace_floats(rows, C, W) + 16, device=dev)
+        variants.append(("wgrad mlp", lambda wws=wws: _lib.call(
+            "gwn_wgrad", dh.data_ptr(), C, C, h.data_ptr(), W, rows, W, 1, 0, rows, dwm.data_ptr(), W,
+            dbm.data_ptr(), wws.data_ptr(), st)))
         gx = [torch.randn(rows, C, device=dev) for _ in range(4)]
         gws = torch.empty(lib.gwn_gram_workspace_floats(N, T * B) + 16, device=dev)
         variants.append(("gram (2 pairs)", lambda gx=gx, gws=gws: _lib.call(
