@@ -72,9 +72,12 @@ def main():
     xs, ys = [], []
     for i in range(nb):
         x, y = synthetic.synthetic_batch(B, N, T, seed=1000 * rank + i)
-        # the reference feeds transpose views (train.py:244-247); keep the same strides
-        xs.append(torch.tensor(x, device=dev))
-        ys.append(torch.tensor(y, device=dev))
+        # the reference feeds transpose views of the loader's [B, T, N, 2] batch (train.py:244-247):
+        # trainx = x.transpose(1, 3), real_val = y.transpose(1, 3)[:, 0]; same strides here
+        xl = torch.tensor(np.ascontiguousarray(x.transpose(0, 3, 2, 1)), device=dev)
+        yl = torch.tensor(np.ascontiguousarray(np.stack([y, y], 1).transpose(0, 3, 2, 1)), device=dev)
+        xs.append(xl.transpose(1, 3))
+        ys.append(yl.transpose(1, 3)[:, 0, :, :])
 
     def barrier():
         if world > 1:
@@ -98,7 +101,9 @@ def main():
     value = samples / elapsed
     ms = 1000.0 * elapsed / args.steps
 
-    # 12-step MAE (train.py:392-403 protocol) of the trained weights on a held-out synthetic batch
+    # 12-step MAE (train.py:392-403 protocol) of the trained weights on a held-out synthetic batch,
+    # and the same number from the fp64 CPU oracle on the same weights and batch (north_star: MAE
+    # within 1e-4 of the reference)
     xt, yt = synthetic.synthetic_batch(B, N, T, seed=99999)
     with torch.no_grad():
         eng.model.eval()
@@ -106,6 +111,7 @@ def main():
         real = torch.tensor(yt, device=dev)
         maes = [util.masked_mae(scaler.inverse_transform(pred[:, :, h]), real[:, :, h], 0.0).item() for h in range(T)]
     mae12 = float(np.mean(maes))
+    mae12_ref = oracle_mae12(eng, sups, xt, yt) if rank == 0 else None
 
     roof = measure_dominant(eng, dev)
     result = None
@@ -118,7 +124,9 @@ def main():
             "config": {"workload": "METR-LA train step B=64/GPU N=207 T=12 fp32 (configs[1])",
                        "global_batch": B * world, "nodes": N, "seq_len": T,
                        "parallelism": "dp%d" % world if world > 1 else "single"},
-            "mae12": round(mae12, 5), "last_train_metrics": [round(v, 5) for v in last],
+            "mae12": round(mae12, 6), "mae12_oracle_f64": round(mae12_ref, 6),
+            "mae12_delta": float("%.3g" % abs(mae12 - mae12_ref)),
+            "last_train_metrics": [round(v, 5) for v in last],
             "step_effective_tflops": round(step_flops() * B * world / (elapsed / args.steps) / 1e12 / world, 3),
             "roofline": roof,
         }
@@ -177,12 +185,40 @@ def measure_dominant(eng, dev, rounds=5):
             "launches_timed": count}
 
 
+def oracle_mae12(eng, sups, xt, yt):
+    """12-step masked MAE of the fp64 CPU oracle (checker only) on the trained weights."""
+    from oracle import gwnet_oracle as orc
+    sd = {k: v.detach().cpu().numpy() for k, v in eng.model.state_dict().items()}
+    p = {k: torch.tensor(v, dtype=torch.float64) for k, v in sd.items()}
+    out = orc.forward(p, [s.detach().cpu().double() for s in sups], torch.tensor(xt, dtype=torch.float64),
+                      orc.Cfg(N), False, p)
+    pred = out.transpose(1, 3)[:, 0] * eng.scaler.std + eng.scaler.mean
+    real = torch.tensor(yt, dtype=torch.float64)
+    return float(np.mean([orc.masked_metrics(pred[:, :, h], real[:, :, h])[0].item() for h in range(T)]))
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds):
     """The CPU restatement (oracle/, kind "port") timing the same training step on the host
-    cores: fp32, autograd backward, clip + Adam, on a bounded sample."""
+    cores: fp32, autograd backward, clip + Adam; 3 warm-up steps, then the median of >= 5 timed
+    steps (BASELINE.md §3 / SURVEY §8d protocol).  Threads: os.cpu_count(), capped by the job's
+    CPU share where the launcher states one (OMP_NUM_THREADS; the GPU box gives each 1-GPU job 16
+    of the machine's cores and os.cpu_count() reports the whole machine)."""
     from gwn_amd import synthetic
     from oracle import gwnet_oracle as orc
-    threads = torch.get_num_threads()
+    nproc = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(nproc, share) if share > 0 else nproc
+    torch.set_num_threads(threads)
     cfg = orc.Cfg(N, dropout=0.3)
     torch.manual_seed(999)
     from gwn_amd.model import gwnet
@@ -192,17 +228,22 @@ def cpu_baseline(seconds):
     tr = orc.Trainer(sd, synthetic.double_transition(adj), cfg, dtype=torch.float32)
     bsz = B
     x, y = synthetic.synthetic_batch(bsz, N, T, seed=5)
-    tr.train(x, y)  # warm-up
+    for _ in range(3):
+        tr.train(x, y)  # warm-up
+    times = []
     t0 = time.perf_counter()
-    steps = 0
     while True:
+        t1 = time.perf_counter()
         tr.train(x, y)
-        steps += 1
-        if time.perf_counter() - t0 >= seconds or steps >= 50:
+        times.append(time.perf_counter() - t1)
+        if len(times) >= 5 and (time.perf_counter() - t0 >= seconds or len(times) >= 30):
             break
-    el = time.perf_counter() - t0
-    return {"value": round(bsz * steps / el, 3), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": "%d train steps of B=%d (N=207, T=12, fp32, dropout 0.3) in %.1f s; calibrated in the build container at 38.4 vs 34.9 samples/s for the reference itself (8 threads)" % (steps, bsz, el)}
+    med = float(np.median(times))
+    return {"value": round(bsz / med, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+            "nproc": nproc, "cpu_model": _cpu_model(), "statistic": "median",
+            "sample": "median of %d timed train steps (after 3 warm-up) of B=%d (N=207, T=12, fp32, dropout 0.3, "
+                      "clip + Adam), %.2f s/step, %d threads; calibrated in the build container at 38.4 vs 34.9 "
+                      "samples/s for the reference itself (8 threads)" % (len(times), bsz, med, threads)}
 
 
 if __name__ == "__main__":

@@ -349,15 +349,24 @@ __global__ void bn_apply_kernel(const float* z, long rows, int c, const float* m
   }
 }
 
+// eval-mode BatchNorm: the running statistics as (mean, rstd) for the backward
+__global__ void bn_running_stats_kernel(const float* rmean, const float* rvar, int c, float eps,
+                                        float* mean, float* rstd) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < c) {
+    mean[j] = rmean[j];
+    rstd[j] = 1.0f / sqrtf(rvar[j] + eps);
+  }
+}
+
 // dz = gamma*rstd*(dy - k1 - xhat*k2); dres[r + row0] = dz; dres rows < row0 zeroed; dh = dropout'(dz)
 __global__ void bn_bwd_apply_kernel(const float* dy, const float* z, long rows, int c,
                                     const float* gamma, const float* mean, const float* rstd,
-                                    const float* sums, float* dres, int res_row0, float* dh,
+                                    const float* sums, float inv_n, float* dres, int res_row0, float* dh,
                                     const unsigned long long* seed_ptr, unsigned long long salt,
                                     float drop_p, float* dgamma, float* dbeta) {
   const long total = rows * c;
   const unsigned long long seed = seed_ptr ? *seed_ptr : 0ull;
-  const float inv_n = 1.0f / (float)rows;
   const long zero_total = (long)res_row0 * c;
   if (blockIdx.x == 0)
     for (int j = threadIdx.x; j < c; j += blockDim.x) {
@@ -989,6 +998,12 @@ int gwn_batchnorm_fwd(const float* z, int rows, int c, const float* gamma, const
   } else {
     bn_apply_kernel<<<grid_for(total), 256, 0, s>>>(z, rows, c, running_mean, nullptr, running_var,
                                                     eps, gamma, beta, out);
+    if (save_mean && save_rstd) {
+      // the statistics an eval-mode backward differentiates through (gwn_batchnorm_bwd, batch_stats 0)
+      GWN_CHECK_LAUNCH();
+      bn_running_stats_kernel<<<(c + 255) / 256, 256, 0, s>>>(running_mean, running_var, c, eps, save_mean,
+                                                             save_rstd);
+    }
   }
   GWN_CHECK_LAUNCH();
   return GWN_OK;
@@ -1012,7 +1027,7 @@ int gwn_batchnorm_fwd_partials(const float* z, int rows, int c, const float* par
 int gwn_batchnorm_bwd(const float* dy, const float* z, int rows, int c, const float* gamma,
                       const float* save_mean, const float* save_rstd, float* dgamma, float* dbeta,
                       float* dres, int res_row0, float* dh, const unsigned long long* seed_ptr,
-                      unsigned long long salt, float drop_p, float* ws, hipStream_t s) {
+                      unsigned long long salt, float drop_p, int batch_stats, float* ws, hipStream_t s) {
   GWN_REQUIRE(rows > 0 && c > 0 && c <= 256 && 256 % c == 0, "batchnorm_bwd: c must divide 256");
   float* part = ws;
   float* sums = ws + (long)RED_BLOCKS * 3 * c;  // [2][c]: sum dy, sum dy*xhat
@@ -1021,9 +1036,11 @@ int gwn_batchnorm_bwd(const float* dy, const float* z, int rows, int c, const fl
   colsum_final_wide_kernel<<<2 * c, 256, 0, s>>>(part, RED_BLOCKS, 2 * c, sums, 0);
   GWN_CHECK_LAUNCH();
   const long total = (long)rows * c + (long)res_row0 * c;
+  // batch statistics: the mean / xhat terms of d(mean), d(var); running statistics: affine only
+  const float inv_n = batch_stats ? 1.0f / (float)rows : 0.0f;
   bn_bwd_apply_kernel<<<grid_for(total), 256, 0, s>>>(dy, z, rows, c, gamma, save_mean, save_rstd, sums,
-                                                      dres, res_row0, dh, seed_ptr, salt, drop_p, dgamma,
-                                                      dbeta);
+                                                      inv_n, dres, res_row0, dh, seed_ptr, salt, drop_p,
+                                                      dgamma, dbeta);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

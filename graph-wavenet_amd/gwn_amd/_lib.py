@@ -163,8 +163,8 @@ _SIGS = [
     ("gwn_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     ("gwn_pad_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
     ("gwn_batchnorm_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                                  c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_u64, c_float, c_void_p,
-                                  c_void_p]),
+                                  c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_u64, c_float, c_int,
+                                  c_void_p, c_void_p]),
     ("gwn_colsum", c_int, [c_void_p, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p]),
     ("gwn_colsum_workspace_floats", c_long, [c_int, c_int]),
     ("gwn_masked_loss", c_int, [c_void_p, c_void_p, c_long, c_long, c_long, c_int, c_int, c_int, c_int,

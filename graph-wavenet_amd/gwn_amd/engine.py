@@ -171,8 +171,13 @@ class trainer():
                 return self._eval_lean(input, real_val)
             return self._phase_grads(input, real_val, False)
         g = self.optimizer.param_groups[0]
+        # everything the captured graph bakes in: shapes, hyper-parameters (kernel arguments), the
+        # flat parameter buffer and the padded supports (device pointers), scaler and BN constants
+        sup_key = tuple((s_.data_ptr(), s_._version) for s_ in (model.supports or []))
+        bn_key = tuple((m.momentum, m.eps) for m in model.bn)
         key = (tuple(input.shape), tuple(real_val.shape), float(g["lr"]), tuple(g["betas"]), float(g["eps"]),
-               float(g["weight_decay"]), self.clip, float(model.dropout), model._flat.data_ptr())
+               float(g["weight_decay"]), self.clip, float(model.dropout), model._flat.data_ptr(), sup_key, bn_key,
+               float(self.scaler.mean), float(self.scaler.std))
         if self.use_graphs and key in self._graphs:
             return self._replay(key, input, real_val)
         if self.use_graphs and self._eager_runs.get(key, 0) >= 1:
@@ -239,8 +244,13 @@ class trainer():
                 dist.broadcast(m.running_var, src)
 
     def _fused_ok(self, input, real_val):
-        return (self.loss is util.masked_mae and input.is_cuda and input.dtype == F32
-                and real_val.dtype == F32 and real_val.dim() == 3)
+        """The fused step indexes real_val as [B, N, out_dim] (engine.py:47-51 broadcasts the
+        prediction [B, T_f, N, out_dim] against real_val[:, None]); any other shape takes the
+        autograd path, where torch's broadcasting rules (and errors) apply as in the reference."""
+        cfg = self.model.executor().cfg
+        return (self.loss is util.masked_mae and input.is_cuda and input.dtype == F32 and input.dim() == 4
+                and real_val.dtype == F32 and real_val.is_cuda
+                and tuple(real_val.shape) == (input.shape[0], cfg.N, cfg.O))
 
     def train(self, input, real_val):
         if not self._fused_ok(input, real_val):

@@ -80,9 +80,10 @@ class PackedLayout:
         map_grad("start_conv.bias", seg_index("start_b", (C,)))
         if cfg.adaptive:
             gather_seg("nv1", flat_range("nodevec1").reshape(-1))
-            map_grad("nodevec1", seg_index("nv1", tuple(flat_off["nodevec1"][1])))
             gather_seg("nv2", flat_range("nodevec2").reshape(-1))
-            map_grad("nodevec2", seg_index("nv2", tuple(flat_off["nodevec2"][1])))
+            if cfg.adp_live:
+                map_grad("nodevec1", seg_index("nv1", tuple(flat_off["nodevec1"][1])))
+                map_grad("nodevec2", seg_index("nv2", tuple(flat_off["nodevec2"][1])))
         for i in range(L):
             fw = flat_range("filter_convs.%d.weight" % i).reshape(C, C, 2)   # [co][ci][tap]
             gw = flat_range("gate_convs.%d.weight" % i).reshape(C, C, 2)
@@ -197,6 +198,9 @@ class Config:
         self.nfixed = len(model.supports) if (self.use_gcn and model.supports is not None) else 0
         self.nsup = self.nfixed + (1 if (self.use_gcn and self.adaptive) else 0)
         self.W = (2 * self.nsup + 1) * self.C if self.use_gcn else self.C
+        # the adaptive support reaches the output only through a gcn of a non-final layer (the
+        # last layer's gcn output is dead, model.py:225-236): otherwise nodevec1/2 keep grad None
+        self.adp_live = bool(self.use_gcn and self.adaptive and self.L > 1)
         self.NP = (self.N + 31) // 32 * 32  # padded support side (zero outside N x N)
         if model.residual_channels != model.dilation_channels:
             raise ValueError("gwn_amd: residual_channels must equal dilation_channels")
@@ -385,9 +389,11 @@ class Executor:
         arr = (ctypes.c_void_p * max(len(sups), 1))(*[s.data_ptr() for s in sups])
         return sups, arr
 
-    def forward(self, flat, fixed_sups, x, training, bn_bufs, acts=None, lead_pad=0):
+    def forward(self, flat, fixed_sups, x, training, bn_bufs, acts=None, lead_pad=0, seed=None):
         """x: reference NCHW input [B, Cin, N, T] (any strides).  ``lead_pad`` extra zero steps
         are prepended (engine.py:44) before the receptive-field pad (model.py:176-178).
+        ``seed``: the dropout counter this forward (and its backward) draws its masks from
+        (default: the executor's own, which the trainer advances after each step).
         Returns (out [B, O, N, T_f], acts)."""
         cfg = self.cfg
         C, N, L = cfg.C, cfg.N, cfg.L
@@ -408,6 +414,7 @@ class Executor:
         if acts is None:
             acts = Acts(cfg, B, ts, self.device, training)
         acts.training = training
+        acts.seed = self.seed if seed is None else seed
         acts.gcn_args = {}
         P = B * N
         tf = ts[-1]
@@ -449,7 +456,7 @@ class Executor:
                               h=ptr(acts.H[i]), ld_h=cfg.W,
                               w_mlp=ptr(self.pk("mlp_w%d" % i)), b_mlp=ptr(self.pk("mlp_b%d" % i)),
                               residual=acts.X[i].data_ptr() + 4 * d * P * C, z=ptr(acts.Z[i]),
-                              seed_ptr=ptr(self.seed), salt=i, drop_p=drop,
+                              seed_ptr=ptr(acts.seed), salt=i, drop_p=drop,
                               bn_partials=ptr(bnpart) if training else None, **self.split_fields(sp, i))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
@@ -653,8 +660,8 @@ class Executor:
                 if not fuse:
                     lib.call("gwn_batchnorm_bwd", ptr(dnext), ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
                              ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(self.gk("bn_g%d" % i)),
-                             ptr(self.gk("bn_b%d" % i)), ptr(dx), d * P, ptr(dh), ptr(self.seed), i,
-                             drop, ptr(ws), st)
+                             ptr(self.gk("bn_b%d" % i)), ptr(dx), d * P, ptr(dh), ptr(acts.seed), i,
+                             drop, 1 if acts.training else 0, ptr(ws), st)
                 gb = _lib.GcnBwdArgs(rows=rows, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
                                      sup=ctypes.cast(acts.sup_arr, ctypes.POINTER(ctypes.c_void_p)),
                                      ld_sup=cfg.NP,
@@ -672,7 +679,7 @@ class Executor:
                     gb.bn_gamma, gb.bn_mean, gb.bn_rstd = ptr(self.pk("bn_g%d" % i)), ptr(acts.mean[i]), ptr(acts.rstd[i])
                     gb.bn_sums, gb.bn_dgamma, gb.bn_dbeta = ptr(sc["bnsums"]), ptr(self.gk("bn_g%d" % i)), ptr(self.gk("bn_b%d" % i))
                     gb.dres, gb.dh_out = dx.data_ptr() + 4 * d * P * C, ptr(dh)
-                    gb.seed_ptr, gb.salt, gb.drop_p = ptr(self.seed), i, drop
+                    gb.seed_ptr, gb.salt, gb.drop_p = ptr(acts.seed), i, drop
                     gb.fg, gb.dskip, gb.ld_dskip = ptr(acts.FG[i]), sc["dskipcat"].data_ptr() + 4 * i * C, L * C
                     gb.skip_row0, gb.dfg = (ts[i + 1] - tf) * P, ptr(dfg)
                 lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)
@@ -704,7 +711,7 @@ class Executor:
         # start conv
         rows0 = ts[0] * P
         wgrad(dnext, C, acts.xin, cfg.Cin, rows0, self.gk("start_w"), ws, self.gk("start_b"))
-        if cfg.use_gcn and cfg.adaptive:
+        if cfg.adp_live:
             lib.call("gwn_adaptive_adj_bwd", ptr(self.pk("nv1")), ptr(self.pk("nv2")), ptr(acts.adp),
                      ptr(sc["dadp"]), N, 10, cfg.NP, ptr(self.gk("nv1")), ptr(self.gk("nv2")), ptr(ws), st)
 

@@ -9,11 +9,13 @@ Below the module boundary nothing is PyTorch compute: every parameter lives in o
 device buffer (``_flat``), the forward is a fixed schedule of libgwn launches (executor.py) and
 the backward is the matching hand-written gradient schedule, wrapped as ONE autograd node.
 """
+import ctypes
+
 import torch
 import torch.nn as nn
 
 from . import _lib
-from .executor import Executor, gemm  # noqa: F401  (gemm re-exported for the op-level modules)
+from .executor import Executor, _ksplit, gemm  # noqa: F401  (gemm re-exported for the op-level modules)
 
 F32 = torch.float32
 
@@ -100,33 +102,111 @@ class _Nconv2Fn(torch.autograd.Function):
         return dx, dA
 
 
+def _gemm_desc(A, lda_m, lda_k, B, ldb_k, ldb_n, C, ldc_m, ldc_n, M, N, K, **kw):
+    d = _lib.GemmDesc()
+    d.A, d.lda_m, d.lda_k = A, lda_m, lda_k
+    d.B, d.ldb_k, d.ldb_n = B, ldb_k, ldb_n
+    d.C, d.ldc_m, d.ldc_n = C, ldc_m, ldc_n
+    d.M, d.N, d.K = M, N, K
+    d.alpha, d.beta = 1.0, 1.0
+    for k, v in kw.items():
+        setattr(d, k, v)
+    return d
+
+
+class _LinearFn(torch.autograd.Function):
+    """1x1 conv over NCHW (``Conv2d(c_in, c_out, (1, 1))``): per sample b, with P = H*W pixels,
+    Y_b[o][p] = sum_i W[o][i] X_b[i][p] + bias[o] -- one batched libgwn GEMM (blockIdx.z = b);
+    backward: dX_b = W^T dY_b (batched), dW = sum_b dY_b X_b^T with db from the GEMM's ones
+    column, K = B*P walked through the two-level index map (fixed-order split-K reduce)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        _require_device(x, weight, bias)
+        x = x.contiguous()
+        B, ci, H, W = x.shape
+        co = weight.shape[0]
+        if weight.shape[1] != ci:
+            raise RuntimeError("linear: weight expects %d input channels, got %d" % (weight.shape[1], ci))
+        w2 = weight.reshape(co, ci).contiguous()
+        P = H * W
+        y = torch.empty(B, co, H, W, device=x.device, dtype=F32)
+        # rows m = pixels p, columns n = output channels o: C(p, o) = y_b[o][p]
+        d = _gemm_desc(x.data_ptr(), 1, P, w2.data_ptr(), 1, ci, y.data_ptr(), 1, P, P, co, ci,
+                       bias_n=bias.data_ptr(), batch=B, a_bstride=ci * P, b_bstride=0, c_bstride=co * P)
+        _lib.call("gwn_gemm", ctypes.byref(d), _lib.stream())
+        ctx.save_for_backward(x, w2)
+        ctx.wshape = tuple(weight.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w2 = ctx.saved_tensors
+        dy = dy.contiguous()
+        B, ci, H, W = x.shape
+        co = w2.shape[0]
+        P = H * W
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            d = _gemm_desc(dy.data_ptr(), 1, P, w2.data_ptr(), ci, 1, dx.data_ptr(), 1, P, P, ci, co,
+                           batch=B, a_bstride=co * P, b_bstride=0, c_bstride=ci * P)
+            _lib.call("gwn_gemm", ctypes.byref(d), _lib.stream())
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dw2 = torch.empty(co, ci, device=x.device, dtype=F32)
+            db = torch.empty(co, device=x.device, dtype=F32)
+            K = B * P
+            ks = _ksplit(co, ci, K)
+            lib = _lib.load()
+            ws = torch.empty(max(1, lib.gwn_gemm_workspace_floats(co, ci, ks)), device=x.device, dtype=F32)
+            # dW(o, i) = sum_k dY(o, k) X(i, k),  k = b*P + p  ->  (k / P) * (c*P) + k % P
+            d = _gemm_desc(dy.data_ptr(), P, 1, x.data_ptr(), 1, P, dw2.data_ptr(), ci, 1, co, ci, K,
+                           a_kin=P, a_ko_stride=co * P, b_kin=P, b_ko_stride=ci * P, ksplit=ks,
+                           part=ws.data_ptr(), ones_out=db.data_ptr())
+            _lib.call("gwn_gemm", ctypes.byref(d), _lib.stream())
+            dw = dw2.view(ctx.wshape)
+        return dx, dw, db
+
+
 class linear(nn.Module):
-    """1x1 convolution container (reference model.py:24-30); holds ``mlp`` for state_dict parity."""
+    """1x1 convolution (reference model.py:24-30): ``mlp`` is the reference's Conv2d (state_dict
+    parity); the forward / backward run on libgwn (``_LinearFn``).  Inside ``gwnet`` the same
+    arithmetic is fused into the diffusion kernel's epilogue instead."""
 
     def __init__(self, c_in, c_out):
         super().__init__()
         self.mlp = torch.nn.Conv2d(c_in, c_out, kernel_size=(1, 1), padding=(0, 0), stride=(1, 1), bias=True)
 
     def forward(self, x):
-        raise NotImplementedError("gwn_amd.linear is evaluated inside gwnet's fused schedule")
+        return _LinearFn.apply(x, self.mlp.weight, self.mlp.bias)
 
 
 class gcn(nn.Module):
-    """Diffusion graph convolution container (reference model.py:32-55).  Inside ``gwnet`` its
-    arithmetic is executed by ``gwn_gcn_fwd`` / ``gwn_gcn_bwd``; the module keeps the parameters
-    (``mlp.mlp``: Conv2d((order*support_len+1)*c_in -> c_out)) and the hyper-parameters."""
+    """Diffusion graph convolution (reference model.py:32-55): for every support A, order hops of
+    nconv (libgwn MFMA GEMMs), the piece-major concat [x, A1 x, A1^2 x, A2 x, ...], the 1x1 conv
+    (libgwn) and dropout.  Standalone use runs these per operator (the concat and the dropout mask
+    are torch data movement around the HIP arithmetic); inside ``gwnet`` the whole block is ONE
+    fused kernel (``gwn_gcn_fwd`` / ``gwn_gcn_bwd``) and this module only holds the parameters."""
 
     def __init__(self, c_in, c_out, dropout, support_len=3, order=2):
         super().__init__()
-        if order != 2:
-            raise ValueError("gwn_amd: diffusion order 2 (the reference default) is implemented")
         self.nconv = nconv()
         self.mlp = linear((order * support_len + 1) * c_in, c_out)
         self.dropout = dropout
         self.order = order
 
     def forward(self, x, support):
-        raise NotImplementedError("gwn_amd.gcn is evaluated inside gwnet's fused schedule")
+        out = [x]
+        for a in support:
+            x1 = self.nconv(x, a)
+            out.append(x1)
+            for _ in range(2, self.order + 1):
+                x2 = self.nconv(x1, a)
+                out.append(x2)
+                x1 = x2
+        h = torch.cat(out, dim=1)
+        h = self.mlp(h)
+        return torch.nn.functional.dropout(h, self.dropout, training=self.training)
 
 
 def _require_device(*ts):
@@ -298,7 +378,13 @@ class _GwnetFn(torch.autograd.Function):
     def forward(ctx, model, x, *params):
         ex = model._executor
         training = model.training
-        out, acts = ex.forward(model._flat, model._fixed_supports(), x, training, model._bn_bufs())
+        seed = None
+        if training and model.dropout > 0:
+            # F.dropout draws a fresh mask on every call (model.py:54): this forward and its
+            # backward use a snapshot of the counter, which then advances for the next forward
+            seed = ex.seed.clone()
+            _lib.call("gwn_increment_u64", _lib.ptr(ex.seed), 1, _lib.stream())
+        out, acts = ex.forward(model._flat, model._fixed_supports(), x, training, model._bn_bufs(), seed=seed)
         if training:
             model._nbt.add_(1)
         ctx.model = model

@@ -330,7 +330,8 @@ long gwn_gram_workspace_floats(int n, int slices);
 /* ---------------------------------------------------------------------------------------------
  * BatchNorm2d (model.py:236, bn = nn.BatchNorm2d(c) model.py:152) over the rows of z [rows][c].
  * train: batch mean / biased variance (eps), running stats updated with `momentum` and the
- * unbiased variance; mean/rstd saved for the backward.  eval: running stats.
+ * unbiased variance; mean/rstd saved for the backward.  eval: running stats (and, when save_mean /
+ * save_rstd are given, the running mean and 1/sqrt(running_var + eps) saved for an eval backward).
  * ------------------------------------------------------------------------------------------- */
 int gwn_batchnorm_fwd(const float* z, int rows, int c, const float* gamma, const float* beta,
                       float* running_mean, float* running_var, float momentum, float eps,
@@ -352,14 +353,16 @@ int gwn_pad_square(const float* src, int n, int ld_src, float* dst, int np, int 
                    hipStream_t stream);
 
 /* BN backward fused with the residual split and the dropout backward of the same layer:
- *   dz = gamma*rstd*(dy - mean(dy) - xhat*mean(dy*xhat));  dgamma, dbeta
+ *   batch_stats != 0 (train-mode forward):  dz = gamma*rstd*(dy - mean(dy) - xhat*mean(dy*xhat))
+ *   batch_stats == 0 (eval-mode forward, running statistics):  dz = gamma*rstd*dy
+ *   dgamma = sum dy*xhat, dbeta = sum dy
  *   dres[r + res_row0] = dz[r]   (the residual path, model.py:234; rows < res_row0 zeroed)
  *   dh[r] = dz[r] * mask(r) / (1-p)   (dropout backward, model.py:54)  */
 int gwn_batchnorm_bwd(const float* dy, const float* z, int rows, int c, const float* gamma,
                       const float* save_mean, const float* save_rstd, float* dgamma,
                       float* dbeta, float* dres, int res_row0, float* dh,
                       const unsigned long long* seed_ptr, unsigned long long salt,
-                      float drop_p, float* workspace, hipStream_t stream);
+                      float drop_p, int batch_stats, float* workspace, hipStream_t stream);
 
 /* Column sums db[j] = sum_r dy[r][j] (bias gradients), fixed order. */
 int gwn_colsum(const float* dy, int rows, int ncol, long ld, float* out, int accumulate,

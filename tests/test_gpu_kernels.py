@@ -252,7 +252,7 @@ def test_batchnorm_fwd_bwd(gpu):
     dres = torch.full((rows + 7, c), float("nan"), device=gpu)
     dh = torch.empty(rows, c, device=gpu)
     _lib.call("gwn_batchnorm_bwd", dy.data_ptr(), z.data_ptr(), rows, c, gamma.data_ptr(), mean.data_ptr(),
-              rstd.data_ptr(), dg.data_ptr(), db.data_ptr(), dres.data_ptr(), 7, dh.data_ptr(), None, 0, 0.0,
+              rstd.data_ptr(), dg.data_ptr(), db.data_ptr(), dres.data_ptr(), 7, dh.data_ptr(), None, 0, 0.0, 1,
               ws.data_ptr(), _lib.stream())
     torch.cuda.synchronize()
     assert rel_err(dh.cpu().numpy(), zc.grad.numpy()) < 1e-4

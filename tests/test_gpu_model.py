@@ -237,7 +237,7 @@ def test_dropout_forward_backward_exact_masks(gpu):
     real = torch.tensor(g["y"], device=gpu).unsqueeze(1)
     loss = util.masked_mae(out.transpose(1, 3) * 19.5 + 54.4, real, 0.0)
     loss.backward()
-    seed = int(m._executor.seed.item())
+    seed = int(m._executor.seed.item()) - 1  # the forward drew from the counter, then advanced it
     cfg = orc.Cfg(16, nhid=16, skip=128, end=256, dropout=0.3)
     B, N, C = 4, 16, 16
     ts = [13]
