@@ -160,9 +160,16 @@ int gram_nsplit(int n, int slices) {
 
 }  // namespace
 
+// Partial-sum floats of a gram launch over AT MOST `slices` slices.  gram_nsplit is not monotone
+// in the slice count (it prefers divisors: 56 slices take 56 splits, 96 take 48), so a workspace
+// sized for the largest layer is bounded by the split target, not by that layer's own split count.
 long gwn_gram_workspace_floats(int n, int slices) {
-  const int np = 32 * ((n + 31) / 32);
-  return (long)gram_nsplit(n, slices) * np * np;
+  const int nt = (n + 31) / 32, np = 32 * nt;
+  int bound = GRAM_WAVES / (nt * ((nt + 1) / 2));
+  bound = (bound / NXCD) * NXCD;
+  if (bound < NXCD) bound = NXCD;
+  if (bound > slices) bound = slices;
+  return (long)bound * np * np;
 }
 
 // dA (+)= sum over slices of X1^T T1 (+ X2^T T2); c = 32 channels per slice row
@@ -180,6 +187,16 @@ int gwn_gram(const float* x1, const float* t1, const float* x2, const float* t2,
   g.n = n; g.nt = (n + 31) / 32; g.slices = slices;
   g.nsplit = gram_nsplit(n, slices);
   g.part = ws;
+  {
+    const long rows = (long)slices * n;  // the loads stay inside rows * ld of each operand
+    GWN_DEBUG_RANGE(x1, ((rows - 1) * ldx + 32) * 4, "gram x1");
+    GWN_DEBUG_RANGE(t1, ((rows - 1) * ldt + 32) * 4, "gram t1");
+    if (x2) GWN_DEBUG_RANGE(x2, ((rows - 1) * ldx + 32) * 4, "gram x2");
+    if (x2) GWN_DEBUG_RANGE(t2, ((rows - 1) * ldt + 32) * 4, "gram t2");
+    const long np = 32L * g.nt;
+    GWN_DEBUG_RANGE(ws, g.nsplit * np * np * 4, "gram partials");
+    GWN_DEBUG_RANGE(dA, ((long)(n - 1) * ld_dA + n) * 4, "gram dA");
+  }
   const int per_split = g.nt * ((g.nt + 1) / 2);
   const int blocks = ((g.nsplit + NXCD - 1) / NXCD) * NXCD * per_split;
   if (g.npairs == 2) gram_kernel<2><<<blocks, 64, 0, s>>>(g);

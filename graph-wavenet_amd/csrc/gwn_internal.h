@@ -4,10 +4,20 @@
 #include <stdint.h>
 #include "../../include/gwn.h"
 
+// After every launch: the launch status; with GWN_SYNC_CHECK=1 in the environment (debugging
+// only) also a device synchronise, so an asynchronous fault is reported at file:line of its kernel.
+int gwn_launch_status(const char* file, int line);
+// GWN_SYNC_CHECK only: [p, p + bytes) must lie inside one device allocation (else an error code)
+int gwn_debug_range(const void* p, long bytes, const char* what);
+#define GWN_DEBUG_RANGE(p, bytes, what)                        \
+  do {                                                         \
+    const int rr_ = gwn_debug_range((p), (bytes), (what));     \
+    if (rr_) return rr_;                                       \
+  } while (0)
 #define GWN_CHECK_LAUNCH()                                   \
   do {                                                       \
-    hipError_t e_ = hipGetLastError();                       \
-    if (e_ != hipSuccess) return gwn_set_error(GWN_ERR_HIP, hipGetErrorString(e_)); \
+    const int rc_ = gwn_launch_status(__FILE__, __LINE__);   \
+    if (rc_) return rc_;                                     \
   } while (0)
 
 #define GWN_REQUIRE(cond, msg)                                \

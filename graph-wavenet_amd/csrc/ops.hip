@@ -3,6 +3,8 @@
 // element-wise kernels below.  All reductions use a fixed order (per-block partials, then an
 // in-order merge), so every result is bitwise reproducible.
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include "gwn_internal.h"
 
@@ -614,9 +616,48 @@ int gwn_set_error(int code, const char* msg) {
   return code;
 }
 
+static int g_sync_check = -1;  // -1: read GWN_SYNC_CHECK on first use
+
+int gwn_launch_status(const char* file, int line) {
+  if (g_sync_check < 0) {
+    const char* e = getenv("GWN_SYNC_CHECK");
+    g_sync_check = (e && e[0] == '1') ? 1 : 0;
+  }
+  hipError_t e_ = hipGetLastError();
+  if (e_ == hipSuccess && g_sync_check == 1) e_ = hipDeviceSynchronize();
+  if (e_ == hipSuccess) return GWN_OK;
+  char buf[256];
+  snprintf(buf, sizeof(buf), "%s (%s:%d)", hipGetErrorString(e_), file, line);
+  return gwn_set_error(GWN_ERR_HIP, buf);
+}
+
+// debugging (GWN_SYNC_CHECK): does [p, p + bytes) lie inside one device allocation?
+int gwn_debug_range(const void* p, long bytes, const char* what) {
+  if (g_sync_check != 1 || !p || bytes <= 0) return GWN_OK;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    char buf[256];
+    snprintf(buf, sizeof(buf), "debug range: %s at %p is not in a device allocation", what, p);
+    return gwn_set_error(GWN_ERR_ARG, buf);
+  }
+  const long off = (long)((const char*)p - (const char*)base);
+  if (off + bytes > (long)size) {
+    char buf[256];
+    snprintf(buf, sizeof(buf), "debug range: %s [%p, +%ld) overruns its allocation [%p, +%zu) by %ld bytes", what,
+             p, bytes, (void*)base, size, off + bytes - (long)size);
+    return gwn_set_error(GWN_ERR_ARG, buf);
+  }
+  return GWN_OK;
+}
+
 extern "C" {
 
 int gwn_version(void) { return 1; }
+/* debugging: 1 = synchronise after every launch (GWN_SYNC_CHECK), 2 = suspended (e.g. while a
+ * stream is being captured into a graph), 0 = off */
+void gwn_set_sync_check(int mode) { g_sync_check = mode; }
 const char* gwn_last_error(void) { return g_err; }
 
 long gwn_abi_sizeof(const char* name) {
@@ -886,7 +927,9 @@ long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup) {
   long w = gwn_gemm_workspace_floats(c, width, gcn_w_ksplit(rows, c, width));
   const long g = gwn_nconv_adj_grad_workspace_floats(n, c, rows / n);
   const long v = gwn_wgrad_workspace_floats(rows, c, width);
+  const long gr = gwn_gram_workspace_floats(n, rows / n);  // any slice count up to rows / n
   if (v > w) w = v;
+  if (gr > w) w = gr;
   return g > w ? g : w;
 }
 

@@ -117,6 +117,7 @@ _STRUCTS = {"gwn_gemm_desc": GemmDesc, "gwn_tcn_args": TcnArgs, "gwn_tcn_bwd_arg
 # (name, restype, argtypes) of every exported entry point declared in include/gwn.h
 _SIGS = [
     ("gwn_version", c_int, []),
+    ("gwn_set_sync_check", None, [c_int]),
     ("gwn_last_error", ctypes.c_char_p, []),
     ("gwn_abi_sizeof", c_long, [ctypes.c_char_p]),
     ("gwn_gemm", c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
@@ -232,7 +233,15 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+_SYNC_CHECK = os.environ.get("GWN_SYNC_CHECK", "0") == "1"
+
+
 def call(name, *args):
-    """Invoke an int-returning entry point and raise on failure."""
-    rc = getattr(load(), name)(*args)
+    """Invoke an int-returning entry point and raise on failure.  With GWN_SYNC_CHECK=1 (debugging)
+    the library synchronises after every kernel, except while the stream is being captured."""
+    lib = load()
+    if _SYNC_CHECK:
+        import torch
+        lib.gwn_set_sync_check(2 if torch.cuda.is_current_stream_capturing() else 1)
+    rc = getattr(lib, name)(*args)
     check(rc, name)

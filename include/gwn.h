@@ -30,6 +30,10 @@ extern "C" {
 #define GWN_ERR_HIP 2
 
 int gwn_version(void);
+/* debugging aid: 1 = synchronise the device after every kernel launch and report a fault at the
+ * kernel's source line (also enabled by GWN_SYNC_CHECK=1 in the environment), 2 = suspended (while
+ * a stream is being captured into a graph), 0 = off (default) */
+void gwn_set_sync_check(int mode);
 const char* gwn_last_error(void);
 /* sizeof of the argument structs below, for bindings that mirror them (ctypes, cgo):
  * "gwn_gemm_desc", "gwn_tcn_args", "gwn_tcn_bwd_args", "gwn_gcn_args", "gwn_gcn_bwd_args";
@@ -325,6 +329,8 @@ long gwn_wgrad_workspace_floats(int R, int J, int Kc);
  * i.e. both pairs (xg, dx1) and (x1, dx2) of gcn.forward's adaptive support in one launch. */
 int gwn_gram(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
              int slices, float* dA, int ld_dA, int accumulate, float* workspace, hipStream_t stream);
+/* workspace for any gwn_gram launch over AT MOST `slices` slices (non-decreasing in slices, so one
+ * query at a schedule's largest layer covers every layer) */
 long gwn_gram_workspace_floats(int n, int slices);
 
 /* ---------------------------------------------------------------------------------------------

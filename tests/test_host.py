@@ -147,3 +147,20 @@ def test_config_rejects_unsupported():
               end_channels=64)
     with pytest.raises(ValueError):
         Config(m)
+
+
+def test_workspace_queries_are_monotone_in_rows():
+    """The executor sizes one workspace from its largest layer: every *_workspace_floats query must
+    be non-decreasing in the row / slice count (round-2 fix: gram's split count prefers divisors of
+    the slice count and is not monotone, its workspace bound is)."""
+    from gwn_amd import _lib
+    lib = _lib.load()
+    for n in (16, 37, 207, 325, 512):
+        prev_g = prev_b = prev_a = 0
+        for slices in range(1, 260):
+            g = lib.gwn_gram_workspace_floats(n, slices)
+            b = lib.gwn_gcn_bwd_workspace_floats(slices * n, n, 32, 3)
+            a = lib.gwn_nconv_adj_grad_workspace_floats(n, 32, slices)
+            assert g >= prev_g and b >= prev_b and a >= prev_a, (n, slices)
+            assert b >= g
+            prev_g, prev_b, prev_a = g, b, a
