@@ -1,13 +1,16 @@
-"""Benchmark: Graph WaveNet training step (fwd+bwd+clip+Adam) at METR-LA shape on libgwn.
+"""Benchmark: Graph WaveNet training step (fwd+bwd+clip+Adam) on libgwn.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config metr|pems|n2048]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...   (N > 1)
 
-A step is ``trainer.train(x, y)`` (reference engine.py:41-58) on one synthetic batch of B=64
-samples per GPU (N=207 sensors, T=12, doubletransition supports + adaptive adjacency, dropout
-0.3, Adam lr 1e-3 wd 1e-4), the batches already resident in HBM.  With N>1 GPUs each rank trains
-its own B=64 shard and the gradients are averaged by one RCCL all-reduce per step (weak scaling).
-Rank 0 prints one JSON line; see DESIGN.md §Measurement for the roofline / baseline fields.
+A step is ``trainer.train(x, y)`` (reference engine.py:41-58) on one synthetic batch per GPU, the
+batches already resident in HBM and handed over as the transpose views train.py:244-247 builds.
+The default config is the headline (BASELINE.json configs[1]): METR-LA shape, B=64 per GPU, N=207
+sensors, T=12, doubletransition supports + adaptive adjacency, dropout 0.3, Adam lr 1e-3 wd 1e-4.
+``--config pems`` is configs[2]'s graph (N=325), ``--config n2048`` configs[4] (N=2048, T=24,
+dense random adjacency, B=32 per GPU).  With N>1 GPUs each rank trains its own shard and the
+gradients are averaged by one RCCL all-reduce per step (weak scaling).  Rank 0 prints one JSON line;
+see DESIGN.md §5 for the roofline / baseline fields.
 """
 import argparse
 import json
@@ -25,7 +28,16 @@ import torch  # noqa: E402
 METRIC = "samples/sec (fwd+bwd) METR-LA B=64 N=207 T=12 at 1/2/4/8 GPUs; 12-step MAE"
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (vector = MFMA), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
-B, N, T = 64, 207, 12
+
+CONFIGS = {
+    # batch per GPU, nodes, steps, graph, workload label, oracle / CPU sample batch
+    "metr": dict(B=64, N=207, T=12, dense=False, graph_seed=0, sample_b=64,
+                 workload="METR-LA train step B=64/GPU N=207 T=12 fp32 (configs[1])"),
+    "pems": dict(B=64, N=325, T=12, dense=False, graph_seed=6, sample_b=16,
+                 workload="PEMS-BAY-shape train step B=64/GPU N=325 T=12 fp32 (configs[2] graph)"),
+    "n2048": dict(B=32, N=2048, T=24, dense=True, graph_seed=15, sample_b=1,
+                  workload="synthetic dense-graph train step B=32/GPU N=2048 T=24 fp32 (configs[4])"),
+}
 
 
 def parse():
@@ -33,12 +45,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="metr", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     return ap.parse_args()
 
 
-def step_flops(n=N, t=T, nhid=32, nsup=3):
+def step_flops(n, t):
     """Algorithmic fwd+bwd FLOP of one sample: the reference's
     full work as torch.utils.flop_counter counts it (incl. full-T skip convs, gconv.7 backward),
     so executed-work savings show up as a higher effective fraction."""
@@ -47,6 +60,8 @@ def step_flops(n=N, t=T, nhid=32, nsup=3):
 
 def main():
     args = parse()
+    cfg = CONFIGS[args.config]
+    B, N, T = cfg["B"], cfg["N"], cfg["T"]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -60,15 +75,16 @@ def main():
 
     torch.manual_seed(999)
     np.random.seed(0)
-    adj = synthetic.random_sensor_graph(N, seed=0)
-    sups = [torch.tensor(a, device=dev) for a in synthetic.double_transition(adj)]
+    adj = synthetic.random_sensor_graph(N, seed=cfg["graph_seed"], dense=cfg["dense"])
+    sups_np = synthetic.double_transition(adj)
+    sups = [torch.tensor(a, device=dev) for a in sups_np]
     scaler = util.StandardScaler(synthetic.SCALER_MEAN, synthetic.SCALER_STD)
     eng = trainer(scaler, 2, T, N, 32, 0.3, 1e-3, 1e-4, dev, sups, True, True, None, 4, 2)
     eng.broadcast_parameters(0)
     ex = eng.model.executor()
     ex.seed.fill_(12345 + 7919 * rank)
 
-    nb = 8  # distinct resident batches, cycled
+    nb = 8 if N <= 512 else 2  # distinct resident batches, cycled
     xs, ys = [], []
     for i in range(nb):
         x, y = synthetic.synthetic_batch(B, N, T, seed=1000 * rank + i)
@@ -104,14 +120,15 @@ def main():
     # 12-step MAE (train.py:392-403 protocol) of the trained weights on a held-out synthetic batch,
     # and the same number from the fp64 CPU oracle on the same weights and batch (north_star: MAE
     # within 1e-4 of the reference)
-    xt, yt = synthetic.synthetic_batch(B, N, T, seed=99999)
+    sb = cfg["sample_b"]
+    xt, yt = synthetic.synthetic_batch(sb, N, T, seed=99999)
     with torch.no_grad():
         eng.model.eval()
         pred = eng.model(torch.tensor(xt, device=dev)).transpose(1, 3)[:, 0]  # [B, N, T]
         real = torch.tensor(yt, device=dev)
         maes = [util.masked_mae(scaler.inverse_transform(pred[:, :, h]), real[:, :, h], 0.0).item() for h in range(T)]
     mae12 = float(np.mean(maes))
-    mae12_ref = oracle_mae12(eng, sups, xt, yt) if rank == 0 else None
+    mae12_ref = oracle_mae12(eng, sups_np, xt, yt, N, T) if rank == 0 else None
 
     roof = measure_dominant(eng, dev)
     result = None
@@ -120,18 +137,18 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (METR-LA tensor format, seeded; random-init weights)",
-            "config": {"workload": "METR-LA train step B=64/GPU N=207 T=12 fp32 (configs[1])",
-                       "global_batch": B * world, "nodes": N, "seq_len": T,
+            "data": "synthetic (%s, seeded; random-init weights)"
+                    % ("METR-LA tensor format" if not cfg["dense"] else "METR-LA tensor format, dense random graph"),
+            "config": {"workload": cfg["workload"], "global_batch": B * world, "nodes": N, "seq_len": T,
                        "parallelism": "dp%d" % world if world > 1 else "single"},
             "mae12": round(mae12, 6), "mae12_oracle_f64": round(mae12_ref, 6),
-            "mae12_delta": float("%.3g" % abs(mae12 - mae12_ref)),
+            "mae12_delta": float("%.3g" % abs(mae12 - mae12_ref)), "mae12_sample_batch": sb,
             "last_train_metrics": [round(v, 5) for v in last],
-            "step_effective_tflops": round(step_flops() * B * world / (elapsed / args.steps) / 1e12 / world, 3),
+            "step_effective_tflops": round(step_flops(N, T) * B * world / (elapsed / args.steps) / 1e12 / world, 3),
             "roofline": roof,
         }
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfg)
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.barrier()
@@ -139,12 +156,13 @@ def main():
 
 
 def measure_dominant(eng, dev, rounds=5):
-    """The dominant kernel is the fused diffusion graph convolution gcn_fwd_fused_kernel<512, true>
-    (gwn_gcn_fwd: 3 supports x 2 hops of 'ncvl,vw->ncwl' + the 224->32 mlp + residual + dropout
-    + BN partials, one launch per layer, 8 per step).  Replay exactly the last training step's 8
-    launches (same arguments and buffers; the replay is idempotent) with HIP events on the
-    launch stream; achieved = algorithmic FLOP / summed launch time, where the algorithmic FLOP
-    of a launch = slices * (K*order*2*C*N^2 + 2*(2K+1)*C*C*N)."""
+    """The dominant kernel is the diffusion graph convolution forward (gwn_gcn_fwd: 3 supports x 2
+    hops of 'ncvl,vw->ncwl' + the 224->32 mlp + residual + dropout + BN partials, one call per
+    layer, 8 per step; for N <= 512 ONE fused launch, gcn_fwd_fused_kernel<512, true>).  Replay
+    exactly the last training step's 8 calls (same arguments and buffers; the replay is
+    idempotent) with HIP events on the launch stream; achieved = algorithmic FLOP / summed time,
+    where the algorithmic FLOP of a call = slices * (K*order*2*C*N^2 + 2*(2K+1)*C*C*N) (SURVEY.md
+    Appendix A)."""
     import ctypes
     from gwn_amd import _lib
     ex = eng.model._executor
@@ -170,13 +188,15 @@ def measure_dominant(eng, dev, rounds=5):
             count += 1
     avg_us = 1000.0 * total_ms / count
     achieved = total_flop / (total_ms / 1000.0) / 1e12
+    fused = N <= 512
     # HBM bytes per launch from the committed PMC passes of this kernel (tools/pmc_dominant.py:
     # separate FETCH_SIZE / WRITE_SIZE rocprofv3 runs of this bench, gfx950 FETCH correction)
     traffic, pmc = None, os.path.join(ROOT, "profiles", "r01", "pmc_gcn_fwd_fused.json")
-    if os.path.exists(pmc):
+    if fused and N == 207 and os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get("traffic_bytes_per_launch")
-    return {"kernel": "gcn_fwd_fused_kernel<512, true> (fused diffusion GCN forward, 8 launches/step)",
+    return {"kernel": ("gcn_fwd_fused_kernel<512, true> (fused diffusion GCN forward, 8 launches/step)" if fused
+                       else "gwn_gcn_fwd large-graph schedule (batched diffusion GEMMs + mlp, 8 calls/step)"),
             "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "traffic_source": "profiles/r01/pmc_gcn_fwd_fused.json" if traffic else None,
@@ -185,13 +205,13 @@ def measure_dominant(eng, dev, rounds=5):
             "launches_timed": count}
 
 
-def oracle_mae12(eng, sups, xt, yt):
+def oracle_mae12(eng, sups_np, xt, yt, N, T):
     """12-step masked MAE of the fp64 CPU oracle (checker only) on the trained weights."""
     from oracle import gwnet_oracle as orc
     sd = {k: v.detach().cpu().numpy() for k, v in eng.model.state_dict().items()}
     p = {k: torch.tensor(v, dtype=torch.float64) for k, v in sd.items()}
-    out = orc.forward(p, [s.detach().cpu().double() for s in sups], torch.tensor(xt, dtype=torch.float64),
-                      orc.Cfg(N), False, p)
+    out = orc.forward(p, [torch.tensor(s, dtype=torch.float64) for s in sups_np],
+                      torch.tensor(xt, dtype=torch.float64), orc.Cfg(N, out_dim=T), False, p)
     pred = out.transpose(1, 3)[:, 0] * eng.scaler.std + eng.scaler.mean
     real = torch.tensor(yt, dtype=torch.float64)
     return float(np.mean([orc.masked_metrics(pred[:, :, h], real[:, :, h])[0].item() for h in range(T)]))
@@ -207,28 +227,31 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(seconds):
+def cpu_baseline(seconds, cfg):
     """The CPU restatement (oracle/, kind "port") timing the same training step on the host
-    cores: fp32, autograd backward, clip + Adam; 3 warm-up steps, then the median of >= 5 timed
-    steps (BASELINE.md §3 / SURVEY §8d protocol).  Threads: os.cpu_count(), capped by the job's
-    CPU share where the launcher states one (OMP_NUM_THREADS; the GPU box gives each 1-GPU job 16
-    of the machine's cores and os.cpu_count() reports the whole machine)."""
+    cores: fp32, autograd backward, clip + Adam; 3 warm-up steps (1 at N=2048), then the median of
+    >= 5 timed steps (>= 3 at N=2048, where a sample step is B=1) -- the BASELINE.md §3 / SURVEY
+    §8d protocol.  Threads: os.cpu_count(), capped by the job's CPU share where the launcher states
+    one (OMP_NUM_THREADS; the GPU box gives each 1-GPU job 16 of the machine's cores and
+    os.cpu_count() reports the whole machine)."""
     from gwn_amd import synthetic
+    from gwn_amd.model import gwnet
     from oracle import gwnet_oracle as orc
+    N, T = cfg["N"], cfg["T"]
     nproc = os.cpu_count() or 1
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     threads = min(nproc, share) if share > 0 else nproc
     torch.set_num_threads(threads)
-    cfg = orc.Cfg(N, dropout=0.3)
+    ocfg = orc.Cfg(N, out_dim=T, dropout=0.3)
     torch.manual_seed(999)
-    from gwn_amd.model import gwnet
-    m = gwnet("cpu", N, 0.3, supports=[torch.zeros(N, N), torch.zeros(N, N)])
+    m = gwnet("cpu", N, 0.3, supports=[torch.zeros(N, N), torch.zeros(N, N)], out_dim=T)
     sd = {k: v.numpy() for k, v in m.state_dict().items()}
-    adj = synthetic.random_sensor_graph(N, seed=0)
-    tr = orc.Trainer(sd, synthetic.double_transition(adj), cfg, dtype=torch.float32)
-    bsz = B
+    adj = synthetic.random_sensor_graph(N, seed=cfg["graph_seed"], dense=cfg["dense"])
+    tr = orc.Trainer(sd, synthetic.double_transition(adj), ocfg, dtype=torch.float32)
+    bsz = cfg["sample_b"]
     x, y = synthetic.synthetic_batch(bsz, N, T, seed=5)
-    for _ in range(3):
+    big = N > 512
+    for _ in range(1 if big else 3):
         tr.train(x, y)  # warm-up
     times = []
     t0 = time.perf_counter()
@@ -236,14 +259,15 @@ def cpu_baseline(seconds):
         t1 = time.perf_counter()
         tr.train(x, y)
         times.append(time.perf_counter() - t1)
-        if len(times) >= 5 and (time.perf_counter() - t0 >= seconds or len(times) >= 30):
+        if len(times) >= (3 if big else 5) and (time.perf_counter() - t0 >= seconds or len(times) >= 30):
             break
     med = float(np.median(times))
     return {"value": round(bsz / med, 3), "unit": "samples/s", "cores": threads, "kind": "port",
             "nproc": nproc, "cpu_model": _cpu_model(), "statistic": "median",
-            "sample": "median of %d timed train steps (after 3 warm-up) of B=%d (N=207, T=12, fp32, dropout 0.3, "
-                      "clip + Adam), %.2f s/step, %d threads; calibrated in the build container at 38.4 vs 34.9 "
-                      "samples/s for the reference itself (8 threads)" % (len(times), bsz, med, threads)}
+            "sample": "median of %d timed train steps of B=%d (N=%d, T=%d, fp32, dropout 0.3, clip + Adam), "
+                      "%.2f s/step, %d threads; the oracle was calibrated in the build container at 38.4 vs "
+                      "34.9 samples/s for the reference itself (METR-LA B=64, 8 threads)"
+                      % (len(times), bsz, N, T, med, threads)}
 
 
 if __name__ == "__main__":
