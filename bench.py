@@ -28,13 +28,15 @@ import torch  # noqa: E402
 METRIC = "samples/sec (fwd+bwd) METR-LA B=64 N=207 T=12 at 1/2/4/8 GPUs; 12-step MAE"
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (vector = MFMA), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 
 CONFIGS = {
     # batch per GPU, nodes, steps, graph, workload label, oracle / CPU sample batch
     "metr": dict(B=64, N=207, T=12, dense=False, graph_seed=0, sample_b=64,
                  workload="METR-LA train step B=64/GPU N=207 T=12 fp32 (configs[1])"),
-    "pems": dict(B=64, N=325, T=12, dense=False, graph_seed=6, sample_b=16,
-                 workload="PEMS-BAY-shape train step B=64/GPU N=325 T=12 fp32 (configs[2] graph)"),
+    "pems": dict(B=64, N=325, T=12, dense=False, graph_seed=6, sample_b=16, dtype="bf16",
+                 workload="PEMS-BAY-shape train step B=64/GPU N=325 T=12, bf16 MFMA operands with fp32 "
+                          "accumulation in the diffusion GCN (configs[2])"),
     "n2048": dict(B=32, N=2048, T=24, dense=True, graph_seed=15, sample_b=1,
                   workload="synthetic dense-graph train step B=32/GPU N=2048 T=24 fp32 (configs[4])"),
 }
@@ -46,6 +48,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="metr", choices=sorted(CONFIGS))
+    ap.add_argument("--dtype", choices=("f32", "bf16"), default=None,
+                    help="override the config's arithmetic precision (pems: bf16, others f32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     return ap.parse_args()
@@ -80,6 +84,8 @@ def main():
     sups = [torch.tensor(a, device=dev) for a in sups_np]
     scaler = util.StandardScaler(synthetic.SCALER_MEAN, synthetic.SCALER_STD)
     eng = trainer(scaler, 2, T, N, 32, 0.3, 1e-3, 1e-4, dev, sups, True, True, None, 4, 2)
+    bf16 = (args.dtype or cfg.get("dtype", "f32")) == "bf16"
+    eng.model.set_compute_dtype("bf16" if bf16 else "fp32")
     eng.broadcast_parameters(0)
     ex = eng.model.executor()
     ex.seed.fill_(12345 + 7919 * rank)
@@ -130,13 +136,13 @@ def main():
     mae12 = float(np.mean(maes))
     mae12_ref = oracle_mae12(eng, sups_np, xt, yt, N, T) if rank == 0 else None
 
-    roof = measure_dominant(eng, dev)
+    roof = measure_dominant(eng, dev, bf16=bf16)
     result = None
     if rank == 0:
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if bf16 else "f32",
             "data": "synthetic (%s, seeded; random-init weights)"
                     % ("METR-LA tensor format" if not cfg["dense"] else "METR-LA tensor format, dense random graph"),
             "config": {"workload": cfg["workload"], "global_batch": B * world, "nodes": N, "seq_len": T,
@@ -155,7 +161,7 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def measure_dominant(eng, dev, rounds=5):
+def measure_dominant(eng, dev, rounds=5, bf16=False):
     """The dominant kernel is the diffusion graph convolution forward (gwn_gcn_fwd: 3 supports x 2
     hops of 'ncvl,vw->ncwl' + the 224->32 mlp + residual + dropout + BN partials, one call per
     layer, 8 per step; for N <= 512 ONE fused launch, gcn_fwd_fused_kernel<512, true>).  Replay
@@ -189,6 +195,17 @@ def measure_dominant(eng, dev, rounds=5):
     avg_us = 1000.0 * total_ms / count
     achieved = total_flop / (total_ms / 1000.0) / 1e12
     fused = N <= 512
+    if bf16:
+        # bf16 operands: arithmetic intensity (~80 FLOP/B algorithmic) sits far below the bf16
+        # ridge (2.5 PF / 8 TB/s = 312 FLOP/B): the kernel is bounded by HBM, priced in bytes
+        gbs = total_bytes / (total_ms / 1000.0) / 1e9
+        return {"kernel": "gcn_fwd_split_kernel<%d, 1, 2> (fused diffusion GCN forward, bf16 operands, "
+                          "8 launches/step)" % ((N + 31) // 32),
+                "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                "mfma_tflops": round(achieved, 3), "mfma_peak_bf16": BF16_PEAK_TFLOPS,
+                "avg_launch_us": round(avg_us, 3), "flop_per_launch_avg": round(total_flop / count, 1),
+                "algorithmic_bytes_per_launch": round(total_bytes / count), "launches_timed": count}
     # HBM bytes per launch from the committed PMC passes of this kernel (tools/pmc_dominant.py:
     # separate FETCH_SIZE / WRITE_SIZE rocprofv3 runs of this bench, gfx950 FETCH correction)
     traffic, pmc = None, os.path.join(ROOT, "profiles", "r01", "pmc_gcn_fwd_fused.json")

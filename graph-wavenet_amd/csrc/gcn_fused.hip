@@ -861,6 +861,7 @@ bool gwn_gcn_fused_eligible(int c, int n, int nsup, int ld_sup) {
 
 bool gwn_gcn_split_eligible(int c, int n, int planes);
 int gwn_gcn_split_fwd_launch(const gwn_gcn_args* g, const FusedFwd& a, hipStream_t s);
+int gwn_gcn_bf16_bwd_launch(const gwn_gcn_bwd_args* g, const FusedBwd& a, hipStream_t s);
 
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
   const int nwt = (g->n + 31) / 32;
@@ -949,6 +950,8 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   else
     GWN_REQUIRE(a.dh != nullptr, "gcn_bwd (fused): dh is required without the BN prologue");
   if (a.dfg) GWN_REQUIRE(a.fg != nullptr, "gcn_bwd (fused): the gate epilogue needs fg");
+  if (g->split_planes == 1) return gwn_gcn_bf16_bwd_launch(g, a, s);
+  GWN_REQUIRE(g->split_planes == 0, "gcn_bwd (fused): split_planes must be 0 (f32) or 1 (bf16)");
   static bool attr_set = false;
   if (!attr_set) {
     ensure_lds_attr(gcn_bwd_fused_kernel<512, false>);
@@ -1038,6 +1041,10 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 namespace {
 
 constexpr int split_row_bytes(int np) { return ((2 * np - 16 + 255) / 256) * 256 + 16; }
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+// bytes of the forward kernel's first LDS region: the P node-feature planes, and the fp32
+// [np][LDR] rows the epilogue stages there (the larger of the two for P = 1)
+constexpr int split_xs_bytes(int np, int P) { return cmax(P * 32 * split_row_bytes(np), np * LDR * 4); }
 
 template <int P>
 __device__ __forceinline__ void split8(const float* x, bf16x8* out) {
@@ -1196,12 +1203,10 @@ __global__ __launch_bounds__(64 * NKB) void gcn_fwd_split_kernel(const FusedFwd 
                                                                  long gstride, int ldg, const void* wsplit) {
   constexpr int NP = NKB * 32;
   constexpr int SB = split_row_bytes(NP);
-  constexpr int IMG = P * 32 * SB;
-  static_assert(NP * LDR * 4 <= IMG, "epilogue staging must fit in the first image");
   extern __shared__ float lds[];
   __shared__ float red[2][64 * NKB];
   char* xs = (char*)lds;
-  char* ys = xs + IMG;
+  char* ys = xs + split_xs_bytes(NP, P);  // the first region also stages the fp32 epilogue rows
   const int n = a.n;
   const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
   const int col = lane & 31, half = lane >> 5;
@@ -1317,10 +1322,124 @@ __global__ void split_mlp_kernel(SplitWArgs wa, int width, __bf16* dst, long lay
   }
 }
 
+// dst[l][piece][c][c'] (bf16) = W_l[c'][piece*32 + c]: the A operand of the backward's channel
+// contraction dP = W^T dh (row c, inputs c' in plain order, matching the dh image rows)
+__global__ void mlpT_bf16_kernel(SplitWArgs wa, int width, __bf16* dst, long layer_stride) {
+  const int l = blockIdx.y;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // over pieces * 32 * 32
+  const int npieces = width / CH;
+  if (e >= npieces * CH * CH) return;
+  const int cp = e & 31, c = (e >> 5) & 31, piece = e >> 10;
+  dst[l * layer_stride + e] = (__bf16)wa.w[l][(long)cp * width + piece * CH + c];
+}
+
+// ---------------------------------------------------------------------------------------------
+// bf16 backward (the schedule of gcn_bwd_fused_kernel with bf16 operands, fp32 accumulation):
+//   dh image: LDS rows [w][32 c'] bf16 (row stride DHB), the B operand of dP = W^T dh;
+//   hop image: one bf16 plane [c][v] (the A operand of the diffusions through G^T);
+//   supports: gwn_split_supports(planes = 1) of the TRANSPOSED supports, i.e. planes of A [w][v].
+constexpr int DHB = 80;  // 64 B of bf16 + 16: the 16 lanes of a ds_read_b128 group hit distinct bank slots
+
+__device__ __forceinline__ f32x16 mlpT_bf16(const void* wt, int piece, const char* dhimg, int w0, int lane,
+                                            f32x16 acc) {
+  const int col = lane & 31, half = lane >> 5;
+  const bf16x8* wp = (const bf16x8*)wt + (piece * CH + col) * 4 + half;  // row c = col, inputs 8h + 16s
+  const char* bp = dhimg + (w0 + col) * DHB + half * 16;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8 a = wp[2 * s];
+    const bf16x8 b = *(const bf16x8*)(bp + 32 * s);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+template <int NKB, int PD>
+__global__ __launch_bounds__(64 * NKB) void gcn_bwd_bf16_kernel(const FusedBwd a, const void* gsplit, long gstride,
+                                                                int ldg, const void* wtsplit) {
+  constexpr int NP = NKB * 32;
+  constexpr int DHI = NP * DHB;        // bf16 dh image; the fp32 rows [w][LDR] of the prologue dh
+                                       // and the epilogue dx are staged at the base as well
+  extern __shared__ float lds[];
+  char* dhimg = (char*)lds;            // aliases the prologue staging (converted in registers)
+  char* img = dhimg + DHI;
+  float* stg = lds;
+  const int n = a.n;
+  const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
+  const int col = lane & 31, half = lane >> 5;
+  const long row0 = (long)blockIdx.x * n;
+
+  SplitG g = split_g(gsplit, NP, ldg, 1, w0 + col, half);
+  SplitPre<1, PD> g0{};
+  if (a.nsup > 0) g0 = split_pre<1, PD>(g);
+  bwd_prologue<EPT>(a, stg, row0, n, NP);  // dh (fp32) for rows < np, zero beyond n
+  __syncthreads();
+  {
+    // fp32 staging -> bf16 dh image (each thread converts the same 16 elements it reads)
+    float v[EPT];
+    const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int w = wb + i * ws;
+      v[i] = (w < NP) ? stg[w * LDR + c] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int w = wb + i * ws;
+      if (w < NP) *(__bf16*)(dhimg + w * DHB + c * 2) = (__bf16)v[i];
+    }
+  }
+  __syncthreads();
+  f32x16 dx = mlpT_bf16(wtsplit, 0, dhimg, w0, lane, zero16());
+  for (int k = 0; k < a.nsup; ++k) {
+    const f32x16 u = mlpT_bf16(wtsplit, 2 + 2 * k, dhimg, w0, lane, zero16());
+    __syncthreads();  // img free: every wave finished the previous diffusion
+    acc_to_planes<NKB, 1>(img, u, w0, lane);
+    if (k == a.adp_index) acc_to_global(a.t2 + row0 * a.ld_t, a.ld_t, u, w0, lane, n);
+    __syncthreads();
+    f32x16 t = mlpT_bf16(wtsplit, 1 + 2 * k, dhimg, w0, lane, zero16());
+    t = diffuse_split<NKB, 1, PD>(img, g, lane, t, g0);  // dx1 = dP_x1 + A dP_x2
+    g0 = split_pre<1, PD>(g);
+    __syncthreads();
+    acc_to_planes<NKB, 1>(img, t, w0, lane);
+    if (k == a.adp_index) acc_to_global(a.t1 + row0 * a.ld_t, a.ld_t, t, w0, lane, n);
+    __syncthreads();
+    dx = diffuse_split<NKB, 1, PD>(img, g, lane, dx, g0);  // dxg += A dx1
+    if (k + 1 < a.nsup) {
+      g = split_g((const char*)gsplit + (k + 1) * gstride * 2, NP, ldg, 1, w0 + col, half);
+      g0 = split_pre<1, PD>(g);
+    }
+  }
+  if (!a.dfg) {
+    acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
+    return;
+  }
+  __syncthreads();  // every wave finished reading the images
+  acc_to_lds(stg, dx, w0, lane);
+  __syncthreads();
+  bwd_gate_epilogue<EPT>(a, stg, row0, n);
+}
+
+template <int NKB>
+void launch_bf16_bwd(const FusedBwd& a, const gwn_gcn_bwd_args* g, int slices, hipStream_t s) {
+  constexpr int NP = NKB * 32;
+  constexpr int PD = NKB > 1 ? 2 : 1;
+  const size_t lds = (size_t)cmax(NP * LDR * 4, NP * DHB + 32 * split_row_bytes(NP));
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gcn_bwd_bf16_kernel<NKB, PD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr_set = true;
+  }
+  gcn_bwd_bf16_kernel<NKB, PD><<<slices, 64 * NKB, lds, s>>>(a, g->supT_split, g->sup_split_stride, g->ld_split,
+                                                             g->wT_split);
+}
+
 template <int NKB, int P, int PD>
 void launch_split(const FusedFwd& a, const gwn_gcn_args* g, int slices, hipStream_t s) {
   constexpr int NP = NKB * 32;
-  const size_t lds = (size_t)2 * P * 32 * split_row_bytes(NP);
+  const size_t lds = (size_t)split_xs_bytes(NP, P) + P * 32 * split_row_bytes(NP);
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gcn_fwd_split_kernel<NKB, P, PD>,
@@ -1335,7 +1454,14 @@ void launch_split(const FusedFwd& a, const gwn_gcn_args* g, int slices, hipStrea
 
 bool gwn_gcn_split_eligible(int c, int n, int planes) {
   const int nkb = (n + 31) / 32;
-  return c == CH && ((planes == 3 && (nkb == 1 || nkb == 7 || nkb == 11)) || (planes == 2 && nkb == 7));
+  return c == CH && n > 0 && ((planes == 1 && nkb <= 16) || (planes == 3 && (nkb == 1 || nkb == 7 || nkb == 11)) ||
+                              (planes == 2 && nkb == 7));
+}
+
+// bf16 operands (planes = 1): one instantiation per node-tile count
+template <int NKB>
+void launch_bf16_fwd(const FusedFwd& a, const gwn_gcn_args* g, int slices, hipStream_t s) {
+  launch_split<NKB, 1, (NKB > 1 ? 2 : 1)>(a, g, slices, s);
 }
 
 int gwn_gcn_split_fwd_launch(const gwn_gcn_args* g, const FusedFwd& a, hipStream_t s) {
@@ -1343,12 +1469,59 @@ int gwn_gcn_split_fwd_launch(const gwn_gcn_args* g, const FusedFwd& a, hipStream
   const int slices = g->rows / g->n;
   GWN_REQUIRE(g->ld_split >= nkb * 32 && g->sup_split_stride % 8 == 0 && g->ld_split % 8 == 0,
               "gcn_fwd (split): bad split-support layout");
-  if (g->split_planes == 3) {
+  if (g->split_planes == 1) {
+    switch (nkb) {
+      case 1: launch_bf16_fwd<1>(a, g, slices, s); break;
+      case 2: launch_bf16_fwd<2>(a, g, slices, s); break;
+      case 3: launch_bf16_fwd<3>(a, g, slices, s); break;
+      case 4: launch_bf16_fwd<4>(a, g, slices, s); break;
+      case 5: launch_bf16_fwd<5>(a, g, slices, s); break;
+      case 6: launch_bf16_fwd<6>(a, g, slices, s); break;
+      case 7: launch_bf16_fwd<7>(a, g, slices, s); break;
+      case 8: launch_bf16_fwd<8>(a, g, slices, s); break;
+      case 9: launch_bf16_fwd<9>(a, g, slices, s); break;
+      case 10: launch_bf16_fwd<10>(a, g, slices, s); break;
+      case 11: launch_bf16_fwd<11>(a, g, slices, s); break;
+      case 12: launch_bf16_fwd<12>(a, g, slices, s); break;
+      case 13: launch_bf16_fwd<13>(a, g, slices, s); break;
+      case 14: launch_bf16_fwd<14>(a, g, slices, s); break;
+      case 15: launch_bf16_fwd<15>(a, g, slices, s); break;
+      default: launch_bf16_fwd<16>(a, g, slices, s); break;
+    }
+  } else if (g->split_planes == 3) {
     if (nkb == 7) launch_split<7, 3, 2>(a, g, slices, s);
     else if (nkb == 11) launch_split<11, 3, 2>(a, g, slices, s);
     else launch_split<1, 3, 1>(a, g, slices, s);
   } else {
     launch_split<7, 2, 2>(a, g, slices, s);
+  }
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_gcn_bf16_bwd_launch(const gwn_gcn_bwd_args* g, const FusedBwd& a, hipStream_t s) {
+  const int nkb = (g->n + 31) / 32;
+  const int slices = g->rows / g->n;
+  GWN_REQUIRE(gwn_gcn_split_eligible(g->c, g->n, 1) && g->supT_split && g->wT_split && g->nsup > 0 &&
+                  g->ld_split >= nkb * 32 && g->sup_split_stride % 8 == 0 && g->ld_split % 8 == 0 && a.sup_batch <= 1,
+              "gcn_bwd (bf16): needs c == 32, n <= 512, nsup >= 1, split transposed supports and weights");
+  switch (nkb) {
+    case 1: launch_bf16_bwd<1>(a, g, slices, s); break;
+    case 2: launch_bf16_bwd<2>(a, g, slices, s); break;
+    case 3: launch_bf16_bwd<3>(a, g, slices, s); break;
+    case 4: launch_bf16_bwd<4>(a, g, slices, s); break;
+    case 5: launch_bf16_bwd<5>(a, g, slices, s); break;
+    case 6: launch_bf16_bwd<6>(a, g, slices, s); break;
+    case 7: launch_bf16_bwd<7>(a, g, slices, s); break;
+    case 8: launch_bf16_bwd<8>(a, g, slices, s); break;
+    case 9: launch_bf16_bwd<9>(a, g, slices, s); break;
+    case 10: launch_bf16_bwd<10>(a, g, slices, s); break;
+    case 11: launch_bf16_bwd<11>(a, g, slices, s); break;
+    case 12: launch_bf16_bwd<12>(a, g, slices, s); break;
+    case 13: launch_bf16_bwd<13>(a, g, slices, s); break;
+    case 14: launch_bf16_bwd<14>(a, g, slices, s); break;
+    case 15: launch_bf16_bwd<15>(a, g, slices, s); break;
+    default: launch_bf16_bwd<16>(a, g, slices, s); break;
   }
   GWN_CHECK_LAUNCH();
   return GWN_OK;
@@ -1364,14 +1537,15 @@ extern "C" long gwn_split_support_elems(int n, int planes) {
 extern "C" int gwn_split_supports(const float* const* sup, int nsup, int n, int ld_sup, int planes, void* dst,
                                   long sup_stride_elems, int ld_dst, hipStream_t s) {
   const int np = (n + 31) / 32 * 32;
-  GWN_REQUIRE(nsup >= 1 && nsup <= 8 && (planes == 2 || planes == 3) && ld_sup >= np && ld_dst >= np &&
+  GWN_REQUIRE(nsup >= 1 && nsup <= 8 && planes >= 1 && planes <= 3 && ld_sup >= np && ld_dst >= np &&
                   sup_stride_elems >= (long)planes * np * ld_dst,
               "split_supports: bad shape");
   SplitSupArgs sa;
   for (int k = 0; k < 8; ++k) sa.src[k] = k < nsup ? sup[k] : nullptr;
   dim3 grid(np / 32, np / 32, nsup);
   if (planes == 3) split_supports_kernel<3><<<grid, 256, 0, s>>>(sa, np, ld_sup, (__bf16*)dst, sup_stride_elems, ld_dst);
-  else split_supports_kernel<2><<<grid, 256, 0, s>>>(sa, np, ld_sup, (__bf16*)dst, sup_stride_elems, ld_dst);
+  else if (planes == 2) split_supports_kernel<2><<<grid, 256, 0, s>>>(sa, np, ld_sup, (__bf16*)dst, sup_stride_elems, ld_dst);
+  else split_supports_kernel<1><<<grid, 256, 0, s>>>(sa, np, ld_sup, (__bf16*)dst, sup_stride_elems, ld_dst);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -1381,7 +1555,7 @@ extern "C" long gwn_split_mlp_elems(int nsup, int planes) { return (long)(2 * ns
 extern "C" int gwn_split_mlp_weights(const float* const* w, int nlayers, int nsup, int planes, void* dst,
                                      long layer_stride_elems, hipStream_t s) {
   const int width = (2 * nsup + 1) * CH;
-  GWN_REQUIRE(nlayers >= 1 && nlayers <= 16 && nsup >= 0 && (planes == 2 || planes == 3) &&
+  GWN_REQUIRE(nlayers >= 1 && nlayers <= 16 && nsup >= 0 && planes >= 1 && planes <= 3 &&
                   layer_stride_elems >= gwn_split_mlp_elems(nsup, planes),
               "split_mlp_weights: bad shape");
   SplitWArgs wa;
@@ -1389,7 +1563,24 @@ extern "C" int gwn_split_mlp_weights(const float* const* w, int nlayers, int nsu
   const int total = (2 * nsup + 1) * CH * CH;
   dim3 grid((total + 255) / 256, nlayers);
   if (planes == 3) split_mlp_kernel<3><<<grid, 256, 0, s>>>(wa, width, (__bf16*)dst, layer_stride_elems);
-  else split_mlp_kernel<2><<<grid, 256, 0, s>>>(wa, width, (__bf16*)dst, layer_stride_elems);
+  else if (planes == 2) split_mlp_kernel<2><<<grid, 256, 0, s>>>(wa, width, (__bf16*)dst, layer_stride_elems);
+  else split_mlp_kernel<1><<<grid, 256, 0, s>>>(wa, width, (__bf16*)dst, layer_stride_elems);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+extern "C" long gwn_bf16_mlpT_elems(int nsup) { return (long)(2 * nsup + 1) * CH * CH; }
+
+extern "C" int gwn_bf16_mlpT_weights(const float* const* w, int nlayers, int nsup, void* dst, long layer_stride_elems,
+                                     hipStream_t s) {
+  const int width = (2 * nsup + 1) * CH;
+  GWN_REQUIRE(nlayers >= 1 && nlayers <= 16 && nsup >= 0 && layer_stride_elems >= gwn_bf16_mlpT_elems(nsup),
+              "bf16_mlpT_weights: bad shape");
+  SplitWArgs wa;
+  for (int l = 0; l < 16; ++l) wa.w[l] = l < nlayers ? w[l] : nullptr;
+  const int total = (2 * nsup + 1) * CH * CH;
+  dim3 grid((total + 255) / 256, nlayers);
+  mlpT_bf16_kernel<<<grid, 256, 0, s>>>(wa, width, (__bf16*)dst, layer_stride_elems);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

@@ -107,6 +107,9 @@ class GcnBwdArgs(ctypes.Structure):
         ("dfg", c_void_p),
         ("layout", c_int),
         ("sup_bstride", c_long), ("sup_batch", c_int),
+        ("split_planes", c_int),
+        ("supT_split", c_void_p), ("sup_split_stride", c_long), ("ld_split", c_int),
+        ("wT_split", c_void_p),
     ]
 
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time
@@ -147,6 +150,8 @@ _SIGS = [
     ("gwn_split_supports", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_long, c_int, c_void_p]),
     ("gwn_split_mlp_elems", c_long, [c_int, c_int]),
     ("gwn_split_mlp_weights", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p]),
+    ("gwn_bf16_mlpT_elems", c_long, [c_int]),
+    ("gwn_bf16_mlpT_weights", c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p]),
     ("gwn_gcn_bwd", c_int, [ctypes.POINTER(GcnBwdArgs), c_void_p]),
     ("gwn_gcn_bwd_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
     ("gwn_wgrad", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,

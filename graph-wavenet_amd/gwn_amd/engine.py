@@ -177,7 +177,7 @@ class trainer():
         bn_key = tuple((m.momentum, m.eps) for m in model.bn)
         key = (tuple(input.shape), tuple(real_val.shape), float(g["lr"]), tuple(g["betas"]), float(g["eps"]),
                float(g["weight_decay"]), self.clip, float(model.dropout), model._flat.data_ptr(), sup_key, bn_key,
-               float(self.scaler.mean), float(self.scaler.std))
+               float(self.scaler.mean), float(self.scaler.std), model.compute_dtype)
         if self.use_graphs and key in self._graphs:
             return self._replay(key, input, real_val)
         if self.use_graphs and self._eager_runs.get(key, 0) >= 1:

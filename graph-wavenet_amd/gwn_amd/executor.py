@@ -255,6 +255,7 @@ class Executor:
         self.cfg = Config(model)
         self.layout = PackedLayout(model, self.cfg)
         self.dropout = model.dropout
+        self.compute_dtype = getattr(model, "compute_dtype", "fp32")
         self.device = None
         self._scratch = {}
 
@@ -274,15 +275,39 @@ class Executor:
 
     # ---------------------------------------------------------------------------------------
     def split_planes(self):
-        """bf16 pieces per operand of the split-MFMA gcn forward (GWN_SPLIT: 3 = fp32 accuracy,
-        0 = the f32-MFMA kernel, the default: at METR-LA shape the split kernel holds one
-        workgroup per CU (101 KB of LDS planes) and measured 223 vs 213 us per T=12 launch,
-        tools/bench_gcn.py).  0 when the shape has no split instantiation."""
+        """MFMA operand format of the fused gcn kernels (include/gwn.h gwn_dtype):
+        * compute dtype bf16 (gwnet.set_compute_dtype): 1 = bf16 operands, fp32 accumulation,
+          forward AND backward (the mixed-precision path of configs[2]);
+        * else GWN_SPLIT=3: the split-bf16 forward at fp32 accuracy (3 pieces; measurements only:
+          at METR-LA shape it holds one workgroup per CU and measured 223 vs 213 us per T=12
+          launch, tools/bench_gcn.py);
+        * else 0: the f32-MFMA kernels (the default: the reference's fp32 arithmetic).
+        0 when the shape has no such instantiation (c != 32, n > 512, no supports)."""
         cfg = self.cfg
-        planes = int(os.environ.get("GWN_SPLIT", "0"))
+        planes = 1 if self.compute_dtype == "bf16" else int(os.environ.get("GWN_SPLIT", "0"))
         if planes == 0 or not cfg.use_gcn or cfg.nsup < 1:
             return 0
         return planes if _lib.load().gwn_gcn_split_supported(cfg.C, cfg.N, planes) else 0
+
+    def split_bwd_operands(self, supT_arr, nsup):
+        """bf16 operands of the fused backward: planes of the transposed supports (the backward
+        diffuses through A) and the transposed mlp weights of every layer (dP = W^T dh)."""
+        cfg = self.cfg
+        lib = _lib.load()
+        st = _lib.stream()
+        sup_el = lib.gwn_split_support_elems(cfg.N, 1)
+        w_el = (lib.gwn_bf16_mlpT_elems(nsup) + 7) // 8 * 8
+        key = ("splitT", nsup)
+        b = self._scratch.get(key)
+        if b is None:
+            b = {"sup": torch.empty(nsup * sup_el, device=self.device, dtype=torch.int16),
+                 "w": torch.empty(cfg.L * w_el, device=self.device, dtype=torch.int16)}
+            self._scratch[key] = b
+        _lib.call("gwn_split_supports", ctypes.cast(supT_arr, ctypes.c_void_p), nsup, cfg.N, cfg.NP, 1,
+                  ptr(b["sup"]), sup_el, cfg.NP, st)
+        w_arr = (ctypes.c_void_p * cfg.L)(*[self.pk("mlp_w%d" % i).data_ptr() for i in range(cfg.L)])
+        _lib.call("gwn_bf16_mlpT_weights", ctypes.cast(w_arr, ctypes.c_void_p), cfg.L, nsup, ptr(b["w"]), w_el, st)
+        return {"sup": b["sup"].data_ptr(), "sup_stride": sup_el, "w": b["w"].data_ptr(), "w_stride_bytes": 2 * w_el}
 
     def split_operands(self, sup_arr, nsup, planes):
         """bf16 piece planes of the supports (transposed) and of every layer's mlp weights, for
@@ -439,6 +464,8 @@ class Executor:
         ws, bnpart = scr["ws"], scr["bnpart"]
         planes = self.split_planes()
         sp = self.split_operands(sup_arr, len(sups), planes) if planes else None
+        acts.sp_bwd = (self.split_bwd_operands(acts.supT_arr, len(sups))
+                       if planes == 1 and training and acts.supT_arr is not None else None)
         for i in range(L):
             d = cfg.dilations[i]
             rows = ts[i + 1] * P
@@ -673,6 +700,10 @@ class Executor:
                                      sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
                                      if acts.supT_arr is not None else None,
                                      skip_weight_grads=1 if overlap else 0)
+                spb = getattr(acts, "sp_bwd", None)
+                if spb is not None:  # bf16 operands (fp32 accumulation) in the fused backward
+                    gb.split_planes, gb.supT_split, gb.sup_split_stride = 1, spb["sup"], spb["sup_stride"]
+                    gb.ld_split, gb.wT_split = cfg.NP, spb["w"] + i * spb["w_stride_bytes"]
                 if fuse:
                     gb.dh = None
                     gb.bn_dy, gb.bn_z = ptr(dnext), ptr(acts.Z[i])

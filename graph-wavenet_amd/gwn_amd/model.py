@@ -10,6 +10,7 @@ device buffer (``_flat``), the forward is a fixed schedule of libgwn launches (e
 the backward is the matching hand-written gradient schedule, wrapped as ONE autograd node.
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -231,6 +232,7 @@ class gwnet(nn.Module):
         self.residual_channels, self.dilation_channels = residual_channels, dilation_channels
         self.skip_channels, self.end_channels = skip_channels, end_channels
         self.kernel_size = kernel_size
+        self.compute_dtype = "bf16" if os.environ.get("GWN_DTYPE", "fp32") in ("bf16", "bfloat16") else "fp32"
 
         # Submodule registration order == reference state_dict order (model.py:95-100).
         for name in ("filter_convs", "gate_convs", "residual_convs", "skip_convs", "bn", "gconv"):
@@ -328,8 +330,23 @@ class gwnet(nn.Module):
             self._executor = Executor(self)
         ex = self._executor
         ex.dropout = self.dropout
+        ex.compute_dtype = self.compute_dtype
         ex.bind(self._flat.device)
         return ex
+
+    def set_compute_dtype(self, dtype):
+        """Arithmetic precision of the diffusion / mlp products (not part of the reference API):
+        "fp32" (default, torch.float32: exact fp32 products, the reference's arithmetic) or "bf16"
+        (torch.bfloat16: bf16 MFMA operands with fp32 accumulation in the fused gcn forward and
+        backward -- mixed precision; parameters, activations, gradients and Adam state stay fp32).
+        Shapes without a bf16 kernel (c != 32, n > 512) keep the fp32 kernels."""
+        if dtype in (torch.bfloat16, "bf16", "bfloat16"):
+            self.compute_dtype = "bf16"
+        elif dtype in (torch.float32, "fp32", "float32", "f32"):
+            self.compute_dtype = "fp32"
+        else:
+            raise ValueError("gwn_amd: compute dtype must be fp32 or bf16, got %r" % (dtype,))
+        return self
 
     def _fixed_supports(self):
         """Device copies of the fixed supports, zero-padded to [NP][NP] (NP = 32*ceil(N/32)), the

@@ -30,6 +30,14 @@ extern "C" {
 #define GWN_ERR_HIP 2
 
 int gwn_version(void);
+
+/* Arithmetic (MFMA operand) precision of the diffusion / mlp products.  Storage stays fp32 in
+ * every mode (activations, weights, gradients, optimizer state); accumulation is always fp32. */
+typedef enum gwn_dtype {
+  GWN_DTYPE_F32 = 0,     /* v_mfma_f32_32x32x2_f32: exact fp32 products (the reference's arithmetic) */
+  GWN_DTYPE_BF16 = 1,    /* bf16 operands, fp32 accumulation (mixed precision, configs[2]) */
+  GWN_DTYPE_BF16X3 = 3   /* 3-piece split bf16 = fp32 accuracy on the bf16 MFMA (forward only) */
+} gwn_dtype;
 /* debugging aid: 1 = synchronise the device after every kernel launch and report a fault at the
  * kernel's source line (also enabled by GWN_SYNC_CHECK=1 in the environment), 2 = suspended (while
  * a stream is being captured into a graph), 0 = off (default) */
@@ -228,12 +236,14 @@ typedef struct gwn_gcn_args {
   const float* bn_running_mean; const float* bn_running_var; const float* bn_weight; const float* bn_bias;
   float bn_eps; float* bn_out;
   int layout;
-  /* split-bf16 path (split_planes = 2 or 3, 0 = off): every product on v_mfma_f32_32x32x16_bf16
-   * over bf16 pieces of the fp32 operands (3 pieces / 6 piece products = fp32 accuracy; 2 pieces
-   * ~1e-5 relative, measurements only).  Needs c == 32, nsup >= 1, 32*ceil(n/32) in {32, 224, 352}
-   * (2 pieces: 224 only), sup_split = gwn_split_supports output (support k at
-   * sup_split + k*sup_split_stride elements, rows ld_split), w_split = gwn_split_mlp_weights
-   * output for this layer.  The fp32 supports `sup` are not read on this path. */
+  /* operand precision of the products (gwn_dtype; 0 = GWN_DTYPE_F32, the f32-MFMA kernels):
+   *   GWN_DTYPE_BF16 (1): bf16 operands, fp32 accumulation (v_mfma_f32_32x32x16_bf16), any
+   *     n <= 512 (the mixed-precision path of configs[2]);
+   *   GWN_DTYPE_BF16X3 (3): every fp32 operand as 3 bf16 pieces, 6 piece products = fp32
+   *     accuracy; 32*ceil(n/32) in {32, 224, 352} (2 pieces: 224 only, measurements only).
+   * Needs c == 32, nsup >= 1, sup_split = gwn_split_supports output with planes = split_planes
+   * (support k at sup_split + k*sup_split_stride elements, rows ld_split), w_split =
+   * gwn_split_mlp_weights output for this layer.  The fp32 supports `sup` are not read. */
   int split_planes;
   const void* sup_split; long sup_split_stride; int ld_split;
   const void* w_split;
@@ -258,6 +268,11 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t stream);
  *   reference's gconv.l.mlp.mlp.weight) writes the pieces in the kernel's input order at
  *   dst + l*layer_stride_elems (>= gwn_split_mlp_elems(nsup, planes)).  Element type: bf16. */
 int gwn_gcn_split_supported(int c, int n, int planes); /* 1 if the split path takes (c, n, planes) */
+/* the bf16 backward's transposed mlp weights: dst[l][piece][c][c'] = bf16(w[l][c'][piece*32 + c]),
+ * at dst + l*layer_stride_elems (>= gwn_bf16_mlpT_elems(nsup)) */
+long gwn_bf16_mlpT_elems(int nsup);
+int gwn_bf16_mlpT_weights(const float* const* w, int nlayers, int nsup, void* dst, long layer_stride_elems,
+                          hipStream_t stream);
 long gwn_split_support_elems(int n, int planes);
 int gwn_split_supports(const float* const* sup, int nsup, int n, int ld_sup, int planes, void* dst,
                        long sup_stride_elems, int ld_dst, hipStream_t stream);
@@ -308,6 +323,13 @@ typedef struct gwn_gcn_bwd_args {
   /* per-sample supports, as gwn_gcn_args (sup and sup_t alike); needs the fused path and
    * adp_index = -1 (the per-sample variant's supports are inputs: no adjacency gradient) */
   long sup_bstride; int sup_batch;
+  /* operand precision of the fused backward's products (gwn_dtype): GWN_DTYPE_F32 (0) or
+   * GWN_DTYPE_BF16 (1: v_mfma_f32_32x32x16_bf16, fp32 accumulation).  bf16 needs
+   * supT_split = gwn_split_supports(sup_t, planes = 1) (support k at + k*sup_split_stride elements,
+   * rows ld_split) and wT_split = gwn_bf16_mlpT_weights output for this layer. */
+  int split_planes;
+  const void* supT_split; long sup_split_stride; int ld_split;
+  const void* wT_split;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);

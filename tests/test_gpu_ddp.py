@@ -1,0 +1,120 @@
+"""The data-parallel trainer on the GPU (bench.py --gpus N): two ranks, each a process
+with its own HIP trainer on cuda:0, joined by a gloo process group (RCCL refuses two ranks on one
+device; the product launches one rank per GPU with the "nccl" backend = RCCL over xGMI, and the
+trainer code path is the same).
+
+Each rank trains its G7 shard (B=2, N=16).  Step 1 runs eagerly; steps 2 and 3 take the captured
+path of engine.trainer._capture: graph 1 (forward, loss, backward) -> eager all-reduce of the flat
+gradient -> graph 2 (clip + Adam).  Checks: step-1 gradients = the mean of the per-shard f64
+reference gradients (g7, norm-rel <= 1e-4), step-1 parameters = clip + Adam on those mean
+gradients (norm-rel <= 1e-4; BN-cancelled biases, analytically 0, within 2 lr), and the parameters
+of both ranks bitwise equal after the captured steps."""
+import math
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT, load_golden, norm_rel, state_dict_of
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out_q):
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gwn_amd import util
+        from gwn_amd.engine import trainer
+        dev = torch.device("cuda:0")
+        g = load_golden("g7_ddp_n16.npz")
+        sups = [torch.tensor(g["sup0"], device=dev), torch.tensor(g["sup1"], device=dev)]
+        eng = trainer(util.StandardScaler(54.4, 19.5), 2, 12, 16, 16, 0.0, 1e-3, 1e-4, dev, sups, True, True,
+                      None, 4, 2)
+        eng.model.load_state_dict({k: torch.tensor(v) for k, v in state_dict_of(g).items()})
+        eng.broadcast_parameters(0)
+        x = torch.tensor(g["x"][2 * rank:2 * rank + 2], device=dev)
+        y = torch.tensor(g["y"][2 * rank:2 * rank + 2], device=dev)
+        eng.train(x, y)
+        torch.cuda.synchronize()
+        grads = {n: p.grad.detach().cpu().numpy().copy() for n, p in eng.model.named_parameters() if p.grad is not None}
+        p1 = {n: p.detach().cpu().numpy().copy() for n, p in eng.model.named_parameters()}
+        for _ in range(2):
+            eng.train(x, y)
+        torch.cuda.synchronize()
+        captured = len(eng._graphs) == 1 and list(eng._graphs.values())[0][1] is not None
+        p3 = eng.model._flat.detach().cpu().numpy().copy()
+        out_q.put((rank, grads, p1, p3, captured))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def _expected_step1(sd, gmean, lr=1e-3, wd=1e-4, clip=5.0, b1=0.9, b2=0.999, eps=1e-8):
+    """clip_grad_norm_(5) + torch.optim.Adam (step 1) on the mean gradient (engine.py:52-55)."""
+    total = math.sqrt(sum(float((v.astype(np.float64) ** 2).sum()) for v in gmean.values()))
+    coef = min(clip / (total + 1e-6), 1.0)
+    out = {}
+    for k, g in gmean.items():
+        p = sd[k].astype(np.float64)
+        gg = g * coef + wd * p
+        m = (1 - b1) * gg
+        v = (1 - b2) * gg * gg
+        out[k] = p - (lr / (1 - b1)) * m / (np.sqrt(v) / math.sqrt(1 - b2) + eps)
+    return out
+
+
+def test_gpu_ddp_two_ranks_captured_step(gpu):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, grads, p1, p3, captured = q.get(timeout=240)
+            res[r] = (grads, p1, p3, captured)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for p in procs:
+        assert p.exitcode == 0
+    g = load_golden("g7_ddp_n16.npz")
+    ref = {k[len("gradmean_f64/"):]: v for k, v in g.items() if k.startswith("gradmean_f64/")}
+    sd = state_dict_of(g)
+    exp = _expected_step1(sd, ref)
+    for r in range(world):
+        grads, p1, p3, captured = res[r]
+        assert captured, "steps 2-3 did not take the two-graph data-parallel path"
+        assert set(grads) == set(ref), sorted(set(grads) ^ set(ref))
+        for k, v in ref.items():
+            if k.endswith("mlp.bias"):
+                assert np.max(np.abs(grads[k])) <= 1e-5 * max(np.max(np.abs(x)) for x in ref.values()), k
+                assert np.max(np.abs(p1[k] - exp[k])) <= 2e-3 + 1e-6, k
+            elif np.linalg.norm(v) > 0:
+                assert norm_rel(grads[k], v) <= 1e-4, (r, k, norm_rel(grads[k], v))
+                assert norm_rel(p1[k], exp[k]) <= 1e-4, (r, k)
+        for k, v in sd.items():  # parameters without a gradient stay where they were
+            if k in p1 and k not in ref:
+                np.testing.assert_array_equal(p1[k], v, err_msg=k)
+    np.testing.assert_array_equal(res[0][1]["start_conv.weight"], res[1][1]["start_conv.weight"])
+    np.testing.assert_array_equal(res[0][2], res[1][2])
+    assert np.all(np.isfinite(res[0][2]))
