@@ -817,8 +817,10 @@ __global__ __launch_bounds__(256, 2) void gcn_bwd_fused4_kernel(const FusedBwd a
 
 // dst (padded [np][ld_dst], zero outside n x n) = src or src^T
 __global__ void pad_copy_kernel(const float* src, int n, int ld_src, float* dst, int ld_dst, int np,
-                                int transpose) {
+                                int transpose, long src_bstride = 0, long dst_bstride = 0) {
   __shared__ float tile[32][33];
+  src += blockIdx.z * src_bstride;  // batched: blockIdx.z walks the matrices
+  dst += blockIdx.z * dst_bstride;
   const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
   for (int r = ty; r < 32; r += 8) {
@@ -1008,6 +1010,17 @@ extern "C" int gwn_pad_square(const float* src, int n, int ld_src, float* dst, i
   GWN_REQUIRE(n > 0 && np >= n && ld_dst >= np, "pad_square: bad shape");
   dim3 grid((np + 31) / 32, (np + 31) / 32);
   pad_copy_kernel<<<grid, 256, 0, s>>>(src, n, ld_src, dst, ld_dst, np, transpose);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+extern "C" int gwn_pad_square_batched(const float* src, int batch, long src_bstride, int n, int ld_src, float* dst,
+                                      int np, int ld_dst, long dst_bstride, int transpose, hipStream_t s) {
+  GWN_REQUIRE(n > 0 && np >= n && ld_dst >= np && batch > 0 && batch <= 65535 && src_bstride >= (long)n * ld_src &&
+                  dst_bstride >= (long)np * ld_dst,
+              "pad_square_batched: bad shape");
+  dim3 grid((np + 31) / 32, (np + 31) / 32, batch);
+  pad_copy_kernel<<<grid, 256, 0, s>>>(src, n, ld_src, dst, ld_dst, np, transpose, src_bstride, dst_bstride);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

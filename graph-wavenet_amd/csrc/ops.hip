@@ -68,9 +68,14 @@ __device__ float block_max(float v, float* sh) {
 
 // ---------------------------------------------------------------------------------------------
 // adaptive adjacency: one block per row v.  logits l[w] = relu(sum_k e1[v][k] e2[k][w])
-__global__ void adp_fwd_kernel(const float* e1, const float* e2, int n, int d, float* adp, int ld) {
+__global__ void adp_fwd_kernel(const float* e1, const float* e2, int n, int d, float* adp, int ld,
+                               long adp_bstride = 0) {
   __shared__ float sh[256];
   const int v = blockIdx.x;
+  // batched (blockIdx.y = sample): embeddings [B][n][d] / [B][d][n], outputs adp_bstride apart
+  e1 += (long)blockIdx.y * n * d;
+  e2 += (long)blockIdx.y * d * n;
+  adp += (long)blockIdx.y * adp_bstride;
   float mx = -INFINITY;
   for (int w = threadIdx.x; w < n; w += 256) {
     float l = 0.0f;
@@ -756,6 +761,15 @@ int gwn_adaptive_adj_fwd(const float* e1, const float* e2, int n, int dd, float*
                          hipStream_t s) {
   GWN_REQUIRE(n > 0 && dd > 0 && ld >= n, "adaptive_adj_fwd: bad shape");
   adp_fwd_kernel<<<n, 256, 0, s>>>(e1, e2, n, dd, adp, ld);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_adaptive_adj_fwd_batched(const float* e1, const float* e2, int batch, int n, int dd, float* adp, int ld,
+                                 long adp_bstride, hipStream_t s) {
+  GWN_REQUIRE(n > 0 && dd > 0 && ld >= n && batch > 0 && batch <= 65535 && adp_bstride >= (long)n * ld,
+              "adaptive_adj_fwd_batched: bad shape");
+  adp_fwd_kernel<<<dim3(n, batch), 256, 0, s>>>(e1, e2, n, dd, adp, ld, adp_bstride);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

@@ -168,6 +168,10 @@ _SIGS = [
     ("gwn_fused_occupancy", c_int, [c_int, c_int]),
     ("gwn_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     ("gwn_pad_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
+    ("gwn_pad_square_batched", c_int, [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_int, c_long, c_int,
+                                       c_void_p]),
+    ("gwn_adaptive_adj_fwd_batched", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_long,
+                                             c_void_p]),
     ("gwn_batchnorm_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_u64, c_float, c_int,
                                   c_void_p, c_void_p]),

@@ -11,7 +11,7 @@ import torch
 
 from . import _lib, util
 from ._lib import ptr
-from .model import gwnet
+from .model import gwnet, gwnet_diff_G
 
 F32 = torch.float32
 _NO_CLIP = 3.0e38
@@ -88,11 +88,19 @@ class trainer():
     def __init__(self, scaler, in_dim, seq_length, num_nodes, nhid, dropout, lrate, wdecay, device, supports,
                  gcn_bool, addaptadj, aptinit, blocks, layers):
         if isinstance(supports, dict):
-            raise NotImplementedError("per-sample graphs (gwnet_diff_G, engine.py:14-25) are out of scope")
-        self.model = gwnet(device, num_nodes, dropout, supports=supports, gcn_bool=gcn_bool,
-                           addaptadj=addaptadj, aptinit=aptinit, in_dim=in_dim, out_dim=seq_length,
-                           residual_channels=nhid, dilation_channels=nhid, skip_channels=nhid * 8,
-                           end_channels=nhid * 16, blocks=blocks, layers=layers)
+            # a different graph per sample (engine.py:14-25): supports = {state: [support stacks]}
+            supports_len = len(next(iter(supports.values())))
+            if gcn_bool and addaptadj:
+                supports_len += 1
+            self.model = gwnet_diff_G(device, num_nodes, dropout, supports_len, gcn_bool=gcn_bool,
+                                      addaptadj=addaptadj, in_dim=in_dim, out_dim=seq_length,
+                                      residual_channels=nhid, dilation_channels=nhid, skip_channels=nhid * 8,
+                                      end_channels=nhid * 16, blocks=blocks, layers=layers)
+        else:
+            self.model = gwnet(device, num_nodes, dropout, supports=supports, gcn_bool=gcn_bool,
+                               addaptadj=addaptadj, aptinit=aptinit, in_dim=in_dim, out_dim=seq_length,
+                               residual_channels=nhid, dilation_channels=nhid, skip_channels=nhid * 8,
+                               end_channels=nhid * 16, blocks=blocks, layers=layers)
         self.model.to(device)
         self.optimizer = FlatAdam(self.model, lr=lrate, weight_decay=wdecay)
         self.loss = util.masked_mae
@@ -247,6 +255,8 @@ class trainer():
         """The fused step indexes real_val as [B, N, out_dim] (engine.py:47-51 broadcasts the
         prediction [B, T_f, N, out_dim] against real_val[:, None]); any other shape takes the
         autograd path, where torch's broadcasting rules (and errors) apply as in the reference."""
+        if isinstance(self.model, gwnet_diff_G):
+            return False  # its forward needs per-sample supports: the reference's train() cannot call it
         cfg = self.model.executor().cfg
         return (self.loss is util.masked_mae and input.is_cuda and input.dtype == F32 and input.dim() == 4
                 and real_val.dtype == F32 and real_val.is_cuda
@@ -292,6 +302,79 @@ class trainer():
         for p, g in self._grad_views:
             if p.grad is not g:
                 p.grad = g
+
+    # ------------------------------------------------------------------------------------------
+    # the synthetic F/E task with per-sample graphs (engine.py:60-117, 132-178)
+    def set_state(self, state):
+        assert state == 'train' or state == 'val' or state == 'test'
+        self.state = state
+
+    def _syn_forward(self, input, adj_idx):
+        input = torch.nn.functional.pad(input, (1, 0, 0, 0))
+        if adj_idx is None:
+            return self.model(input)
+        assert self.state is not None, 'set train/val/test state first'
+        supports = self.supports[self.state]
+        supports = [supports[i][adj_idx] for i in range(len(supports))]
+        aptinit = self.aptinit[self.state]
+        if aptinit is not None:
+            aptinit = aptinit[adj_idx]
+        return self.model(input, supports, aptinit)
+
+    @staticmethod
+    def _syn_pool(predict, F_t, G, adj_idx, pooltype):
+        """F: the prediction averaged over consecutive groups of F_t output steps and expanded back;
+        E: every cluster of G.assign_dict replaced by its node mean (engine.py:86-105).  The E pooling
+        writes into ``predict`` in place, as the reference does."""
+        F = None
+        if pooltype == 'avg':
+            F = predict.reshape(*predict.shape[:-1], -1, F_t).mean(-1)
+            F = F.unsqueeze(-1).repeat(*[1] * len(F.shape), F_t)
+            F = F.view(*F.shape[:-2], -1)
+            if not isinstance(G, list):
+                assign_dict = G.assign_dict
+                for k in range(len(assign_dict)):
+                    predict[:, :, assign_dict[k], :] = predict[:, :, assign_dict[k], :].mean(
+                        2, keepdim=True).repeat(1, 1, len(assign_dict[k]), 1)
+            else:
+                for sample in range(len(predict)):
+                    assign_dict = G[adj_idx[sample]].assign_dict
+                    for k in range(len(assign_dict)):
+                        predict[sample:sample + 1, :, assign_dict[k], :] = predict[sample:sample + 1, :, assign_dict[k], :].mean(
+                            2, keepdim=True).repeat(1, 1, len(assign_dict[k]), 1)
+        return F, predict
+
+    def train_syn(self, input, real, F_t, G, adj_idx=None, pooltype='avg'):
+        """engine.py:60-117: output p = 1 sequence, pooled to F (time) and E (graph clusters)."""
+        self.model.train()
+        self.optimizer.zero_grad()
+        output = self._syn_forward(input, adj_idx).transpose(1, 3)
+        predict = self.scaler.inverse_transform(output)
+        F, predict = self._syn_pool(predict, F_t, G, adj_idx, pooltype)
+        loss = self.loss(torch.cat((F, predict), 1), real, 0.0)
+        loss.backward()
+        if self.clip is not None:
+            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip)
+        self.optimizer.step()
+        mape = util.masked_mape(predict, real, 0.0).item()
+        rmse = util.masked_rmse(predict, real, 0.0).item()
+        return loss.item(), mape, rmse
+
+    def eval_syn(self, input, real, F_t, G, adj_idx=None, pooltype='avg'):
+        """engine.py:132-178: the same pooling in eval mode; also returns (F, predict)."""
+        same_G = not isinstance(G, list)
+        self.model.eval()
+        if not same_G:
+            assert adj_idx is not None, 'adj index needed.'
+        with torch.no_grad():
+            output = self._syn_forward(input, None if same_G else adj_idx)
+        output = output.transpose(1, 3)
+        predict = self.scaler.inverse_transform(output)
+        F, predict = self._syn_pool(predict, F_t, G, adj_idx, pooltype)
+        loss = self.loss(torch.cat((F, predict), 1), real, 0.0)
+        mape = util.masked_mape(predict, real, 0.0).item()
+        rmse = util.masked_rmse(predict, real, 0.0).item()
+        return loss.item(), mape, rmse, F, predict
 
     # ------------------------------------------------------------------------------------------
     # generic path for a user-supplied loss: the model is still one libgwn autograd node

@@ -78,7 +78,7 @@ class PackedLayout:
         map_grad("start_conv.weight", seg_index("start_w", (C, Cin, 1, 1)))
         gather_seg("start_b", flat_range("start_conv.bias"))
         map_grad("start_conv.bias", seg_index("start_b", (C,)))
-        if cfg.adaptive:
+        if cfg.adp_params:
             gather_seg("nv1", flat_range("nodevec1").reshape(-1))
             gather_seg("nv2", flat_range("nodevec2").reshape(-1))
             if cfg.adp_live:
@@ -186,21 +186,33 @@ class Config:
         self.E = model.end_channels
         self.O = model.out_dim
         self.L = model.blocks * model.layers
+        # gwnet: dilations 1, 2, 4, ... per block; gwnet_diff_G starts every block at 4 (model.py:291)
+        first = getattr(model, "first_dilation", 1)
         self.dilations = []
         for _ in range(model.blocks):
-            d = 1
+            d = first
             for _ in range(model.layers):
                 self.dilations.append(d)
                 d *= 2
         self.R = model.receptive_field
         self.adaptive = bool(model.gcn_bool and model.addaptadj)
-        self.use_gcn = bool(model.gcn_bool and model.supports is not None)
-        self.nfixed = len(model.supports) if (self.use_gcn and model.supports is not None) else 0
-        self.nsup = self.nfixed + (1 if (self.use_gcn and self.adaptive) else 0)
+        # per-sample graphs (gwnet_diff_G): every support, the adaptive one included, is a
+        # [B][N][N] input of the call; the adaptive embeddings are not parameters
+        self.per_sample = bool(getattr(model, "per_sample_graphs", False))
+        if self.per_sample:
+            self.use_gcn = bool(model.gcn_bool)
+            self.nsup = model.supports_len if self.use_gcn else 0
+            self.nfixed = self.nsup
+            self.adp_params = False
+        else:
+            self.use_gcn = bool(model.gcn_bool and model.supports is not None)
+            self.nfixed = len(model.supports) if (self.use_gcn and model.supports is not None) else 0
+            self.nsup = self.nfixed + (1 if (self.use_gcn and self.adaptive) else 0)
+            self.adp_params = bool(self.use_gcn and self.adaptive)  # trained nodevec1 / nodevec2
         self.W = (2 * self.nsup + 1) * self.C if self.use_gcn else self.C
         # the adaptive support reaches the output only through a gcn of a non-final layer (the
         # last layer's gcn output is dead, model.py:225-236): otherwise nodevec1/2 keep grad None
-        self.adp_live = bool(self.use_gcn and self.adaptive and self.L > 1)
+        self.adp_live = bool(self.adp_params and self.L > 1)
         self.NP = (self.N + 31) // 32 * 32  # padded support side (zero outside N x N)
         if model.residual_channels != model.dilation_channels:
             raise ValueError("gwn_amd: residual_channels must equal dilation_channels")
@@ -241,7 +253,7 @@ class Acts:
         self.skr = e(tf * P, cfg.S)
         self.e1 = e(tf * P, cfg.E)
         self.y = e(tf * P, cfg.O)
-        self.adp = torch.zeros(cfg.NP, cfg.NP, device=device, dtype=F32) if cfg.adaptive else None
+        self.adp = torch.zeros(cfg.NP, cfg.NP, device=device, dtype=F32) if cfg.adp_params else None
         self.training = training
 
 
@@ -269,8 +281,10 @@ class Executor:
         self.uidx = lay.uidx_cpu.to(device)
         self.packed = torch.zeros(lay.total, device=device, dtype=F32)
         self.gpacked = torch.zeros(lay.total, device=device, dtype=F32)
-        self.seed = torch.zeros(1, device=device, dtype=torch.int64)
-        self.seed.fill_(int(torch.randint(0, 2 ** 62, (1,)).item()))
+        # the dropout counter's start value comes from the DEVICE generator (seeded by
+        # torch.manual_seed like the CPU one): the CPU stream stays exactly the reference's, whose
+        # only CPU draws are the model init and gwnet_diff_G's per-call embeddings (model.py:324-329)
+        self.seed = torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
         self._scratch = {}
 
     # ---------------------------------------------------------------------------------------
@@ -409,16 +423,18 @@ class Executor:
 
     def supports(self, fixed, acts):
         sups = list(fixed) if self.cfg.use_gcn else []
-        if self.cfg.use_gcn and self.cfg.adaptive:
+        if self.cfg.adp_params:
             sups.append(acts.adp)
         arr = (ctypes.c_void_p * max(len(sups), 1))(*[s.data_ptr() for s in sups])
         return sups, arr
 
-    def forward(self, flat, fixed_sups, x, training, bn_bufs, acts=None, lead_pad=0, seed=None):
+    def forward(self, flat, fixed_sups, x, training, bn_bufs, acts=None, lead_pad=0, seed=None, sup_batch=1):
         """x: reference NCHW input [B, Cin, N, T] (any strides).  ``lead_pad`` extra zero steps
         are prepended (engine.py:44) before the receptive-field pad (model.py:176-178).
         ``seed``: the dropout counter this forward (and its backward) draws its masks from
         (default: the executor's own, which the trainer advances after each step).
+        ``sup_batch`` > 1: per-sample supports (gwnet_diff_G): each of ``fixed_sups`` is a padded
+        [B][NP][NP] buffer, sample b of slice (t, b) diffusing with matrix b.
         Returns (out [B, O, N, T_f], acts)."""
         cfg = self.cfg
         C, N, L = cfg.C, cfg.N, cfg.L
@@ -434,6 +450,8 @@ class Executor:
             acts = None
         if ts[-1] < 1:
             raise RuntimeError("gwnet: input too short for the receptive field")
+        if sup_batch > 1 and sup_batch != B:
+            raise RuntimeError("gwnet: per-sample supports for %d samples, input batch %d" % (sup_batch, B))
         st = _lib.stream()
         self.pack_params(flat)
         if acts is None:
@@ -444,25 +462,31 @@ class Executor:
         P = B * N
         tf = ts[-1]
         lib = _lib
-        if cfg.adaptive and cfg.use_gcn:
+        if cfg.adp_params:
             lib.call("gwn_adaptive_adj_fwd", ptr(self.pk("nv1")), ptr(self.pk("nv2")), N, 10,
                      ptr(acts.adp), cfg.NP, st)
         sups, sup_arr = self.supports(fixed_sups, acts)
         acts.sups, acts.sup_arr = sups, sup_arr
         acts.supT_arr = None
+        acts.sup_batch = sup_batch
+        sq = cfg.NP * cfg.NP
         if training and sups:
             # transposed supports: the fused backward computes A·x as (A^T)^T·x on the forward kernel path
-            if getattr(acts, "supT", None) is None or len(acts.supT) != len(sups):
-                acts.supT = [torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32) for _ in sups]
+            if getattr(acts, "supT", None) is None or len(acts.supT) != len(sups) or acts.supT[0].numel() != sq * sup_batch:
+                acts.supT = [torch.empty(sup_batch * sq, device=self.device, dtype=F32) for _ in sups]
             for s_, t_ in zip(sups, acts.supT):
-                lib.call("gwn_pad_square", ptr(s_), N, cfg.NP, ptr(t_), cfg.NP, cfg.NP, 1, st)
+                if sup_batch > 1:
+                    lib.call("gwn_pad_square_batched", ptr(s_), sup_batch, sq, N, cfg.NP, ptr(t_), cfg.NP, cfg.NP, sq,
+                             1, st)
+                else:
+                    lib.call("gwn_pad_square", ptr(s_), N, cfg.NP, ptr(t_), cfg.NP, cfg.NP, 1, st)
             acts.supT_arr = (ctypes.c_void_p * len(sups))(*[t.data_ptr() for t in acts.supT])
         sx = x.stride()
         lib.call("gwn_start_conv_fwd", ptr(x), sx[0], sx[1], sx[2], sx[3], B, cin, N, t_in, ts[0],
                  ptr(self.pk("start_w")), ptr(self.pk("start_b")), C, ptr(acts.X[0]), ptr(acts.xin), st)
         scr = self.scratch(B, ts)
         ws, bnpart = scr["ws"], scr["bnpart"]
-        planes = self.split_planes()
+        planes = self.split_planes() if sup_batch <= 1 else 0
         sp = self.split_operands(sup_arr, len(sups), planes) if planes else None
         acts.sp_bwd = (self.split_bwd_operands(acts.supT_arr, len(sups))
                        if planes == 1 and training and acts.supT_arr is not None else None)
@@ -484,7 +508,8 @@ class Executor:
                               w_mlp=ptr(self.pk("mlp_w%d" % i)), b_mlp=ptr(self.pk("mlp_b%d" % i)),
                               residual=acts.X[i].data_ptr() + 4 * d * P * C, z=ptr(acts.Z[i]),
                               seed_ptr=ptr(acts.seed), salt=i, drop_p=drop,
-                              bn_partials=ptr(bnpart) if training else None, **self.split_fields(sp, i))
+                              bn_partials=ptr(bnpart) if training else None,
+                              sup_bstride=sq if sup_batch > 1 else 0, sup_batch=sup_batch, **self.split_fields(sp, i))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
             rm, rv, mom, eps = bn_bufs[i]
@@ -528,7 +553,7 @@ class Executor:
         """The lean inference schedule needs the fused GCN path and the NT head GEMMs."""
         cfg = self.cfg
         return (os.environ.get("GWN_LEAN_EVAL", "1") != "0" and cfg.C == 32 and cfg.N <= 512
-                and cfg.nsup <= 8 and self._head_nt())
+                and cfg.nsup <= 8 and self._head_nt() and not cfg.per_sample)
 
     def _infer_bufs(self, B, ts):
         key = ("infer", B, tuple(ts))
@@ -542,7 +567,7 @@ class Executor:
         maxrows = max(ts[i + 1] for i in range(L)) * P
         b = {"x0": e(ts[0] * P, C), "xa": e(maxrows, C), "xb": e(maxrows, C), "xg": e(maxrows, C),
              "skipcat": e(tf * P, L * C), "skr": e(tf * P, cfg.S), "e1": e(tf * P, cfg.E), "y": e(tf * P, cfg.O),
-             "adp": torch.zeros(cfg.NP, cfg.NP, device=self.device, dtype=F32) if cfg.adaptive else None,
+             "adp": torch.zeros(cfg.NP, cfg.NP, device=self.device, dtype=F32) if cfg.adp_params else None,
              "metrics": e(4),
              "ws": e(_lib.load().gwn_masked_loss_workspace_floats(B, cfg.O, cfg.N, tf) + 16)}
         self._scratch[key] = b
@@ -572,7 +597,7 @@ class Executor:
         tf = ts[-1]
         bf = self._infer_bufs(B, ts)
         sups = list(fixed_sups) if cfg.use_gcn else []
-        if cfg.use_gcn and cfg.adaptive:
+        if cfg.adp_params:
             _lib.call("gwn_adaptive_adj_fwd", ptr(self.pk("nv1")), ptr(self.pk("nv2")), N, 10, ptr(bf["adp"]),
                       cfg.NP, st)
             sups.append(bf["adp"])
@@ -672,7 +697,7 @@ class Executor:
         dnext = None
         bufs = [sc["dxa"], sc["dxb"]]
         first_adp = True
-        adp_index = cfg.nsup - 1 if (cfg.use_gcn and cfg.adaptive) else -1
+        adp_index = cfg.nsup - 1 if cfg.adp_params else -1
         for i in range(L - 1, -1, -1):
             d = cfg.dilations[i]
             rows = ts[i + 1] * P
@@ -700,6 +725,9 @@ class Executor:
                                      sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
                                      if acts.supT_arr is not None else None,
                                      skip_weight_grads=1 if overlap else 0)
+                sb = getattr(acts, "sup_batch", 1)
+                if sb > 1:
+                    gb.sup_bstride, gb.sup_batch = cfg.NP * cfg.NP, sb
                 spb = getattr(acts, "sp_bwd", None)
                 if spb is not None:  # bf16 operands (fp32 accumulation) in the fused backward
                     gb.split_planes, gb.supT_split, gb.sup_split_stride = 1, spb["sup"], spb["sup_stride"]

@@ -210,6 +210,21 @@ class gcn(nn.Module):
         return torch.nn.functional.dropout(h, self.dropout, training=self.training)
 
 
+class gcn2(nn.Module):
+    """Diffusion graph convolution with per-sample supports (reference model.py:57-80): as ``gcn``
+    with ``nconv2`` ('ncvl,nvw->ncwl', one [N, N] support per sample).  Standalone it runs the libgwn
+    per-sample GEMMs; inside ``gwnet_diff_G`` the fused kernel with per-sample supports runs instead."""
+
+    def __init__(self, c_in, c_out, dropout, support_len=3, order=2):
+        super().__init__()
+        self.nconv = nconv2()
+        self.mlp = linear((order * support_len + 1) * c_in, c_out)
+        self.dropout = dropout
+        self.order = order
+
+    forward = gcn.forward
+
+
 def _require_device(*ts):
     for t in ts:
         if not (t.is_cuda and t.dtype == F32):
@@ -369,6 +384,10 @@ class gwnet(nn.Module):
             self._sup_cache = (key, padded)
         return self._sup_cache[1]
 
+    def _call_supports(self):
+        """(padded supports, sup_batch) of the forward being run: gwnet's fixed supports."""
+        return self._fixed_supports(), 1
+
     def _bn_bufs(self):
         out = []
         for m in self.bn:
@@ -386,6 +405,121 @@ class gwnet(nn.Module):
         return _GwnetFn.apply(self, input, *self.parameters())
 
 
+class gwnet_diff_G(gwnet):
+    """Graph WaveNet with a different graph per sample (reference model.py:244-407), drop-in:
+    same ctor signature, submodule tree / state_dict and RNG consumption order as the reference
+    (no node-embedding parameters; every block's dilations start at 4), and
+    ``forward(input, supports, aptinit)`` with ``supports`` a list of [B, N, N] tensors.
+
+    The reference's adaptive adjacency (model.py:324-329) draws fresh embeddings E1 [B, N, 10],
+    E2 [B, 10, N] from the CPU generator on every call -- they are not registered parameters, so
+    they are never trained and their gradient is discarded.  This is reproduced as it stands: the
+    same two ``torch.randn`` draws in the same order (bit-identical under the same seed), the
+    per-sample softmax(relu(E1_b E2_b)) on the GPU (gwn_adaptive_adj_fwd_batched), appended as the
+    last support, and no gradient through it.  ``aptinit`` must be None: the reference stops at an
+    ``ipdb.set_trace()`` there (model.py:331, "fix this").  The diffusion runs in the fused kernels
+    with per-sample supports (sup_batch = B), so it needs residual_channels = 32 and N <= 512."""
+
+    def __init__(self, device, num_nodes, dropout=0.3, supports_len=0, gcn_bool=True, addaptadj=True, in_dim=2,
+                 out_dim=12, residual_channels=32, dilation_channels=32, skip_channels=256, end_channels=512,
+                 kernel_size=2, blocks=4, layers=2):
+        nn.Module.__init__(self)
+        self.dropout = dropout
+        self.blocks = blocks
+        self.layers = layers
+        self.gcn_bool = gcn_bool
+        self.addaptadj = addaptadj
+        self.device = device
+        self.num_nodes = num_nodes
+        self.in_dim, self.out_dim = in_dim, out_dim
+        self.residual_channels, self.dilation_channels = residual_channels, dilation_channels
+        self.skip_channels, self.end_channels = skip_channels, end_channels
+        self.kernel_size = kernel_size
+        self.compute_dtype = "fp32"
+        self.supports = None
+        self.supports_len = supports_len
+        self.first_dilation = 4
+        self.per_sample_graphs = True
+        for name in ("filter_convs", "gate_convs", "residual_convs", "skip_convs", "bn", "gconv"):
+            setattr(self, name, nn.ModuleList())
+        self.start_conv = nn.Conv2d(in_channels=in_dim, out_channels=residual_channels, kernel_size=(1, 1))
+        receptive_field = 1
+        rc, dc, k = residual_channels, dilation_channels, kernel_size
+        for _ in range(blocks):
+            scope, dilation = kernel_size - 1, 4
+            for _ in range(layers):
+                self.filter_convs.append(nn.Conv2d(rc, dc, kernel_size=(1, k), dilation=dilation))
+                self.gate_convs.append(nn.Conv2d(rc, dc, kernel_size=(1, k), dilation=dilation))
+                self.residual_convs.append(nn.Conv2d(dc, rc, kernel_size=(1, 1)))
+                self.skip_convs.append(nn.Conv2d(dc, skip_channels, kernel_size=(1, 1)))
+                self.bn.append(nn.BatchNorm2d(rc))
+                dilation *= 2
+                receptive_field += scope
+                scope *= 2
+                if gcn_bool:
+                    self.gconv.append(gcn2(dc, rc, dropout, support_len=supports_len))
+        self.end_conv_1 = nn.Conv2d(skip_channels, end_channels, kernel_size=(1, 1), bias=True)
+        self.end_conv_2 = nn.Conv2d(end_channels, out_dim, kernel_size=(1, 1), bias=True)
+        self.receptive_field = receptive_field
+        self._executor = None
+        self._flat = None
+        self._flat_ptrs = None
+        self._nbt = None
+        self._sup_cache = (None, None)
+        self._call = None
+        self._place(device)
+
+    def _call_supports(self):
+        return self._call
+
+    def forward(self, input, supports, aptinit):
+        ex = self.executor()
+        B = input.shape[0]
+        N = self.num_nodes
+        sups = list(supports) if supports is not None else None
+        adp = None
+        if self.gcn_bool and self.addaptadj:
+            if sups is None:
+                sups = []
+            if aptinit is not None:
+                raise NotImplementedError("gwnet_diff_G: the reference's aptinit path stops at ipdb.set_trace() "
+                                          "(model.py:331); pass aptinit=None")
+            # model.py:324-329: two fresh CPU draws per call, in this order
+            nv1 = torch.randn(B, N, 10)
+            nv2 = torch.randn(B, 10, N)
+            adp = (nv1, nv2)
+        if not self.gcn_bool or sups is None:
+            raise NotImplementedError("gwnet_diff_G: only the graph-convolution path (gcn_bool with supports or "
+                                      "addaptadj) is built on libgwn")
+        nsup = len(sups) + (1 if adp is not None else 0)
+        if nsup != self.supports_len:
+            raise RuntimeError("gwnet_diff_G: built for %d supports, got %d" % (self.supports_len, nsup))
+        np_ = (N + 31) // 32 * 32
+        sq = np_ * np_
+        dev = self._flat.device
+        st = _lib.stream()
+        padded = []
+        for a in sups:
+            src = a.detach().to(dev, F32).contiguous()
+            if tuple(src.shape) != (B, N, N):
+                raise RuntimeError("gwnet_diff_G: supports must be [%d, %d, %d], got %s" % (B, N, N, tuple(src.shape)))
+            dst = torch.empty(B * sq, device=dev, dtype=F32)
+            _lib.call("gwn_pad_square_batched", src.data_ptr(), B, N * N, N, N, dst.data_ptr(), np_, np_, sq, 0, st)
+            padded.append(dst)
+        if adp is not None:
+            e1 = adp[0].to(dev)
+            e2 = adp[1].to(dev)
+            dst = torch.zeros(B * sq, device=dev, dtype=F32)
+            _lib.call("gwn_adaptive_adj_fwd_batched", e1.data_ptr(), e2.data_ptr(), B, N, 10, dst.data_ptr(), np_,
+                      sq, st)
+            padded.append(dst)
+        self._call = (padded, B)
+        try:
+            return _GwnetFn.apply(self, input, *self.parameters())
+        finally:
+            self._call = None
+
+
 class _GwnetFn(torch.autograd.Function):
     """The whole gwnet forward as one autograd node; its backward is libgwn's gradient schedule.
     Parameters that never reach the output (``residual_convs`` on the gcn path, the last layer's
@@ -401,7 +535,8 @@ class _GwnetFn(torch.autograd.Function):
             # backward use a snapshot of the counter, which then advances for the next forward
             seed = ex.seed.clone()
             _lib.call("gwn_increment_u64", _lib.ptr(ex.seed), 1, _lib.stream())
-        out, acts = ex.forward(model._flat, model._fixed_supports(), x, training, model._bn_bufs(), seed=seed)
+        sups, sup_batch = model._call_supports()
+        out, acts = ex.forward(model._flat, sups, x, training, model._bn_bufs(), seed=seed, sup_batch=sup_batch)
         if training:
             model._nbt.add_(1)
         ctx.model = model

@@ -137,6 +137,12 @@ int gwn_adaptive_adj_fwd(const float* e1, const float* e2, int n, int d, float* 
 int gwn_adaptive_adj_bwd(const float* e1, const float* e2, const float* adp, const float* dadp,
                          int n, int d, int ld_adp, float* de1, float* de2, float* workspace,
                          hipStream_t stream);
+/* per-sample adaptive adjacencies of gwnet_diff_G (model.py:342-344: softmax(relu(E1_b @ E2_b),
+ * dim=2) with E1 [batch][n][d], E2 [batch][d][n]); sample b written at adp + b*adp_bstride as
+ * [n][ld_adp] (columns >= n zero).  Forward only: the reference draws these embeddings afresh
+ * per call (model.py:324-329) and never trains them. */
+int gwn_adaptive_adj_fwd_batched(const float* e1, const float* e2, int batch, int n, int d, float* adp,
+                                 int ld_adp, long adp_bstride, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Input padding + start_conv (model.py:176-181): x is the reference NCHW input [B][cin][n][t]
@@ -379,6 +385,10 @@ int gwn_fused_occupancy(int n, int backward);
 /* dst [np][ld_dst] = src (or src^T if transpose) inside [n][n], zero elsewhere (np >= n) */
 int gwn_pad_square(const float* src, int n, int ld_src, float* dst, int np, int ld_dst, int transpose,
                    hipStream_t stream);
+/* the same for `batch` matrices src + b*src_bstride -> dst + b*dst_bstride (per-sample supports of
+ * gwnet_diff_G, model.py:244-407) */
+int gwn_pad_square_batched(const float* src, int batch, long src_bstride, int n, int ld_src, float* dst, int np,
+                           int ld_dst, long dst_bstride, int transpose, hipStream_t stream);
 
 /* BN backward fused with the residual split and the dropout backward of the same layer:
  *   batch_stats != 0 (train-mode forward):  dz = gamma*rstd*(dy - mean(dy) - xhat*mean(dy*xhat))

@@ -48,6 +48,14 @@ def _install_shims():
         return orig(self, input, weight, bias)
 
     nn.Conv1d._conv_forward = _conv_forward
+    # The reference's Utils/ has no __init__.py (a namespace package), and a regular package of
+    # the same name anywhere on sys.path wins over it -- graph-wavenet_amd/Utils (the drop-in shim)
+    # would be imported as "the reference's" util.  Drop this repo's package dir from the path
+    # (gwn_amd.synthetic is already imported) and any cached Utils, then put the reference first.
+    pkg = os.path.normpath(os.path.join(HERE, "..", "..", "graph-wavenet_amd"))
+    sys.path[:] = [p for p in sys.path if os.path.normpath(os.path.abspath(p or ".")) != pkg]
+    for name in [m for m in sys.modules if m == "Utils" or m.startswith("Utils.") or m in ("model", "engine")]:
+        del sys.modules[name]
     sys.path.insert(0, REF)
 
 
@@ -94,6 +102,8 @@ def main():
     import model as ref_model  # /root/reference/model.py
     import engine as ref_engine  # /root/reference/engine.py
     import Utils.util as util  # /root/reference/Utils/util.py
+    for mod in (ref_model, ref_engine, util):
+        assert os.path.abspath(mod.__file__).startswith(REF + "/"), mod.__file__
 
     torch.set_num_threads(8)
     N = 207

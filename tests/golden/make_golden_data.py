@@ -37,6 +37,8 @@ def main():
     import torch
     import generate_training_data as gtd  # noqa: E402  (the reference module)
     from Utils import util  # noqa: E402
+    for mod in (gtd, util):
+        assert os.path.abspath(mod.__file__).startswith(REF + "/"), mod.__file__
 
     g = {}
     df = frame()

@@ -96,3 +96,24 @@ def test_gcn_module_train_mode_dropout(gpu):
     kept = y != 0
     np.testing.assert_allclose(y[kept].detach().cpu().numpy(), (ye[kept] / 0.7).detach().cpu().numpy(),
                                rtol=1e-5, atol=1e-6)
+
+
+def test_gcn2_module_vs_reference(gpu):
+    """gcn2 (model.py:57-80, per-sample supports) standalone on libgwn against the reference's own
+    outputs and f64 gradients (g9: B=3, C=4, N=37, T=5, two supports, order 2, eval mode)."""
+    from gwn_amd.model import gcn2
+    g = load_golden("g9_nconv2_n37.npz")
+    m = gcn2(4, g["gcn2/w"].shape[0], 0.0, support_len=2).to(gpu)
+    with torch.no_grad():
+        m.mlp.mlp.weight.copy_(torch.tensor(g["gcn2/w"]).reshape(m.mlp.mlp.weight.shape))
+        m.mlp.mlp.bias.copy_(torch.tensor(g["gcn2/b"]))
+    m.eval()
+    x = torch.tensor(g["x"], device=gpu, dtype=torch.float32, requires_grad=True)
+    sups = [torch.tensor(g["gcn2/s0"], device=gpu, dtype=torch.float32),
+            torch.tensor(g["gcn2/s1"], device=gpu, dtype=torch.float32)]
+    h = m(x, sups)
+    assert rel_err(h.detach().cpu().numpy(), g["gcn2/h"]) <= 1e-4
+    h.backward(torch.tensor(g["gcn2/gh"], device=gpu, dtype=torch.float32))
+    assert norm_rel(x.grad.cpu().numpy(), g["gcn2/dx"]) <= 1e-4
+    assert norm_rel(m.mlp.mlp.weight.grad.cpu().numpy().reshape(g["gcn2/dw"].shape), g["gcn2/dw"]) <= 1e-4
+    assert norm_rel(m.mlp.mlp.bias.grad.cpu().numpy(), g["gcn2/db"]) <= 1e-4
