@@ -206,17 +206,20 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
                 "mfma_tflops": round(achieved, 3), "mfma_peak_bf16": BF16_PEAK_TFLOPS,
                 "avg_launch_us": round(avg_us, 3), "flop_per_launch_avg": round(total_flop / count, 1),
                 "algorithmic_bytes_per_launch": round(total_bytes / count), "launches_timed": count}
-    # HBM bytes per launch from the committed PMC passes of this kernel (tools/pmc_dominant.py:
-    # separate FETCH_SIZE / WRITE_SIZE rocprofv3 runs of this bench, gfx950 FETCH correction)
-    traffic, pmc = None, os.path.join(ROOT, "profiles", "r01", "pmc_gcn_fwd_fused.json")
+    # HBM bytes per launch and MFMA busy fraction from the committed PMC passes of this kernel over
+    # this bench (tools/pmc.sh + tools/pmc_summary.py: separate --pmc runs for FETCH_SIZE,
+    # WRITE_SIZE and the SQ counters; FETCH x2 per the gfx950 correction)
+    traffic, mfma_busy, pmc = None, None, os.path.join(ROOT, "profiles", "r02", "pmc_bench_metr.json")
     if fused and N == 207 and os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get("traffic_bytes_per_launch")
+            rec = json.load(f).get("gcn_fwd_fused_kernel", {})
+        traffic, mfma_busy = rec.get("hbm_bytes_per_dispatch"), rec.get("mfma_busy_frac")
     return {"kernel": ("gcn_fwd_fused_kernel<512, true> (fused diffusion GCN forward, 8 launches/step)" if fused
                        else "gwn_gcn_fwd large-graph schedule (batched diffusion GEMMs + mlp, 8 calls/step)"),
             "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-            "traffic_source": "profiles/r01/pmc_gcn_fwd_fused.json" if traffic else None,
+            "traffic_source": "profiles/r02/pmc_bench_metr.json" if traffic else None,
+            "pmc_mfma_busy_frac": mfma_busy,
             "avg_launch_us": round(avg_us, 3), "flop_per_launch_avg": round(total_flop / count, 1),
             "algorithmic_bytes_per_launch": round(total_bytes / count),
             "launches_timed": count}

@@ -11,7 +11,7 @@ ARGS=("$@")
 declare -A GROUPS_
 GROUPS_[fetch]="FETCH_SIZE"
 GROUPS_[write]="WRITE_SIZE"
-GROUPS_[sq]="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_LDS"
+GROUPS_[sq]="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_LDS GRBM_GUI_ACTIVE"
 GROUPS_[lds]="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_VALU SQ_ACTIVE_INST_MFMA"
 GROUPS_[l2]="TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum"
 for p in ${PASSES:-fetch write sq lds}; do
