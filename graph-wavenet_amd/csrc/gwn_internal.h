@@ -54,6 +54,12 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
 int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT, float* dxg, long ld_dxg,
                              float* t1, float* t2, long ld_t, hipStream_t s);
 
+// Large-graph diffusion (bigdiff.hip): y_s = G^T x_s (+ y0) over all slices, n > 512, c = 32
+bool gwn_bigdiff_eligible(int n, int c, const float* G, int ldg, const float* x, long ldx, const float* y, long ldy,
+                          const float* y0, long ldy0);
+int gwn_bigdiff(const float* G, int ldg, const float* x, long ldx, float* y, long ldy, const float* y0, long ldy0,
+                int n, int slices, hipStream_t s);
+
 // Weight-stationary row GEMMs of the gated TCN (rowgemm.hip), c = 32
 int gwn_rowgemm_tcn_fwd(const gwn_tcn_args* a, hipStream_t s);
 int gwn_rowgemm_tcn_bwd_data(const gwn_tcn_bwd_args* a, hipStream_t s);

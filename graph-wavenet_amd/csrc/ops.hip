@@ -688,6 +688,8 @@ long gwn_gemm_workspace_floats(int M, int N, int ksplit) {
 int gwn_nconv(const float* A, int lda, int transpose_a, const float* x, long ldx, float* y, long ldy,
               const float* y0, long ldy0, int n, int c, int slices, hipStream_t s) {
   GWN_REQUIRE(n > 0 && c > 0 && slices > 0, "nconv: bad shape");
+  if (transpose_a && gwn_bigdiff_eligible(n, c, A, lda, x, ldx, y, ldy, y0, ldy0))
+    return gwn_bigdiff(A, lda, x, ldx, y, ldy, y0, ldy0, n, slices, s);  // n > 512: large-graph kernel
   gwn_gemm_desc d = gemm_zero();
   d.A = A;
   if (transpose_a) { d.lda_m = 1; d.lda_k = lda; } else { d.lda_m = lda; d.lda_k = 1; }
@@ -1009,12 +1011,15 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   d.M = a->rows; d.N = width; d.K = c;
   rc = gwn_gemm_launch(d, s);
   if (rc) return rc;
+  // A x = (A^T)^T x: with the transposed supports the products run on the transpose_a = 1 kernels
+  // (the large-graph diffusion for n > 512)
+  const float* const* sa = a->sup_t ? a->sup_t : a->sup;
+  const int ta = a->sup_t ? 1 : 0;
   for (int k = 0; k < a->nsup; ++k) {
     float* t1 = a->dhcat + (1 + 2 * k) * c;        // dL/dx1 (gets the x2 path added)
     const float* t2 = a->dhcat + (2 + 2 * k) * c;  // dL/dx2
     // x2 = A^T x1  =>  dx1 += A dx2
-    rc = gwn_nconv(a->sup[k], a->ld_sup, 0, t2, a->ld_dhcat, t1, a->ld_dhcat, t1, a->ld_dhcat, n, c,
-                   slices, s);
+    rc = gwn_nconv(sa[k], a->ld_sup, ta, t2, a->ld_dhcat, t1, a->ld_dhcat, t1, a->ld_dhcat, n, c, slices, s);
     if (rc) return rc;
     if (wgrads && k == a->adp_index && a->dadp) {
       // dA = sum xg (x) dx1  +  sum x1 (x) dx2
@@ -1026,8 +1031,8 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
       if (rc) return rc;
     }
     // x1 = A^T xg  =>  dxg += A dx1   (dxg is piece 0 of dhcat)
-    rc = gwn_nconv(a->sup[k], a->ld_sup, 0, t1, a->ld_dhcat, a->dhcat, a->ld_dhcat, a->dhcat,
-                   a->ld_dhcat, n, c, slices, s);
+    rc = gwn_nconv(sa[k], a->ld_sup, ta, t1, a->ld_dhcat, a->dhcat, a->ld_dhcat, a->dhcat, a->ld_dhcat, n, c,
+                   slices, s);
     if (rc) return rc;
   }
   return GWN_OK;
