@@ -75,6 +75,10 @@ __device__ __forceinline__ const float* slice_sup(const Args& a, const float* ba
 
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
+// bf16 kernels: support batches prefetched ahead of their MFMAs (whole hop up to this many)
+#ifndef GWN_BF16_PD
+#define GWN_BF16_PD 11
+#endif
 #ifndef GWN_EXP
 // kernel experiments (timing only; 1-16 give wrong results): 1 no G loads, 2 no LDS A reads,
 // 4 no W loads, 16 no phase barriers (forward); 32 = forward hop pieces stored straight from the
@@ -1437,7 +1441,9 @@ __global__ __launch_bounds__(64 * NKB) void gcn_bwd_bf16_kernel(const FusedBwd a
 template <int NKB>
 void launch_bf16_bwd(const FusedBwd& a, const gwn_gcn_bwd_args* g, int slices, hipStream_t s) {
   constexpr int NP = NKB * 32;
-  constexpr int PD = NKB > 1 ? 2 : 1;
+  // whole-hop prefetch where a workgroup holds a CU on its own anyway (9+ node tiles); below that
+  // its extra registers would cost the second co-resident workgroup (N=207: 144 vs 104 VGPRs)
+  constexpr int PD = NKB >= 9 ? (NKB < GWN_BF16_PD ? NKB : GWN_BF16_PD) : (NKB > 1 ? 2 : 1);
   const size_t lds = (size_t)cmax(NP * LDR * 4, NP * DHB + 32 * split_row_bytes(NP));
   static bool attr_set = false;
   if (!attr_set) {
@@ -1472,9 +1478,12 @@ bool gwn_gcn_split_eligible(int c, int n, int planes) {
 }
 
 // bf16 operands (planes = 1): one instantiation per node-tile count
+// The whole hop's support fragments (NKB batches x 32 B per lane) are issued one phase ahead of
+// the hop: with bf16 operands a batch is 2 MFMAs (64 cycles), far shorter than an L2 round trip,
+// so a short prefetch distance leaves every batch waiting on its loads
 template <int NKB>
 void launch_bf16_fwd(const FusedFwd& a, const gwn_gcn_args* g, int slices, hipStream_t s) {
-  launch_split<NKB, 1, (NKB > 1 ? 2 : 1)>(a, g, slices, s);
+  launch_split<NKB, 1, (NKB < GWN_BF16_PD ? NKB : GWN_BF16_PD)>(a, g, slices, s);
 }
 
 int gwn_gcn_split_fwd_launch(const gwn_gcn_args* g, const FusedFwd& a, hipStream_t s) {

@@ -40,7 +40,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long by
 }
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
-template <int NP>
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ bf16x8 to_bf16x8(const float4& a, const float4& b) {
+  bf16x8 r;
+  r[0] = (__bf16)a.x; r[1] = (__bf16)a.y; r[2] = (__bf16)a.z; r[3] = (__bf16)a.w;
+  r[4] = (__bf16)b.x; r[5] = (__bf16)b.y; r[6] = (__bf16)b.z; r[7] = (__bf16)b.w;
+  return r;
+}
+
+// BF16: the same loads, each lane's 16 channels (16h .. 16h+15) as two bf16x8 K-groups of
+// v_mfma_f32_32x32x16_bf16 (K permuted alike on both operands: group s of half h = channels
+// 16h + 8s .. +7), 2 MFMAs per tile and slice instead of 16 (the bf16 mode's adaptive-support
+// gradient; fp32 accumulation)
+template <int NP, bool BF16 = false>
 __global__ __launch_bounds__(64) void gram_kernel(const Gram g) {
   const int lane = threadIdx.x, half = lane >> 5, col = lane & 31;
   const int ntp = (g.nt + 1) / 2;  // column tile pairs
@@ -93,16 +106,25 @@ __global__ __launch_bounds__(64) void gram_kernel(const Gram g) {
       if (p + 1 < NP) load(s, p + 1, na, nb);
       else load(s + 1, 0, na, nb);
       __builtin_amdgcn_sched_barrier(0);
+      if (BF16) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[q].x, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[4 + q].x, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, fb[q].y, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, fb[4 + q].y, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, fb[q].z, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, fb[4 + q].z, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, fb[q].w, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, fb[4 + q].w, acc1, 0, 0, 0);
+        for (int sg = 0; sg < 2; ++sg) {
+          const bf16x8 av = to_bf16x8(fa[2 * sg], fa[2 * sg + 1]);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, to_bf16x8(fb[2 * sg], fb[2 * sg + 1]), acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, to_bf16x8(fb[4 + 2 * sg], fb[5 + 2 * sg]), acc1, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[q].x, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].x, fb[4 + q].x, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, fb[q].y, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].y, fb[4 + q].y, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, fb[q].z, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].z, fb[4 + q].z, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, fb[q].w, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q].w, fb[4 + q].w, acc1, 0, 0, 0);
+        }
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -175,6 +197,11 @@ long gwn_gram_workspace_floats(int n, int slices) {
 // dA (+)= sum over slices of X1^T T1 (+ X2^T T2); c = 32 channels per slice row
 int gwn_gram(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
              int slices, float* dA, int ld_dA, int accumulate, float* ws, hipStream_t s) {
+  return gwn_gram_dtype(x1, t1, x2, t2, ldx, ldt, n, slices, dA, ld_dA, accumulate, ws, 0, s);
+}
+
+int gwn_gram_dtype(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
+                   int slices, float* dA, int ld_dA, int accumulate, float* ws, int bf16, hipStream_t s) {
   GWN_REQUIRE(n > 0 && slices > 0 && x1 && t1 && ws, "gram: bad arguments");
   GWN_REQUIRE(((uintptr_t)x1 & 15) == 0 && ((uintptr_t)t1 & 15) == 0 && (ldx & 3) == 0 && (ldt & 3) == 0 &&
                   (!x2 || (((uintptr_t)x2 & 15) == 0 && ((uintptr_t)t2 & 15) == 0)),
@@ -199,8 +226,13 @@ int gwn_gram(const float* x1, const float* t1, const float* x2, const float* t2,
   }
   const int per_split = g.nt * ((g.nt + 1) / 2);
   const int blocks = ((g.nsplit + NXCD - 1) / NXCD) * NXCD * per_split;
-  if (g.npairs == 2) gram_kernel<2><<<blocks, 64, 0, s>>>(g);
-  else gram_kernel<1><<<blocks, 64, 0, s>>>(g);
+  if (bf16) {
+    if (g.npairs == 2) gram_kernel<2, true><<<blocks, 64, 0, s>>>(g);
+    else gram_kernel<1, true><<<blocks, 64, 0, s>>>(g);
+  } else {
+    if (g.npairs == 2) gram_kernel<2><<<blocks, 64, 0, s>>>(g);
+    else gram_kernel<1><<<blocks, 64, 0, s>>>(g);
+  }
   GWN_CHECK_LAUNCH();
   const long outs = (long)n * n;
   gram_reduce_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(ws, g.nsplit, n, 32 * g.nt, dA, ld_dA,

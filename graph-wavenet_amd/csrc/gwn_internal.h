@@ -60,6 +60,10 @@ bool gwn_bigdiff_eligible(int n, int c, const float* G, int ldg, const float* x,
 int gwn_bigdiff(const float* G, int ldg, const float* x, long ldx, float* y, long ldy, const float* y0, long ldy0,
                 int n, int slices, hipStream_t s);
 
+// gwn_gram with the operand precision of the bf16 mode (bf16 != 0: bf16 MFMA operands, fp32 sums)
+int gwn_gram_dtype(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
+                   int slices, float* dA, int ld_dA, int accumulate, float* ws, int bf16, hipStream_t s);
+
 // Weight-stationary row GEMMs of the gated TCN (rowgemm.hip), c = 32
 int gwn_rowgemm_tcn_fwd(const gwn_tcn_args* a, hipStream_t s);
 int gwn_rowgemm_tcn_bwd_data(const gwn_tcn_bwd_args* a, hipStream_t s);

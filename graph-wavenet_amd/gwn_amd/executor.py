@@ -490,6 +490,14 @@ class Executor:
         sp = self.split_operands(sup_arr, len(sups), planes) if planes else None
         acts.sp_bwd = (self.split_bwd_operands(acts.supT_arr, len(sups))
                        if planes == 1 and training and acts.supT_arr is not None else None)
+        # the last layer's gcn + bn only update bn[L-1]'s running statistics (their output is dead,
+        # model.py:225-236): GWN_TAIL_OVERLAP=1 runs them on a second stream beside the head GEMMs
+        # (the head needs only the skip sum), joined before the forward returns.  Off by default:
+        # measured 17,843 vs 17,854 samples/s (round 2) -- the head GEMMs already fill the chip
+        tail_side = (training and L > 1 and os.environ.get("GWN_TAIL_OVERLAP", "0") != "0"
+                     and torch.cuda.is_available() and x.is_cuda)
+        main = torch.cuda.current_stream() if tail_side else None
+        tail_done = None
         for i in range(L):
             d = cfg.dilations[i]
             rows = ts[i + 1] * P
@@ -501,6 +509,15 @@ class Executor:
             lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), st)
             if i == L - 1 and not training:
                 continue  # the last gcn / bn output is dead in eval (only skip reaches the output)
+            side_ctx = None
+            if tail_side and i == L - 1:
+                side = self._side_stream()
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+                side_ctx = torch.cuda.stream(side)
+                side_ctx.__enter__()
+                st = _lib.stream()
             drop = float(self.dropout) if (training and cfg.use_gcn) else 0.0
             ga = _lib.GcnArgs(rows=rows, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
                               sup=ctypes.cast(sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=cfg.NP,
@@ -521,10 +538,17 @@ class Executor:
                 lib.call("gwn_batchnorm_fwd", ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
                          ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps, 0,
                          ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(ws), st)
+            if side_ctx is not None:
+                tail_done = torch.cuda.Event()
+                tail_done.record(torch.cuda.current_stream())
+                side_ctx.__exit__(None, None, None)
+                st = _lib.stream()
         rows_f = tf * P
         self._head_fwd(acts.skipcat, acts.skr, acts.e1, acts.y, rows_f, ws)
         out = torch.empty(B, cfg.O, N, tf, device=self.device, dtype=F32)
         lib.call("gwn_to_nchw", ptr(acts.y), B, cfg.O, N, tf, ptr(out), st)
+        if tail_done is not None:
+            main.wait_event(tail_done)
         return out, acts
 
     def _head_fwd(self, skipcat, skr, e1, y, rows_f, ws):
