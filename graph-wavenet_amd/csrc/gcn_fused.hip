@@ -266,10 +266,18 @@ __device__ __forceinline__ void acc_to_global(float* dst, long ld, const f32x16&
   }
 }
 
+// LDS image index of (row w, channel c): padded rows [np][LDR], or (PL, the balanced layout)
+// channel-half planes [2][np][16]
+template <bool PL>
+__device__ __forceinline__ int img_idx(int w, int c, int np) {
+  return PL ? ((c >> 4) * np + w) * 16 + (c & 15) : w * LDR + c;
+}
+
+template <bool PL = false>
 __device__ __forceinline__ void global_to_lds(const float* src, long ld, int n, int np, float* buf) {
   for (int e = threadIdx.x; e < np * CH; e += blockDim.x) {
     const int w = e >> 5, c = e & 31;
-    buf[w * LDR + c] = (w < n) ? src[(long)w * ld + c] : 0.0f;
+    buf[img_idx<PL>(w, c, np)] = (w < n) ? src[(long)w * ld + c] : 0.0f;
   }
 }
 
@@ -358,10 +366,10 @@ __device__ __forceinline__ void fwd_epilogue(const FusedFwd& a, float* ys, float
 // backward prologue: dh of the slice into LDS (rows >= n zero), either loaded or computed by the
 // BatchNorm backward of this layer's output (same arithmetic as bn_bwd_apply_kernel, ops.hip):
 //   dz = gamma*rstd*(dy - k1 - xhat*k2) -> residual gradient dres; dropout'(dz) -> dh (LDS + HBM)
-template <int NEPT>
+template <int NEPT, bool PL = false>
 __device__ __forceinline__ void bwd_prologue(const FusedBwd& a, float* dhs, long row0, int n, int np) {
   if (!a.bn_dy) {
-    global_to_lds(a.dh + row0 * CH, CH, n, np, dhs);
+    global_to_lds<PL>(a.dh + row0 * CH, CH, n, np, dhs);
     return;
   }
   if (blockIdx.x == 0 && threadIdx.x < CH) {
@@ -396,7 +404,7 @@ __device__ __forceinline__ void bwd_prologue(const FusedBwd& a, float* dhs, long
       }
       a.dh_out[idx] = v;
     }
-    if (w < np) dhs[w * LDR + c] = v;
+    if (w < np) dhs[img_idx<PL>(w, c, np)] = v;
   }
 }
 
@@ -819,6 +827,274 @@ __global__ __launch_bounds__(256, 2) void gcn_bwd_fused4_kernel(const FusedBwd a
   bwd_gate_epilogue<EPT4>(a, buf, row0, n);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Balanced layout (v_mfma_f32_16x16x4_f32), n <= 256: four waves, one per SIMD, equal work.
+//
+// The 32x32 tile-wave layout lands 7 node tiles (n = 207) on the 4 SIMDs as 2,2,2,1, so the busiest
+// SIMD carries 2/7 of the slice instead of 1/4, and a lone workgroup (the last round of a layer,
+// or the small T = 1 layers) leaves three SIMDs mostly idle.  Here every product D'[c][w] of the
+// slice is cut in four equal quarters: wave (hc, hw) owns channels 16hc..16hc+15 of the 16*NKB
+// nodes from hw*16*NKB (NKB 16x16 tiles; np = 32*NKB).  The costs: a support fragment feeds one
+// channel half (each G element is loaded twice per slice, ~32 B/clk/CU of L2 at full MFMA rate),
+// and the forward mlp's contraction over channels is split between the two channel-half waves,
+// whose partial outputs are summed once per slice, in a fixed order, before the epilogue.
+// LDS images are channel-half planes [2][np][16] (img_idx<true>): the A fragment of a k-step
+// (4 rows x 16 channels) is 256 contiguous bytes, and an accumulator tile (4 consecutive channels
+// of 16 rows per lane group) is written back as one ds_write_b128 per lane.
+//
+// 16x16x4 f32 operand layout (lane l = 16 g + i, i = l & 15, g = l >> 4):
+//   A[m = i][k = g], B[k = g][n = i], D register r: D[m = 4 g + r][n = i].
+// The mlp contracts over channels straight from the accumulator: k-slot g of MFMA step j is channel
+// 4g + j of the half (register j of the accumulator), with the weights indexed to match.
+//
+// Measured (tools/bench_gcn.py, n = 207, round 2): 5 % slower than the tile-wave layout at T = 12
+// and 11-27 % slower at T = 7 / T = 1 (forward and backward), although its busiest SIMD carries
+// 13 % fewer MFMA cycles.  Each 32-cycle 16x16x4 MFMA needs a 4-row x 64-B support fragment (four
+// cache lines) where the 64-cycle 32x32x2 needs two: four times the L1 line rate per MFMA cycle,
+// and a single wave per SIMD when one workgroup per CU is left.  Selectable (layout 3), never
+// auto-selected; parity-tested with the other layouts.
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 zero4() {
+  f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+  return z;
+}
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// acc[t][c][w] += sum_v img[v][c] * G[v][w] over the wave's quarter, v < 16 * nb16
+template <int NKB>
+__device__ __forceinline__ void bal_diffuse(const float* img, const float* G, int ld, int np, int nb16, int hc,
+                                            int hw, int lane, f32x4 (&acc)[NKB]) {
+  const int g = lane >> 4, i = lane & 15;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, np * ld * 4, 0x00020000);
+  const int voff = (g * ld + hw * 16 * NKB + i) * 4;
+  const float* ap = img + (hc * np + g) * 16 + i;
+  // batch b = nodes 16b..16b+15 = 4 k-steps; two register sets, batch b+1 loads issued before
+  // batch b's MFMAs (a third set, two batches ahead, measured 25 % slower: register pressure)
+  float ga[4][NKB], gb[4][NKB];
+  auto gload = [&](int b, float (&gr)[4][NKB]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < NKB; ++t) gr[j][t] = bload(rs, voff + 64 * t, (16 * b + 4 * j) * ld * 4);
+  };
+  auto step = [&](int b, float (&gr)[4][NKB]) {
+    float av[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) av[j] = ap[(16 * b + 4 * j) * 16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < NKB; ++t) acc[t] = mfma4(av[j], gr[j][t], acc[t]);
+  };
+  gload(0, ga);
+  int b = 0;
+  for (; b + 2 < nb16; b += 2) {
+    gload(b + 1, gb);
+    step(b, ga);
+    gload(b + 2, ga);
+    step(b + 1, gb);
+  }
+  if (b + 1 < nb16) {
+    gload(b + 1, gb);
+    step(b, ga);
+    step(b + 1, gb);
+  } else {
+    step(b, ga);
+  }
+}
+
+// hacc[hp][t][c'][w] += sum_{c in half hc} W[16hp + c'][off + c] * d[t][c][w]
+template <int NKB>
+__device__ __forceinline__ void bal_mlp(const float* W, int ld_w, int off, int hc, int lane, const f32x4 (&d)[NKB],
+                                        f32x4 (&hacc)[2][NKB]) {
+  const int g = lane >> 4, i = lane & 15;
+  float wf[2][4];
+#pragma unroll
+  for (int hp = 0; hp < 2; ++hp)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wf[hp][j] = W[(long)(16 * hp + i) * ld_w + off + 16 * hc + 4 * g + j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int hp = 0; hp < 2; ++hp)
+#pragma unroll
+      for (int t = 0; t < NKB; ++t) hacc[hp][t] = mfma4(wf[hp][j], d[t][j], hacc[hp][t]);
+}
+
+// acc[t][c][w] += sum_{c'} W[c'][off + c] * dimg[w][c']     (dP = W^T dh, dimg in planes)
+template <int NKB>
+__device__ __forceinline__ void bal_mlpT(const float* W, int ld_w, int off, const float* dimg, int np, int hc, int hw,
+                                         int lane, f32x4 (&acc)[NKB]) {
+  const int g = lane >> 4, i = lane & 15;
+  float wa[2][4];
+#pragma unroll
+  for (int hp = 0; hp < 2; ++hp)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wa[hp][j] = W[(long)(16 * hp + 4 * g + j) * ld_w + off + 16 * hc + i];
+#pragma unroll
+  for (int hp = 0; hp < 2; ++hp) {
+    f32x4 bv[NKB];
+#pragma unroll
+    for (int t = 0; t < NKB; ++t) bv[t] = *(const f32x4*)(dimg + (hp * np + 16 * (hw * NKB + t) + i) * 16 + 4 * g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < NKB; ++t) acc[t] = mfma4(wa[hp][j], bv[t][j], acc[t]);
+  }
+}
+
+// the wave's quarter of D'[c][w] into a plane image / into rows w < n of dst (16-B aligned rows)
+template <int NKB>
+__device__ __forceinline__ void bal_to_img(float* img, const f32x4 (&d)[NKB], int np, int hc, int hw, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+  for (int t = 0; t < NKB; ++t) *(f32x4*)(img + (hc * np + 16 * (hw * NKB + t) + i) * 16 + 4 * g) = d[t];
+}
+
+template <int NKB, bool NT>
+__device__ __forceinline__ void bal_to_global(float* dst, long ld, const f32x4 (&d)[NKB], int hc, int hw, int lane,
+                                              int n) {
+  const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+  for (int t = 0; t < NKB; ++t) {
+    const int w = 16 * (hw * NKB + t) + i;
+    if (w < n) {
+      f32x4* p = (f32x4*)(dst + (long)w * ld + 16 * hc + 4 * g);
+      if (NT) __builtin_nontemporal_store(d[t], p);
+      else *p = d[t];
+    }
+  }
+}
+
+// the wave's quarter of D'[c][w] (c in half hc, or c' = 16hp + ... for the mlp halves) into padded
+// rows S[w][LDR]; ADD: S = d + S
+template <int NKB, bool ADD>
+__device__ __forceinline__ void bal_to_rows(float* S, const f32x4 (&d)[NKB], int c0, int hw, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+  for (int t = 0; t < NKB; ++t) {
+    float* p = S + (16 * (hw * NKB + t) + i) * LDR + c0 + 4 * g;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[r] = ADD ? d[t][r] + p[r] : d[t][r];
+  }
+}
+
+template <int NKB>
+__device__ __forceinline__ void bal_zero(f32x4 (&d)[NKB]) {
+#pragma unroll
+  for (int t = 0; t < NKB; ++t) d[t] = zero4();
+}
+
+template <int NKB>
+__global__ __launch_bounds__(256, 2) void gcn_fwd_bal_kernel(const FusedFwd a) {
+  extern __shared__ float lds[];
+  __shared__ float red[2][256];
+  constexpr int np = 32 * NKB;
+  const int n = a.n, nb16 = (n + 15) >> 4;
+  float* xs = lds;            // x (piece 0), planes
+  float* ys = lds + np * CH;  // hop-1 output, planes
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hc = wave & 1, hw = wave >> 1;
+  const long row0 = (long)blockIdx.x * n;
+  float* hs = (float*)a.h + row0 * a.ld_h;
+  for (int e = threadIdx.x; e < np * 8; e += 256) {  // x rows as float4s, rows >= n zero
+    const int w = e >> 3, q = e & 7;
+    f32x4 v = zero4();
+    if (w < n) v = *(const f32x4*)(hs + (long)w * a.ld_h + 4 * q);
+    *(f32x4*)(xs + ((q >> 2) * np + w) * 16 + 4 * (q & 3)) = v;
+  }
+  __syncthreads();
+  f32x4 hacc[2][NKB];
+  bal_zero(hacc[0]);
+  bal_zero(hacc[1]);
+  {
+    f32x4 x[NKB];
+    const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+    for (int t = 0; t < NKB; ++t) x[t] = *(const f32x4*)(xs + (hc * np + 16 * (hw * NKB + t) + i) * 16 + 4 * g);
+    bal_mlp(a.w_mlp, a.ld_w, 0, hc, lane, x, hacc);
+  }
+  for (int k = 0; k < a.nsup; ++k) {
+    const float* G = slice_sup(a, a.sup[k]);
+    f32x4 d[NKB];
+    bal_zero(d);
+    bal_diffuse(xs, G, a.ld_sup, np, nb16, hc, hw, lane, d);
+    bal_mlp(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, hc, lane, d, hacc);
+    if (a.store_pieces) bal_to_global<NKB, true>(hs + (1 + 2 * k) * CH, a.ld_h, d, hc, hw, lane, n);
+    __syncthreads();  // ys is free: every wave finished the previous support's hop 2
+    bal_to_img(ys, d, np, hc, hw, lane);
+    __syncthreads();
+    bal_zero(d);
+    bal_diffuse(ys, G, a.ld_sup, np, nb16, hc, hw, lane, d);
+    bal_mlp(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, hc, lane, d, hacc);
+    if (a.store_pieces) bal_to_global<NKB, true>(hs + (2 + 2 * k) * CH, a.ld_h, d, hc, hw, lane, n);
+  }
+  // mlp output = channel-half-0 partial + channel-half-1 partial (fixed order), rows [np][LDR]
+  float* S = lds;
+  __syncthreads();
+  if (hc == 1) {
+    bal_to_rows<NKB, false>(S, hacc[0], 0, hw, lane);
+    bal_to_rows<NKB, false>(S, hacc[1], 16, hw, lane);
+  }
+  __syncthreads();
+  if (hc == 0) {
+    bal_to_rows<NKB, true>(S, hacc[0], 0, hw, lane);
+    bal_to_rows<NKB, true>(S, hacc[1], 16, hw, lane);
+  }
+  __syncthreads();
+  fwd_epilogue<4 * NKB>(a, S, red[0], red[1], row0, n);
+}
+
+template <int NKB>
+__global__ __launch_bounds__(256, 2) void gcn_bwd_bal_kernel(const FusedBwd a) {
+  extern __shared__ float lds[];
+  constexpr int np = 32 * NKB;
+  const int n = a.n, nb16 = (n + 15) >> 4;
+  float* dhs = lds;            // dh, planes
+  float* buf = lds + np * CH;  // dP_x2 / dx1, planes
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hc = wave & 1, hw = wave >> 1;
+  const long row0 = (long)blockIdx.x * n;
+
+  bwd_prologue<4 * NKB, true>(a, dhs, row0, n, np);
+  __syncthreads();
+  f32x4 dx[NKB];
+  bal_zero(dx);
+  bal_mlpT(a.w_mlp, a.ld_w, 0, dhs, np, hc, hw, lane, dx);
+  for (int k = 0; k < a.nsup; ++k) {
+    const float* GT = slice_sup(a, a.supT[k]);
+    {
+      f32x4 u[NKB];
+      bal_zero(u);
+      bal_mlpT(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, np, hc, hw, lane, u);
+      __syncthreads();
+      bal_to_img(buf, u, np, hc, hw, lane);
+      if (k == a.adp_index) bal_to_global<NKB, false>(a.t2 + row0 * a.ld_t, a.ld_t, u, hc, hw, lane, n);
+    }
+    __syncthreads();
+    f32x4 t[NKB];
+    bal_zero(t);
+    bal_mlpT(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, np, hc, hw, lane, t);
+    bal_diffuse(buf, GT, a.ld_sup, np, nb16, hc, hw, lane, t);  // dx1 = dP_x1 + A dP_x2
+    __syncthreads();
+    bal_to_img(buf, t, np, hc, hw, lane);
+    if (k == a.adp_index) bal_to_global<NKB, false>(a.t1 + row0 * a.ld_t, a.ld_t, t, hc, hw, lane, n);
+    __syncthreads();
+    bal_diffuse(buf, GT, a.ld_sup, np, nb16, hc, hw, lane, dx);  // dxg += A dx1
+  }
+  if (!a.dfg) {
+    bal_to_global<NKB, false>(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, hc, hw, lane, n);
+    return;
+  }
+  __syncthreads();  // every wave finished reading dhs / buf
+  bal_to_rows<NKB, false>(lds, dx, 16 * hc, hw, lane);
+  __syncthreads();
+  bwd_gate_epilogue<4 * NKB>(a, lds, row0, n);
+}
+
 // dst (padded [np][ld_dst], zero outside n x n) = src or src^T
 __global__ void pad_copy_kernel(const float* src, int n, int ld_src, float* dst, int ld_dst, int np,
                                 int transpose, long src_bstride = 0, long dst_bstride = 0) {
@@ -859,6 +1135,26 @@ void ensure_lds_attr(K kern) {
 // operand latency, plus the dead 8th tile slot); it is only auto-selected when all 8 slots are real.
 bool use_4wave(int layout, int nwt) { return layout == 2 || (layout == 0 && nwt == 8); }
 
+inline bool al16(const void* q, long ld) { return ((((uintptr_t)q) & 15) | (ld & 3)) == 0; }
+
+// layout 0 (auto) resolves through GWN_GCN_LAYOUT when set (measurements), else the default below
+int auto_layout() {
+  static int v = [] {
+    const char* e = getenv("GWN_GCN_LAYOUT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+#define GWN_BAL_CASE(K, N) \
+  case N: K<N><<<slices, 256, lds, s>>>(a); break;
+#define GWN_BAL_SWITCH(K)                                                                    \
+  switch (nwt) {                                                                             \
+    GWN_BAL_CASE(K, 1) GWN_BAL_CASE(K, 2) GWN_BAL_CASE(K, 3) GWN_BAL_CASE(K, 4)             \
+    GWN_BAL_CASE(K, 5) GWN_BAL_CASE(K, 6) GWN_BAL_CASE(K, 7) GWN_BAL_CASE(K, 8)             \
+    default: break;                                                                          \
+  }
+
 }  // namespace
 
 bool gwn_gcn_fused_eligible(int c, int n, int nsup, int ld_sup) {
@@ -872,8 +1168,8 @@ int gwn_gcn_bf16_bwd_launch(const gwn_gcn_bwd_args* g, const FusedBwd& a, hipStr
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
   const int nwt = (g->n + 31) / 32;
   GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_fwd (fused): supports must be padded to 32*ceil(n/32)");
-  GWN_REQUIRE(g->layout >= 0 && g->layout <= 2 && !(g->layout == 2 && nwt > 8),
-              "gcn_fwd (fused): layout 2 (4-wave) needs n <= 256");
+  GWN_REQUIRE(g->layout >= 0 && g->layout <= 3 && !(g->layout >= 2 && nwt > 8),
+              "gcn_fwd (fused): layouts 2 (4-wave) and 3 (balanced) need n <= 256");
   FusedFwd a;
   a.h = g->h; a.ld_h = g->ld_h;
   for (int k = 0; k < 8; ++k) a.sup[k] = (k < g->nsup) ? g->sup[k] : nullptr;
@@ -910,7 +1206,11 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
     attr_set = true;
   }
   const int slices = g->rows / g->n;
-  if (use_4wave(g->layout, nwt)) gcn_fwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
+  const int layout = g->layout ? g->layout : auto_layout();
+  if (layout == 3) {
+    GWN_REQUIRE(nwt <= 8 && al16(a.h, a.ld_h), "gcn_fwd (fused): layout 3 (balanced) needs n <= 256 and 16-B rows of h");
+    GWN_BAL_SWITCH(gcn_fwd_bal_kernel)
+  } else if (use_4wave(layout, nwt)) gcn_fwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
   else {
     // + one store wave when hop pieces are stored through LDS rows (h 16-B aligned, ld % 4 == 0)
     const bool rows_ok = !(GWN_EXP & 32) && ((((uintptr_t)a.h) & 15) | (a.ld_h & 3)) == 0;
@@ -931,8 +1231,8 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
                              float* t1, float* t2, long ld_t, hipStream_t s) {
   const int nwt = (g->n + 31) / 32;
   GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_bwd (fused): supports must be padded to 32*ceil(n/32)");
-  GWN_REQUIRE(g->layout >= 0 && g->layout <= 2 && !(g->layout == 2 && nwt > 8),
-              "gcn_bwd (fused): layout 2 (4-wave) needs n <= 256");
+  GWN_REQUIRE(g->layout >= 0 && g->layout <= 3 && !(g->layout >= 2 && nwt > 8),
+              "gcn_bwd (fused): layouts 2 (4-wave) and 3 (balanced) need n <= 256");
   FusedBwd a;
   a.dh = g->dh;
   for (int k = 0; k < 8; ++k) a.supT[k] = (k < g->nsup) ? supT[k] : nullptr;
@@ -969,7 +1269,13 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   }
   const size_t lds = fused_lds_bytes(g->n);
   const int slices = g->rows / g->n;
-  if (use_4wave(g->layout, nwt)) gcn_bwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
+  const int layout = g->layout ? g->layout : auto_layout();
+  if (layout == 3) {
+    GWN_REQUIRE(nwt <= 8 && (a.dfg || al16(a.dxg, a.ld_dxg)) &&
+                    (a.adp_index < 0 || (al16(a.t1, a.ld_t) && al16(a.t2, a.ld_t))),
+                "gcn_bwd (fused): layout 3 (balanced) needs n <= 256 and 16-B rows of dxg / t1 / t2");
+    GWN_BAL_SWITCH(gcn_bwd_bal_kernel)
+  } else if (use_4wave(layout, nwt)) gcn_bwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
   else if (half_last_batch(g->n)) {
     if (nwt <= 8) gcn_bwd_fused_kernel<512, true><<<slices, 64 * nwt, lds, s>>>(a);
     else gcn_bwd_fused_kernel<1024, true><<<slices, 64 * nwt, lds, s>>>(a);

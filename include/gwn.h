@@ -237,7 +237,8 @@ typedef struct gwn_gcn_args {
    *   bn_out != NULL, bn_out[r][j] = (z - running_mean[j]) / sqrt(running_var[j] + bn_eps) *
    *   weight[j] + bias[j] is written instead of z (z may be NULL, bn_partials must be NULL).
    * layout: wave layout of the fused kernels, 0 = auto (4-wave only when n fills 8 node tiles,
-   *   225..256), 1 = one wave per 32-node tile, 2 = 4-wave (n <= 256). */
+   *   225..256; GWN_GCN_LAYOUT overrides auto), 1 = one wave per 32-node tile, 2 = 4-wave
+   *   (n <= 256), 3 = balanced 16x16 quarters (n <= 256, 16-B aligned rows; measured slower). */
   int no_pieces;
   const float* bn_running_mean; const float* bn_running_var; const float* bn_weight; const float* bn_bias;
   float bn_eps; float* bn_out;

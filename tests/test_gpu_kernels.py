@@ -322,8 +322,8 @@ def test_gemm_nt(gpu, M, N, K, epi):
 
 @pytest.mark.parametrize("n", [16, 96, 207, 256])
 def test_gcn_fused_layouts_agree(gpu, n):
-    """The 4-wave layout (default for n <= 256) and the one-wave-per-tile layout of the fused
-    gcn forward / backward against each other and against fp64 (model.py:41-55): hop pieces,
+    """The wave layouts of the fused gcn forward / backward (one wave per 32-node tile, 4-wave,
+    balanced 16x16 quarters) against each other and against fp64 (model.py:41-55): hop pieces,
     z, BN partials, dxg and the adaptive-support pieces t1 / t2."""
     import ctypes
     from gwn_amd import _lib
@@ -347,7 +347,7 @@ def test_gcn_fused_layouts_agree(gpu, n):
     dh = torch.randn(rows, C, device=gpu)
     seed = torch.zeros(1, device=gpu, dtype=torch.int64)
     outs = []
-    for layout in (1, 0):
+    for layout in (1, 0, 3):
         h = torch.zeros(rows, W, device=gpu)
         h[:, :C] = xg
         z = torch.empty(rows, C, device=gpu)
@@ -390,9 +390,10 @@ def test_gcn_fused_layouts_agree(gpu, n):
         assert rel_err(dhc[:, :C].cpu().numpy(), dxg.reshape(rows, C).numpy()) <= 2e-6
         means = bnp.view(S, 3, C)[:, 1].cpu().double()
         assert rel_err(means.numpy(), Z.view(S, n, C).mean(1).numpy()) <= 1e-5
-    # the two layouts: same products in the same k order per tile -> identical up to fma rounding
-    for a_, b_ in zip(outs[0], outs[1]):
-        assert rel_err(a_.cpu().numpy(), b_.cpu().numpy()) <= 1e-6
+    # the layouts: the same products, k order / channel split differ -> identical up to fma rounding
+    for other in outs[1:]:
+        for a_, b_ in zip(outs[0], other):
+            assert rel_err(a_.cpu().numpy(), b_.cpu().numpy()) <= 1e-6
 
 
 @pytest.mark.parametrize("n,planes", [(16, 3), (207, 3), (325, 3), (207, 2)])
@@ -567,7 +568,7 @@ def test_nconv2_vs_fp64(gpu, B, C, N, T):
         assert torch.all(err <= bound), float((err / bound).max())
 
 
-@pytest.mark.parametrize("n,layout", [(16, 0), (207, 0), (207, 1), (96, 2)])
+@pytest.mark.parametrize("n,layout", [(16, 0), (207, 0), (207, 1), (96, 2), (207, 3), (40, 3)])
 def test_gcn_fused_per_sample_supports(gpu, n, layout):
     """Fused gcn forward / backward with one support set per sample (gcn2, model.py:57-80: the
     per-sample-graph variant's 'ncvl,nvw->ncwl' diffusions): slice s = t*Bs + b diffuses with

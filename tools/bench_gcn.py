@@ -76,8 +76,8 @@ def main():
         gf.seed_ptr, gf.salt, gf.drop_p = seed.data_ptr(), 3, 0.3
         gf.fg, gf.dskip, gf.ld_dskip, gf.skip_row0, gf.dfg = fgb.data_ptr(), dskb.data_ptr(), 8 * C, 0, dfgb.data_ptr()
         variants = []
-        for lay in (0, 1):
-            tag = "" if lay == 0 else " L1"
+        for lay in ((0, 1, 3) if NP <= 256 else (0, 1)):
+            tag = "" if lay == 0 else " L%d" % lay
             ga_l = _lib.GcnArgs.from_buffer_copy(ga)
             ga_l.layout = lay
             gd_l = _lib.GcnBwdArgs.from_buffer_copy(gd)
@@ -88,9 +88,12 @@ def main():
                          ("bwd-data" + tag, lambda a=gd_l: _lib.call("gwn_gcn_bwd", ctypes.byref(a), st)),
                          ("bwd-data+bn+gate" + tag, lambda a=gf_l: _lib.call("gwn_gcn_bwd", ctypes.byref(a), st))]
         variants.append(("bwd (+wgrad, gram)", lambda: _lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)))
-        ga_np = _lib.GcnArgs.from_buffer_copy(ga)
-        ga_np.no_pieces = 1
-        variants.append(("fwd no pieces", lambda a=ga_np: _lib.call("gwn_gcn_fwd", ctypes.byref(a), st)))
+        for lay in ((0, 3) if NP <= 256 else (0,)):
+            ga_np = _lib.GcnArgs.from_buffer_copy(ga)
+            ga_np.no_pieces = 1
+            ga_np.layout = lay
+            variants.append(("fwd no pieces" + ("" if lay == 0 else " L%d" % lay),
+                             lambda a=ga_np: _lib.call("gwn_gcn_fwd", ctypes.byref(a), st)))
         wws = torch.empty(lib.gwn_wgrad_workspace_floats(rows, C, W) + 16, device=dev)
         variants.append(("wgrad mlp", lambda wws=wws: _lib.call(
             "gwn_wgrad", dh.data_ptr(), C, C, h.data_ptr(), W, rows, W, 1, 0, rows, dwm.data_ptr(), W,
