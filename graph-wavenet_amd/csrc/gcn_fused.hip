@@ -49,6 +49,7 @@ struct FusedFwd {
   // eval BatchNorm folded into the epilogue (running statistics): x_out = bn(z); z not written
   const float* bn_rm; const float* bn_rv; const float* bn_g; const float* bn_b; float bn_eps; float* x_out;
   long sup_bstride; int sup_batch;  // per-sample supports (sup_batch > 1): sample b = slice % sup_batch
+  const float* res_mean; const float* res_scale; const float* res_shift;  // (residual - mean) * scale + shift
 };
 
 struct FusedBwd {
@@ -301,6 +302,10 @@ __device__ __forceinline__ void fwd_epilogue(const FusedFwd& a, float* ys, float
   const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
   const float bias = a.b_mlp[c];
   float bmu = 0.0f, brs = 1.0f, bg = 1.0f, bb = 0.0f;
+  // the layer below's BatchNorm applied to the residual on load (gwn_batchnorm_fwd_fold)
+  const bool raff = a.res_scale != nullptr;
+  const float rmu = raff ? a.res_mean[c] : 0.0f;
+  const float rsc = raff ? a.res_scale[c] : 1.0f, rsh = raff ? a.res_shift[c] : 0.0f;
   if (a.x_out) {  // eval BatchNorm, the arithmetic of bn_apply_kernel (ops.hip)
     bmu = a.bn_rm[c];
     brs = 1.0f / sqrtf(a.bn_rv[c] + a.bn_eps);
@@ -325,7 +330,7 @@ __device__ __forceinline__ void fwd_epilogue(const FusedFwd& a, float* ys, float
         const float u = gwn_uniform(seed, a.salt, (unsigned long long)m * CH + c);
         v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
       }
-      v += res[i];
+      v += raff ? fmaf(res[i] - rmu, rsc, rsh) : res[i];
       if (a.x_out) {
         a.x_out[m * CH + c] = (v - bmu) * brs * bg + bb;
       } else {
@@ -1182,6 +1187,9 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.bn_rm = g->bn_running_mean; a.bn_rv = g->bn_running_var; a.bn_g = g->bn_weight; a.bn_b = g->bn_bias;
   a.bn_eps = g->bn_eps; a.x_out = g->bn_out;
   a.sup_bstride = g->sup_bstride; a.sup_batch = g->sup_batch;
+  a.res_mean = g->residual_mean; a.res_scale = g->residual_scale; a.res_shift = g->residual_shift;
+  GWN_REQUIRE(!a.res_scale == !a.res_shift && !a.res_scale == !a.res_mean,
+              "gcn_fwd (fused): residual_mean, residual_scale and residual_shift go together");
   if (a.sup_batch > 1)
     GWN_REQUIRE(!g->split_planes && (g->rows / g->n) % a.sup_batch == 0,
                 "gcn_fwd (per-sample supports): slices must be a multiple of sup_batch, no split path");

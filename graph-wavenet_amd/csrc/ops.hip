@@ -298,13 +298,11 @@ __global__ void bn_partial_kernel(const float* z, long rows, int c, float* part)
   }
 }
 
-__global__ void bn_finalize_kernel(const float* part, int nparts, int c, float momentum, float eps,
-                                   float* running_mean, float* running_var, float* save_mean,
-                                   float* save_rstd) {
-  // one block per channel: each thread merges a strided subset of the partials (Chan), then a
-  // fixed-order tree merge over the 256 threads
+// Chan merge of the per-chunk BatchNorm partials [nparts][3][c] of channel j over one 256-thread
+// block (strided subsets per thread, then a fixed-order tree); thread 0 returns the totals
+__device__ void bn_merge_channel(const float* part, int nparts, int c, int j, double& n_out, double& mean_out,
+                                 double& m2_out) {
   __shared__ double sn[256], sm[256], sq[256];
-  const int j = blockIdx.x;
   double n = 0.0, mean = 0.0, m2 = 0.0;
   for (int i = threadIdx.x; i < nparts; i += 256) {
     const float* pp = part + (long)i * 3 * c;
@@ -332,8 +330,17 @@ __global__ void bn_finalize_kernel(const float* part, int nparts, int c, float m
     }
     __syncthreads();
   }
+  n_out = sn[0]; mean_out = sm[0]; m2_out = sq[0];
+}
+
+__global__ void bn_finalize_kernel(const float* part, int nparts, int c, float momentum, float eps,
+                                   float* running_mean, float* running_var, float* save_mean,
+                                   float* save_rstd) {
+  // one block per channel
+  const int j = blockIdx.x;
+  double n, mean, m2;
+  bn_merge_channel(part, nparts, c, j, n, mean, m2);
   if (threadIdx.x != 0) return;
-  n = sn[0]; mean = sm[0]; m2 = sq[0];
   const double var = (n > 0.0) ? m2 / n : 0.0;
   save_mean[j] = (float)mean;
   save_rstd[j] = (float)(1.0 / sqrt(var + (double)eps));
@@ -354,6 +361,54 @@ __global__ void bn_apply_kernel(const float* z, long rows, int c, const float* m
     const float rs = rstd ? rstd[j] : 1.0f / sqrtf(rvar[j] + eps);
     out[idx] = (z[idx] - mean[j]) * rs * gamma[j] + beta[j];
   }
+}
+
+// bn_finalize_kernel + the scale of the normalisation folded into the next gated TCN
+// (gwn_batchnorm_fwd_fold), one block per channel j: the merge, then column j of both taps of the
+// next layer's weights (w_next [2c][2c]: row = output channel, column = tap*c + ci) scaled by
+// scale[j]; block 0 also folds beta into the bias (independent of the statistics)
+__global__ void bn_finalize_fold_kernel(const float* part, int nparts, int c, float momentum, float eps,
+                                        const float* gamma, const float* beta, float* running_mean,
+                                        float* running_var, float* save_mean, float* save_rstd, float* scale,
+                                        const float* w_next, const float* b_next, float* w_fold, float* b_fold) {
+  __shared__ float ssc;
+  __shared__ float bp[256];
+  const int j = blockIdx.x;
+  // the weight operands do not depend on the statistics: loaded before the merge (latency hidden)
+  const bool wcol = w_next && (int)threadIdx.x < 4 * c;  // (row, tap) pairs of column j
+  const long we = (long)(threadIdx.x >> 1) * 2 * c + (threadIdx.x & 1) * c + j;
+  const float wv = wcol ? w_next[we] : 0.0f;
+  // b_fold[row] = b_next[row] + sum_k w_next[row][k] * beta[k % c]: block j folds rows j and j + c,
+  // one product per thread, fixed-order tree per row
+  const int half = threadIdx.x / (2 * c), k = threadIdx.x % (2 * c);
+  const int row = j + half * c;
+  const bool brow = w_next && half < 2;
+  const float bv = brow ? w_next[(long)row * 2 * c + k] * beta[k % c] : 0.0f;
+  double n, mean, m2;
+  bn_merge_channel(part, nparts, c, j, n, mean, m2);
+  if (threadIdx.x == 0) {
+    const double var = (n > 0.0) ? m2 / n : 0.0;
+    const float rs = (float)(1.0 / sqrt(var + (double)eps));
+    save_mean[j] = (float)mean;
+    save_rstd[j] = rs;
+    if (running_mean) {
+      const double unbiased = (n > 1.0) ? m2 / (n - 1.0) : var;
+      running_mean[j] = (float)((1.0 - momentum) * running_mean[j] + momentum * mean);
+      running_var[j] = (float)((1.0 - momentum) * running_var[j] + momentum * unbiased);
+    }
+    const float sc = rs * gamma[j];  // bn(z) = (z - mean) * sc + beta
+    scale[j] = sc;
+    ssc = sc;
+  }
+  if (!w_next) return;
+  bp[threadIdx.x] = bv;
+  __syncthreads();
+  if (wcol) w_fold[we] = wv * ssc;
+  for (int w = c; w > 0; w >>= 1) {
+    if (brow && k < w) bp[threadIdx.x] += bp[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (brow && k == 0) b_fold[row] = b_next[row] + bp[threadIdx.x];
 }
 
 // eval-mode BatchNorm: the running statistics as (mean, rstd) for the backward
@@ -816,7 +871,7 @@ int gwn_gated_tcn_fwd(const gwn_tcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a->c % 16 == 0, "gated_tcn_fwd: channels must be a multiple of 16");
   const int c = a->c, P = a->P, t_out = a->t_in - a->dilation;
   if (c == 32 && aligned16(a->x) && aligned16(a->fg)) return gwn_rowgemm_tcn_fwd(a, s);
-  GWN_REQUIRE(a->fg != nullptr, "gated_tcn_fwd: fg may only be NULL on the c == 32 path");
+  GWN_REQUIRE(a->fg != nullptr && !a->x_mean, "gated_tcn_fwd: fg may only be NULL (and x_mean set) on the c == 32 path");
   gwn_gemm_desc d = gemm_zero();
   d.A = a->x; d.lda_m = c; d.lda_k = 1; d.a_kin = c; d.a_row_shift = a->dilation * P;
   d.a_rows = a->t_in * P;
@@ -860,9 +915,10 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
   if (a->skip_weight_grads) {
     // caller computes dW_fg / db_fg itself (gwn_wgrad)
   } else if (c % 32 == 0) {
-    rc = gwn_wgrad(a->dfg, 2 * c, 2 * c, a->x, c, (long)a->t_in * P, c, 2, (long)a->dilation * P, (int)rows,
-                   a->dw_fg, 2 * c, a->db_fg, a->workspace, s);
+    rc = gwn_wgrad_bn(a->dfg, 2 * c, 2 * c, a->x, c, (long)a->t_in * P, c, 2, (long)a->dilation * P, (int)rows,
+                      a->x_mean, a->x_scale, a->x_shift, a->dw_fg, 2 * c, a->db_fg, a->workspace, s);
   } else {
+    GWN_REQUIRE(!a->x_mean && !a->x_scale && !a->x_shift, "gated_tcn_bwd: x_mean / x_scale / x_shift need c % 32 == 0");
     d.A = a->dfg; d.lda_m = 1; d.lda_k = 2 * c;
     d.B = a->x; d.ldb_k = c; d.ldb_n = 1; d.b_nin = c; d.b_no_stride = (long)a->dilation * P * c;
     d.C = a->dw_fg; d.ldc_m = 2 * c; d.ldc_n = 1;
@@ -910,7 +966,8 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   const int c = a->c, n = a->n, slices = a->rows / n;
   if (gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup)) return gwn_gcn_fused_fwd_launch(a, a->bn_partials, s);
   GWN_REQUIRE(a->sup_batch <= 1, "gcn_fwd: per-sample supports need the fused path (c == 32, n <= 512)");
-  GWN_REQUIRE(!a->no_pieces && !a->bn_out, "gcn_fwd: no_pieces / bn_out need the fused path (c == 32, n <= 512)");
+  GWN_REQUIRE(!a->no_pieces && !a->bn_out && !a->residual_scale && !a->residual_mean,
+              "gcn_fwd: no_pieces / bn_out / residual_scale need the fused path (c == 32, n <= 512)");
   const int width = (2 * a->nsup + 1) * c;
   for (int k = 0; k < a->nsup; ++k) {
     float* x1 = a->h + (1 + 2 * k) * c;
@@ -1082,6 +1139,20 @@ int gwn_batchnorm_fwd_partials(const float* z, int rows, int c, const float* par
   const long total = (long)rows * c;
   bn_apply_kernel<<<grid_for(total), 256, 0, s>>>(z, rows, c, save_mean, save_rstd, nullptr, eps, gamma,
                                                   beta, out);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_batchnorm_fwd_fold(const float* partials, int nparts, int c, const float* gamma, const float* beta,
+                           float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
+                           float* save_rstd, float* scale, const float* w_next, const float* b_next, float* w_fold,
+                           float* b_fold, hipStream_t s) {
+  GWN_REQUIRE(c == 32 && nparts > 0 && partials && gamma && beta && save_mean && save_rstd && scale,
+              "batchnorm_fwd_fold: needs c == 32, the partials, gamma / beta and the outputs");
+  GWN_REQUIRE(!w_next || (b_next && w_fold && b_fold && w_fold != w_next),
+              "batchnorm_fwd_fold: w_next needs b_next, w_fold, b_fold (w_fold not aliasing w_next)");
+  bn_finalize_fold_kernel<<<c, 256, 0, s>>>(partials, nparts, c, momentum, eps, gamma, beta, running_mean,
+                                            running_var, save_mean, save_rstd, scale, w_next, b_next, w_fold, b_fold);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

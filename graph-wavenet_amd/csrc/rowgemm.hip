@@ -28,6 +28,7 @@ struct RowGemm {
   long acc_row0;                                                 // STORE + accumulate: rows < acc_row0 not accumulated
   const float* bn_z; const float* bn_mean; const float* bn_rstd; // BNSTAT: per-wave partials of sum C and
   float* bn_part;                                                //   sum C*xhat(bn_z), [wave][2][32]
+  const float* center;                                           // CENTER: A[.][h*a_tap + j] - center[j]
 };
 
 // Branch-free gate nonlinearities on v_exp_f32 / v_rcp_f32: absolute error ~1e-7 (a few ulp of
@@ -56,8 +57,11 @@ __device__ __forceinline__ float ld32(__amdgpu_buffer_rsrc_t r, int off) {
 // g = cols 2c+1 (tile 1) — so every lane owns channel c = col of both and writes full rows:
 // xg[m][c] = tanh(f) * sigmoid(g) (128 B per row) and fg[m][2c .. 2c+1] = (tanh f, sigmoid g).
 // STORE: ntiles waves share a chunk, one 32-column tile each.
-template <int KH, bool GATE, bool BNSTAT>
-__global__ __launch_bounds__(256) void rowgemm_kernel(const RowGemm p) {
+#ifndef GWN_ROWGEMM_WPE
+#define GWN_ROWGEMM_WPE  // measurement hook: -DGWN_ROWGEMM_WPE='__attribute__((amdgpu_waves_per_eu(2)))'
+#endif
+template <int KH, bool GATE, bool BNSTAT, bool CENTER = false>
+__global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowGemm p) {
   constexpr int NQ = KH / 4;  // float4 per lane per chunk
   constexpr int NT = GATE ? 2 : 1;
   const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
@@ -119,6 +123,10 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(const RowGemm p) {
     bn[0] = 0.0f;
   }
   if (wave >= nwaves) return;  // after the block-wide staging barrier
+  // CENTER (BatchNorm on load, gwn_batchnorm_fwd_fold): the column means are wave-uniform
+  float cmu[KH];
+#pragma unroll
+  for (int j = 0; j < KH; ++j) cmu[j] = CENTER ? p.center[j] : 0.0f;
   // BNSTAT (N = 32: channel n = col): running sums of the final C and C*xhat over this wave's rows
   const __amdgpu_buffer_rsrc_t rz = rsrc(BNSTAT ? p.bn_z : p.C, BNSTAT ? (long)p.M * 32 * 4 : 0);
   const float bmu = BNSTAT ? p.bn_mean[col] : 0.0f, brs = BNSTAT ? p.bn_rstd[col] : 0.0f;
@@ -151,7 +159,11 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(const RowGemm p) {
       for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const float av[4] = {a[q].x, a[q].y, a[q].z, a[q].w};
+      float av[4] = {a[q].x, a[q].y, a[q].z, a[q].w};
+      if (CENTER) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) av[e] -= cmu[4 * q + e];
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -203,7 +215,7 @@ inline int rowgemm_grid(int M, int ntiles, bool gate) {
   return (waves + 3) / 4;  // 4 | 4*grid, so every tile gets grid*4/ntiles waves
 }
 
-template <int KH, bool GATE, bool BNSTAT = false>
+template <int KH, bool GATE, bool BNSTAT = false, bool CENTER = false>
 int launch(const RowGemm& p, hipStream_t s) {
   GWN_REQUIRE((long)p.a_rows * p.lda * 4 < 0x7fff0000L && (long)p.M * p.ldc * 4 < 0x7fff0000L &&
                   (long)p.M * p.ld_aux * 4 < 0x7fff0000L && (long)p.M * p.ld_aux2 * 4 < 0x7fff0000L,
@@ -216,7 +228,7 @@ int launch(const RowGemm& p, hipStream_t s) {
   (void)nchunks;
   const int grid = rowgemm_grid(p.M, p.ntiles, GATE);
   const size_t lds = GATE ? (size_t)64 * (2 * KH + 4) * sizeof(float) : 0;
-  rowgemm_kernel<KH, GATE, BNSTAT><<<grid, 256, lds, s>>>(p);
+  rowgemm_kernel<KH, GATE, BNSTAT, CENTER><<<grid, 256, lds, s>>>(p);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -238,6 +250,8 @@ int gwn_rowgemm_tcn_fwd(const gwn_tcn_args* a, hipStream_t s) {
   p.aux = a->fg; p.ld_aux = a->fg ? 2 * c : 0;  // no fg: an empty window drops the stores
   p.aux2 = a->skipcat; p.ld_aux2 = a->ld_skip; p.aux2_row0 = a->skip_row0;
   p.M = t_out * P; p.ntiles = 2;
+  p.center = a->x_mean;
+  if (p.center) return launch<32, true, false, true>(p, s);
   return launch<32, true>(p, s);
 }
 

@@ -28,6 +28,7 @@ struct Wgrad {
   const float* X; long ldx; long x_rows; int Kt, ntaps; long shift;
   int R, nblk;
   float* part;  // [nblk][J*Kc + J]
+  const float* x_mean; const float* x_scale; const float* x_shift;  // AFF: X = (X - mean) * scale + shift
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long bytes) {
@@ -38,6 +39,7 @@ __device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, int off) {
 }
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
+template <bool AFF>
 __global__ __launch_bounds__(1024) void wgrad_kernel(const Wgrad g) {
   const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar) tile
@@ -51,6 +53,9 @@ __global__ __launch_bounds__(1024) void wgrad_kernel(const Wgrad g) {
   const long xshift = (long)tap * g.shift;
   const __amdgpu_buffer_rsrc_t ry = rsrc(g.dY, (long)r1 * g.ldy * 4);
   const __amdgpu_buffer_rsrc_t rx = rsrc(g.X, (r1 + xshift) * g.ldx * 4);
+  // AFF (BatchNorm on load): zero rows past r1 become finite junk, but their dY rows are zero too
+  const float xmu = AFF ? g.x_mean[xc + col] : 0.0f;
+  const float xsc = AFF ? g.x_scale[xc + col] : 1.0f, xsh = AFF ? g.x_shift[xc + col] : 0.0f;
   auto load = [&](int r, float* a, float* b) {
     const int oy = (int)(((long)(r + half) * g.ldy + 32 * jt + col) * 4);
     const int ox = (int)((((long)(r + half) + xshift) * g.ldx + xc + col) * 4);
@@ -58,6 +63,10 @@ __global__ __launch_bounds__(1024) void wgrad_kernel(const Wgrad g) {
     for (int s = 0; s < D; ++s) {
       a[s] = bld(ry, oy + (int)(2 * s * g.ldy * 4));
       b[s] = bld(rx, ox + (int)(2 * s * g.ldx * 4));
+    }
+    if (AFF) {
+#pragma unroll
+      for (int s = 0; s < D; ++s) b[s] = fmaf(b[s] - xmu, xsc, xsh);
     }
   };
 
@@ -144,6 +153,15 @@ long gwn_wgrad_workspace_floats(int R, int J, int Kc) {
 // dW[j][k] = sum_r dY[r][j] X[r + (k / Kt) * shift][k % Kt]; db[j] = sum_r dY[r][j] (db may be NULL)
 int gwn_wgrad(const float* dY, long ldy, int J, const float* X, long ldx, long x_rows, int Kt, int ntaps,
               long shift, int R, float* dW, long ld_w, float* db, float* ws, hipStream_t s) {
+  return gwn_wgrad_bn(dY, ldy, J, X, ldx, x_rows, Kt, ntaps, shift, R, nullptr, nullptr, nullptr, dW, ld_w, db, ws,
+                      s);
+}
+
+// the same with X = (X - x_mean[k % Kt]) * x_scale[k % Kt] + x_shift[k % Kt] on load (all NULL: plain)
+int gwn_wgrad_bn(const float* dY, long ldy, int J, const float* X, long ldx, long x_rows, int Kt, int ntaps,
+                 long shift, int R, const float* x_mean, const float* x_scale, const float* x_shift, float* dW,
+                 long ld_w, float* db, float* ws, hipStream_t s) {
+  GWN_REQUIRE(!x_scale == !x_shift && !x_scale == !x_mean, "wgrad: x_mean, x_scale and x_shift go together");
   const int Kc = Kt * ntaps;
   GWN_REQUIRE(J % 32 == 0 && Kt % 32 == 0 && R > 0 && ws, "wgrad: J and Kt must be multiples of 32");
   const int wpb = (J / 32) * (Kc / 32);
@@ -156,7 +174,9 @@ int gwn_wgrad(const float* dY, long ldy, int J, const float* X, long ldx, long x
   g.X = X; g.ldx = ldx; g.x_rows = x_rows; g.Kt = Kt; g.ntaps = ntaps; g.shift = shift;
   g.R = R; g.nblk = wgrad_nblk(R, wpb);
   g.part = ws;
-  wgrad_kernel<<<g.nblk, 64 * wpb, 0, s>>>(g);
+  g.x_mean = x_mean; g.x_scale = x_scale; g.x_shift = x_shift;
+  if (x_scale) wgrad_kernel<true><<<g.nblk, 64 * wpb, 0, s>>>(g);
+  else wgrad_kernel<false><<<g.nblk, 64 * wpb, 0, s>>>(g);
   GWN_CHECK_LAUNCH();
   const int outs = J * Kc + J;
   wgrad_reduce_kernel<<<(outs + 31) / 32, 256, 0, s>>>(ws, g.nblk, J, Kc, dW, ld_w, db);

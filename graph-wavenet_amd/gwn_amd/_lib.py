@@ -46,6 +46,7 @@ class TcnArgs(ctypes.Structure):
         ("xg", c_void_p), ("ld_xg", c_long),
         ("fg", c_void_p),
         ("skipcat", c_void_p), ("ld_skip", c_long), ("skip_row0", c_int),
+        ("x_mean", c_void_p),
     ]
 
 
@@ -62,6 +63,7 @@ class TcnBwdArgs(ctypes.Structure):
         ("skip_weight_grads", c_int),
         ("dfg_ready", c_int), ("acc_row0", c_long),
         ("bn_z", c_void_p), ("bn_mean", c_void_p), ("bn_rstd", c_void_p), ("bn_sums", c_void_p),
+        ("x_mean", c_void_p), ("x_scale", c_void_p), ("x_shift", c_void_p),
     ]
 
 
@@ -83,6 +85,7 @@ class GcnArgs(ctypes.Structure):
         ("sup_split", c_void_p), ("sup_split_stride", c_long), ("ld_split", c_int),
         ("w_split", c_void_p),
         ("sup_bstride", c_long), ("sup_batch", c_int),
+        ("residual_mean", c_void_p), ("residual_scale", c_void_p), ("residual_shift", c_void_p),
     ]
 
 
@@ -157,6 +160,8 @@ _SIGS = [
     ("gwn_wgrad", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,
                           c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     ("gwn_wgrad_workspace_floats", c_long, [c_int, c_int, c_int]),
+    ("gwn_wgrad_bn", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,
+                             c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     ("gwn_gram", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_int,
                          c_int, c_void_p, c_void_p]),
     ("gwn_gram_workspace_floats", c_long, [c_int, c_int]),
@@ -165,6 +170,9 @@ _SIGS = [
     ("gwn_batchnorm_workspace_floats", c_long, [c_int, c_int]),
     ("gwn_batchnorm_fwd_partials", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("gwn_batchnorm_fwd_fold", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+                                       c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p]),
     ("gwn_fused_occupancy", c_int, [c_int, c_int]),
     ("gwn_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     ("gwn_pad_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),

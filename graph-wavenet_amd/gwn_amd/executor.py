@@ -255,6 +255,12 @@ class Acts:
         self.y = e(tf * P, cfg.O)
         self.adp = torch.zeros(cfg.NP, cfg.NP, device=device, dtype=F32) if cfg.adp_params else None
         self.training = training
+        # BatchNorm on load (gwn_batchnorm_fwd_fold): per layer the scale of its normalisation
+        # (bn(z) = (z - mean) * scale + beta) and the next layer's TCN weights / bias with it folded in
+        self.bn_scale = e(L, C)
+        self.w_fold = e(L, 4 * C * C)
+        self.b_fold = e(L, 2 * C)
+        self.bn_fold = False
 
 
 class _HeadBufs:
@@ -498,11 +504,16 @@ class Executor:
                      and torch.cuda.is_available() and x.is_cuda)
         main = torch.cuda.current_stream() if tail_side else None
         tail_done = None
+        # train mode: BatchNorm i is applied on load by its consumers (TCN weights of layer i+1
+        # folded, residual affine in gcn epilogue i+1, affine in the TCN weight gradient) instead
+        # of materialising bn(z) (one HBM pass and one launch fewer per layer)
+        fold = training and self._bn_fold_ok(sup_batch)
+        acts.bn_fold = fold
         for i in range(L):
             d = cfg.dilations[i]
             rows = ts[i + 1] * P
-            ta = _lib.TcnArgs(x=ptr(acts.X[i]), t_in=ts[i], P=P, c=C, dilation=d,
-                              w_fg=ptr(self.pk("fg_w%d" % i)), b_fg=ptr(self.pk("fg_b%d" % i)),
+            xin, wfg, bfg, raff = self.layer_input(acts, i)
+            ta = _lib.TcnArgs(x=xin, x_mean=raff[0], t_in=ts[i], P=P, c=C, dilation=d, w_fg=wfg, b_fg=bfg,
                               xg=ptr(acts.H[i]), ld_xg=cfg.W, fg=ptr(acts.FG[i]),
                               skipcat=acts.skipcat.data_ptr() + 4 * i * C, ld_skip=L * C,
                               skip_row0=(ts[i + 1] - tf) * P)
@@ -523,14 +534,25 @@ class Executor:
                               sup=ctypes.cast(sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=cfg.NP,
                               h=ptr(acts.H[i]), ld_h=cfg.W,
                               w_mlp=ptr(self.pk("mlp_w%d" % i)), b_mlp=ptr(self.pk("mlp_b%d" % i)),
-                              residual=acts.X[i].data_ptr() + 4 * d * P * C, z=ptr(acts.Z[i]),
+                              residual=xin + 4 * d * P * C, z=ptr(acts.Z[i]),
                               seed_ptr=ptr(acts.seed), salt=i, drop_p=drop,
                               bn_partials=ptr(bnpart) if training else None,
-                              sup_bstride=sq if sup_batch > 1 else 0, sup_batch=sup_batch, **self.split_fields(sp, i))
+                              sup_bstride=sq if sup_batch > 1 else 0, sup_batch=sup_batch,
+                              residual_mean=raff[0], residual_scale=raff[1], residual_shift=raff[2],
+                              **self.split_fields(sp, i))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
             rm, rv, mom, eps = bn_bufs[i]
-            if training:
+            if fold:
+                nxt = i + 1 < L
+                lib.call("gwn_batchnorm_fwd_fold", ptr(bnpart), rows // N, C, ptr(self.pk("bn_g%d" % i)),
+                         ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps, ptr(acts.mean[i]), ptr(acts.rstd[i]),
+                         acts.bn_scale[i].data_ptr(),
+                         ptr(self.pk("fg_w%d" % (i + 1))) if nxt else None,
+                         ptr(self.pk("fg_b%d" % (i + 1))) if nxt else None,
+                         acts.w_fold[i + 1].data_ptr() if nxt else None,
+                         acts.b_fold[i + 1].data_ptr() if nxt else None, st)
+            elif training:
                 lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnpart), rows // N,
                          ptr(self.pk("bn_g%d" % i)), ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps,
                          ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), st)
@@ -550,6 +572,23 @@ class Executor:
         if tail_done is not None:
             main.wait_event(tail_done)
         return out, acts
+
+    def _bn_fold_ok(self, sup_batch):
+        """BatchNorm on load needs the fused gcn forward (its epilogue applies the residual affine)
+        and C = 32 (the fold kernel); GWN_BN_FOLD=0 materialises bn(z) instead."""
+        cfg = self.cfg
+        return (os.environ.get("GWN_BN_FOLD", "1") != "0" and cfg.C == 32 and cfg.N <= 512
+                and (not cfg.use_gcn or cfg.nsup <= 8))
+
+    def layer_input(self, acts, i):
+        """(x, w_fg, b_fg, (mean, scale, shift)) of layer i's gated TCN / residual: the normalised
+        activation X[i] with the layer's own weights, or -- BatchNorm folded -- the pre-BN z of
+        layer i-1 with the folded weights and bn(z) = (z - mean) * scale + beta for the residual
+        and the TCN weight gradient."""
+        if i == 0 or not acts.bn_fold:
+            return ptr(acts.X[i]), ptr(self.pk("fg_w%d" % i)), ptr(self.pk("fg_b%d" % i)), (None, None, None)
+        return (ptr(acts.Z[i - 1]), acts.w_fold[i].data_ptr(), acts.b_fold[i].data_ptr(),
+                (ptr(acts.mean[i - 1]), acts.bn_scale[i - 1].data_ptr(), ptr(self.pk("bn_b%d" % (i - 1)))))
 
     def _head_fwd(self, skipcat, skr, e1, y, rows_f, ws):
         """skip sum (relu'd) -> end_conv_1 (+relu) -> end_conv_2 (model.py:216-222, 238-240)."""
@@ -771,7 +810,9 @@ class Executor:
                 if adp_index >= 0:
                     first_adp = False
                 dxg, ld_dxg, acc = dhc, cfg.W, 1
-            tb = _lib.TcnBwdArgs(x=ptr(acts.X[i]), t_in=ts[i], P=P, c=C, dilation=d,
+            xin, _, _, raff = self.layer_input(acts, i)
+            tb = _lib.TcnBwdArgs(x=xin, x_mean=raff[0], x_scale=raff[1], x_shift=raff[2], t_in=ts[i], P=P, c=C,
+                                 dilation=d,
                                  w_fg=ptr(self.pk("fg_w%d" % i)), fg=ptr(acts.FG[i]),
                                  dxg=ptr(dxg), ld_dxg=ld_dxg,
                                  dskip=sc["dskipcat"].data_ptr() + 4 * i * C, ld_dskip=L * C,
@@ -849,9 +890,10 @@ class Executor:
         ev = torch.cuda.Event()
         ev.record(main)
         side.wait_event(ev)
-        _lib.call("gwn_wgrad", ptr(dfg), 2 * C, 2 * C, ptr(acts.X[i]), C, acts.ts[i] * P, C, 2,
-                  cfg.dilations[i] * P, rows, ptr(self.gk("fg_w%d" % i)), 2 * C, ptr(self.gk("fg_b%d" % i)),
-                  ptr(sc["ws_side"]), side.cuda_stream)
+        xin, _, _, raff = self.layer_input(acts, i)
+        _lib.call("gwn_wgrad_bn", ptr(dfg), 2 * C, 2 * C, xin, C, acts.ts[i] * P, C, 2,
+                  cfg.dilations[i] * P, rows, raff[0], raff[1], raff[2], ptr(self.gk("fg_w%d" % i)), 2 * C,
+                  ptr(self.gk("fg_b%d" % i)), ptr(sc["ws_side"]), side.cuda_stream)
         done = torch.cuda.Event()
         done.record(side)
         return done

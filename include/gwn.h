@@ -172,6 +172,10 @@ typedef struct gwn_tcn_args {
   float* xg; long ld_xg;
   float* fg;
   float* skipcat; long ld_skip; int skip_row0;
+  /* x_mean [c] (c == 32 row-GEMM path): x holds the PRE-BatchNorm z of the layer below and the
+   * input used is x - x_mean; w_fg / b_fg are then the folded weights of gwn_batchnorm_fwd_fold
+   * (BatchNorm applied on load, centred before any product). */
+  const float* x_mean;
 } gwn_tcn_args;
 /* fg may be NULL when no backward follows (inference; c == 32 row-GEMM path): the (tanh, sigmoid)
  * pairs are then not stored. */
@@ -204,6 +208,10 @@ typedef struct gwn_tcn_bwd_args {
    *   (fixed-order partials in the workspace, then an in-order merge). */
   int dfg_ready; long acc_row0;
   const float* bn_z; const float* bn_mean; const float* bn_rstd; float* bn_sums;
+  /* x_mean / x_scale / x_shift [c]: x holds the PRE-BatchNorm z of the layer below and the TCN
+   * input is (z - x_mean[ci]) * x_scale[ci] + x_shift[ci] (gwn_batchnorm_fwd_fold; the weight
+   * gradient applies it on load).  c % 32 == 0 path only. */
+  const float* x_mean; const float* x_scale; const float* x_shift;
 } gwn_tcn_bwd_args;
 int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t stream);
 long gwn_gated_tcn_bwd_workspace_floats(int t_in, int P, int c, int dilation);
@@ -258,6 +266,11 @@ typedef struct gwn_gcn_args {
    * slice s = t*sup_batch + b diffuses with support k at sup[k] + b*sup_bstride (floats), same
    * padded [np][ld_sup] layout.  Fused path only (c == 32, n <= 512), f32 MFMA (split_planes 0). */
   long sup_bstride; int sup_batch;
+  /* residual_mean / residual_scale / residual_shift [c] (fused path): residual holds the
+   * PRE-BatchNorm z of the layer below; the residual added is
+   * (residual - residual_mean[j]) * residual_scale[j] + residual_shift[j]
+   * (BatchNorm applied on load with gwn_batchnorm_fwd_fold's mean / scale and the BN bias). */
+  const float* residual_mean; const float* residual_scale; const float* residual_shift;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -352,6 +365,12 @@ long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);
 int gwn_wgrad(const float* dY, long ldy, int J, const float* X, long ldx, long x_rows, int Kt, int ntaps,
               long shift, int R, float* dW, long ld_w, float* db, float* workspace, hipStream_t stream);
 long gwn_wgrad_workspace_floats(int R, int J, int Kc);
+/* the same with X = (Xz - x_mean[k % Kt]) * x_scale[k % Kt] + x_shift[k % Kt] applied on load
+ * (Xz = the pre-BatchNorm z of gwn_batchnorm_fwd_fold; rows past R carry dY = 0, so zero-padded
+ * rows never reach dW) */
+int gwn_wgrad_bn(const float* dY, long ldy, int J, const float* X, long ldx, long x_rows, int Kt, int ntaps,
+                 long shift, int R, const float* x_mean, const float* x_scale, const float* x_shift, float* dW,
+                 long ld_w, float* db, float* workspace, hipStream_t stream);
 
 /* Adjacency gradient of order-2 diffusion over all slices (c = 32 channels per row):
  *   dA[v][w] (+)= sum_s sum_c X1[s*n + v][c] T1[s*n + w][c]  (+ same for X2, T2 when non-NULL)
@@ -379,6 +398,19 @@ int gwn_batchnorm_fwd_partials(const float* z, int rows, int c, const float* par
                                const float* gamma, const float* beta, float* running_mean,
                                float* running_var, float momentum, float eps, float* out,
                                float* save_mean, float* save_rstd, hipStream_t stream);
+/* BatchNorm applied on load instead of a normalised copy (train mode, c == 32): merge the partials
+ * and update the running statistics as gwn_batchnorm_fwd_partials; instead of writing bn(z), emit
+ * scale[j] = gamma[j] * rstd[j] (bn(z) = (z - mean) * scale + beta) and fold it into the NEXT
+ * layer's gated TCN (its only matrix consumer, model.py:206-212), which then reads z - mean:
+ *   w_fold[n][tap*c + ci] = w_next[n][tap*c + ci] * scale[ci],
+ *   b_fold[n] = b_next[n] + sum_{tap,ci} w_next[n][tap*c + ci] * beta[ci].
+ * The residual add (gwn_gcn_args.residual_*) and the TCN weight gradient (gwn_tcn_bwd_args.x_*)
+ * apply (z - mean) * scale + beta on load.  Centring first keeps the products as well
+ * conditioned as on bn(z) itself.  w_next == NULL: statistics and scale only. */
+int gwn_batchnorm_fwd_fold(const float* partials, int nparts, int c, const float* gamma, const float* beta,
+                           float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
+                           float* save_rstd, float* scale, const float* w_next, const float* b_next, float* w_fold,
+                           float* b_fold, hipStream_t stream);
 /* dst[j][i] = src[i][j] for an n x n matrix (supports for the fused backward) */
 int gwn_transpose(const float* src, int n, int ld_src, float* dst, int ld_dst, hipStream_t stream);
 /* diagnostics: resident workgroups per CU of the fused gcn kernel (forward, or backward != 0) */

@@ -20,6 +20,13 @@ the arithmetic of:
 Parity is PINNED: tests/test_oracle.py checks this restatement against the golden vectors in
 tests/golden/*.npz, which tests/golden/make_golden.py produced by running the reference itself.
 Default dtype is float64 (the "truth" the fp32 HIP path is compared against).
+
+Branch pinning (gradient tests only): the head's two ReLUs and the masked MAE (|pred - real|) are
+kinked.  An element within fp32 rounding of a kink takes either branch in two equally valid
+evaluations, and its gradient jumps.  ``forward`` / ``masked_metrics`` therefore accept the
+branch the fp32 run took (``masks``: ReLU masks of the skip sum and of end_conv_1, the sign of
+pred - real).  The value on that branch equals the plain one up to rounding; its gradient is the
+one-sided gradient of that branch.
 """
 import math
 
@@ -129,9 +136,17 @@ def batchnorm(x, gamma, beta, rmean, rvar, training, momentum=0.1, eps=1e-5):
         + beta.view(1, -1, 1, 1)
 
 
-def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None):
+def _relu(x, masks, key):
+    """relu, or -- branch pinned -- x * mask (masks[key]: the branch taken, 1 = positive side)."""
+    if masks is None or key not in masks:
+        return torch.relu(x)
+    return x * masks[key].to(x.dtype)
+
+
+def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, masks=None):
     """gwnet forward.  p: dict of parameter tensors (state_dict names); supports: list of [N,N]
-    fixed supports; x: [B, Cin, N, T]; bn_state: dict name->buffer updated in train mode."""
+    fixed supports; x: [B, Cin, N, T]; bn_state: dict name->buffer updated in train mode;
+    masks: optional ReLU branches {"skip": [B,S,N,T_f], "e1": [B,E,N,T_f]} (module docstring)."""
     t = x.shape[-1]
     if t < cfg.receptive_field:
         x = torch.nn.functional.pad(x, (cfg.receptive_field - t, 0, 0, 0))
@@ -164,12 +179,13 @@ def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None):
         rm = bn_state["bn.%d.running_mean" % i] if bn_state is not None else None
         rv = bn_state["bn.%d.running_var" % i] if bn_state is not None else None
         h = batchnorm(h, p["bn.%d.weight" % i], p["bn.%d.bias" % i], rm, rv, training)
-    y = torch.relu(pointwise(torch.relu(skip), p["end_conv_1.weight"], p["end_conv_1.bias"]))
+    y = _relu(pointwise(_relu(skip, masks, "skip"), p["end_conv_1.weight"], p["end_conv_1.bias"]), masks, "e1")
     return pointwise(y, p["end_conv_2.weight"], p["end_conv_2.bias"])
 
 
-def masked_metrics(pred, real, null_val=0.0):
-    """(mae, mape, rmse) with the zero-label mask renormalised by its mean (util.py:510-552)."""
+def masked_metrics(pred, real, null_val=0.0, sign=None):
+    """(mae, mape, rmse) with the zero-label mask renormalised by its mean (util.py:510-552).
+    sign: optional branch of |pred - real| (module docstring)."""
     mask = (real != null_val).float()          # the reference builds the mask in fp32 (.float())
     mask = mask / mask.mean()
     mask = torch.where(torch.isnan(mask), torch.zeros_like(mask), mask)
@@ -178,31 +194,34 @@ def masked_metrics(pred, real, null_val=0.0):
         return torch.where(torch.isnan(v), torch.zeros_like(v), v).mean()
 
     diff = pred - real
-    mae = fin(diff.abs() * mask)
-    mape = fin(diff.abs() / real * mask)
+    adiff = diff.abs() if sign is None else diff * sign.to(diff.dtype)
+    mae = fin(adiff * mask)
+    mape = fin(adiff / real * mask)
     rmse = torch.sqrt(fin(diff * diff * mask))
     return mae, mape, rmse
 
 
-def engine_loss(p, supports, x, real_val, cfg, scaler_mean, scaler_std, bn_state=None, training=True):
-    """engine.py:41-51 up to the loss: pad 1, forward, inverse scale, masked MAE."""
+def engine_loss(p, supports, x, real_val, cfg, scaler_mean, scaler_std, bn_state=None, training=True, masks=None):
+    """engine.py:41-51 up to the loss: pad 1, forward, inverse scale, masked MAE.
+    masks: optional branches (module docstring; "sign": [B,1,N,T_out] of pred - real)."""
     x = torch.nn.functional.pad(x, (1, 0, 0, 0))
-    out = forward(p, supports, x, cfg, training, bn_state)
+    out = forward(p, supports, x, cfg, training, bn_state, masks=masks)
     pred = out.transpose(1, 3) * scaler_std + scaler_mean
     real = real_val.unsqueeze(1)
-    mae, mape, rmse = masked_metrics(pred, real)
+    mae, mape, rmse = masked_metrics(pred, real, sign=None if masks is None else masks.get("sign"))
     return out, mae, mape, rmse
 
 
-def grads(sd, supports, x, real_val, cfg, scaler_mean, scaler_std, dtype=F64):
+def grads(sd, supports, x, real_val, cfg, scaler_mean, scaler_std, dtype=F64, masks=None):
     """Per-parameter gradients of the engine loss (train mode); params that do not reach the
-    output get no entry (the reference leaves their .grad None)."""
+    output get no entry (the reference leaves their .grad None).  masks: optional branch pinning
+    (module docstring)."""
     p = {k: torch.tensor(np.asarray(v), dtype=dtype, requires_grad=True) for k, v in sd.items()
          if not _is_buffer(k)}
     bn = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in sd.items() if "running" in k}
     sups = [torch.tensor(np.asarray(a), dtype=dtype) for a in supports]
     out, mae, mape, rmse = engine_loss(p, sups, torch.tensor(x, dtype=dtype), torch.tensor(real_val, dtype=dtype),
-                                       cfg, scaler_mean, scaler_std, bn)
+                                       cfg, scaler_mean, scaler_std, bn, masks=masks)
     names = list(p.keys())
     gs = torch.autograd.grad(mae, [p[n] for n in names], allow_unused=True)
     g = {n: gi for n, gi in zip(names, gs) if gi is not None}

@@ -223,6 +223,70 @@ def test_gated_tcn_matches_reference_golden(gpu):
     assert rel_err(got, g["tcn_d2"]) < 1e-5
 
 
+def test_batchnorm_fold_vs_materialised(gpu):
+    """gwn_batchnorm_fwd_fold (BatchNorm applied on load): from per-chunk partials of z with a large
+    channel offset (|mean| ~ 20 sigma), the saved statistics and running stats against fp64, then
+    the next gated TCN on z with the folded weights (x_mean = the batch mean) against the same TCN
+    on bn(z) with the original weights, and the TCN weight gradient with the affine applied on
+    load (gwn_tcn_bwd_args.x_mean / x_scale / x_shift) against the plain one on bn(z)."""
+    from gwn_amd import _lib
+    torch.manual_seed(16)
+    C, P, T, d = 32, 40, 6, 2
+    rows = T * P
+    z64 = torch.randn(rows, C, dtype=torch.float64) * (0.5 + torch.rand(C, dtype=torch.float64)) \
+        + 20.0 * torch.randn(C, dtype=torch.float64)
+    z = z64.float()
+    chunks = torch.split(z.double(), 37)  # ragged chunks, as the per-slice partials
+    part = torch.stack([torch.stack([torch.full((C,), float(ch.shape[0]), dtype=torch.float64), ch.mean(0),
+                                     ((ch - ch.mean(0)) ** 2).sum(0)]) for ch in chunks]).float().to(gpu)
+    gamma, beta = torch.randn(C, device=gpu), torch.randn(C, device=gpu)
+    rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    mean, rstd, scale = (torch.empty(C, device=gpu) for _ in range(3))
+    wfg = torch.randn(2 * C, 2 * C, device=gpu) * 0.2
+    bfg = torch.randn(2 * C, device=gpu)
+    wfold, bfold = torch.empty_like(wfg), torch.empty_like(bfg)
+    _lib.call("gwn_batchnorm_fwd_fold", part.data_ptr(), len(chunks), C, gamma.data_ptr(), beta.data_ptr(),
+              rm.data_ptr(), rv.data_ptr(), 0.1, 1e-5, mean.data_ptr(), rstd.data_ptr(), scale.data_ptr(),
+              wfg.data_ptr(), bfg.data_ptr(), wfold.data_ptr(), bfold.data_ptr(), _lib.stream())
+    zd = z.double()
+    mu, var = zd.mean(0), zd.var(0, unbiased=False)
+    torch.cuda.synchronize()
+    assert rel_err(mean.cpu().numpy(), mu.numpy()) < 1e-6
+    assert rel_err(rstd.cpu().numpy(), (1 / torch.sqrt(var + 1e-5)).numpy()) < 1e-6
+    assert rel_err(rm.cpu().numpy(), (0.1 * mu).numpy()) < 1e-6
+    assert rel_err(rv.cpu().numpy(), (0.9 + 0.1 * zd.var(0, unbiased=True)).numpy()) < 1e-6
+    assert rel_err(scale.cpu().numpy(), (gamma.double().cpu() * rstd.double().cpu()).numpy()) < 1e-6
+    # the TCN on z (folded, centred) = the TCN on bn(z)
+    zg = z.to(gpu)
+    xn = ((zg - mean) * rstd * gamma + beta).contiguous()
+    out = {}
+    for tag, x, w, b, xm in (("plain", xn, wfg, bfg, None), ("fold", zg, wfold, bfold, mean.data_ptr())):
+        xg = torch.empty((T - d) * P, C, device=gpu)
+        fg = torch.empty((T - d) * P, 2 * C, device=gpu)
+        a = _lib.TcnArgs(x=x.data_ptr(), t_in=T, P=P, c=C, dilation=d, w_fg=w.data_ptr(), b_fg=b.data_ptr(),
+                         xg=xg.data_ptr(), ld_xg=C, fg=fg.data_ptr(), skipcat=None, ld_skip=0, skip_row0=0, x_mean=xm)
+        _lib.call("gwn_gated_tcn_fwd", ctypes.byref(a), _lib.stream())
+        out[tag] = (xg, fg)
+    torch.cuda.synchronize()
+    assert rel_err(out["fold"][0].cpu().numpy(), out["plain"][0].cpu().numpy()) < 5e-6
+    assert rel_err(out["fold"][1].cpu().numpy(), out["plain"][1].cpu().numpy()) < 5e-6
+    # TCN weight gradient with BatchNorm on load
+    R = (T - d) * P
+    dfg = torch.randn(R, 2 * C, device=gpu)
+    lib = _lib.load()
+    ws = torch.empty(lib.gwn_wgrad_workspace_floats(R, 2 * C, 2 * C) + 16, device=gpu)
+    dw = {k: torch.empty(2 * C, 2 * C, device=gpu) for k in ("plain", "fold")}
+    db = {k: torch.empty(2 * C, device=gpu) for k in ("plain", "fold")}
+    _lib.call("gwn_wgrad", dfg.data_ptr(), 2 * C, 2 * C, xn.data_ptr(), C, rows, C, 2, d * P, R,
+              dw["plain"].data_ptr(), 2 * C, db["plain"].data_ptr(), ws.data_ptr(), _lib.stream())
+    _lib.call("gwn_wgrad_bn", dfg.data_ptr(), 2 * C, 2 * C, zg.data_ptr(), C, rows, C, 2, d * P, R,
+              mean.data_ptr(), scale.data_ptr(), beta.data_ptr(), dw["fold"].data_ptr(), 2 * C,
+              db["fold"].data_ptr(), ws.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    assert rel_err(dw["fold"].cpu().numpy(), dw["plain"].cpu().numpy()) < 5e-6
+    assert torch.equal(db["fold"], db["plain"])
+
+
 def test_batchnorm_fwd_bwd(gpu):
     from gwn_amd import _lib
     torch.manual_seed(6)

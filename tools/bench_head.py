@@ -1,5 +1,5 @@
 """Head-GEMM shapes (skip / end_conv_1 / end_conv_2 and their backward at T_f = 1, B = 64, N = 207):
-libgwn's gwn_gemm vs the vendor BLAS behind torch.mm, HIP-event timed.  Usage: python tools/bench_head.py"""
+libgwn's gwn_gemm vs the vendor BLAS libraries behind torch.mm (rocBLAS and hipBLASLt), HIP-event timed.  Usage: python tools/bench_head.py"""
 import ctypes
 import os
 import sys
@@ -55,6 +55,9 @@ def main():
             A = torch.randn(M, K, device=dev)
         B = torch.randn(K, N, device=dev)
         C = torch.empty(M, N, device=dev)
+        torch.backends.cuda.preferred_blas_library("cublaslt")
+        t_lt = timeit(lambda: torch.mm(A, B, out=C))
+        torch.backends.cuda.preferred_blas_library("cublas")
         t_torch = timeit(lambda: torch.mm(A, B, out=C))
         ks = 1
         if K > 4 * max(M, N):
@@ -62,8 +65,10 @@ def main():
             ks = max(1, min(1024 // tiles, K // 256))
         ws = torch.empty(max(1, _lib.load().gwn_gemm_workspace_floats(M, N, ks)), device=dev)
         t_gwn = timeit(lambda: gwn_mm(A, B, C, ks, ws))
-        print("%-9s M=%6d N=%4d K=%6d  torch.mm %7.1f us (%5.1f TF)   gwn_gemm %7.1f us (%5.1f TF)"
-              % (name, M, N, K, t_torch, flop / t_torch / 1e6, t_gwn, flop / t_gwn / 1e6), flush=True)
+        print("%-9s M=%6d N=%4d K=%6d  rocBLAS %7.1f us (%5.1f TF)  hipBLASLt %7.1f us (%5.1f TF)  "
+              "gwn_gemm %7.1f us (%5.1f TF)"
+              % (name, M, N, K, t_torch, flop / t_torch / 1e6, t_lt, flop / t_lt / 1e6, t_gwn, flop / t_gwn / 1e6),
+              flush=True)
 
 
 if __name__ == "__main__":
