@@ -189,8 +189,9 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
             slices = ga.rows // N
             total_ms += e0.elapsed_time(e1)
             total_flop += slices * (K * 2 * 2.0 * C * N * N + 2.0 * (2 * K + 1) * C * C * N)
-            # compulsory bytes: xg + residual in, 2K hop outputs + z out
-            total_bytes += slices * N * C * 4.0 * (2 + 2 * K + 1)
+            # compulsory bytes: xg + residual in, 2K hop outputs + z out; the
+            # last layer (output dead but for BN running stats) stores no hop pieces
+            total_bytes += slices * N * C * 4.0 * (2 + (0 if ga.no_pieces else 2 * K) + 1)
             count += 1
     avg_us = 1000.0 * total_ms / count
     achieved = total_flop / (total_ms / 1000.0) / 1e12

@@ -537,6 +537,9 @@ class Executor:
                               residual=xin + 4 * d * P * C, z=ptr(acts.Z[i]),
                               seed_ptr=ptr(acts.seed), salt=i, drop_p=drop,
                               bn_partials=ptr(bnpart) if training else None,
+                              # the last layer's gcn output only feeds bn[L-1]'s running statistics:
+                              # no backward reads its hop pieces
+                              no_pieces=1 if i == L - 1 and self._fused_gcn() else 0,
                               sup_bstride=sq if sup_batch > 1 else 0, sup_batch=sup_batch,
                               residual_mean=raff[0], residual_scale=raff[1], residual_shift=raff[2],
                               **self.split_fields(sp, i))
@@ -573,12 +576,16 @@ class Executor:
             main.wait_event(tail_done)
         return out, acts
 
+    def _fused_gcn(self):
+        """gwn_gcn_fwd takes the fused path (c == 32, n <= 512, nsup <= 8; include/gwn.h)."""
+        cfg = self.cfg
+        return cfg.C == 32 and cfg.N <= 512 and (not cfg.use_gcn or cfg.nsup <= 8)
+
     def _bn_fold_ok(self, sup_batch):
         """BatchNorm on load needs the fused gcn forward (its epilogue applies the residual affine)
         and C = 32 (the fold kernel); GWN_BN_FOLD=0 materialises bn(z) instead."""
         cfg = self.cfg
-        return (os.environ.get("GWN_BN_FOLD", "1") != "0" and cfg.C == 32 and cfg.N <= 512
-                and (not cfg.use_gcn or cfg.nsup <= 8))
+        return os.environ.get("GWN_BN_FOLD", "1") != "0" and self._fused_gcn()
 
     def layer_input(self, acts, i):
         """(x, w_fg, b_fg, (mean, scale, shift)) of layer i's gated TCN / residual: the normalised
