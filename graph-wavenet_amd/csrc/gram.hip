@@ -200,6 +200,12 @@ int gwn_gram(const float* x1, const float* t1, const float* x2, const float* t2,
   return gwn_gram_dtype(x1, t1, x2, t2, ldx, ldt, n, slices, dA, ld_dA, accumulate, ws, 0, s);
 }
 
+// the same contraction on bf16 MFMA operands with fp32 accumulation (the bf16 mode's gram)
+int gwn_gram_bf16(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
+                  int slices, float* dA, int ld_dA, int accumulate, float* ws, hipStream_t s) {
+  return gwn_gram_dtype(x1, t1, x2, t2, ldx, ldt, n, slices, dA, ld_dA, accumulate, ws, 1, s);
+}
+
 int gwn_gram_dtype(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
                    int slices, float* dA, int ld_dA, int accumulate, float* ws, int bf16, hipStream_t s) {
   GWN_REQUIRE(n > 0 && slices > 0 && x1 && t1 && ws, "gram: bad arguments");

@@ -725,6 +725,7 @@ long gwn_abi_sizeof(const char* name) {
   if (!strcmp(name, "gwn_gemm_desc")) return (long)sizeof(gwn_gemm_desc);
   if (!strcmp(name, "gwn_tcn_args")) return (long)sizeof(gwn_tcn_args);
   if (!strcmp(name, "gwn_tcn_bwd_args")) return (long)sizeof(gwn_tcn_bwd_args);
+  if (!strcmp(name, "gwn_reduce_seg")) return (long)sizeof(gwn_reduce_seg);
   if (!strcmp(name, "gwn_gcn_args")) return (long)sizeof(gwn_gcn_args);
   if (!strcmp(name, "gwn_gcn_bwd_args")) return (long)sizeof(gwn_gcn_bwd_args);
   return -1;

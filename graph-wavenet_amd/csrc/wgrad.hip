@@ -133,6 +133,51 @@ __global__ void wgrad_reduce_kernel(const float* part, int nblk, int J, int Kc, 
   else if (db) db[idx - J * Kc] = sh[ej];
 }
 
+// One launch reduces many partial sets (the deferred weight gradients of a whole backward,
+// gwn_reduce_partials): block b belongs to the segment whose block range holds it; each block sums
+// 32 consecutive outputs of its segment over the segment's partials with the wgrad_reduce_kernel
+// scheme (8 partial lanes x 4 chains, fixed-order tree); output i < J*Kc -> out[(i / Kc) * ld + i % Kc],
+// else out2[i - J*Kc].
+constexpr int MAXSEG = 32;  // the table travels as a kernel argument (<= 4 KB)
+struct SegTable {
+  gwn_reduce_seg seg[MAXSEG];
+  int first_block[MAXSEG + 1];
+  int nseg;
+};
+
+__global__ void reduce_segments_kernel(const SegTable t) {
+  __shared__ float sh[256];
+  int si = 0;
+  while (si + 1 < t.nseg && (int)blockIdx.x >= t.first_block[si + 1]) ++si;
+  const gwn_reduce_seg& g = t.seg[si];
+  const int ej = threadIdx.x & 31, l = threadIdx.x >> 5;
+  const long i = (long)(blockIdx.x - t.first_block[si]) * 32 + ej;
+  const long jk = (long)g.J * g.Kc, outs = jk + g.J;
+  float v0 = 0.0f, v1 = 0.0f, v2 = 0.0f, v3 = 0.0f;
+  if (i < outs) {
+    const float* p = g.part + i;
+    const long st = g.part_stride;
+    int b = l;
+    for (; b + 24 < g.nparts; b += 32) {
+      v0 += p[(long)b * st];
+      v1 += p[(long)(b + 8) * st];
+      v2 += p[(long)(b + 16) * st];
+      v3 += p[(long)(b + 24) * st];
+    }
+    for (; b < g.nparts; b += 8) v0 += p[(long)b * st];
+  }
+  sh[threadIdx.x] = (v0 + v1) + (v2 + v3);
+  __syncthreads();
+#pragma unroll
+  for (int w = 4; w > 0; w >>= 1) {
+    if (l < w) sh[threadIdx.x] += sh[threadIdx.x + 32 * w];
+    __syncthreads();
+  }
+  if (l != 0 || i >= outs) return;
+  if (i < jk) g.out[(i / g.Kc) * g.ld_out + i % g.Kc] = sh[ej];
+  else if (g.out2) g.out2[i - jk] = sh[ej];
+}
+
 int wgrad_nblk(int R, int waves_per_blk) {
   // a whole number of workgroups per CU (256 CUs), ~WGRAD_WAVES_PER_CU waves per CU; >= 256 rows per workgroup
   int per_cu = WGRAD_WAVES_PER_CU / waves_per_blk;
@@ -144,6 +189,11 @@ int wgrad_nblk(int R, int waves_per_blk) {
 }
 
 }  // namespace
+
+int gwn_wgrad_partial_count(int R, int J, int Kc) {
+  if (J < 32 || Kc < 32 || J % 32 || Kc % 32 || R <= 0) return 0;
+  return wgrad_nblk(R, (J / 32) * (Kc / 32));
+}
 
 long gwn_wgrad_workspace_floats(int R, int J, int Kc) {
   if (J < 32 || Kc < 32 || J % 32 || Kc % 32 || R <= 0) return 0;  // not eligible: no workspace
@@ -178,8 +228,41 @@ int gwn_wgrad_bn(const float* dY, long ldy, int J, const float* X, long ldx, lon
   if (x_scale) wgrad_kernel<true><<<g.nblk, 64 * wpb, 0, s>>>(g);
   else wgrad_kernel<false><<<g.nblk, 64 * wpb, 0, s>>>(g);
   GWN_CHECK_LAUNCH();
+  if (!dW) return GWN_OK;  // partials only (gwn_wgrad_partials)
   const int outs = J * Kc + J;
   wgrad_reduce_kernel<<<(outs + 31) / 32, 256, 0, s>>>(ws, g.nblk, J, Kc, dW, ld_w, db);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+// partials only: part [gwn_wgrad_partial_count(R, J, Kc)][J*Kc + J], reduced later by
+// gwn_reduce_partials (kind 0)
+int gwn_wgrad_partials(const float* dY, long ldy, int J, const float* X, long ldx, long x_rows, int Kt, int ntaps,
+                       long shift, int R, const float* x_mean, const float* x_scale, const float* x_shift, float* part,
+                       hipStream_t s) {
+  GWN_REQUIRE(part != nullptr, "wgrad_partials: part is required");
+  return gwn_wgrad_bn(dY, ldy, J, X, ldx, x_rows, Kt, ntaps, shift, R, x_mean, x_scale, x_shift, nullptr, 0, nullptr,
+                      part, s);
+}
+
+int gwn_reduce_partials(const gwn_reduce_seg* segs, int nseg, hipStream_t s) {
+  GWN_REQUIRE(nseg >= 0 && nseg <= MAXSEG && (nseg == 0 || segs), "reduce_partials: 0..32 segments");
+  SegTable t = {};
+  int blocks = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const gwn_reduce_seg& g = segs[i];
+    GWN_REQUIRE(g.part && g.out && g.nparts > 0 && g.part_stride >= (long)g.J * g.Kc + g.J && g.J > 0 && g.Kc > 0 &&
+                    g.ld_out >= g.Kc,
+                "reduce_partials: segment needs part, out, nparts > 0, J, Kc, ld_out >= Kc, stride >= J*Kc + J");
+    const long outs = (long)g.J * g.Kc + g.J;
+    t.seg[i] = g;
+    t.first_block[i] = blocks;
+    blocks += (int)((outs + 31) / 32);
+  }
+  t.first_block[nseg] = blocks;
+  t.nseg = nseg;
+  if (!blocks) return GWN_OK;
+  reduce_segments_kernel<<<blocks, 256, 0, s>>>(t);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

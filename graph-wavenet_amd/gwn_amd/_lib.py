@@ -89,6 +89,14 @@ class GcnArgs(ctypes.Structure):
     ]
 
 
+class ReduceSeg(ctypes.Structure):
+    _fields_ = [
+        ("part", c_void_p), ("nparts", c_int), ("part_stride", c_long),
+        ("J", c_int), ("Kc", c_int),
+        ("out", c_void_p), ("ld_out", c_long), ("out2", c_void_p),
+    ]
+
+
 class GcnBwdArgs(ctypes.Structure):
     _fields_ = [
         ("rows", c_int), ("n", c_int), ("c", c_int), ("nsup", c_int),
@@ -160,11 +168,17 @@ _SIGS = [
     ("gwn_wgrad", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,
                           c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     ("gwn_wgrad_workspace_floats", c_long, [c_int, c_int, c_int]),
+    ("gwn_wgrad_partial_count", c_int, [c_int, c_int, c_int]),
+    ("gwn_wgrad_partials", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("gwn_reduce_partials", c_int, [ctypes.POINTER(ReduceSeg), c_int, c_void_p]),
     ("gwn_wgrad_bn", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,
                              c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     ("gwn_gram", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_int,
                          c_int, c_void_p, c_void_p]),
     ("gwn_gram_workspace_floats", c_long, [c_int, c_int]),
+    ("gwn_gram_bf16", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_int,
+                              c_int, c_void_p, c_void_p]),
     ("gwn_batchnorm_fwd", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                   c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gwn_batchnorm_workspace_floats", c_long, [c_int, c_int]),

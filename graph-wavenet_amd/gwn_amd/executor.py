@@ -409,6 +409,16 @@ class Executor:
             need.append(lib.gwn_gemm_workspace_floats(M_, N_, _ksplit(M_, N_, K_)))
         need.append(lib.gwn_gemm_workspace_floats(tf * P, cfg.O, _ksplit_thin(tf * P, cfg.O, cfg.E)))
         s["ws"] = e(int(max(need)) + 16)
+        # deferred weight gradients (_defer_ok): per-layer wgrad partials, reduced by one launch at
+        # the end of the backward
+        if cfg.C % 32 == 0 and cfg.W % 32 == 0:
+            pm, pt = [], []
+            for i in range(L):
+                rows = ts[i + 1] * P
+                pm.append(e(max(1, lib.gwn_wgrad_partial_count(rows, C, cfg.W)) * (C * cfg.W + C)))
+                pt.append(e(max(1, lib.gwn_wgrad_partial_count(rows, 2 * C, 2 * C)) * (4 * C * C + 2 * C)))
+            s["part_mlp"], s["part_tcn"] = pm, pt
+
         side_need = [lib.gwn_wgrad_workspace_floats(maxrows, C, cfg.W),
                      lib.gwn_wgrad_workspace_floats(maxrows, 2 * C, 2 * C),
                      lib.gwn_gram_workspace_floats(N, maxrows // N)]
@@ -729,6 +739,9 @@ class Executor:
         # fused layer backward: BN backward in the gcn_bwd prologue, gate backward in its epilogue,
         # the next BN's statistics in the TCN input-gradient epilogue (3 launches fewer per layer)
         fuse = self._fuse_ok(acts)
+        # weight / adjacency gradients as partials, one reduction launch for the whole backward
+        defer = not overlap and fuse and self._defer_ok(sc)
+        segs = []
         main = torch.cuda.current_stream()
         side = self._side_stream() if overlap else None
 
@@ -794,7 +807,7 @@ class Executor:
                                      accumulate_dadp=0 if first_adp else 1, workspace=ptr(ws),
                                      sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
                                      if acts.supT_arr is not None else None,
-                                     skip_weight_grads=1 if overlap else 0)
+                                     skip_weight_grads=1 if (overlap or defer) else 0)
                 sb = getattr(acts, "sup_batch", 1)
                 if sb > 1:
                     gb.sup_bstride, gb.sup_batch = cfg.NP * cfg.NP, sb
@@ -814,6 +827,8 @@ class Executor:
                 lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)
                 if overlap:
                     self._side_gcn_grads(main, side, acts, i, rows, dh, dhc, adp_index, first_adp, sc)
+                if defer:
+                    self._defer_gcn_grads(acts, i, rows, dh, dhc, adp_index, first_adp, sc, segs, st)
                 if adp_index >= 0:
                     first_adp = False
                 dxg, ld_dxg, acc = dhc, cfg.W, 1
@@ -826,7 +841,7 @@ class Executor:
                                  skip_row0=(ts[i + 1] - tf) * P, dfg=ptr(dfg),
                                  dw_fg=ptr(self.gk("fg_w%d" % i)), db_fg=ptr(self.gk("fg_b%d" % i)),
                                  dx=ptr(dx), accumulate_dx=acc, workspace=ptr(ws),
-                                 skip_weight_grads=1 if overlap else 0)
+                                 skip_weight_grads=1 if (overlap or defer) else 0)
             if fuse:
                 if dnext is not None:
                     tb.dfg_ready, tb.acc_row0 = 1, d * P
@@ -836,9 +851,21 @@ class Executor:
             lib.call("gwn_gated_tcn_bwd", ctypes.byref(tb), st)
             if overlap:
                 side_done[i] = self._side_tcn_grads(main, side, acts, i, rows, dfg, sc)
+            if defer:
+                part = sc["part_tcn"][i]
+                lib.call("gwn_wgrad_partials", ptr(dfg), 2 * C, 2 * C, xin, C, ts[i] * P, C, 2, d * P, rows,
+                         raff[0], raff[1], raff[2], ptr(part), st)
+                segs.append(_lib.ReduceSeg(part=ptr(part), nparts=_lib.load().gwn_wgrad_partial_count(rows, 2 * C, 2 * C),
+                                           part_stride=4 * C * C + 2 * C, J=2 * C, Kc=2 * C,
+                                           out=ptr(self.gk("fg_w%d" % i)), ld_out=2 * C,
+                                           out2=ptr(self.gk("fg_b%d" % i))))
             dnext = dx
         if overlap:
             main.wait_event(side_done[0])  # dadp and every side-stream weight gradient are complete
+        if defer:
+            for k in range(0, len(segs), 32):  # <= 32 segments per launch (include/gwn.h)
+                chunk = segs[k:k + 32]
+                lib.call("gwn_reduce_partials", (_lib.ReduceSeg * len(chunk))(*chunk), len(chunk), st)
         # start conv
         rows0 = ts[0] * P
         wgrad(dnext, C, acts.xin, cfg.Cin, rows0, self.gk("start_w"), ws, self.gk("start_b"))
@@ -870,6 +897,35 @@ class Executor:
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
+
+    def _defer_ok(self, sc):
+        """Deferred weight / adjacency gradients (GWN_DEFER_WGRAD=0: each reduced in its own
+        launches right after its layer)."""
+        return os.environ.get("GWN_DEFER_WGRAD", "1") != "0" and "part_mlp" in sc
+
+    def _defer_gcn_grads(self, acts, i, rows, dh, dhc, adp_index, first_adp, sc, segs, st):
+        """Layer i's dW_mlp / db_mlp partials for the end-of-backward reduction, and its share of
+        the adaptive-support gradient (gwn_gram, reduced into dadp right away: deferring its
+        partials too wrote 12.8 MB of fresh partial slots per layer and slowed every gram launch
+        by 20-30 %, more than the 7 reduce launches it saved)."""
+        cfg = self.cfg
+        C, W = cfg.C, cfg.W
+        lib = _lib
+        part = sc["part_mlp"][i]
+        lib.call("gwn_wgrad_partials", ptr(dh), C, C, ptr(acts.H[i]), W, rows, W, 1, 0, rows, None, None, None,
+                 ptr(part), st)
+        segs.append(_lib.ReduceSeg(part=ptr(part), nparts=_lib.load().gwn_wgrad_partial_count(rows, C, W),
+                                   part_stride=C * W + C, J=C, Kc=W, out=ptr(self.gk("mlp_w%d" % i)),
+                                   ld_out=W, out2=ptr(self.gk("mlp_b%d" % i))))
+        if adp_index >= 0:
+            h = acts.H[i].data_ptr()
+            t = dhc.data_ptr()
+            if getattr(acts, "sp_bwd", None) is not None:  # bf16 mode: the bf16-MFMA gram
+                lib.call("gwn_gram_bf16", h, t + 4 * C, h + 4 * (1 + 2 * adp_index) * C, t + 4 * 2 * C, W, W, cfg.N,
+                         rows // cfg.N, ptr(sc["dadp"]), cfg.NP, 0 if first_adp else 1, ptr(sc["ws"]), st)
+            else:
+                lib.call("gwn_gram", h, t + 4 * C, h + 4 * (1 + 2 * adp_index) * C, t + 4 * 2 * C, W, W, cfg.N,
+                         rows // cfg.N, ptr(sc["dadp"]), cfg.NP, 0 if first_adp else 1, ptr(sc["ws"]), st)
 
     def _side_gcn_grads(self, main, side, acts, i, rows, dh, dhc, adp_index, first_adp, sc):
         """dW_mlp / db_mlp (gwn_wgrad) and the adaptive-support gradient (gwn_gram) of layer i on

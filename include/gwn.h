@@ -372,11 +372,30 @@ int gwn_wgrad_bn(const float* dY, long ldy, int J, const float* X, long ldx, lon
                  long shift, int R, const float* x_mean, const float* x_scale, const float* x_shift, float* dW,
                  long ld_w, float* db, float* workspace, hipStream_t stream);
 
+/* Deferred reduction (one launch for the weight gradients of a whole backward):
+ * gwn_wgrad_partials writes the gwn_wgrad_partial_count(R, J, Kc) workgroup partials
+ * [count][J*Kc + J] of a gwn_wgrad_bn problem without reducing them; gwn_reduce_partials then sums
+ * every segment's partials in a fixed order (deterministic) in ONE launch: out [J][ld_out] = dW,
+ * out2 [J] = db (may be NULL).  At most 32 segments per call. */
+typedef struct gwn_reduce_seg {
+  const float* part; int nparts; long part_stride;  /* partial p at part + p * part_stride */
+  int J, Kc;
+  float* out; long ld_out; float* out2;
+} gwn_reduce_seg;
+int gwn_wgrad_partial_count(int R, int J, int Kc);
+int gwn_wgrad_partials(const float* dY, long ldy, int J, const float* X, long ldx, long x_rows, int Kt, int ntaps,
+                       long shift, int R, const float* x_mean, const float* x_scale, const float* x_shift, float* part,
+                       hipStream_t stream);
+int gwn_reduce_partials(const gwn_reduce_seg* segs, int nseg, hipStream_t stream);
+
 /* Adjacency gradient of order-2 diffusion over all slices (c = 32 channels per row):
  *   dA[v][w] (+)= sum_s sum_c X1[s*n + v][c] T1[s*n + w][c]  (+ same for X2, T2 when non-NULL)
  * i.e. both pairs (xg, dx1) and (x1, dx2) of gcn.forward's adaptive support in one launch. */
 int gwn_gram(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
              int slices, float* dA, int ld_dA, int accumulate, float* workspace, hipStream_t stream);
+/* gwn_gram on bf16 MFMA operands with fp32 accumulation (the bf16 mode, gwn_dtype BF16) */
+int gwn_gram_bf16(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
+                  int slices, float* dA, int ld_dA, int accumulate, float* workspace, hipStream_t stream);
 /* workspace for any gwn_gram launch over AT MOST `slices` slices (non-decreasing in slices, so one
  * query at a schedule's largest layer covers every layer) */
 long gwn_gram_workspace_floats(int n, int slices);

@@ -287,6 +287,50 @@ def test_batchnorm_fold_vs_materialised(gpu):
     assert torch.equal(db["fold"], db["plain"])
 
 
+def test_deferred_wgrad_reduction_bitwise(gpu):
+    """gwn_wgrad_partials + ONE gwn_reduce_partials over several problems (the deferred weight
+    gradients of a backward) give exactly gwn_wgrad's / gwn_wgrad_bn's results: the same partials,
+    summed in the same fixed order."""
+    from gwn_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(21)
+    C, P, T, d = 32, 207 * 4, 5, 2
+    R = (T - d) * P
+    probs = []
+    # gcn mlp: dY [R][32], X = h [R][224]
+    probs.append(dict(dY=torch.randn(R, C, device=gpu), J=C, X=torch.randn(R, 7 * C, device=gpu), ldx=7 * C,
+                      x_rows=R, Kt=7 * C, ntaps=1, shift=0, aff=(None, None, None)))
+    # gated TCN with BatchNorm on load: dY = dfg [R][64], X = z [T*P][32], two taps
+    z = torch.randn(T * P, C, device=gpu) * 2 + 5
+    aff = (torch.randn(C, device=gpu) + 5, torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu))
+    probs.append(dict(dY=torch.randn(R, 2 * C, device=gpu), J=2 * C, X=z, ldx=C, x_rows=T * P, Kt=C, ntaps=2,
+                      shift=d * P, aff=aff))
+    segs, ref = [], []
+    for pr in probs:
+        J, Kc = pr["J"], pr["Kt"] * pr["ntaps"]
+        a = [None if t is None else t.data_ptr() for t in pr["aff"]]
+        ws = torch.empty(lib.gwn_wgrad_workspace_floats(R, J, Kc) + 16, device=gpu)
+        dw, db = torch.empty(J, Kc, device=gpu), torch.empty(J, device=gpu)
+        _lib.call("gwn_wgrad_bn", pr["dY"].data_ptr(), J, J, pr["X"].data_ptr(), pr["ldx"], pr["x_rows"], pr["Kt"],
+                  pr["ntaps"], pr["shift"], R, a[0], a[1], a[2], dw.data_ptr(), Kc, db.data_ptr(), ws.data_ptr(),
+                  _lib.stream())
+        ref.append((dw, db))
+        cnt = lib.gwn_wgrad_partial_count(R, J, Kc)
+        part = torch.empty(cnt * (J * Kc + J), device=gpu)
+        _lib.call("gwn_wgrad_partials", pr["dY"].data_ptr(), J, J, pr["X"].data_ptr(), pr["ldx"], pr["x_rows"],
+                  pr["Kt"], pr["ntaps"], pr["shift"], R, a[0], a[1], a[2], part.data_ptr(), _lib.stream())
+        dw2, db2 = torch.full((J, Kc + 3), 7.0, device=gpu), torch.empty(J, device=gpu)
+        segs.append((_lib.ReduceSeg(part=part.data_ptr(), nparts=cnt, part_stride=J * Kc + J, J=J, Kc=Kc,
+                                    out=dw2.data_ptr(), ld_out=Kc + 3, out2=db2.data_ptr()), part, dw2, db2))
+    arr = (_lib.ReduceSeg * len(segs))(*[sg[0] for sg in segs])
+    _lib.call("gwn_reduce_partials", arr, len(segs), _lib.stream())
+    torch.cuda.synchronize()
+    for (dw, db), (_, _, dw2, db2) in zip(ref, segs):
+        assert torch.equal(dw2[:, :dw.shape[1]], dw)
+        assert torch.equal(db2, db)
+        assert torch.all(dw2[:, dw.shape[1]:] == 7.0)
+
+
 def test_batchnorm_fwd_bwd(gpu):
     from gwn_amd import _lib
     torch.manual_seed(6)

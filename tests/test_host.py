@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     # every ctypes mirror has the size of the C struct it mirrors (the library reports them)
     for name, mirror in (("gwn_gemm_desc", _lib.GemmDesc), ("gwn_tcn_args", _lib.TcnArgs),
                          ("gwn_tcn_bwd_args", _lib.TcnBwdArgs), ("gwn_gcn_args", _lib.GcnArgs),
-                         ("gwn_gcn_bwd_args", _lib.GcnBwdArgs)):
+                         ("gwn_gcn_bwd_args", _lib.GcnBwdArgs), ("gwn_reduce_seg", _lib.ReduceSeg)):
         assert lib.gwn_abi_sizeof(name.encode()) == ctypes.sizeof(mirror), name
 
 
