@@ -742,6 +742,7 @@ class Executor:
         # weight / adjacency gradients as partials, one reduction launch for the whole backward
         defer = not overlap and fuse and self._defer_ok(sc)
         segs = []
+        gram_now = None
         main = torch.cuda.current_stream()
         side = self._side_stream() if overlap else None
 
@@ -828,7 +829,9 @@ class Executor:
                 if overlap:
                     self._side_gcn_grads(main, side, acts, i, rows, dh, dhc, adp_index, first_adp, sc)
                 if defer:
-                    self._defer_gcn_grads(acts, i, rows, dh, dhc, adp_index, first_adp, sc, segs, st)
+                    self._defer_gcn_grads(acts, i, rows, dh, sc, segs, st)
+                    if adp_index >= 0:  # issued after the layer's TCN backward (below)
+                        gram_now = (dhc, first_adp)
                 if adp_index >= 0:
                     first_adp = False
                 dxg, ld_dxg, acc = dhc, cfg.W, 1
@@ -859,6 +862,9 @@ class Executor:
                                            part_stride=4 * C * C + 2 * C, J=2 * C, Kc=2 * C,
                                            out=ptr(self.gk("fg_w%d" % i)), ld_out=2 * C,
                                            out2=ptr(self.gk("fg_b%d" % i))))
+                if gram_now is not None:
+                    self._defer_gram(acts, i, rows, gram_now[0], adp_index, gram_now[1], sc, st)
+                    gram_now = None
             dnext = dx
         if overlap:
             main.wait_event(side_done[0])  # dadp and every side-stream weight gradient are complete
@@ -903,29 +909,28 @@ class Executor:
         launches right after its layer)."""
         return os.environ.get("GWN_DEFER_WGRAD", "1") != "0" and "part_mlp" in sc
 
-    def _defer_gcn_grads(self, acts, i, rows, dh, dhc, adp_index, first_adp, sc, segs, st):
-        """Layer i's dW_mlp / db_mlp partials for the end-of-backward reduction, and its share of
-        the adaptive-support gradient (gwn_gram, reduced into dadp right away: deferring its
-        partials too wrote 12.8 MB of fresh partial slots per layer and slowed every gram launch
-        by 20-30 %, more than the 7 reduce launches it saved)."""
+    def _defer_gcn_grads(self, acts, i, rows, dh, sc, segs, st):
+        """Layer i's dW_mlp / db_mlp partials for the end-of-backward reduction."""
         cfg = self.cfg
         C, W = cfg.C, cfg.W
-        lib = _lib
         part = sc["part_mlp"][i]
-        lib.call("gwn_wgrad_partials", ptr(dh), C, C, ptr(acts.H[i]), W, rows, W, 1, 0, rows, None, None, None,
-                 ptr(part), st)
+        _lib.call("gwn_wgrad_partials", ptr(dh), C, C, ptr(acts.H[i]), W, rows, W, 1, 0, rows, None, None, None,
+                  ptr(part), st)
         segs.append(_lib.ReduceSeg(part=ptr(part), nparts=_lib.load().gwn_wgrad_partial_count(rows, C, W),
                                    part_stride=C * W + C, J=C, Kc=W, out=ptr(self.gk("mlp_w%d" % i)),
                                    ld_out=W, out2=ptr(self.gk("mlp_b%d" % i))))
-        if adp_index >= 0:
-            h = acts.H[i].data_ptr()
-            t = dhc.data_ptr()
-            if getattr(acts, "sp_bwd", None) is not None:  # bf16 mode: the bf16-MFMA gram
-                lib.call("gwn_gram_bf16", h, t + 4 * C, h + 4 * (1 + 2 * adp_index) * C, t + 4 * 2 * C, W, W, cfg.N,
-                         rows // cfg.N, ptr(sc["dadp"]), cfg.NP, 0 if first_adp else 1, ptr(sc["ws"]), st)
-            else:
-                lib.call("gwn_gram", h, t + 4 * C, h + 4 * (1 + 2 * adp_index) * C, t + 4 * 2 * C, W, W, cfg.N,
-                         rows // cfg.N, ptr(sc["dadp"]), cfg.NP, 0 if first_adp else 1, ptr(sc["ws"]), st)
+
+    def _defer_gram(self, acts, i, rows, dhc, adp_index, first_adp, sc, st):
+        """Layer i's share of the adaptive-support gradient (gwn_gram, reduced into dadp right away:
+        deferring its partials too wrote 12.8 MB of fresh partial slots per layer and slowed every
+        gram launch by 20-30 %, more than the 7 reduce launches it saved)."""
+        cfg = self.cfg
+        C, W = cfg.C, cfg.W
+        h = acts.H[i].data_ptr()
+        t = dhc.data_ptr()
+        fn = "gwn_gram_bf16" if getattr(acts, "sp_bwd", None) is not None else "gwn_gram"
+        _lib.call(fn, h, t + 4 * C, h + 4 * (1 + 2 * adp_index) * C, t + 4 * 2 * C, W, W, cfg.N, rows // cfg.N,
+                  ptr(sc["dadp"]), cfg.NP, 0 if first_adp else 1, ptr(sc["ws"]), st)
 
     def _side_gcn_grads(self, main, side, acts, i, rows, dh, dhc, adp_index, first_adp, sc):
         """dW_mlp / db_mlp (gwn_wgrad) and the adaptive-support gradient (gwn_gram) of layer i on
