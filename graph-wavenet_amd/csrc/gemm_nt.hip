@@ -146,6 +146,121 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const NtArgs p) {
   }
 }
 
+// Thin N (N <= 32, the head's end_conv_2 forward: N = 12 outputs over K = 512 channels): one
+// 32-row block per workgroup, the K tiles dealt round-robin to its 4 waves (k-split, so 4x as many
+// loads in flight as a 128-row block), straight from global memory: lane (i, h) reads the 16
+// contiguous floats k0 + 16h .. of row i of A and of B (the MFMA's permuted K, as above).  The
+// waves' partial tiles are summed through LDS in a fixed order (wave 0 + 1 + 2 + 3), then the
+// epilogue.  HBM-bound: 414 workgroups at M = 13248 instead of 104.
+__global__ __launch_bounds__(256) void gemm_nt_thin_kernel(const NtArgs p) {
+  __shared__ float red[3][16][64];
+  const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, col = lane & 31, wave = tid >> 6;
+  const int m0 = blockIdx.x * 32;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(p.A, ((long)(p.M - 1) * p.lda + p.K) * 4);
+  const __amdgpu_buffer_rsrc_t rb = rsrc(p.B, ((long)(p.N - 1) * p.ldb + p.K) * 4);
+  const int nk = (p.K + BK - 1) / BK;
+  float4 a[4], b[4];
+  auto load = [&](int kt) {
+    const int k = kt * BK + 16 * half;
+    const bool kin = kt < nk;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kq = k + 4 * q;
+      const int oa = (kin && m0 + col < p.M && kq < p.K) ? (int)(((long)(m0 + col) * p.lda + kq) * 4) : OOR;
+      const int ob = (kin && col < p.N && kq < p.K) ? (int)(((long)col * p.ldb + kq) * 4) : OOR;
+      a[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, oa, 0, 0));
+      b[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rb, ob, 0, 0));
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  load(wave);
+  for (int kt = wave; kt < nk; kt += 4) {
+    float af[16], bf[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      af[4 * q] = a[q].x; af[4 * q + 1] = a[q].y; af[4 * q + 2] = a[q].z; af[4 * q + 3] = a[q].w;
+      bf[4 * q] = b[q].x; bf[4 * q + 1] = b[q].y; bf[4 * q + 2] = b[q].z; bf[4 * q + 3] = b[q].w;
+    }
+    load(kt + 4);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
+  }
+  if (wave > 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave - 1][r][lane] = acc[r];
+  }
+  __syncthreads();
+  if (wave > 0) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = ((acc[r] + red[0][r][lane]) + red[1][r][lane]) + red[2][r][lane];
+  const __amdgpu_buffer_rsrc_t rc = rsrc(p.C, ((long)(p.M - 1) * p.ldc + p.N) * 4);
+  const int n = col;
+  const bool nok = n < p.N;
+  const float bn = (p.bias && nok) ? p.bias[n] : 0.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + crow(r, half);
+    const bool ok = nok && m < p.M;
+    float v = acc[r] + bn;
+    if (p.relu) v = fmaxf(v, 0.0f);
+    if (p.mask) v = (ok && p.mask[(long)m * p.ldmask + n] > 0.0f) ? v : 0.0f;
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rc, ok ? (int)(((long)m * p.ldc + n) * 4) : OOR,
+                                          0, 0);
+  }
+}
+
+// Small K (K <= 32, 16-B aligned rows: the head's end_conv_2 input gradient, K = 12): an
+// element-wise streaming kernel.  Thread t owns output columns 4t .. 4t+3 and keeps their B rows
+// (K x 4 floats) in registers; workgroups stride over the rows: per row one broadcast read of
+// A's K values, one float4 of the mask, K x 4 FMAs, one float4 store.  HBM-bound (mask in, C out).
+template <int KQ>
+__global__ __launch_bounds__(256) void gemm_nt_smallk_kernel(const NtArgs p) {
+  const int n4 = blockIdx.y * blockDim.x + threadIdx.x;  // column quad
+  const int n = 4 * n4;
+  const bool nok = n < p.N;
+  float4 w[4][KQ];  // w[c][q] = B[n + c][4q .. 4q+3]
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+      w[c][q] = (nok && 4 * q < p.K) ? *(const float4*)(p.B + (long)(n + c) * p.ldb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.bias && nok) bias = *(const float4*)(p.bias + n);
+  if (!nok) return;
+  for (int m = blockIdx.x; m < p.M; m += gridDim.x) {
+    const float* ar = p.A + (long)m * p.lda;
+    float4 av[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) av[q] = (4 * q < p.K) ? *(const float4*)(ar + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 mk = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (p.mask) mk = *(const float4*)(p.mask + (long)m * p.ldmask + n);
+    float o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float v = 0.0f;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        v = fmaf(av[q].x, w[c][q].x, v);
+        v = fmaf(av[q].y, w[c][q].y, v);
+        v = fmaf(av[q].z, w[c][q].z, v);
+        v = fmaf(av[q].w, w[c][q].w, v);
+      }
+      o[c] = v;
+    }
+    const float bb[4] = {bias.x, bias.y, bias.z, bias.w};
+    const float mm[4] = {mk.x, mk.y, mk.z, mk.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      o[c] += bb[c];
+      if (p.relu) o[c] = fmaxf(o[c], 0.0f);
+      if (p.mask) o[c] = mm[c] > 0.0f ? o[c] : 0.0f;
+    }
+    *(float4*)(p.C + (long)m * p.ldc + n) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 template <int BM, int BN, int WGM, int WGN>
 void launch(const NtArgs& p, hipStream_t s) {
   dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN);
@@ -166,8 +281,28 @@ extern "C" int gwn_gemm_nt(const float* A, long lda, const float* B, long ldb, f
                   ((long)M * ldc + N) * 4 < 0x7fff0000L,
               "gemm_nt: operand beyond a 2 GB buffer window");
   NtArgs p = {A, lda, B, ldb, C, ldc, M, N, K, bias, relu, mask, ldmask};
+  // small K (the K x 4 B values per thread fit in registers) and 16-B aligned rows everywhere
+  const bool quads = N % 4 == 0 && K % 4 == 0 && ldc % 4 == 0 && al16(C) && (!bias || al16(bias)) &&
+                     (!mask || (ldmask % 4 == 0 && al16(mask)));
+  if (K <= 32 && N >= 64 && quads) {
+    const int kq = K / 4;
+    const int threads = N / 4 < 256 ? N / 4 : 256;
+    dim3 grid(M < 2048 ? M : 2048, (N / 4 + threads - 1) / threads);
+    switch (kq) {
+      case 1: gemm_nt_smallk_kernel<1><<<grid, threads, 0, s>>>(p); break;
+      case 2: gemm_nt_smallk_kernel<2><<<grid, threads, 0, s>>>(p); break;
+      case 3: gemm_nt_smallk_kernel<3><<<grid, threads, 0, s>>>(p); break;
+      case 4: gemm_nt_smallk_kernel<4><<<grid, threads, 0, s>>>(p); break;
+      case 5: gemm_nt_smallk_kernel<5><<<grid, threads, 0, s>>>(p); break;
+      case 6: gemm_nt_smallk_kernel<6><<<grid, threads, 0, s>>>(p); break;
+      case 7: gemm_nt_smallk_kernel<7><<<grid, threads, 0, s>>>(p); break;
+      default: gemm_nt_smallk_kernel<8><<<grid, threads, 0, s>>>(p); break;
+    }
+    GWN_CHECK_LAUNCH();
+    return GWN_OK;
+  }
   // tile choice: enough workgroups for 256 CUs (two resident per CU), wide N tiles when N allows
-  if (N <= 32) launch<128, 32, 4, 1>(p, s);
+  if (N <= 32) gemm_nt_thin_kernel<<<(M + 31) / 32, 256, 0, s>>>(p);
   else if (N % 128 == 0 && (long)((M + 127) / 128) * (N / 128) >= 384) launch<128, 128, 2, 2>(p, s);
   else launch<128, 64, 2, 2>(p, s);
   GWN_CHECK_LAUNCH();

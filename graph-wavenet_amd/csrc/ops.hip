@@ -634,7 +634,7 @@ __global__ void to_nchw_kernel(const float* y, int B, int o, int n, int t, float
   }
 }
 
-__global__ void from_nchw_kernel(const float* dout, int B, int o, int n, int t, float* dy) {
+__global__ void from_nchw_kernel(const float* dout, int B, int o, int n, int t, float* dy, int ld) {
   const long total = (long)B * o * n * t;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
        idx += (long)gridDim.x * blockDim.x) {
@@ -644,7 +644,10 @@ __global__ void from_nchw_kernel(const float* dout, int B, int o, int n, int t, 
     const long r2 = r1 / n;
     const int oo = (int)(r2 % o);
     const int b = (int)(r2 / o);
-    dy[(((long)tt * B + b) * n + v) * o + oo] = dout[idx];
+    float* row = dy + (((long)tt * B + b) * n + v) * ld;
+    row[oo] = dout[idx];
+    if (oo == 0)
+      for (int c = o; c < ld; ++c) row[c] = 0.0f;  // zero padding columns
   }
 }
 
@@ -1249,8 +1252,13 @@ int gwn_to_nchw(const float* y, int B, int o, int n, int t, float* out, hipStrea
 }
 
 int gwn_from_nchw(const float* dout, int B, int o, int n, int t, float* dy, hipStream_t s) {
+  return gwn_from_nchw_ld(dout, B, o, n, t, dy, o, s);
+}
+
+int gwn_from_nchw_ld(const float* dout, int B, int o, int n, int t, float* dy, int ld_dy, hipStream_t s) {
+  GWN_REQUIRE(ld_dy >= o, "from_nchw: ld_dy < o");
   const long total = (long)B * o * n * t;
-  from_nchw_kernel<<<grid_for(total), 256, 0, s>>>(dout, B, o, n, t, dy);
+  from_nchw_kernel<<<grid_for(total), 256, 0, s>>>(dout, B, o, n, t, dy, ld_dy);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

@@ -153,9 +153,10 @@ __global__ void reduce_segments_kernel(const SegTable t) {
   const int ej = threadIdx.x & 31, l = threadIdx.x >> 5;
   const long i = (long)(blockIdx.x - t.first_block[si]) * 32 + ej;
   const long jk = (long)g.J * g.Kc, outs = jk + g.J;
+  const long dbo = g.db_off ? g.db_off : jk;
   float v0 = 0.0f, v1 = 0.0f, v2 = 0.0f, v3 = 0.0f;
   if (i < outs) {
-    const float* p = g.part + i;
+    const float* p = g.part + (i < jk ? i : dbo + (i - jk));
     const long st = g.part_stride;
     int b = l;
     for (; b + 24 < g.nparts; b += 32) {
@@ -251,9 +252,11 @@ int gwn_reduce_partials(const gwn_reduce_seg* segs, int nseg, hipStream_t s) {
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {
     const gwn_reduce_seg& g = segs[i];
-    GWN_REQUIRE(g.part && g.out && g.nparts > 0 && g.part_stride >= (long)g.J * g.Kc + g.J && g.J > 0 && g.Kc > 0 &&
-                    g.ld_out >= g.Kc,
-                "reduce_partials: segment needs part, out, nparts > 0, J, Kc, ld_out >= Kc, stride >= J*Kc + J");
+    const long dbo = g.db_off ? g.db_off : (long)g.J * g.Kc;
+    GWN_REQUIRE(g.part && g.out && g.nparts > 0 && g.J > 0 && g.Kc > 0 && g.ld_out >= g.Kc &&
+                    dbo >= (long)g.J * g.Kc && g.part_stride >= dbo + g.J,
+                "reduce_partials: segment needs part, out, nparts > 0, J, Kc, ld_out >= Kc, db_off >= J*Kc, "
+                "stride >= db_off + J");
     const long outs = (long)g.J * g.Kc + g.J;
     t.seg[i] = g;
     t.first_block[i] = blocks;

@@ -94,6 +94,7 @@ class ReduceSeg(ctypes.Structure):
         ("part", c_void_p), ("nparts", c_int), ("part_stride", c_long),
         ("J", c_int), ("Kc", c_int),
         ("out", c_void_p), ("ld_out", c_long), ("out2", c_void_p),
+        ("db_off", c_long),
     ]
 
 
@@ -209,6 +210,7 @@ _SIGS = [
     ("gwn_gather", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p]),
     ("gwn_to_nchw", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("gwn_from_nchw", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    ("gwn_from_nchw_ld", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     ("gwn_sum_vectors", c_int, [c_void_p, c_int, c_int, c_long, c_void_p, c_void_p]),
     ("gwn_increment_u64", c_int, [c_void_p, c_u64, c_void_p]),
     ("gwn_horizon_metrics", c_int, [c_void_p, c_long, c_long, c_long, c_void_p, c_long, c_long, c_long, c_int,

@@ -185,6 +185,7 @@ class Config:
         self.S = model.skip_channels
         self.E = model.end_channels
         self.O = model.out_dim
+        self.OP = (self.O + 31) // 32 * 32  # output gradient rows padded to whole 32-column tiles
         self.L = model.blocks * model.layers
         # gwnet: dilations 1, 2, 4, ... per block; gwnet_diff_G starts every block at 4 (model.py:291)
         first = getattr(model, "first_dilation", 1)
@@ -375,7 +376,7 @@ class Executor:
         e = lambda *s_: torch.empty(*s_, device=self.device, dtype=F32)  # noqa: E731
         maxrows = max(ts[i + 1] for i in range(L)) * P
         s = {
-            "dy": e(tf * P, cfg.O),
+            "dy": e(tf * P, cfg.OP),  # the output gradient, rows padded to 32 columns (zeros)
             "de1": e(tf * P, cfg.E),
             "dsk": e(tf * P, cfg.S),
             "dskipcat": e(tf * P, L * C),
@@ -418,6 +419,8 @@ class Executor:
                 pm.append(e(max(1, lib.gwn_wgrad_partial_count(rows, C, cfg.W)) * (C * cfg.W + C)))
                 pt.append(e(max(1, lib.gwn_wgrad_partial_count(rows, 2 * C, 2 * C)) * (4 * C * C + 2 * C)))
             s["part_mlp"], s["part_tcn"] = pm, pt
+            if cfg.E % 32 == 0 and (cfg.OP // 32) * (cfg.E // 32) <= 16:  # end_conv_2's weight gradient
+                s["part_e2"] = e(max(1, lib.gwn_wgrad_partial_count(tf * P, cfg.OP, cfg.E)) * (cfg.OP * cfg.E + cfg.OP))
 
         side_need = [lib.gwn_wgrad_workspace_floats(maxrows, C, cfg.W),
                      lib.gwn_wgrad_workspace_floats(maxrows, 2 * C, 2 * C),
@@ -729,7 +732,8 @@ class Executor:
         st = _lib.stream()
         lib = _lib
         dout = dout.contiguous()
-        lib.call("gwn_from_nchw", ptr(dout), B, O, N, tf, ptr(sc["dy"]), st)
+        OP = cfg.OP
+        lib.call("gwn_from_nchw_ld", ptr(dout), B, O, N, tf, ptr(sc["dy"]), OP, st)
         # Weight / adjacency gradients (head wgrads, gwn_wgrad, gwn_gram: off the critical path)
         # run on a second stream when the fused data path is on (C = 32), overlapping the input
         # gradients that follow; in the layers the buffers they read (dh, dhcat, dfg) alternate by
@@ -746,23 +750,32 @@ class Executor:
         main = torch.cuda.current_stream()
         side = self._side_stream() if overlap else None
 
-        def head_wgrad(dY, J, X, Kc, w, b):
+        def head_wgrad(dY, J, X, Kc, w, b, ldy=None):
             if not overlap:
-                wgrad(dY, J, X, Kc, rows_f, w, ws, b)
+                wgrad(dY, J, X, Kc, rows_f, w, ws, b, ldy=ldy)
                 return
             ev = torch.cuda.Event()
             ev.record(main)
             side.wait_event(ev)
             with torch.cuda.stream(side):
-                wgrad(dY, J, X, Kc, rows_f, w, sc["ws_side"], b)
+                wgrad(dY, J, X, Kc, rows_f, w, sc["ws_side"], b, ldy=ldy)
 
         nt = self._head_nt()
-        # end_conv_2
-        head_wgrad(sc["dy"], O, acts.e1, E, self.gk("e2_w"), self.gk("e2_b"))
-        if nt:
-            gemm_nt(sc["dy"], O, self.pk("e2_wT"), O, sc["de1"], E, rows_f, E, O, mask=acts.e1, ldmask=E)
+        # end_conv_2: its weight gradient from the 32-column padded output gradient on the row
+        # reduction kernel (deferred), else the split-K GEMM
+        if defer and "part_e2" in sc:
+            part = sc["part_e2"]
+            lib.call("gwn_wgrad_partials", ptr(sc["dy"]), OP, OP, ptr(acts.e1), E, rows_f, E, 1, 0, rows_f,
+                     None, None, None, ptr(part), st)
+            segs.append(_lib.ReduceSeg(part=ptr(part), nparts=_lib.load().gwn_wgrad_partial_count(rows_f, OP, E),
+                                       part_stride=OP * E + OP, J=O, Kc=E, out=ptr(self.gk("e2_w")), ld_out=E,
+                                       out2=ptr(self.gk("e2_b")), db_off=OP * E))
         else:
-            gemm(sc["dy"], O, 1, self.pk("e2_w"), E, 1, sc["de1"], E, 1, M=rows_f, N=E, K=O,
+            head_wgrad(sc["dy"], O, acts.e1, E, self.gk("e2_w"), self.gk("e2_b"), ldy=OP)
+        if nt:
+            gemm_nt(sc["dy"], OP, self.pk("e2_wT"), O, sc["de1"], E, rows_f, E, O, mask=acts.e1, ldmask=E)
+        else:
+            gemm(sc["dy"], OP, 1, self.pk("e2_w"), E, 1, sc["de1"], E, 1, M=rows_f, N=E, K=O,
                  epi=2, mask=acts.e1, ldmask=E)
         # end_conv_1
         head_wgrad(sc["de1"], E, acts.skr, S, self.gk("e1_w"), self.gk("e1_b"))
@@ -1014,8 +1027,9 @@ def gemm_nt(A, lda, B, ldb, Cout, ldc, M, N, K, bias=None, relu=0, mask=None, ld
               ldmask, _lib.stream())
 
 
-def wgrad(dY, J, X, Kc, rows, out, ws, bias_out=None):
-    """out[j][k] = sum_r dY[r][j] * X[r][k]   (1x1 conv weight gradient, split over rows);
-    bias_out[j] = sum_r dY[r][j] from the same launch (the GEMM's ones column)."""
+def wgrad(dY, J, X, Kc, rows, out, ws, bias_out=None, ldy=None):
+    """out[j][k] = sum_r dY[r][j] * X[r][k]   (1x1 conv weight gradient, split over rows; dY rows
+    ldy >= J floats apart); bias_out[j] = sum_r dY[r][j] from the same launch (the GEMM's ones
+    column)."""
     ks = _ksplit(J, Kc, rows)
-    gemm(dY, 1, J, X, Kc, 1, out, Kc, 1, M=J, N=Kc, K=rows, ksplit=ks, part=ws, ones_out=bias_out)
+    gemm(dY, 1, ldy or J, X, Kc, 1, out, Kc, 1, M=J, N=Kc, K=rows, ksplit=ks, part=ws, ones_out=bias_out)

@@ -379,8 +379,10 @@ int gwn_wgrad_bn(const float* dY, long ldy, int J, const float* X, long ldx, lon
  * out2 [J] = db (may be NULL).  At most 32 segments per call. */
 typedef struct gwn_reduce_seg {
   const float* part; int nparts; long part_stride;  /* partial p at part + p * part_stride */
-  int J, Kc;
+  int J, Kc;                                        /* rows / columns written (J <= the problem's) */
   float* out; long ld_out; float* out2;
+  long db_off;  /* offset of db within a partial (0 = J*Kc; a problem computed with more rows than
+                 * are written, e.g. a 12-row weight from a 32-row padded gradient: J_pad * Kc) */
 } gwn_reduce_seg;
 int gwn_wgrad_partial_count(int R, int J, int Kc);
 int gwn_wgrad_partials(const float* dY, long ldy, int J, const float* X, long ldx, long x_rows, int Kt, int ntaps,
@@ -488,6 +490,8 @@ int gwn_gather(const float* src, const int* idx, float* dst, long count, hipStre
 int gwn_to_nchw(const float* y, int B, int o, int n, int t, float* out, hipStream_t stream);
 /* dy[(t*B + b)*n + v][o] = dout[b][o][v][t] */
 int gwn_from_nchw(const float* dout, int B, int o, int n, int t, float* dy, hipStream_t stream);
+/* the same into rows of ld_dy >= o floats, columns o .. ld_dy-1 zeroed (a 32-wide padded gradient) */
+int gwn_from_nchw_ld(const float* dout, int B, int o, int n, int t, float* dy, int ld_dy, hipStream_t stream);
 /* sum of `count` vectors of length len spaced by stride: out[j] = sum_i x[i*stride + j] */
 int gwn_sum_vectors(const float* x, int count, int len, long stride, float* out,
                     hipStream_t stream);
