@@ -100,13 +100,19 @@ __global__ void adp_fwd_kernel(const float* e1, const float* e2, int n, int d, f
 }
 
 // dlogit[v][w] = adp*(dadp - sum_w' adp*dadp) * [pre > 0]
+// row v of dL = relu'(E1 E2) * softmax'(dadp) and, from the same block, row v of dE1 = dL E2^T
+// (the embedding rank d <= ADP_MAXD: per-thread partials over its w, fixed-order block sums)
+constexpr int ADP_MAXD = 16;
 __global__ void adp_bwd_kernel(const float* e1, const float* e2, const float* adp, const float* dadp,
-                               int n, int d, int ld, float* dl) {
+                               int n, int d, int ld, float* dl, float* de1) {
   __shared__ float sh[256];
   const int v = blockIdx.x;
   float dot = 0.0f;
   for (int w = threadIdx.x; w < n; w += 256) dot += adp[(long)v * ld + w] * dadp[(long)v * ld + w];
   dot = block_sum<256>(dot, sh);
+  float pe[ADP_MAXD];
+#pragma unroll
+  for (int k = 0; k < ADP_MAXD; ++k) pe[k] = 0.0f;
   for (int w = threadIdx.x; w < ld; w += 256) {
     float g = 0.0f;
     if (w < n) {
@@ -114,9 +120,61 @@ __global__ void adp_bwd_kernel(const float* e1, const float* e2, const float* ad
       for (int k = 0; k < d; ++k) l = fmaf(e1[(long)v * d + k], e2[(long)k * n + w], l);
       const float a = adp[(long)v * ld + w];
       g = (l > 0.0f) ? a * (dadp[(long)v * ld + w] - dot) : 0.0f;
+#pragma unroll
+      for (int k = 0; k < ADP_MAXD; ++k)
+        if (k < d) pe[k] = fmaf(g, e2[(long)k * n + w], pe[k]);
     }
     dl[(long)v * ld + w] = g;
   }
+  // all d sums in one fixed-order tree (8 barriers, not 8 per value)
+  __shared__ float shk[ADP_MAXD][256];
+#pragma unroll
+  for (int k = 0; k < ADP_MAXD; ++k)
+    if (k < d) shk[k][threadIdx.x] = pe[k];
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) {
+#pragma unroll
+      for (int k = 0; k < ADP_MAXD; ++k)
+        if (k < d) shk[k][threadIdx.x] += shk[k][threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if ((int)threadIdx.x < d) de1[(long)v * d + threadIdx.x] = shk[threadIdx.x][0];
+}
+
+// dE2[k][w] = sum_v e1[v][k] dL[v][w]: 16 columns w per 1024-thread block, 64 lanes over v
+// (v mod 64) each holding all d partial sums, folded by a fixed-order tree over the lanes
+__global__ __launch_bounds__(1024) void adp_bwd_e2_kernel(const float* e1, const float* dl, int n, int d, int ld,
+                                                          float* de2) {
+  __shared__ float sh[64][ADP_MAXD][16];
+  const int tw = threadIdx.x & 15, tv = threadIdx.x >> 4;
+  const int w = blockIdx.x * 16 + tw;
+  float acc[ADP_MAXD];
+#pragma unroll
+  for (int k = 0; k < ADP_MAXD; ++k) acc[k] = 0.0f;
+  if (w < n) {
+    for (int v = tv; v < n; v += 64) {
+      const float g = dl[(long)v * ld + w];
+#pragma unroll
+      for (int k = 0; k < ADP_MAXD; ++k)
+        if (k < d) acc[k] = fmaf(e1[(long)v * d + k], g, acc[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < ADP_MAXD; ++k) sh[tv][k][tw] = acc[k];
+  __syncthreads();
+  for (int st = 32; st > 0; st >>= 1) {
+    if (tv < st) {
+#pragma unroll
+      for (int k = 0; k < ADP_MAXD; ++k) sh[tv][k][tw] += sh[tv + st][k][tw];
+    }
+    __syncthreads();
+  }
+  if (tv != 0 || w >= n) return;
+#pragma unroll
+  for (int k = 0; k < ADP_MAXD; ++k)
+    if (k < d) de2[(long)k * n + w] = sh[0][k][tw];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -837,24 +895,13 @@ int gwn_adaptive_adj_fwd_batched(const float* e1, const float* e2, int batch, in
 
 int gwn_adaptive_adj_bwd(const float* e1, const float* e2, const float* adp, const float* dadp, int n,
                          int dd, int ld, float* de1, float* de2, float* ws, hipStream_t s) {
-  GWN_REQUIRE(n > 0 && dd > 0 && ld >= n, "adaptive_adj_bwd: bad shape");
-  adp_bwd_kernel<<<n, 256, 0, s>>>(e1, e2, adp, dadp, n, dd, ld, ws);
+  GWN_REQUIRE(n > 0 && dd > 0 && dd <= ADP_MAXD && ld >= n, "adaptive_adj_bwd: bad shape (embedding rank <= 16)");
+  // dL and dE1[v][k] = sum_w dL[v][w] e2[k][w] (one block per v), then dE2[k][w] = sum_v e1[v][k] dL[v][w]
+  adp_bwd_kernel<<<n, 256, 0, s>>>(e1, e2, adp, dadp, n, dd, ld, ws, de1);
   GWN_CHECK_LAUNCH();
-  // dE1[v][k] = sum_w dl[v][w] * e2[k][w]
-  gwn_gemm_desc d = gemm_zero();
-  d.A = ws; d.lda_m = ld; d.lda_k = 1;
-  d.B = e2; d.ldb_k = 1; d.ldb_n = n;
-  d.C = de1; d.ldc_m = dd; d.ldc_n = 1;
-  d.M = n; d.N = dd; d.K = n;
-  int rc = gwn_gemm_launch(d, s);
-  if (rc) return rc;
-  // dE2[k][w] = sum_v e1[v][k] * dl[v][w]
-  d = gemm_zero();
-  d.A = e1; d.lda_m = 1; d.lda_k = dd;
-  d.B = ws; d.ldb_k = ld; d.ldb_n = 1;
-  d.C = de2; d.ldc_m = n; d.ldc_n = 1;
-  d.M = dd; d.N = n; d.K = n;
-  return gwn_gemm_launch(d, s);
+  adp_bwd_e2_kernel<<<(n + 15) / 16, 1024, 0, s>>>(e1, ws, n, dd, ld, de2);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
 }
 
 // ---------------------------------------------------------------------------------------------

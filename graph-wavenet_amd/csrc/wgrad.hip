@@ -179,6 +179,45 @@ __global__ void reduce_segments_kernel(const SegTable t) {
   else if (g.out2) g.out2[i - jk] = sh[ej];
 }
 
+// Narrow inputs (the start conv: Kc = in_dim = 2 channels, J = 32): 256-thread workgroups over
+// contiguous row ranges, thread (row lane l, channel j) accumulating dY[r][j] * X[r][k] (k < Kc)
+// and dY[r][j] over rows r = l mod 8; the 8 row lanes are folded in a fixed order and the
+// workgroup partial [J*Kc + J] written for gwn_reduce_partials.
+constexpr int SMALL_KC = 4, SMALL_BLK = 512, SMALL_ROWS = 64;  // <= 512 workgroups (partials to reduce)
+__global__ __launch_bounds__(256) void wgrad_small_kernel(const float* dY, long ldy, int J, const float* X, long ldx,
+                                                          int Kc, int R, float* part) {
+  __shared__ float sh[SMALL_KC + 1][256];
+  const int j = threadIdx.x % J, l = threadIdx.x / J, lanes = 256 / J;
+  const int r0 = (int)((long)R * blockIdx.x / gridDim.x), r1 = (int)((long)R * (blockIdx.x + 1) / gridDim.x);
+  float acc[SMALL_KC + 1];
+#pragma unroll
+  for (int k = 0; k <= SMALL_KC; ++k) acc[k] = 0.0f;
+  if (l < lanes) {
+#pragma unroll 8
+    for (int r = r0 + l; r < r1; r += lanes) {
+      const float dy = dY[(long)r * ldy + j];
+#pragma unroll
+      for (int k = 0; k < SMALL_KC; ++k)
+        if (k < Kc) acc[k] = fmaf(dy, X[(long)r * ldx + k], acc[k]);
+      acc[SMALL_KC] += dy;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k <= SMALL_KC; ++k) sh[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  if (l != 0) return;
+  float* out = part + (long)blockIdx.x * (J * Kc + J);
+#pragma unroll
+  for (int k = 0; k <= SMALL_KC; ++k) {
+    if (k < Kc || k == SMALL_KC) {
+      float v = 0.0f;
+      for (int q = 0; q < lanes; ++q) v += sh[k][q * J + j];
+      if (k < Kc) out[j * Kc + k] = v;
+      else out[J * Kc + j] = v;
+    }
+  }
+}
+
 int wgrad_nblk(int R, int waves_per_blk) {
   // a whole number of workgroups per CU (256 CUs), ~WGRAD_WAVES_PER_CU waves per CU; >= 256 rows per workgroup
   int per_cu = WGRAD_WAVES_PER_CU / waves_per_blk;
@@ -192,7 +231,12 @@ int wgrad_nblk(int R, int waves_per_blk) {
 }  // namespace
 
 int gwn_wgrad_partial_count(int R, int J, int Kc) {
-  if (J < 32 || Kc < 32 || J % 32 || Kc % 32 || R <= 0) return 0;
+  if (R <= 0) return 0;
+  if (Kc <= SMALL_KC && J > 0 && J <= 256 && 256 % J == 0) {
+    const int nb = (R + SMALL_ROWS - 1) / SMALL_ROWS;
+    return nb < SMALL_BLK ? nb : SMALL_BLK;
+  }
+  if (J < 32 || Kc < 32 || J % 32 || Kc % 32) return 0;
   return wgrad_nblk(R, (J / 32) * (Kc / 32));
 }
 
@@ -242,6 +286,12 @@ int gwn_wgrad_partials(const float* dY, long ldy, int J, const float* X, long ld
                        long shift, int R, const float* x_mean, const float* x_scale, const float* x_shift, float* part,
                        hipStream_t s) {
   GWN_REQUIRE(part != nullptr, "wgrad_partials: part is required");
+  if (Kt * ntaps <= SMALL_KC && J > 0 && J <= 256 && 256 % J == 0) {  // narrow inputs (1x1, no affine)
+    GWN_REQUIRE(ntaps == 1 && !x_mean && !x_scale && !x_shift && x_rows >= R, "wgrad_partials: narrow form is 1x1, plain");
+    wgrad_small_kernel<<<gwn_wgrad_partial_count(R, J, Kt), 256, 0, s>>>(dY, ldy, J, X, ldx, Kt, R, part);
+    GWN_CHECK_LAUNCH();
+    return GWN_OK;
+  }
   return gwn_wgrad_bn(dY, ldy, J, X, ldx, x_rows, Kt, ntaps, shift, R, x_mean, x_scale, x_shift, nullptr, 0, nullptr,
                       part, s);
 }

@@ -127,6 +127,7 @@ class trainer():
         key = (B, tuple(ts), training)
         acts = self._acts.get(key)
         out, acts = ex.forward(model._flat, model._fixed_supports(), input, training, model._bn_bufs(),
+                               fixed_t=model._fixed_supports_t(),
                                acts=acts, lead_pad=1)
         self._acts[key] = acts
         if training:

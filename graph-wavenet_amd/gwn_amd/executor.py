@@ -419,6 +419,8 @@ class Executor:
                 pm.append(e(max(1, lib.gwn_wgrad_partial_count(rows, C, cfg.W)) * (C * cfg.W + C)))
                 pt.append(e(max(1, lib.gwn_wgrad_partial_count(rows, 2 * C, 2 * C)) * (4 * C * C + 2 * C)))
             s["part_mlp"], s["part_tcn"] = pm, pt
+            if cfg.Cin <= 4 and 256 % C == 0:  # the start conv's weight gradient (narrow form)
+                s["part_start"] = e(max(1, lib.gwn_wgrad_partial_count(ts[0] * P, C, cfg.Cin)) * (C * cfg.Cin + C))
             if cfg.E % 32 == 0 and (cfg.OP // 32) * (cfg.E // 32) <= 16:  # end_conv_2's weight gradient
                 s["part_e2"] = e(max(1, lib.gwn_wgrad_partial_count(tf * P, cfg.OP, cfg.E)) * (cfg.OP * cfg.E + cfg.OP))
 
@@ -447,13 +449,16 @@ class Executor:
         arr = (ctypes.c_void_p * max(len(sups), 1))(*[s.data_ptr() for s in sups])
         return sups, arr
 
-    def forward(self, flat, fixed_sups, x, training, bn_bufs, acts=None, lead_pad=0, seed=None, sup_batch=1):
+    def forward(self, flat, fixed_sups, x, training, bn_bufs, acts=None, lead_pad=0, seed=None, sup_batch=1,
+                fixed_t=None):
         """x: reference NCHW input [B, Cin, N, T] (any strides).  ``lead_pad`` extra zero steps
         are prepended (engine.py:44) before the receptive-field pad (model.py:176-178).
         ``seed``: the dropout counter this forward (and its backward) draws its masks from
         (default: the executor's own, which the trainer advances after each step).
         ``sup_batch`` > 1: per-sample supports (gwnet_diff_G): each of ``fixed_sups`` is a padded
         [B][NP][NP] buffer, sample b of slice (t, b) diffusing with matrix b.
+        ``fixed_t``: padded transposes of ``fixed_sups`` kept by the caller (they change only with the
+        supports); the backward's transposes of the others are built here.
         Returns (out [B, O, N, T_f], acts)."""
         cfg = self.cfg
         C, N, L = cfg.C, cfg.N, cfg.L
@@ -493,13 +498,18 @@ class Executor:
             # transposed supports: the fused backward computes A·x as (A^T)^T·x on the forward kernel path
             if getattr(acts, "supT", None) is None or len(acts.supT) != len(sups) or acts.supT[0].numel() != sq * sup_batch:
                 acts.supT = [torch.empty(sup_batch * sq, device=self.device, dtype=F32) for _ in sups]
-            for s_, t_ in zip(sups, acts.supT):
+            nfix = len(fixed_t) if (fixed_t is not None and sup_batch <= 1 and cfg.use_gcn) else 0
+            for k, (s_, t_) in enumerate(zip(sups, acts.supT)):
+                if k < nfix:
+                    continue  # the caller's cached transpose (below)
                 if sup_batch > 1:
                     lib.call("gwn_pad_square_batched", ptr(s_), sup_batch, sq, N, cfg.NP, ptr(t_), cfg.NP, cfg.NP, sq,
                              1, st)
                 else:
                     lib.call("gwn_pad_square", ptr(s_), N, cfg.NP, ptr(t_), cfg.NP, cfg.NP, 1, st)
-            acts.supT_arr = (ctypes.c_void_p * len(sups))(*[t.data_ptr() for t in acts.supT])
+            acts.supT_arr = (ctypes.c_void_p * len(sups))(*[(fixed_t[k] if k < nfix else acts.supT[k]).data_ptr()
+                                                             for k in range(len(sups))])
+            acts.supT_keep = fixed_t  # alive as long as the activations reference them
         sx = x.stride()
         lib.call("gwn_start_conv_fwd", ptr(x), sx[0], sx[1], sx[2], sx[3], B, cin, N, t_in, ts[0],
                  ptr(self.pk("start_w")), ptr(self.pk("start_b")), C, ptr(acts.X[0]), ptr(acts.xin), st)
@@ -881,13 +891,21 @@ class Executor:
             dnext = dx
         if overlap:
             main.wait_event(side_done[0])  # dadp and every side-stream weight gradient are complete
+        # start conv
+        rows0 = ts[0] * P
+        if defer and "part_start" in sc:
+            part = sc["part_start"]
+            lib.call("gwn_wgrad_partials", ptr(dnext), C, C, ptr(acts.xin), cfg.Cin, rows0, cfg.Cin, 1, 0, rows0,
+                     None, None, None, ptr(part), st)
+            segs.append(_lib.ReduceSeg(part=ptr(part), nparts=_lib.load().gwn_wgrad_partial_count(rows0, C, cfg.Cin),
+                                       part_stride=C * cfg.Cin + C, J=C, Kc=cfg.Cin, out=ptr(self.gk("start_w")),
+                                       ld_out=cfg.Cin, out2=ptr(self.gk("start_b"))))
+        else:
+            wgrad(dnext, C, acts.xin, cfg.Cin, rows0, self.gk("start_w"), ws, self.gk("start_b"))
         if defer:
             for k in range(0, len(segs), 32):  # <= 32 segments per launch (include/gwn.h)
                 chunk = segs[k:k + 32]
                 lib.call("gwn_reduce_partials", (_lib.ReduceSeg * len(chunk))(*chunk), len(chunk), st)
-        # start conv
-        rows0 = ts[0] * P
-        wgrad(dnext, C, acts.xin, cfg.Cin, rows0, self.gk("start_w"), ws, self.gk("start_b"))
         if cfg.adp_live:
             lib.call("gwn_adaptive_adj_bwd", ptr(self.pk("nv1")), ptr(self.pk("nv2")), ptr(acts.adp),
                      ptr(sc["dadp"]), N, 10, cfg.NP, ptr(self.gk("nv1")), ptr(self.gk("nv2")), ptr(ws), st)

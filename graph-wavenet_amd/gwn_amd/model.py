@@ -290,7 +290,7 @@ class gwnet(nn.Module):
         self._flat = None
         self._flat_ptrs = None
         self._nbt = None
-        self._sup_cache = (None, None)
+        self._sup_cache = (None, None, None)
         self._place(device)
 
     def _add_layer(self, dilation):
@@ -373,7 +373,7 @@ class gwnet(nn.Module):
             dev = self._flat.device
             n = self.num_nodes
             np_ = (n + 31) // 32 * 32
-            padded = []
+            padded, padded_t = [], []
             for s in self.supports:
                 src = s.detach().to(dev, F32).contiguous()
                 if tuple(src.shape) != (n, n):
@@ -381,8 +381,17 @@ class gwnet(nn.Module):
                 dst = torch.empty(np_, np_, device=dev, dtype=F32)
                 _lib.call("gwn_pad_square", src.data_ptr(), n, n, dst.data_ptr(), np_, np_, 0, _lib.stream())
                 padded.append(dst)
-            self._sup_cache = (key, padded)
+                # and its padded transpose, for the fused backward (A x computed as (A^T)^T x)
+                dst_t = torch.empty(np_, np_, device=dev, dtype=F32)
+                _lib.call("gwn_pad_square", src.data_ptr(), n, n, dst_t.data_ptr(), np_, np_, 1, _lib.stream())
+                padded_t.append(dst_t)
+            self._sup_cache = (key, padded, padded_t)
         return self._sup_cache[1]
+
+    def _fixed_supports_t(self):
+        """Padded transposes of the fixed supports (cached with them, see _fixed_supports)."""
+        self._fixed_supports()
+        return self._sup_cache[2] if self.supports else []
 
     def _call_supports(self):
         """(padded supports, sup_batch) of the forward being run: gwnet's fixed supports."""
@@ -465,7 +474,7 @@ class gwnet_diff_G(gwnet):
         self._flat = None
         self._flat_ptrs = None
         self._nbt = None
-        self._sup_cache = (None, None)
+        self._sup_cache = (None, None, None)
         self._call = None
         self._place(device)
 
@@ -536,7 +545,9 @@ class _GwnetFn(torch.autograd.Function):
             seed = ex.seed.clone()
             _lib.call("gwn_increment_u64", _lib.ptr(ex.seed), 1, _lib.stream())
         sups, sup_batch = model._call_supports()
-        out, acts = ex.forward(model._flat, sups, x, training, model._bn_bufs(), seed=seed, sup_batch=sup_batch)
+        fixed_t = model._fixed_supports_t() if sup_batch <= 1 else None
+        out, acts = ex.forward(model._flat, sups, x, training, model._bn_bufs(), seed=seed, sup_batch=sup_batch,
+                               fixed_t=fixed_t)
         if training:
             model._nbt.add_(1)
         ctx.model = model

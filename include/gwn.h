@@ -374,7 +374,8 @@ int gwn_wgrad_bn(const float* dY, long ldy, int J, const float* X, long ldx, lon
 
 /* Deferred reduction (one launch for the weight gradients of a whole backward):
  * gwn_wgrad_partials writes the gwn_wgrad_partial_count(R, J, Kc) workgroup partials
- * [count][J*Kc + J] of a gwn_wgrad_bn problem without reducing them; gwn_reduce_partials then sums
+ * [count][J*Kc + J] of a gwn_wgrad_bn problem without reducing them (also for narrow 1x1 inputs,
+ * Kc <= 4 with J | 256: the start conv); gwn_reduce_partials then sums
  * every segment's partials in a fixed order (deterministic) in ONE launch: out [J][ld_out] = dW,
  * out2 [J] = db (may be NULL).  At most 32 segments per call. */
 typedef struct gwn_reduce_seg {

@@ -331,6 +331,32 @@ def test_deferred_wgrad_reduction_bitwise(gpu):
         assert torch.all(dw2[:, dw.shape[1]:] == 7.0)
 
 
+def test_narrow_wgrad_partials_vs_fp64(gpu):
+    """The narrow form of gwn_wgrad_partials (Kc <= 4: the start conv's dW [32][2] and db over all
+    positions) through gwn_reduce_partials, against fp64; ragged row counts."""
+    from gwn_amd import _lib
+    lib = _lib.load()
+    for R, J, Kc in ((172224, 32, 2), (1001, 32, 3), (37, 64, 1)):
+        torch.manual_seed(R + Kc)
+        dY = torch.randn(R, J, dtype=torch.float64)
+        X = torch.randn(R, Kc, dtype=torch.float64)
+        cnt = lib.gwn_wgrad_partial_count(R, J, Kc)
+        part = torch.empty(cnt * (J * Kc + J), device=gpu)
+        dYd, Xd = dY.float().to(gpu), X.float().to(gpu)
+        _lib.call("gwn_wgrad_partials", dYd.data_ptr(), J, J, Xd.data_ptr(), Kc, R, Kc, 1, 0, R, None, None, None,
+                  part.data_ptr(), _lib.stream())
+        dw, db = torch.empty(J, Kc, device=gpu), torch.empty(J, device=gpu)
+        seg = (_lib.ReduceSeg * 1)(_lib.ReduceSeg(part=part.data_ptr(), nparts=cnt, part_stride=J * Kc + J, J=J, Kc=Kc,
+                                                  out=dw.data_ptr(), ld_out=Kc, out2=db.data_ptr()))
+        _lib.call("gwn_reduce_partials", seg, 1, _lib.stream())
+        torch.cuda.synchronize()
+        ref_w, ref_b = dY.t() @ X, dY.sum(0)
+        bound_w = 2.0 ** -22 * R * (dY.abs().t() @ X.abs()) + 1e-30
+        bound_b = 2.0 ** -22 * R * dY.abs().sum(0) + 1e-30
+        assert torch.all((dw.double().cpu() - ref_w).abs() <= bound_w)
+        assert torch.all((db.double().cpu() - ref_b).abs() <= bound_b)
+
+
 def test_batchnorm_fwd_bwd(gpu):
     from gwn_amd import _lib
     torch.manual_seed(6)

@@ -1,6 +1,5 @@
 #!/bin/bash
-# scratch GPU command (one gpurun call): head kernels (thin-N / small-K NT GEMM, deferred end_conv_2
-# weight gradient): suite + bench + trace
+# scratch GPU command (one gpurun call): adaptive-adjacency backward + start conv wgrad changes
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
