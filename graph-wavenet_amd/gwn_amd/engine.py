@@ -111,6 +111,8 @@ class trainer():
         self.state = None
         self._acts = {}
         self._host_metrics = torch.zeros(4, dtype=F32).pin_memory() if torch.cuda.is_available() else None
+        self._metrics_ready = torch.cuda.Event() if torch.cuda.is_available() else None
+        self._metrics_early = False
         # HIP-graph replay of the fused training step (GWN_GRAPHS=0 disables): the ~240 launches
         # of a step are captured once per (shape, hyper-parameter) key and replayed
         self.use_graphs = os.environ.get("GWN_GRAPHS", "1") != "0"
@@ -120,6 +122,18 @@ class trainer():
     # ------------------------------------------------------------------------------------------
     def _phase_grads(self, input, real_val, training):
         """pad -> forward -> masked loss (+ its gradient) -> backward -> flat gradient buffer."""
+        m, acts, dout = self._phase_loss(input, real_val, training)
+        if training:
+            self._phase_backward(acts, dout)
+        return m
+
+    def _phase_backward(self, acts, dout):
+        ex = self.model._executor
+        ex.backward(acts, dout)
+        ex.unpack_grads(self.optimizer.grad_flat)
+
+    def _phase_loss(self, input, real_val, training):
+        """pad -> forward -> masked loss (+ its gradient); returns (metrics, saved state, dout)."""
         model = self.model
         ex = model._executor
         B, _, _, T = input.shape
@@ -138,10 +152,7 @@ class trainer():
         _lib.call("gwn_masked_loss", ptr(out), ptr(real_val), rs[0], rs[1], rs[2], B, ex.cfg.O, ex.cfg.N,
                   ts[-1], float(self.scaler.mean), float(self.scaler.std), ptr(sc["metrics"]), ptr(dout),
                   ptr(sc["ws"]), _lib.stream())
-        if training:
-            ex.backward(acts, dout)
-            ex.unpack_grads(self.optimizer.grad_flat)
-        return sc["metrics"]
+        return sc["metrics"], acts, dout
 
     def _eval_lean(self, input, real_val):
         """engine.py:119-130 on the lean inference schedule: pad 1, eval forward (no saved state),
@@ -199,29 +210,41 @@ class trainer():
         return m
 
     def _capture(self, key, input, real_val):
-        """Capture the step as one graph (single process) or two graphs around the gradient
-        all-reduce (data parallel: the collective stays eager)."""
+        """Capture the step as graphs: g0 = forward + loss, g1 = backward (+ clip + Adam in a single
+        process; data parallel: the all-reduce stays eager between g1 and g2 = clip + Adam).  The
+        metrics are read back between g0 and g1 (_replay), so train() returns while the GPU still
+        runs the backward and the host prepares the next step meanwhile: no idle GPU between steps."""
         sx = torch.empty_like(input).copy_(input)
         sy = torch.empty_like(real_val).copy_(real_val)
         torch.cuda.synchronize()
+        g0 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g0):
+            m, acts, dout = self._phase_loss(sx, sy, True)
         g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1):
-            m = self._phase_grads(sx, sy, True)
+        with torch.cuda.graph(g1, pool=g0.pool()):
+            self._phase_backward(acts, dout)
             if not self._distributed():
                 self._phase_update()
         g2 = None
         if self._distributed():
             g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2):
+            with torch.cuda.graph(g2, pool=g0.pool()):
                 self._phase_update()
-        self._graphs[key] = (g1, g2, sx, sy, m)
+        # dout lives in g0's pool and is read by g1: the entry keeps it (and acts) referenced
+        self._graphs[key] = (g0, g1, g2, sx, sy, m, (acts, dout))
 
     def _replay(self, key, input, real_val):
-        g1, g2, sx, sy, m = self._graphs[key]
+        g0, g1, g2, sx, sy, m, _ = self._graphs[key]
         if sx.data_ptr() != input.data_ptr():
             sx.copy_(input)
         if sy.data_ptr() != real_val.data_ptr():
             sy.copy_(real_val)
+        g0.replay()
+        if self._host_metrics is not None:
+            # the three metrics leave as soon as the loss is known; _read waits for this event only
+            self._host_metrics[:3].copy_(m[:3], non_blocking=True)
+            self._metrics_ready.record()
+            self._metrics_early = True
         g1.replay()
         if g2 is not None:
             self._allreduce_grads()
@@ -278,7 +301,14 @@ class trainer():
         return self._read(m)
 
     def _read(self, m):
-        if self._host_metrics is not None:
+        if self._metrics_early:
+            # replayed step: the metrics were copied right after the loss; the backward and the
+            # update stay queued behind them (stream order keeps every later use of the parameters
+            # and gradients correct, as for any asynchronous torch work)
+            self._metrics_early = False
+            self._metrics_ready.synchronize()
+            v = self._host_metrics.tolist()
+        elif self._host_metrics is not None:
             self._host_metrics[:3].copy_(m[:3], non_blocking=True)
             torch.cuda.current_stream().synchronize()
             v = self._host_metrics.tolist()
