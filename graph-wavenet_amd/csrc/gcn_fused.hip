@@ -50,6 +50,7 @@ struct FusedFwd {
   const float* bn_rm; const float* bn_rv; const float* bn_g; const float* bn_b; float bn_eps; float* x_out;
   long sup_bstride; int sup_batch;  // per-sample supports (sup_batch > 1): sample b = slice % sup_batch
   const float* res_mean; const float* res_scale; const float* res_shift;  // (residual - mean) * scale + shift
+  int ksplit, slices; float* kws; int* kcnt;  // support split (ksplit > 1): see unit_of()
 };
 
 struct FusedBwd {
@@ -66,6 +67,7 @@ struct FusedBwd {
   // optional gate-backward epilogue (dfg instead of dxg)
   const float* fg; const float* dskip; long ld_dskip; long skip_row0; float* dfg;
   long sup_bstride; int sup_batch;  // per-sample supports, as FusedFwd
+  int ksplit, slices; float* kws; int* kcnt;  // support split, as FusedFwd
 };
 
 // support k of this workgroup's slice (per-sample supports: sample = slice % sup_batch)
@@ -75,6 +77,75 @@ __device__ __forceinline__ const float* slice_sup(const Args& a, const float* ba
 }
 
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+// Work unit of this workgroup: a whole slice (ksplit <= 1), or support k0 of a slice (ksplit = nsup
+// workgroups per slice).  The ksplit units of a slice are blockIdx i, i + 8, i + 16, ...: with the
+// round-robin workgroup-to-XCD dispatch they share one XCD's L2 (partial sums written and read
+// there).  Returns false for the padding workgroups of the last group of 8 slices.
+struct Unit {
+  int slice, k0, k1;
+};
+template <typename Args>
+__device__ __forceinline__ bool unit_of(const Args& a, Unit& u) {
+  if (a.ksplit <= 1) {
+    u.slice = blockIdx.x; u.k0 = 0; u.k1 = a.nsup;
+    return true;
+  }
+  const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+  u.k0 = j % a.ksplit; u.k1 = u.k0 + 1;
+  u.slice = (j / a.ksplit) * 8 + x;
+  return u.slice < a.slices;
+}
+
+// Support split hand-off (MI355X_MICROARCH.md, inter-workgroup visibility: write-through payload,
+// counter add behind a barrier, write-through loads by the last arriver; no L2 write-back fence --
+// an agent release per unit, i.e. a buffer_wbl2 of the XCD's L2 full of fresh hop pieces, cost
+// ~50 us per launch).  cache-policy aux 16 = sc1 (write-through store / L1-bypassing load).
+constexpr int SC1 = 16;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// partial D'[c][w] tile -> rows w of part [n][32] as 16-B sc1 stores (rows >= n dropped by the
+// buffer range)
+__device__ __forceinline__ void acc_to_part(float* part, int n, const f32x16& d, int w0, int lane) {
+  const int half = lane >> 5, col = lane & 31;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)part, (short)0, n * CH * 4, 0x00020000);
+  const int voff = (w0 + col) * CH * 4;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    // (hipcc 7.2 splats {bit_cast(unsigned, d[i]), ...} to d[0]: go through float4)
+    const float4 v = make_float4(d[4 * g], d[4 * g + 1], d[4 * g + 2], d[4 * g + 3]);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff + crow(4 * g, half) * 4, 0, SC1);
+  }
+}
+
+// count this unit's (already stored) partial; true in the slice's last unit to arrive, which also
+// resets the counter for the next launch
+__device__ __forceinline__ bool split_arrive(int* cnt, int parts, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's partial stores have completed
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = (atomicAdd(cnt, 1) == parts - 1);
+  __syncthreads();
+  if (!*flag) return false;
+  if (threadIdx.x == 0) atomicExch(cnt, 0);
+  return true;
+}
+
+// sum of the parts partials [parts][np][32] of a slice, in part order, into LDS rows [n][LDR]
+// (16-B sc1 loads)
+__device__ __forceinline__ void split_sum_to_lds(const float* part, int parts, int n, int np, float* buf) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)part, (short)0, parts * np * CH * 4, 0x00020000);
+  for (int e = threadIdx.x; e < n * 8; e += blockDim.x) {
+    float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, e * 16, 0, SC1));
+    for (int p = 1; p < parts; ++p) {
+      const float4 q = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, e * 16, p * np * CH * 4, SC1));
+      v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+    }
+    float* b = buf + (e >> 3) * LDR + 4 * (e & 7);
+    b[0] = v.x; b[1] = v.y; b[2] = v.z; b[3] = v.w;
+  }
+}
+
 
 // bf16 kernels: support batches prefetched ahead of their MFMAs (whole hop up to this many)
 #ifndef GWN_BF16_PD
@@ -296,7 +367,7 @@ __device__ __forceinline__ f32x16 zero16() {
 // epilogue: index m*32 + c), residual -> z (+ per-slice BN partials), or -> bn(z) in eval mode
 template <int NEPT>
 __device__ __forceinline__ void fwd_epilogue(const FusedFwd& a, float* ys, float* red0, float* red1, long row0,
-                                             int n) {
+                                             int n, int slice) {
   const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
   const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
   const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
@@ -361,7 +432,7 @@ __device__ __forceinline__ void fwd_epilogue(const FusedFwd& a, float* ys, float
   if (threadIdx.x < 32) {
     float m2 = 0.0f;
     for (int i = 0; i < ngroups; ++i) m2 += red1[i * 32 + c];
-    float* pp = a.bn_part + (long)blockIdx.x * 3 * CH;
+    float* pp = a.bn_part + (long)slice * 3 * CH;
     pp[c] = (float)n;
     pp[CH + c] = mean;
     pp[2 * CH + c] = m2;
@@ -372,12 +443,13 @@ __device__ __forceinline__ void fwd_epilogue(const FusedFwd& a, float* ys, float
 // BatchNorm backward of this layer's output (same arithmetic as bn_bwd_apply_kernel, ops.hip):
 //   dz = gamma*rstd*(dy - k1 - xhat*k2) -> residual gradient dres; dropout'(dz) -> dh (LDS + HBM)
 template <int NEPT, bool PL = false>
-__device__ __forceinline__ void bwd_prologue(const FusedBwd& a, float* dhs, long row0, int n, int np) {
+__device__ __forceinline__ void bwd_prologue(const FusedBwd& a, float* dhs, long row0, int n, int np,
+                                             bool lead = true, bool first = blockIdx.x == 0) {
   if (!a.bn_dy) {
     global_to_lds<PL>(a.dh + row0 * CH, CH, n, np, dhs);
     return;
   }
-  if (blockIdx.x == 0 && threadIdx.x < CH) {
+  if (first && threadIdx.x < CH) {
     if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
     if (a.bn_dgamma) a.bn_dgamma[threadIdx.x] = a.bn_sums[CH + threadIdx.x];
   }
@@ -401,13 +473,13 @@ __device__ __forceinline__ void bwd_prologue(const FusedBwd& a, float* dhs, long
       const long idx = (row0 + w) * CH + c;
       const float xhat = (zv[i] - mu) * rs;
       const float dz = gm * rs * (dy[i] - k1 - xhat * k2);
-      a.dres[idx] = dz;
+      if (lead) a.dres[idx] = dz;
       v = dz;
       if (a.drop_p > 0.0f) {
         const float u = gwn_uniform(seed, a.salt, (unsigned long long)idx);
         v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
       }
-      a.dh_out[idx] = v;
+      if (lead) a.dh_out[idx] = v;
     }
     if (w < np) dhs[img_idx<PL>(w, c, np)] = v;
   }
@@ -454,6 +526,9 @@ template <int MAXT, bool HL>
 __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a) {
   extern __shared__ float lds[];
   __shared__ float red[2][MAXT];
+  __shared__ int last_unit;
+  Unit u;
+  if (!unit_of(a, u)) return;
   const int n = a.n;
   const int nkb = (n + 31) >> 5;
   const int np = nkb * 32;
@@ -462,7 +537,7 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, w0 = wave * 32;
   const bool compute = wave < nkb;
   const bool store_wave = (int)(blockDim.x >> 6) > nkb;  // block-uniform
-  const long row0 = (long)blockIdx.x * n;
+  const long row0 = (long)u.slice * n;
   const long ldh = a.ld_h, pstride = CH;  // piece p of row w at hs + w*ldh + p*pstride
   const float* hs = a.h + row0 * ldh;
   // hop pieces: by the store wave (whole rows through LDS), else straight from the accumulators
@@ -484,12 +559,12 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
   const unsigned long long t_cyc0 = __builtin_amdgcn_s_memtime(), t_real0 = __builtin_amdgcn_s_memrealtime();
 #endif
   // software pipeline: every G first batch / W fragment set is issued one phase before use
-  GBatch g0 = (a.nsup > 0 && compute) ? g_first(slice_sup(a, a.sup[0]), a.ld_sup, nkb, w0, lane) : GBatch{};
+  GBatch g0 = (u.k1 > u.k0 && compute) ? g_first(slice_sup(a, a.sup[u.k0]), a.ld_sup, nkb, w0, lane) : GBatch{};
   global_to_lds(hs, ldh, n, np, xs);
   __syncthreads();
   f32x16 hacc = zero16();
-  if (compute) hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
-  for (int k = 0; k < a.nsup; ++k) {
+  if (compute && u.k0 == 0) hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
+  for (int k = u.k0; k < u.k1; ++k) {
     const float* G = slice_sup(a, a.sup[k]);
     f32x16 d = zero16();
     if (compute) {
@@ -510,7 +585,7 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
 #endif
     if (compute) {
       d = diffuse<HL>(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
-      if (k + 1 < a.nsup) g0 = g_first(slice_sup(a, a.sup[k + 1]), a.ld_sup, nkb, w0, lane);
+      if (k + 1 < u.k1) g0 = g_first(slice_sup(a, a.sup[k + 1]), a.ld_sup, nkb, w0, lane);
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
       hacc = mlp_from_acc(wf, d, hacc);
       if (a.store_pieces && !store_wave) acc_to_global((float*)hs + (2 + 2 * k) * pstride, ldh, d, w0, lane, n);
@@ -525,9 +600,16 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
     }
   }
   __syncthreads();
-  if (compute) acc_to_lds(ys, hacc, w0, lane);
+  if (a.ksplit > 1) {  // partial mlp sum of this support; the slice's last unit runs the epilogue
+    float* part = a.kws + (long)u.slice * a.ksplit * np * CH;
+    if (compute) acc_to_part(part + (long)u.k0 * np * CH, n, hacc, w0, lane);
+    if (!split_arrive(a.kcnt + u.slice, a.ksplit, &last_unit)) return;
+    split_sum_to_lds(part, a.ksplit, n, np, ys);
+  } else if (compute) {
+    acc_to_lds(ys, hacc, w0, lane);
+  }
   __syncthreads();
-  fwd_epilogue<EPT>(a, ys, red[0], red[1], row0, n);
+  fwd_epilogue<EPT>(a, ys, red[0], red[1], row0, n, u.slice);
 #if GWN_EXP & 256
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -545,19 +627,23 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
 template <int MAXT, bool HL>
 __global__ __launch_bounds__(MAXT, 4) void gcn_bwd_fused_kernel(const FusedBwd a) {
   extern __shared__ float lds[];
+  __shared__ int last_unit;
+  Unit un;
+  if (!unit_of(a, un)) return;
   const int n = a.n;
   const int nkb = (int)(blockDim.x >> 6);
   const int np = nkb * 32;
   float* dhs = lds;
   float* buf = lds + np * LDR;
   const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
-  const long row0 = (long)blockIdx.x * n;
+  const long row0 = (long)un.slice * n;
 
-  GBatch g0 = (a.nsup > 0) ? g_first(slice_sup(a, a.supT[0]), a.ld_sup, nkb, w0, lane) : GBatch{};
-  bwd_prologue<EPT>(a, dhs, row0, n, np);
+  GBatch g0 = (un.k1 > un.k0) ? g_first(slice_sup(a, a.supT[un.k0]), a.ld_sup, nkb, w0, lane) : GBatch{};
+  // the BN-backward prologue's HBM outputs (dres, dh, BN dgamma / dbeta) come from support 0's unit
+  bwd_prologue<EPT>(a, dhs, row0, n, np, un.k0 == 0, un.slice == 0 && un.k0 == 0);
   __syncthreads();
-  f32x16 dx = mlpT_from_lds(a.w_mlp, a.ld_w, 0, dhs, w0, lane, zero16());
-  for (int k = 0; k < a.nsup; ++k) {
+  f32x16 dx = (un.k0 == 0) ? mlpT_from_lds(a.w_mlp, a.ld_w, 0, dhs, w0, lane, zero16()) : zero16();
+  for (int k = un.k0; k < un.k1; ++k) {
     const float* GT = slice_sup(a, a.supT[k]);
     {
       const f32x16 u = mlpT_from_lds(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, w0, lane, zero16());
@@ -574,7 +660,21 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_bwd_fused_kernel(const FusedBwd a
     if (k == a.adp_index) acc_to_global(a.t1 + row0 * a.ld_t, a.ld_t, t, w0, lane, n);
     __syncthreads();
     dx = diffuse<HL>(buf, GT, a.ld_sup, nkb, w0, lane, dx, g0);  // dxg += A dx1
-    if (k + 1 < a.nsup) g0 = g_first(slice_sup(a, a.supT[k + 1]), a.ld_sup, nkb, w0, lane);
+    if (k + 1 < un.k1) g0 = g_first(slice_sup(a, a.supT[k + 1]), a.ld_sup, nkb, w0, lane);
+  }
+  if (a.ksplit > 1) {  // partial input gradient of this support; the slice's last unit finishes
+    float* part = a.kws + (long)un.slice * a.ksplit * np * CH;
+    acc_to_part(part + (long)un.k0 * np * CH, n, dx, w0, lane);
+    if (!split_arrive(a.kcnt + un.slice, a.ksplit, &last_unit)) return;
+    split_sum_to_lds(part, a.ksplit, n, np, buf);
+    __syncthreads();
+    if (a.dfg) {
+      bwd_gate_epilogue<EPT>(a, buf, row0, n);
+    } else {
+      for (int e = threadIdx.x; e < n * CH; e += blockDim.x)
+        a.dxg[(row0 + (e >> 5)) * a.ld_dxg + (e & 31)] = buf[(e >> 5) * LDR + (e & 31)];
+    }
+    return;
   }
   if (!a.dfg) {
     acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
@@ -757,7 +857,7 @@ __global__ __launch_bounds__(256, 2) void gcn_fwd_fused4_kernel(const FusedFwd a
   for (int i = 0; i < TPW; ++i)
     if (tv[i]) acc_to_lds(ys, hacc[i], w0[i], lane);
   __syncthreads();
-  fwd_epilogue<EPT4>(a, ys, red[0], red[1], row0, n);
+  fwd_epilogue<EPT4>(a, ys, red[0], red[1], row0, n, blockIdx.x);
 }
 
 __global__ __launch_bounds__(256, 2) void gcn_bwd_fused4_kernel(const FusedBwd a) {
@@ -1051,7 +1151,7 @@ __global__ __launch_bounds__(256, 2) void gcn_fwd_bal_kernel(const FusedFwd a) {
     bal_to_rows<NKB, true>(S, hacc[1], 16, hw, lane);
   }
   __syncthreads();
-  fwd_epilogue<4 * NKB>(a, S, red[0], red[1], row0, n);
+  fwd_epilogue<4 * NKB>(a, S, red[0], red[1], row0, n, blockIdx.x);
 }
 
 template <int NKB>
@@ -1160,6 +1260,34 @@ int auto_layout() {
     default: break;                                                                          \
   }
 
+// Support split policy.  Measured per layer (round 2, n = 207, B = 64, 256 CUs; fwd / bwd us,
+// whole slices -> split): a unit costs about half a slice, not a third (it still stages the whole
+// slice in LDS, hands off its partial sum and one of three runs the epilogue), so the split only pays
+// where the whole-slice launch leaves most CUs idle: 64 slices 63.5 -> 37.8 (fwd); 192 slices
+// 68 -> 78 / 67 -> 79; 448 slices 115 -> 147 / 111 -> 148; 640 slices 174 -> 212 / 167 -> 201.
+// Default: split when every unit gets a CU of its own (slices * nsup <= CUs); GWN_KSPLIT_SLICES
+// overrides with a slice-count threshold (0 = never split).
+int ksplit_max_slices(int nsup) {
+  static int v = [] {
+    const char* e = getenv("GWN_KSPLIT_SLICES");
+    if (e) return atoi(e);
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 0;
+    return -cus;  // negative: a CU count, divided by nsup below
+  }();
+  return v >= 0 ? v : (-v) / nsup;
+}
+
+template <typename G>
+int pick_ksplit(const G* g, int slices, int nwt) {
+  if (!g->ksplit_ws || !g->ksplit_count || g->nsup < 2 || g->ksplit == 1 || g->sup_batch > 1 || nwt > 15)
+    return 1;
+  if (g->ksplit == g->nsup) return g->nsup;
+  return slices <= ksplit_max_slices(g->nsup) ? g->nsup : 1;
+}
+
 }  // namespace
 
 bool gwn_gcn_fused_eligible(int c, int n, int nsup, int ld_sup) {
@@ -1188,6 +1316,8 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.bn_eps = g->bn_eps; a.x_out = g->bn_out;
   a.sup_bstride = g->sup_bstride; a.sup_batch = g->sup_batch;
   a.res_mean = g->residual_mean; a.res_scale = g->residual_scale; a.res_shift = g->residual_shift;
+  a.ksplit = 1; a.slices = g->rows / g->n; a.kws = g->ksplit_ws; a.kcnt = g->ksplit_count;
+  GWN_REQUIRE(g->ksplit == 0 || g->ksplit == 1 || g->ksplit == g->nsup, "gcn_fwd: ksplit must be 0, 1 or nsup");
   GWN_REQUIRE(!a.res_scale == !a.res_shift && !a.res_scale == !a.res_mean,
               "gcn_fwd (fused): residual_mean, residual_scale and residual_shift go together");
   if (a.sup_batch > 1)
@@ -1223,12 +1353,14 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
     // + one store wave when hop pieces are stored through LDS rows (h 16-B aligned, ld % 4 == 0)
     const bool rows_ok = !(GWN_EXP & 32) && ((((uintptr_t)a.h) & 15) | (a.ld_h & 3)) == 0;
     const int waves = nwt + ((a.store_pieces && rows_ok && nwt < 16) ? 1 : 0);
+    a.ksplit = pick_ksplit(g, slices, nwt);
+    const int grid = a.ksplit > 1 ? (slices + 7) / 8 * 8 * a.ksplit : slices;
     if (half_last_batch(g->n)) {
-      if (waves <= 8) gcn_fwd_fused_kernel<512, true><<<slices, 64 * waves, lds, s>>>(a);
-      else gcn_fwd_fused_kernel<1024, true><<<slices, 64 * waves, lds, s>>>(a);
+      if (waves <= 8) gcn_fwd_fused_kernel<512, true><<<grid, 64 * waves, lds, s>>>(a);
+      else gcn_fwd_fused_kernel<1024, true><<<grid, 64 * waves, lds, s>>>(a);
     } else {
-      if (waves <= 8) gcn_fwd_fused_kernel<512, false><<<slices, 64 * waves, lds, s>>>(a);
-      else gcn_fwd_fused_kernel<1024, false><<<slices, 64 * waves, lds, s>>>(a);
+      if (waves <= 8) gcn_fwd_fused_kernel<512, false><<<grid, 64 * waves, lds, s>>>(a);
+      else gcn_fwd_fused_kernel<1024, false><<<grid, 64 * waves, lds, s>>>(a);
     }
   }
   GWN_CHECK_LAUNCH();
@@ -1255,6 +1387,8 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   a.seed_ptr = g->seed_ptr; a.salt = g->salt; a.drop_p = g->drop_p; a.inv_rows = 1.0f / (float)g->rows;
   a.fg = g->fg; a.dskip = g->dskip; a.ld_dskip = g->ld_dskip; a.skip_row0 = g->skip_row0; a.dfg = g->dfg;
   a.sup_bstride = g->sup_bstride; a.sup_batch = g->sup_batch;
+  a.ksplit = 1; a.slices = g->rows / g->n; a.kws = g->ksplit_ws; a.kcnt = g->ksplit_count;
+  GWN_REQUIRE(g->ksplit == 0 || g->ksplit == 1 || g->ksplit == g->nsup, "gcn_bwd: ksplit must be 0, 1 or nsup");
   if (a.sup_batch > 1)
     GWN_REQUIRE((g->rows / g->n) % a.sup_batch == 0 && g->adp_index < 0,
                 "gcn_bwd (per-sample supports): slices must be a multiple of sup_batch, adp_index -1");
@@ -1284,12 +1418,16 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
                 "gcn_bwd (fused): layout 3 (balanced) needs n <= 256 and 16-B rows of dxg / t1 / t2");
     GWN_BAL_SWITCH(gcn_bwd_bal_kernel)
   } else if (use_4wave(layout, nwt)) gcn_bwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
-  else if (half_last_batch(g->n)) {
-    if (nwt <= 8) gcn_bwd_fused_kernel<512, true><<<slices, 64 * nwt, lds, s>>>(a);
-    else gcn_bwd_fused_kernel<1024, true><<<slices, 64 * nwt, lds, s>>>(a);
-  } else {
-    if (nwt <= 8) gcn_bwd_fused_kernel<512, false><<<slices, 64 * nwt, lds, s>>>(a);
-    else gcn_bwd_fused_kernel<1024, false><<<slices, 64 * nwt, lds, s>>>(a);
+  else {
+    a.ksplit = pick_ksplit(g, slices, nwt);
+    const int grid = a.ksplit > 1 ? (slices + 7) / 8 * 8 * a.ksplit : slices;
+    if (half_last_batch(g->n)) {
+      if (nwt <= 8) gcn_bwd_fused_kernel<512, true><<<grid, 64 * nwt, lds, s>>>(a);
+      else gcn_bwd_fused_kernel<1024, true><<<grid, 64 * nwt, lds, s>>>(a);
+    } else {
+      if (nwt <= 8) gcn_bwd_fused_kernel<512, false><<<grid, 64 * nwt, lds, s>>>(a);
+      else gcn_bwd_fused_kernel<1024, false><<<grid, 64 * nwt, lds, s>>>(a);
+    }
   }
   GWN_CHECK_LAUNCH();
   return GWN_OK;
@@ -1598,7 +1736,7 @@ __global__ __launch_bounds__(64 * NKB) void gcn_fwd_split_kernel(const FusedFwd 
   __syncthreads();
   acc_to_lds((float*)xs, hacc, w0, lane);
   __syncthreads();
-  fwd_epilogue<EPT>(a, (float*)xs, red[0], red[1], row0, n);
+  fwd_epilogue<EPT>(a, (float*)xs, red[0], red[1], row0, n, blockIdx.x);
 }
 
 // dst[s][p][w][v] (bf16, [np][ld_dst] per plane) = piece p of G_s^T, G_s = padded support [np][ld_src]

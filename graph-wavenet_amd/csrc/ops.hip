@@ -1057,6 +1057,11 @@ long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup) {
   return g > w ? g : w;
 }
 
+long gwn_gcn_ksplit_ws_floats(int rows, int n, int nsup) {
+  if (rows <= 0 || n <= 0 || nsup <= 0) return 0;
+  return (long)(rows / n) * nsup * ((n + 31) / 32 * 32) * 32;
+}
+
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_bwd: rows must be slices*n");
   const int c = a->c, n = a->n, slices = a->rows / n;

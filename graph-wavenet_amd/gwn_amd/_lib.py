@@ -86,6 +86,7 @@ class GcnArgs(ctypes.Structure):
         ("w_split", c_void_p),
         ("sup_bstride", c_long), ("sup_batch", c_int),
         ("residual_mean", c_void_p), ("residual_scale", c_void_p), ("residual_shift", c_void_p),
+        ("ksplit", c_int), ("ksplit_ws", c_void_p), ("ksplit_count", c_void_p),
     ]
 
 
@@ -122,6 +123,7 @@ class GcnBwdArgs(ctypes.Structure):
         ("split_planes", c_int),
         ("supT_split", c_void_p), ("sup_split_stride", c_long), ("ld_split", c_int),
         ("wT_split", c_void_p),
+        ("ksplit", c_int), ("ksplit_ws", c_void_p), ("ksplit_count", c_void_p),
     ]
 
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time
@@ -166,6 +168,7 @@ _SIGS = [
     ("gwn_bf16_mlpT_weights", c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p]),
     ("gwn_gcn_bwd", c_int, [ctypes.POINTER(GcnBwdArgs), c_void_p]),
     ("gwn_gcn_bwd_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
+    ("gwn_gcn_ksplit_ws_floats", c_long, [c_int, c_int, c_int]),
     ("gwn_wgrad", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,
                           c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     ("gwn_wgrad_workspace_floats", c_long, [c_int, c_int, c_int]),

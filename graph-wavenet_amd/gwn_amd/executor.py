@@ -430,6 +430,11 @@ class Executor:
         for (M_, N_, K_) in ((cfg.O, cfg.E, tf * P), (cfg.E, cfg.S, tf * P), (cfg.S, L * C, tf * P)):
             side_need.append(lib.gwn_gemm_workspace_floats(M_, N_, _ksplit(M_, N_, K_)))
         s["ws_side"] = e(int(max(side_need)) + 16)
+        # support split of the fused gcn kernels (gwn_gcn_args.ksplit): partial sums + per-slice
+        # counters (zero, and left zero by every launch)
+        if self._fused_gcn() and cfg.use_gcn and cfg.nsup >= 2:
+            s["kws"] = e(int(lib.gwn_gcn_ksplit_ws_floats(maxrows, N, cfg.nsup)))
+            s["kcnt"] = torch.zeros(maxrows // N, device=self.device, dtype=torch.int32)
         self._scratch[key] = s
         return s
 
@@ -565,7 +570,7 @@ class Executor:
                               no_pieces=1 if i == L - 1 and self._fused_gcn() else 0,
                               sup_bstride=sq if sup_batch > 1 else 0, sup_batch=sup_batch,
                               residual_mean=raff[0], residual_scale=raff[1], residual_shift=raff[2],
-                              **self.split_fields(sp, i))
+                              **self.split_fields(sp, i), **self.ksplit_fields(scr))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
             rm, rv, mom, eps = bn_bufs[i]
@@ -598,6 +603,13 @@ class Executor:
         if tail_done is not None:
             main.wait_event(tail_done)
         return out, acts
+
+    @staticmethod
+    def ksplit_fields(scr):
+        """gwn_gcn_args / gwn_gcn_bwd_args fields of the support split (auto policy in the library)."""
+        if "kws" not in scr:
+            return {}
+        return {"ksplit": 0, "ksplit_ws": scr["kws"].data_ptr(), "ksplit_count": scr["kcnt"].data_ptr()}
 
     def _fused_gcn(self):
         """gwn_gcn_fwd takes the fused path (c == 32, n <= 512, nsup <= 8; include/gwn.h)."""
@@ -831,7 +843,8 @@ class Executor:
                                      accumulate_dadp=0 if first_adp else 1, workspace=ptr(ws),
                                      sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
                                      if acts.supT_arr is not None else None,
-                                     skip_weight_grads=1 if (overlap or defer) else 0)
+                                     skip_weight_grads=1 if (overlap or defer) else 0,
+                                     **self.ksplit_fields(sc))
                 sb = getattr(acts, "sup_batch", 1)
                 if sb > 1:
                     gb.sup_bstride, gb.sup_batch = cfg.NP * cfg.NP, sb

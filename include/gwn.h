@@ -271,6 +271,16 @@ typedef struct gwn_gcn_args {
    * (residual - residual_mean[j]) * residual_scale[j] + residual_shift[j]
    * (BatchNorm applied on load with gwn_batchnorm_fwd_fold's mean / scale and the BN bias). */
   const float* residual_mean; const float* residual_scale; const float* residual_shift;
+  /* support split (fused tile-wave path, shared supports, nsup >= 2): each slice becomes nsup
+   * workgroups, one per support (its two hops + its share of the mlp, piece 0 with support 0),
+   * whose partial mlp sums [np][c] go to ksplit_ws; the last of them to finish (ksplit_count[slice],
+   * a device counter that is zero on entry and left zero) adds them in support order and runs the
+   * epilogue.  Finer work units for layers with too few slices to occupy the chip (a unit costs
+   * about half a slice, so auto splits only when slices * nsup <= CUs; GWN_KSPLIT_SLICES = a slice
+   * threshold overrides).  ksplit: 0 = auto,
+   * 1 = off, nsup = always.  ksplit_ws: gwn_gcn_ksplit_ws_floats(rows, n, nsup) floats,
+   * ksplit_count: rows / n ints; NULL = no split. */
+  int ksplit; float* ksplit_ws; int* ksplit_count;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -350,9 +360,15 @@ typedef struct gwn_gcn_bwd_args {
   int split_planes;
   const void* supT_split; long sup_split_stride; int ld_split;
   const void* wT_split;
+  /* support split of the fused f32 backward, as gwn_gcn_args (partial input gradients, the last
+   * workgroup of a slice adds them in support order and runs the store / gate epilogue) */
+  int ksplit; float* ksplit_ws; int* ksplit_count;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);
+/* partial-sum floats of the support split (gwn_gcn_args.ksplit_ws / gwn_gcn_bwd_args.ksplit_ws):
+ * (rows / n) * nsup * 32*ceil(n/32) * 32 */
+long gwn_gcn_ksplit_ws_floats(int rows, int n, int nsup);
 
 /* ---------------------------------------------------------------------------------------------
  * Weight + bias gradients of a channels-last 1x1 / dilated conv, the row reduction

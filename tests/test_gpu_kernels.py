@@ -457,12 +457,14 @@ def test_gemm_nt(gpu, M, N, K, epi):
 @pytest.mark.parametrize("n", [16, 96, 207, 256])
 def test_gcn_fused_layouts_agree(gpu, n):
     """The wave layouts of the fused gcn forward / backward (one wave per 32-node tile, 4-wave,
-    balanced 16x16 quarters) against each other and against fp64 (model.py:41-55): hop pieces,
-    z, BN partials, dxg and the adaptive-support pieces t1 / t2."""
+    balanced 16x16 quarters) and the support split of the tile-wave layout (one workgroup per
+    (slice, support), partial sums combined by the slice's last workgroup) against each other and
+    against fp64 (model.py:41-55): hop pieces, z, BN partials, dxg and the adaptive-support pieces
+    t1 / t2."""
     import ctypes
     from gwn_amd import _lib
     torch.manual_seed(n)
-    C, K, S = 32, 3, 5
+    C, K, S = 32, 3, 11
     NP = (n + 31) // 32 * 32
     W = (2 * K + 1) * C
     rows = S * n
@@ -481,7 +483,10 @@ def test_gcn_fused_layouts_agree(gpu, n):
     dh = torch.randn(rows, C, device=gpu)
     seed = torch.zeros(1, device=gpu, dtype=torch.int64)
     outs = []
-    for layout in (1, 0, 3):
+    kws = torch.empty(_lib.load().gwn_gcn_ksplit_ws_floats(rows, n, K), device=gpu)
+    kcnt = torch.zeros(S, device=gpu, dtype=torch.int32)
+    for layout, ksplit in ((1, 1), (0, 1), (3, 1), (1, K)):
+        kf = dict(ksplit=ksplit, ksplit_ws=kws.data_ptr(), ksplit_count=kcnt.data_ptr())
         h = torch.zeros(rows, W, device=gpu)
         h[:, :C] = xg
         z = torch.empty(rows, C, device=gpu)
@@ -489,17 +494,18 @@ def test_gcn_fused_layouts_agree(gpu, n):
         ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)),
                           ld_sup=NP, h=h.data_ptr(), ld_h=W, w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(),
                           residual=res.data_ptr(), z=z.data_ptr(), seed_ptr=seed.data_ptr(), salt=0, drop_p=0.0,
-                          bn_partials=bnp.data_ptr(), layout=layout)
+                          bn_partials=bnp.data_ptr(), layout=layout, **kf)
         _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
         dhc = torch.zeros(rows, W, device=gpu)
         gb = _lib.GcnBwdArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)),
                              ld_sup=NP, h=h.data_ptr(), ld_h=W, w_mlp=wm.data_ptr(), dh=dh.data_ptr(),
                              dhcat=dhc.data_ptr(), ld_dhcat=W, adp_index=K - 1, accumulate_dadp=0,
                              sup_t=ctypes.cast(arrT, ctypes.POINTER(ctypes.c_void_p)), skip_weight_grads=1,
-                             layout=layout)
+                             layout=layout, **kf)
         _lib.call("gwn_gcn_bwd", ctypes.byref(gb), _lib.stream())
         torch.cuda.synchronize()
         outs.append((h.clone(), z.clone(), bnp.clone(), dhc.clone()))
+        assert int(kcnt.abs().sum()) == 0  # the split leaves its counters zero
     # fp64 truth
     X = xg.double().cpu().view(S, n, C)
     A = [s[:n, :n].double().cpu() for s in sups]
@@ -518,16 +524,18 @@ def test_gcn_fused_layouts_agree(gpu, n):
         dx1 = dP[:, :, (1 + 2 * k) * C:(2 + 2 * k) * C] + torch.einsum("swc,vw->svc", dx2, a)
         dxg = dxg + torch.einsum("swc,vw->svc", dx1, a)
     del D
+    # fp32 rounding floor (max-abs error / max-abs value): the support split adds the partial
+    # sums in another order than the MFMA chains (measured 2.02e-6 on dxg at n = 207)
     for h, z, bnp, dhc in outs:
-        assert rel_err(h.cpu().numpy(), H.numpy()) <= 2e-6
-        assert rel_err(z.cpu().numpy(), Z.numpy()) <= 2e-6
-        assert rel_err(dhc[:, :C].cpu().numpy(), dxg.reshape(rows, C).numpy()) <= 2e-6
+        assert rel_err(h.cpu().numpy(), H.numpy()) <= 4e-6
+        assert rel_err(z.cpu().numpy(), Z.numpy()) <= 4e-6
+        assert rel_err(dhc[:, :C].cpu().numpy(), dxg.reshape(rows, C).numpy()) <= 4e-6
         means = bnp.view(S, 3, C)[:, 1].cpu().double()
         assert rel_err(means.numpy(), Z.view(S, n, C).mean(1).numpy()) <= 1e-5
     # the layouts: the same products, k order / channel split differ -> identical up to fma rounding
     for other in outs[1:]:
         for a_, b_ in zip(outs[0], other):
-            assert rel_err(a_.cpu().numpy(), b_.cpu().numpy()) <= 1e-6
+            assert rel_err(a_.cpu().numpy(), b_.cpu().numpy()) <= 2e-6
 
 
 @pytest.mark.parametrize("n,planes", [(16, 3), (207, 3), (325, 3), (207, 2)])
