@@ -347,6 +347,35 @@ __device__ __forceinline__ int img_idx(int w, int c, int np) {
 
 template <bool PL = false>
 __device__ __forceinline__ void global_to_lds(const float* src, long ld, int n, int np, float* buf) {
+  if ((((uintptr_t)src) & 15) == 0 && (ld & 3) == 0) {
+    // 16-B buffer loads, four per thread in flight before its first LDS write (the element loop
+    // below compiles to load -> s_waitcnt vmcnt(0) -> write per element: one memory round trip per
+    // element, 14 per thread for a 207-node slice); rows >= n read zeros (out of range)
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((long)n * ld * 4), 0x00020000);
+    const int total = np * 8;  // float4s of the [np][32] image
+    for (int e0 = 0; e0 < total; e0 += 4 * (int)blockDim.x) {
+      float4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = e0 + threadIdx.x + i * blockDim.x;
+        const int off = e < total ? (int)(((long)(e >> 3) * ld + 4 * (e & 7)) * 4) : 0x7ffffff0;
+        v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = e0 + threadIdx.x + i * blockDim.x;
+        if (e < total) {
+          const int w = e >> 3, c = 4 * (e & 7);
+          buf[img_idx<PL>(w, c, np)] = v[i].x;
+          buf[img_idx<PL>(w, c + 1, np)] = v[i].y;
+          buf[img_idx<PL>(w, c + 2, np)] = v[i].z;
+          buf[img_idx<PL>(w, c + 3, np)] = v[i].w;
+        }
+      }
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < np * CH; e += blockDim.x) {
     const int w = e >> 5, c = e & 31;
     buf[img_idx<PL>(w, c, np)] = (w < n) ? src[(long)w * ld + c] : 0.0f;
