@@ -1,14 +1,15 @@
 #!/bin/bash
-# scratch GPU command (one gpurun call): GPU suite, bench x2 (metr) + pems bf16, kernel trace
+# scratch GPU command (one gpurun call): gram-on-side-stream mode -- model tests with it on, A/B bench
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_all.log 2>&1 || { tail -30 gpurun_out/t_all.log; exit 1; }
-tail -2 gpurun_out/t_all.log
+GWN_GRAM_SIDE=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_ddp.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t_side.log 2>&1 || { tail -30 gpurun_out/t_side.log; exit 1; }
+tail -2 gpurun_out/t_side.log
 for rep in 1 2; do
-timeout -k 10 200 python bench.py --no-cpu-baseline --steps 40 > gpurun_out/b_$rep.json 2>gpurun_out/b.err || exit 1
-python -c "import json;d=json.load(open('gpurun_out/b_$rep.json'));print('bench',d['value'],d['ms_per_step'],d['roofline']['frac'])"
+for gs in 0 1; do
+GWN_GRAM_SIDE=$gs timeout -k 10 200 python bench.py --no-cpu-baseline --steps 40 > gpurun_out/gs_${gs}_$rep.json 2>gpurun_out/gs.err || exit 1
+python -c "import json;d=json.load(open('gpurun_out/gs_${gs}_$rep.json'));print('gram_side',$gs,d['value'],d['ms_per_step'])"
 done
-timeout -k 10 200 python bench.py --config pems --no-cpu-baseline --steps 20 > gpurun_out/b_pems.json 2>gpurun_out/b.err || exit 1
-python -c "import json;d=json.load(open('gpurun_out/b_pems.json'));print('pems',d['value'],d['ms_per_step'])"
-rm -rf gpurun_out/prof && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err
+done
+GWN_GRAM_SIDE=1 timeout -k 10 200 python bench.py --config pems --no-cpu-baseline --steps 20 > gpurun_out/gs_pems.json 2>gpurun_out/gs.err || exit 1
+python -c "import json;d=json.load(open('gpurun_out/gs_pems.json'));print('pems gram_side',d['value'],d['ms_per_step'])"
