@@ -69,8 +69,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal on a one-GPU box (never the driver's run): GWN_DIST_BACKEND=gloo GWN_SHARE_DEVICE=1
+    # puts every rank on cuda:0 over gloo (RCCL refuses two ranks on one device)
+    if os.environ.get("GWN_SHARE_DEVICE", "0") != "0":
+        local = 0
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("GWN_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
