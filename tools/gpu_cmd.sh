@@ -1,7 +1,10 @@
 #!/bin/bash
-# scratch GPU command (one gpurun call): rehearse bench.py's N=2 data-parallel path on one GPU (gloo)
+# scratch GPU command (one gpurun call): GPU suite + smoke + headline bench on the final tree
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-GWN_DIST_BACKEND=gloo GWN_SHARE_DEVICE=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 10 --warmup 3 > gpurun_out/b_n2.json 2> gpurun_out/b_n2.err || { tail -30 gpurun_out/b_n2.err; exit 1; }
-cat gpurun_out/b_n2.json
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_all.log 2>&1 || { tail -30 gpurun_out/t_all.log; exit 1; }
+tail -2 gpurun_out/t_all.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+timeout -k 10 400 python -u bench.py > gpurun_out/b_final.json 2> gpurun_out/b_final.err || exit 1
+python -c "import json;d=json.load(open('gpurun_out/b_final.json'));print('bench',d['value'],d['ms_per_step'],d['roofline']['frac'],d['cpu_baseline']['value'])"
