@@ -131,6 +131,20 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const NtArgs p) {
     const int n = n0 + wn * WTN + 32 * t + col;
     const bool nok = n < p.N;
     const float bn = (p.bias && nok) ? p.bias[n] : 0.0f;
+    // the column's mask values, all loaded before the first store (a load after a store to a
+    // possibly aliasing C would wait for it: one memory round trip per element)
+    float mk[TM][16];
+    if (p.mask) {
+      const __amdgpu_buffer_rsrc_t rm = rsrc(p.mask, ((long)(p.M - 1) * p.ldmask + p.N) * 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * WTM + 32 * i + crow(r, half);
+          mk[i][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                   rm, (nok && m < p.M) ? (int)(((long)m * p.ldmask + n) * 4) : OOR, 0, 0));
+        }
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -139,7 +153,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const NtArgs p) {
         const bool ok = nok && m < p.M;
         float v = acc[i][t][r] + bn;
         if (p.relu) v = fmaxf(v, 0.0f);
-        if (p.mask) v = (ok && p.mask[(long)m * p.ldmask + n] > 0.0f) ? v : 0.0f;
+        if (p.mask) v = mk[i][r] > 0.0f ? v : 0.0f;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rc,
                                               ok ? (int)(((long)m * p.ldc + n) * 4) : OOR, 0, 0);
       }
@@ -199,13 +213,23 @@ __global__ __launch_bounds__(256) void gemm_nt_thin_kernel(const NtArgs p) {
   const int n = col;
   const bool nok = n < p.N;
   const float bn = (p.bias && nok) ? p.bias[n] : 0.0f;
+  float mk[16];
+  if (p.mask) {
+    const __amdgpu_buffer_rsrc_t rm = rsrc(p.mask, ((long)(p.M - 1) * p.ldmask + p.N) * 4);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + crow(r, half);
+      mk[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            rm, (nok && m < p.M) ? (int)(((long)m * p.ldmask + n) * 4) : OOR, 0, 0));
+    }
+  }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int m = m0 + crow(r, half);
     const bool ok = nok && m < p.M;
     float v = acc[r] + bn;
     if (p.relu) v = fmaxf(v, 0.0f);
-    if (p.mask) v = (ok && p.mask[(long)m * p.ldmask + n] > 0.0f) ? v : 0.0f;
+    if (p.mask) v = mk[r] > 0.0f ? v : 0.0f;
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rc, ok ? (int)(((long)m * p.ldc + n) * 4) : OOR,
                                           0, 0);
   }
