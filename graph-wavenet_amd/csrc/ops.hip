@@ -203,6 +203,39 @@ __global__ void start_conv_kernel(const float* x, long sb, long sc, long sn, lon
   }
 }
 
+// c == 32, cin <= 4: one wave = two rows x 32 output channels, 32-bit row arithmetic (the generic
+// kernel's per-element 64-bit divisions made a 22 MB write take 23 us); the cin input values of a
+// row are one broadcast load each, lane co == 0 also copies them to xin
+template <int CIN>
+__global__ __launch_bounds__(256) void start_conv32_kernel(const float* x, long sb, long sc, long sn, long st, int B,
+                                                           int n, int t, int t0, const float* W, const float* bias,
+                                                           float* out, float* xin) {
+  const int rows = t0 * B * n;
+  const int co = threadIdx.x & 31;
+  const float bco = bias[co];
+  float w[CIN];
+#pragma unroll
+  for (int ci = 0; ci < CIN; ++ci) w[ci] = W[co * CIN + ci];
+  const int pad = t0 - t;
+  for (int row = blockIdx.x * 8 + (threadIdx.x >> 5); row < rows; row += gridDim.x * 8) {
+    const int v = row % n, tb = row / n, b = tb % B, ts = tb / B - pad;
+    float xv[CIN];
+#pragma unroll
+    for (int ci = 0; ci < CIN; ++ci)
+      xv[ci] = ts >= 0 ? x[b * sb + ci * sc + v * sn + (long)ts * st] : 0.0f;
+    float acc = bco;
+#pragma unroll
+    for (int ci = 0; ci < CIN; ++ci) acc = fmaf(w[ci], xv[ci], acc);
+    if (co < CIN && xin) {
+      float mine = xv[0];
+#pragma unroll
+      for (int ci = 1; ci < CIN; ++ci) mine = (co == ci) ? xv[ci] : mine;
+      xin[(long)row * CIN + co] = mine;
+    }
+    out[(long)row * 32 + co] = acc;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // gated TCN backward element-wise part: dfg from dxg (+ skip grad) and the saved tanh/sigmoid.
 __global__ void gate_bwd_kernel(const float* dxg, long ld_dxg, const float* dskip, long ld_dskip,
@@ -925,8 +958,19 @@ int gwn_start_conv_fwd(const float* x, long sb, long sc, long sn, long st, int B
                        hipStream_t s) {
   GWN_REQUIRE(t0 >= t && B > 0 && n > 0 && c > 0 && cin > 0, "start_conv: bad shape");
   const long total = (long)t0 * B * n * c;
-  start_conv_kernel<<<grid_for(total), 256, 0, s>>>(x, sb, sc, sn, st, B, cin, n, t, t0, W, bias, c,
-                                                    out, xin);
+  const long rows = (long)t0 * B * n;
+  if (c == 32 && cin >= 1 && cin <= 4 && rows < (1L << 30)) {
+    const int grid = (int)((rows + 7) / 8 < 8192 ? (rows + 7) / 8 : 8192);
+    switch (cin) {
+      case 1: start_conv32_kernel<1><<<grid, 256, 0, s>>>(x, sb, sc, sn, st, B, n, t, t0, W, bias, out, xin); break;
+      case 2: start_conv32_kernel<2><<<grid, 256, 0, s>>>(x, sb, sc, sn, st, B, n, t, t0, W, bias, out, xin); break;
+      case 3: start_conv32_kernel<3><<<grid, 256, 0, s>>>(x, sb, sc, sn, st, B, n, t, t0, W, bias, out, xin); break;
+      default: start_conv32_kernel<4><<<grid, 256, 0, s>>>(x, sb, sc, sn, st, B, n, t, t0, W, bias, out, xin); break;
+    }
+  } else {
+    start_conv_kernel<<<grid_for(total), 256, 0, s>>>(x, sb, sc, sn, st, B, cin, n, t, t0, W, bias, c,
+                                                      out, xin);
+  }
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
