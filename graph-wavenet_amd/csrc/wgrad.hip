@@ -183,11 +183,13 @@ __global__ void reduce_segments_kernel(const SegTable t) {
 // contiguous row ranges, thread (row lane l, channel j) accumulating dY[r][j] * X[r][k] (k < Kc)
 // and dY[r][j] over rows r = l mod 8; the 8 row lanes are folded in a fixed order and the
 // workgroup partial [J*Kc + J] written for gwn_reduce_partials.
-constexpr int SMALL_KC = 4, SMALL_BLK = 512, SMALL_ROWS = 64;  // <= 512 workgroups (partials to reduce)
-__global__ __launch_bounds__(256) void wgrad_small_kernel(const float* dY, long ldy, int J, const float* X, long ldx,
-                                                          int Kc, int R, float* part) {
-  __shared__ float sh[SMALL_KC + 1][256];
-  const int j = threadIdx.x % J, l = threadIdx.x / J, lanes = 256 / J;
+// 1024-thread workgroups (round 2; 256 took 25 us for the start conv's 22 MB dY: too few loads in
+// flight for a latency-bound stream with the partial count capped for the reduction)
+constexpr int SMALL_KC = 4, SMALL_BLK = 512, SMALL_ROWS = 64, SMALL_T = 1024;  // <= 512 workgroups (partials to reduce)
+__global__ __launch_bounds__(SMALL_T) void wgrad_small_kernel(const float* dY, long ldy, int J, const float* X, long ldx,
+                                                              int Kc, int R, float* part) {
+  __shared__ float sh[SMALL_KC + 1][SMALL_T];
+  const int j = threadIdx.x % J, l = threadIdx.x / J, lanes = SMALL_T / J;
   const int r0 = (int)((long)R * blockIdx.x / gridDim.x), r1 = (int)((long)R * (blockIdx.x + 1) / gridDim.x);
   float acc[SMALL_KC + 1];
 #pragma unroll
@@ -288,7 +290,7 @@ int gwn_wgrad_partials(const float* dY, long ldy, int J, const float* X, long ld
   GWN_REQUIRE(part != nullptr, "wgrad_partials: part is required");
   if (Kt * ntaps <= SMALL_KC && J > 0 && J <= 256 && 256 % J == 0) {  // narrow inputs (1x1, no affine)
     GWN_REQUIRE(ntaps == 1 && !x_mean && !x_scale && !x_shift && x_rows >= R, "wgrad_partials: narrow form is 1x1, plain");
-    wgrad_small_kernel<<<gwn_wgrad_partial_count(R, J, Kt), 256, 0, s>>>(dY, ldy, J, X, ldx, Kt, R, part);
+    wgrad_small_kernel<<<gwn_wgrad_partial_count(R, J, Kt), SMALL_T, 0, s>>>(dY, ldy, J, X, ldx, Kt, R, part);
     GWN_CHECK_LAUNCH();
     return GWN_OK;
   }
