@@ -3,6 +3,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config metr|pems|n2048]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...   (N > 1)
 
+``--gpus N`` with N > 1 and no launcher around it starts the N ranks itself (a child
+torch.distributed.run, before anything touches the GPU) and exits with their status; under a
+launcher WORLD_SIZE must equal N.
+
 A step is ``trainer.train(x, y)`` (reference engine.py:41-58) on one synthetic batch per GPU, the
 batches already resident in HBM and handed over as the transpose views train.py:244-247 builds.
 The default config is the headline (BASELINE.json configs[1]): METR-LA shape, B=64 per GPU, N=207
@@ -52,6 +56,7 @@ def parse():
                     help="override the config's arithmetic precision (pems: bf16, others f32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--plan-only", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -62,13 +67,45 @@ def step_flops(n, t):
     return {(207, 12): 3.3962e9, (325, 12): 7.0994e9, (2048, 24): 585.82e9}[(n, t)]
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """``--gpus N`` (N > 1) without a launcher around us: start N ranks, one per GPU, as a CHILD
+    ``torch.distributed.run`` (never an exec; nothing here has touched the GPU yet), wait for
+    them and return their exit status.  Rank 0 prints the one JSON line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     cfg = CONFIGS[args.config]
     B, N, T = cfg["B"], cfg["N"], cfg["T"]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (launch one rank per GPU)" % (args.gpus, world))
+    if args.plan_only:
+        # launcher check without a GPU (tests/test_host.py): every rank reports its place
+        print(json.dumps({"plan": True, "rank": rank, "world": world, "local_rank": local,
+                          "master": "%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT"))}),
+              flush=True)
+        return
     # rehearsal on a one-GPU box (never the driver's run): GWN_DIST_BACKEND=gloo GWN_SHARE_DEVICE=1
     # puts every rank on cuda:0 over gloo (RCCL refuses two ranks on one device)
     if os.environ.get("GWN_SHARE_DEVICE", "0") != "0":
@@ -223,8 +260,13 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
         with open(pmc) as f:
             rec = json.load(f).get("gcn_fwd_fused_kernel", {})
         traffic, mfma_busy = rec.get("hbm_bytes_per_dispatch"), rec.get("mfma_busy_frac")
-    return {"kernel": ("gcn_fwd_fused_kernel<512, true> (fused diffusion GCN forward, 8 launches/step)" if fused
-                       else "gwn_gcn_fwd large-graph schedule (batched diffusion GEMMs + mlp, 8 calls/step)"),
+    if fused:
+        kname = ("gcn_fwd_pow_kernel<512> (fused diffusion GCN forward, power schedule, 8 launches/step)"
+                 if ex._pow_ok(1) else "gcn_fwd_fused_kernel<512, true> (fused diffusion GCN forward, chained hops, "
+                                       "8 launches/step)")
+    else:
+        kname = "gwn_gcn_fwd large-graph schedule (batched diffusion GEMMs + mlp, 8 calls/step)"
+    return {"kernel": kname,
             "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
             "traffic_source": "profiles/r02/pmc_bench_metr.json" if traffic else None,

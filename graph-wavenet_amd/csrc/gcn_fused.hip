@@ -14,14 +14,16 @@
 // The node features never leave LDS between hops; only the pieces needed by the backward
 // (x1, x2 per support) and the layer output are written to HBM, as full coalesced rows.
 //
-// Two wave layouts of the same schedule:
-//   * 225 <= n <= 256 ("4-wave"; selectable for any n <= 256): 256 threads = one wave per SIMD; wave v owns the node tiles
-//     {v, v + 4}.  Every LDS A value feeds two MFMAs, every wave runs two independent accumulator
-//     chains, and the W fragments of the mlp are loaded once for both tiles.  A tile slot beyond
-//     the last node tile (e.g. tile 7 for n <= 224) is computed on finite don't-care columns and
-//     never stored, so the four waves run the same instruction stream (no divergent barriers).
-//   * otherwise ("tile-wave"): one wave per 32-node tile (up to 16 waves, n <= 512).  At n = 207
-//     (7 tiles) it beats the 4-wave layout by 10-23 % (tools/bench_gcn.py, round 1).
+// Wave layout: one wave per 32-node tile (up to 16 waves, n <= 512).
+//
+// Two schedules of the diffusion chain:
+//   * "power" (gcn_fwd_pow_kernel / gcn_bwd_pow_kernel, shared supports with their squares given):
+//     both hops of a support come from the node features in ONE pass over the LDS image, against
+//     A_k and A_k^2 (two accumulators per A-operand read), so the waves of a slice never wait on
+//     each other between hops; the backward diffuses dh through A_k^T and (A_k^2)^T and applies
+//     the transposed mlp per node (dx = W0^T dh + sum_k W1k^T A_k^T dh + W2k^T (A_k^2)^T dh).
+//   * "chain" (gcn_fwd_fused_kernel / gcn_bwd_fused_kernel): hop 2 diffuses hop 1's output,
+//     staged through LDS between barriers (per-sample supports, or no squares given).
 //
 // Contract on the supports: [np][ld] with np = 32*ceil(n/32) <= ld, ZERO outside [n][n]
 // (the executor keeps padded copies), so the K loop runs whole 32-node batches unguarded.
@@ -35,8 +37,6 @@ constexpr int CH = 32;   // channels (one MFMA tile)
 constexpr int LDR = 33;  // LDS row stride (floats): conflict-free row and column reads
 constexpr int KB = 16;   // k-steps (32 nodes) per batch of the K loop
 constexpr int EPT = 16;  // tile-wave epilogue elements per thread: np*32 / (64*np/32) = 16 for every n
-constexpr int EPT4 = 32; // 4-wave epilogue elements per thread: covers np <= 256 with 256 threads
-constexpr int TPW = 2;   // node tiles per wave in the 4-wave layout
 
 struct FusedFwd {
   const float* h; long ld_h;
@@ -127,6 +127,11 @@ __device__ __forceinline__ bool split_arrive(int* cnt, int parts, int* flag) {
   __syncthreads();
   if (!*flag) return false;
   if (threadIdx.x == 0) atomicExch(cnt, 0);
+  // the partials are read with sc1 loads (L1 bypass); the agent-scope acquire additionally
+  // invalidates this CU's L1, so the hand-off does not rest on the load policy alone
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   return true;
 }
 
@@ -146,26 +151,11 @@ __device__ __forceinline__ void split_sum_to_lds(const float* part, int parts, i
   }
 }
 
-
 // bf16 kernels: support batches prefetched ahead of their MFMAs (whole hop up to this many)
-#ifndef GWN_BF16_PD
-#define GWN_BF16_PD 11
-#endif
-#ifndef GWN_EXP
-// kernel experiments (timing only; 1-16 give wrong results): 1 no G loads, 2 no LDS A reads,
-// 4 no W loads, 16 no phase barriers (forward); 32 = forward hop pieces stored straight from the
-// accumulators by the compute waves instead of by a store wave through LDS (correct, slower);
-// 256 = clock diagnostic (per-workgroup cycles / real-time ticks after the BN partials,
-// tools/clock_gcn.py)
-#define GWN_EXP 0
-#endif
+constexpr int GWN_BF16_PD = 11;
 
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-#if GWN_EXP & 1
-  return (float)(voff + soff) * 1e-9f;
-#else
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-#endif
 }
 
 // the last 32-node K batch holds at most 16 real nodes: its upper 8 k-steps (2 nodes each) only
@@ -194,13 +184,7 @@ __device__ __forceinline__ GBatch w_frags(const float* W, int ld_w, int off, int
   const float* wp = W + (long)col * ld_w + off;
   GBatch f;
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-#if GWN_EXP & 4
-    f.v[s] = (float)(off + s) * 1e-6f + (float)lane * 1e-9f;
-#else
-    f.v[s] = wp[crow(s, half)];
-#endif
-  }
+  for (int s = 0; s < 16; ++s) f.v[s] = wp[crow(s, half)];
   return f;
 }
 
@@ -222,13 +206,7 @@ __device__ __forceinline__ f32x16 diffuse(const float* buf, const float* G, int 
   auto lds_batch = [&](int kb, float* av) {
     const float* bp = buf + (32 * kb + half) * LDR + col;
 #pragma unroll
-    for (int j = 0; j < KB; ++j) {
-#if GWN_EXP & 2
-      av[j] = (float)(kb * KB + j) * 1e-9f + (float)lane * 1e-12f + bp[0] * 1e-30f;
-#else
-      av[j] = bp[2 * j * LDR];
-#endif
-    }
+    for (int j = 0; j < KB; ++j) av[j] = bp[2 * j * LDR];
   };
   auto g_batch = [&](int kb, float* g) {
 #pragma unroll
@@ -338,14 +316,9 @@ __device__ __forceinline__ void acc_to_global(float* dst, long ld, const f32x16&
   }
 }
 
-// LDS image index of (row w, channel c): padded rows [np][LDR], or (PL, the balanced layout)
-// channel-half planes [2][np][16]
-template <bool PL>
-__device__ __forceinline__ int img_idx(int w, int c, int np) {
-  return PL ? ((c >> 4) * np + w) * 16 + (c & 15) : w * LDR + c;
-}
+// LDS image index of (row w, channel c): padded rows [np][LDR]
+__device__ __forceinline__ int img_idx(int w, int c) { return w * LDR + c; }
 
-template <bool PL = false>
 __device__ __forceinline__ void global_to_lds(const float* src, long ld, int n, int np, float* buf) {
   if ((((uintptr_t)src) & 15) == 0 && (ld & 3) == 0) {
     // 16-B buffer loads, four per thread in flight before its first LDS write (the element loop
@@ -367,10 +340,10 @@ __device__ __forceinline__ void global_to_lds(const float* src, long ld, int n, 
         const int e = e0 + threadIdx.x + i * blockDim.x;
         if (e < total) {
           const int w = e >> 3, c = 4 * (e & 7);
-          buf[img_idx<PL>(w, c, np)] = v[i].x;
-          buf[img_idx<PL>(w, c + 1, np)] = v[i].y;
-          buf[img_idx<PL>(w, c + 2, np)] = v[i].z;
-          buf[img_idx<PL>(w, c + 3, np)] = v[i].w;
+          buf[img_idx(w, c)] = v[i].x;
+          buf[img_idx(w, c + 1)] = v[i].y;
+          buf[img_idx(w, c + 2)] = v[i].z;
+          buf[img_idx(w, c + 3)] = v[i].w;
         }
       }
     }
@@ -378,7 +351,7 @@ __device__ __forceinline__ void global_to_lds(const float* src, long ld, int n, 
   }
   for (int e = threadIdx.x; e < np * CH; e += blockDim.x) {
     const int w = e >> 5, c = e & 31;
-    buf[img_idx<PL>(w, c, np)] = (w < n) ? src[(long)w * ld + c] : 0.0f;
+    buf[img_idx(w, c)] = (w < n) ? src[(long)w * ld + c] : 0.0f;
   }
 }
 
@@ -471,11 +444,11 @@ __device__ __forceinline__ void fwd_epilogue(const FusedFwd& a, float* ys, float
 // backward prologue: dh of the slice into LDS (rows >= n zero), either loaded or computed by the
 // BatchNorm backward of this layer's output (same arithmetic as bn_bwd_apply_kernel, ops.hip):
 //   dz = gamma*rstd*(dy - k1 - xhat*k2) -> residual gradient dres; dropout'(dz) -> dh (LDS + HBM)
-template <int NEPT, bool PL = false>
+template <int NEPT>
 __device__ __forceinline__ void bwd_prologue(const FusedBwd& a, float* dhs, long row0, int n, int np,
                                              bool lead = true, bool first = blockIdx.x == 0) {
   if (!a.bn_dy) {
-    global_to_lds<PL>(a.dh + row0 * CH, CH, n, np, dhs);
+    global_to_lds(a.dh + row0 * CH, CH, n, np, dhs);
     return;
   }
   if (first && threadIdx.x < CH) {
@@ -510,7 +483,7 @@ __device__ __forceinline__ void bwd_prologue(const FusedBwd& a, float* dhs, long
       }
       if (lead) a.dh_out[idx] = v;
     }
-    if (w < np) dhs[img_idx<PL>(w, c, np)] = v;
+    if (w < np) dhs[img_idx(w, c)] = v;
   }
 }
 
@@ -583,10 +556,6 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
     }
   };
 
-#if GWN_EXP & 256
-  // clock diagnostic: shader cycles and 100 MHz real-time ticks over the workgroup's life
-  const unsigned long long t_cyc0 = __builtin_amdgcn_s_memtime(), t_real0 = __builtin_amdgcn_s_memrealtime();
-#endif
   // software pipeline: every G first batch / W fragment set is issued one phase before use
   GBatch g0 = (u.k1 > u.k0 && compute) ? g_first(slice_sup(a, a.sup[u.k0]), a.ld_sup, nkb, w0, lane) : GBatch{};
   global_to_lds(hs, ldh, n, np, xs);
@@ -602,16 +571,12 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
       GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
       hacc = mlp_from_acc(wf, d, hacc);
     }
-#if !(GWN_EXP & 16)
     __syncthreads();  // ys is free: every wave finished the previous support's hop 2 (and its store)
-#endif
     if (compute) {
       acc_to_lds(ys, d, w0, lane);
       if (a.store_pieces && !store_wave) acc_to_global((float*)hs + (1 + 2 * k) * pstride, ldh, d, w0, lane, n);
     }
-#if !(GWN_EXP & 16)
     __syncthreads();
-#endif
     if (compute) {
       d = diffuse<HL>(ys, G, a.ld_sup, nkb, w0, lane, zero16(), g0);
       if (k + 1 < u.k1) g0 = g_first(slice_sup(a, a.sup[k + 1]), a.ld_sup, nkb, w0, lane);
@@ -639,18 +604,6 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_fused_kernel(const FusedFwd a
   }
   __syncthreads();
   fwd_epilogue<EPT>(a, ys, red[0], red[1], row0, n, u.slice);
-#if GWN_EXP & 256
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    // past the per-slice BN partials: [slices][3][32] floats, then 4 floats per workgroup
-    float* dg = a.bn_part + (long)gridDim.x * 3 * CH + 4 * blockIdx.x;
-    dg[0] = (float)(c1 - t_cyc0);
-    dg[1] = (float)(r1 - t_real0);
-    dg[2] = (float)(t_real0 & 0xffffffull);  // start tick (low 24 bits)
-    dg[3] = (float)__smid();
-  }
-#endif
 }
 
 template <int MAXT, bool HL>
@@ -716,520 +669,234 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_bwd_fused_kernel(const FusedBwd a
 }
 
 // ---------------------------------------------------------------------------------------------
-// 4-wave layout (n <= 256): wave v owns node tiles {v, v + 4}
+// "power" schedule: both hops of a support in one pass over the LDS image.
+//
+// D1'[c][w] = sum_v img[v][c] G1[v][w],  D2'[c][w] = sum_v img[v][c] G2[v][w]   (G2 = G1^2)
+// K runs in 16-node batches of KP = 8 k-steps (k-step j of batch b: nodes 16 b + 2 j + {0, 1}, the
+// lane half picks one); one LDS A-operand read feeds the two MFMAs of a k-step (two independent
+// accumulator chains).  The B fragments of batch b + 1 (both supports) are issued before batch b's
+// 16 MFMAs; loads past the padded support (np rows) return zeros (buffer range), so the loop body
+// has no branch around a load and the waits stay counted.  nb = ceil(n / 16) batches: a last
+// 32-node tile with at most 16 real nodes costs half a tile (n = 207: 104 of 112 k-steps).
+constexpr int KP = 8;
 
-struct GBatch2 {
-  float v[TPW][KB];
+struct GPair {
+  float a[KP], b[KP];
 };
 
-__device__ __forceinline__ GBatch2 g_first2(const float* G, int ld, int nkb, const int* w0, int lane) {
-  GBatch2 g;
+struct GPairSrc {
+  __amdgpu_buffer_rsrc_t r1, r2;
+  int voff, rowb;
+};
+
+__device__ __forceinline__ GPairSrc gp_src(const float* G1, const float* G2, int ld, int np, int w0, int lane) {
+  GPairSrc s;
+  s.r1 = __builtin_amdgcn_make_buffer_rsrc((void*)G1, (short)0, np * ld * 4, 0x00020000);
+  s.r2 = __builtin_amdgcn_make_buffer_rsrc((void*)G2, (short)0, np * ld * 4, 0x00020000);
+  s.voff = ((lane >> 5) * ld + w0 + (lane & 31)) * 4;
+  s.rowb = 2 * ld * 4;
+  return s;
+}
+
+__device__ __forceinline__ GPair gp_load(const GPairSrc& s, int batch) {
+  GPair g;
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const GBatch b = g_first(G, ld, nkb, w0[i], lane);
-#pragma unroll
-    for (int j = 0; j < KB; ++j) g.v[i][j] = b.v[j];
+  for (int j = 0; j < KP; ++j) {
+    g.a[j] = bload(s.r1, s.voff, (batch * KP + j) * s.rowb);
+    g.b[j] = bload(s.r2, s.voff, (batch * KP + j) * s.rowb);
   }
   return g;
 }
 
-// acc[i] += D' of tile i (diffuse() for TPW tiles sharing every A operand); g0 = g_first2(G, ...)
-__device__ __forceinline__ void diffuse2(const float* buf, const float* G, int ld, int nkb, const int* w0,
-                                         int lane, f32x16* acc, const GBatch2& g0) {
-  const int half = lane >> 5, col = lane & 31;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, nkb * 32 * ld * 4, 0x00020000);
-  int voff[TPW];
+// acc1 += img * G1, acc2 += img * G2 over n nodes; g0 = gp_load(src, 0) (issued by the caller a
+// phase ahead)
+__device__ __forceinline__ void diffuse_pair(const float* img, const GPairSrc& src, int n, int lane, f32x16& acc1,
+                                             f32x16& acc2, const GPair& g0) {
+  const int nb = (n + 15) >> 4;
+  const float* bp = img + (lane >> 5) * LDR + (lane & 31);
+  auto mfma_batch = [&](int b, const GPair& g) {
+    float av[KP];
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) voff[i] = (half * ld + w0[i] + col) * 4;
-  const int rowb = 2 * ld * 4;
-  float ga[TPW][KB], gb[TPW][KB];
+    for (int j = 0; j < KP; ++j) av[j] = bp[(16 * b + 2 * j) * LDR];
 #pragma unroll
-  for (int i = 0; i < TPW; ++i)
-#pragma unroll
-    for (int j = 0; j < KB; ++j) ga[i][j] = g0.v[i][j];
-  auto lds_batch = [&](int kb, float* av) {
-    const float* bp = buf + (32 * kb + half) * LDR + col;
-#pragma unroll
-    for (int j = 0; j < KB; ++j) av[j] = bp[2 * j * LDR];
+    for (int j = 0; j < KP; ++j) {
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], g.a[j], acc1, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], g.b[j], acc2, 0, 0, 0);
+    }
   };
-  auto g_batch = [&](int kb, float (*g)[KB]) {
-#pragma unroll
-    for (int i = 0; i < TPW; ++i)
-#pragma unroll
-      for (int j = 0; j < KB; ++j) g[i][j] = bload(rs, voff[i], (kb * KB + j) * rowb);
-  };
-  auto mfma_batch = [&](const float* av, float (*g)[KB]) {
-#pragma unroll
-    for (int j = 0; j < KB; ++j)
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], g[i][j], acc[i], 0, 0, 0);
-  };
-  int kb = 0;
-  for (; kb + 2 < nkb; kb += 2) {
-    float av[KB];
-    g_batch(kb + 1, gb);
-    lds_batch(kb, av);
-    mfma_batch(av, ga);
-    g_batch(kb + 2, ga);
-    lds_batch(kb + 1, av);
-    mfma_batch(av, gb);
+  GPair ga = g0, gb;
+  int b = 0;
+  for (; b + 1 < nb; b += 2) {
+    gb = gp_load(src, b + 1);
+    mfma_batch(b, ga);
+    ga = gp_load(src, b + 2);  // past the last batch: zeros or zero rows, never used
+    mfma_batch(b + 1, gb);
   }
-  float av[KB];
-  if (kb + 1 < nkb) {
-    g_batch(kb + 1, gb);
-    lds_batch(kb, av);
-    mfma_batch(av, ga);
-    lds_batch(kb + 1, av);
-    mfma_batch(av, gb);
-  } else {
-    lds_batch(kb, av);
-    mfma_batch(av, ga);
-  }
+  if (b < nb) mfma_batch(b, ga);
 }
 
-__device__ __forceinline__ void mlp_from_lds2(const float* W, int ld_w, int off, const float* buf, const int* w0,
-                                              int lane, f32x16* acc) {
-  const int half = lane >> 5, col = lane & 31;
-  const float* wp = W + (long)col * ld_w + off;
-  float wf[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) wf[s] = wp[2 * s + half];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const float* bp = buf + (w0[i] + col) * LDR;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s], bp[2 * s + half], acc[i], 0, 0, 0);
-  }
-}
-
-__device__ __forceinline__ void mlpT_from_lds2(const float* W, int ld_w, int off, const float* buf, const int* w0,
-                                               int lane, f32x16* acc) {
+// acc[c][v] += sum_c' W[c'][off + c] * E[c'][v]  (transposed mlp on an accumulator: MFMA s takes
+// its K pair from accumulator row crow(s, half), the A fragment is W's row of that channel)
+__device__ __forceinline__ f32x16 mlpT_from_acc(const float* W, int ld_w, int off, const f32x16& e, int lane,
+                                                f32x16 acc) {
   const int half = lane >> 5, col = lane & 31;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, CH * ld_w * 4, 0x00020000);
-  const int voff = (half * ld_w + off + col) * 4;
+  const int voff = (4 * half * ld_w + off + col) * 4;
   float wf[16];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) wf[s] = bload(rs, voff, 2 * s * ld_w * 4);
+  for (int s = 0; s < 16; ++s) wf[s] = bload(rs, voff, ((s & 3) + 8 * (s >> 2)) * ld_w * 4);
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const float* bp = buf + (w0[i] + col) * LDR;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s], bp[2 * s + half], acc[i], 0, 0, 0);
-  }
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s], e[s], acc, 0, 0, 0);
+  return acc;
 }
 
-// launch bounds (256 threads, >= 2 waves per SIMD): <= 256 VGPRs, two workgroups per CU
-__global__ __launch_bounds__(256, 2) void gcn_fwd_fused4_kernel(const FusedFwd a) {
+struct PowSup {
+  const float* g2[8];  // forward: A_k^2; backward: (A_k^2)^T
+};
+
+// Forward: h pieces 1 + 2k, 2 + 2k = A_k^T-diffused xg and (A_k^2)^T-diffused xg (the reference's
+// x1 = nconv(x, A), x2 = nconv(x1, A) up to fp32 reassociation), mlp, then the chain kernel's
+// epilogue (bias, dropout, residual, z, BN partials) on the whole slice.  The only barriers are
+// the staging one and the two around the epilogue: each wave runs its tile's 6 diffusions and
+// mlp on its own.  Hop pieces leave straight from the accumulators (4 x 16-B stores per lane).
+template <int MAXT>
+__global__ __launch_bounds__(MAXT, 4) void gcn_fwd_pow_kernel(const FusedFwd a, const PowSup p) {
   extern __shared__ float lds[];
-  __shared__ float red[2][256];
+  __shared__ float red[2][MAXT];
+  __shared__ int last_unit;
+  Unit u;
+  if (!unit_of(a, u)) return;
   const int n = a.n;
   const int nkb = (n + 31) >> 5;
   const int np = nkb * 32;
   float* xs = lds;
-  float* ys = lds + np * LDR;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long row0 = (long)blockIdx.x * n;
-  const float* hs = a.h + row0 * a.ld_h;
-  int w0[TPW];
-  bool tv[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    w0[i] = 32 * (wv + 4 * i);
-    tv[i] = wv + 4 * i < nkb;
-  }
+  const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
+  const long row0 = (long)u.slice * n;
+  const long ldh = a.ld_h;
+  float* hs = (float*)a.h + row0 * ldh;
 
-  GBatch2 g0 = (a.nsup > 0) ? g_first2(slice_sup(a, a.sup[0]), a.ld_sup, nkb, w0, lane) : GBatch2{};
-  global_to_lds(hs, a.ld_h, n, np, xs);
+  GPairSrc src = gp_src(a.sup[u.k0 < u.k1 ? u.k0 : 0], p.g2[u.k0 < u.k1 ? u.k0 : 0], a.ld_sup, np, w0, lane);
+  GPair g0 = (u.k1 > u.k0) ? gp_load(src, 0) : GPair{};
+  global_to_lds(hs, ldh, n, np, xs);
   __syncthreads();
-  f32x16 hacc[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) hacc[i] = zero16();
-  mlp_from_lds2(a.w_mlp, a.ld_w, 0, xs, w0, lane, hacc);
-  for (int k = 0; k < a.nsup; ++k) {
-    const float* G = slice_sup(a, a.sup[k]);
-    f32x16 d[TPW];
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) d[i] = zero16();
-    diffuse2(xs, G, a.ld_sup, nkb, w0, lane, d, g0);
-    g0 = g_first2(G, a.ld_sup, nkb, w0, lane);  // hop 2 re-reads the same support
-    {
-      const GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) hacc[i] = mlp_from_acc(wf, d[i], hacc[i]);
+  f32x16 hacc = zero16();
+  if (u.k0 == 0) hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
+  for (int k = u.k0; k < u.k1; ++k) {
+    f32x16 d1 = zero16(), d2 = zero16();
+    diffuse_pair(xs, src, n, lane, d1, d2, g0);
+    if (k + 1 < u.k1) {
+      src = gp_src(a.sup[k + 1], p.g2[k + 1], a.ld_sup, np, w0, lane);
+      g0 = gp_load(src, 0);
     }
-    __syncthreads();  // ys is free once every wave finished the previous support's hop 2
-#pragma unroll
-    for (int i = 0; i < TPW; ++i)
-      if (tv[i]) acc_to_lds(ys, d[i], w0[i], lane);
+    GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
+    hacc = mlp_from_acc(wf, d1, hacc);
+    wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
+    hacc = mlp_from_acc(wf, d2, hacc);
     if (a.store_pieces) {
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) acc_to_global((float*)hs + (1 + 2 * k) * CH, a.ld_h, d[i], w0[i], lane, n);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) d[i] = zero16();
-    diffuse2(ys, G, a.ld_sup, nkb, w0, lane, d, g0);
-    if (k + 1 < a.nsup) g0 = g_first2(slice_sup(a, a.sup[k + 1]), a.ld_sup, nkb, w0, lane);
-    {
-      const GBatch wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) hacc[i] = mlp_from_acc(wf, d[i], hacc[i]);
-    }
-    if (a.store_pieces) {
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) acc_to_global((float*)hs + (2 + 2 * k) * CH, a.ld_h, d[i], w0[i], lane, n);
+      acc_to_global(hs + (1 + 2 * k) * CH, ldh, d1, w0, lane, n);
+      acc_to_global(hs + (2 + 2 * k) * CH, ldh, d2, w0, lane, n);
     }
   }
+  __syncthreads();  // every wave is done with the node image: it stages the mlp output now
+  if (a.ksplit > 1) {
+    float* part = a.kws + (long)u.slice * a.ksplit * np * CH;
+    acc_to_part(part + (long)u.k0 * np * CH, n, hacc, w0, lane);
+    if (!split_arrive(a.kcnt + u.slice, a.ksplit, &last_unit)) return;
+    split_sum_to_lds(part, a.ksplit, n, np, xs);
+  } else {
+    acc_to_lds(xs, hacc, w0, lane);
+  }
   __syncthreads();
-#pragma unroll
-  for (int i = 0; i < TPW; ++i)
-    if (tv[i]) acc_to_lds(ys, hacc[i], w0[i], lane);
-  __syncthreads();
-  fwd_epilogue<EPT4>(a, ys, red[0], red[1], row0, n, blockIdx.x);
+  fwd_epilogue<EPT>(a, xs, red[0], red[1], row0, n, u.slice);
 }
 
-__global__ __launch_bounds__(256, 2) void gcn_bwd_fused4_kernel(const FusedBwd a) {
+// Backward: dx = W0^T dh + sum_k [W_{1+2k}^T (A_k dh) + W_{2+2k}^T (A_k^2 dh)] (node-wise mlp
+// commutes with the node diffusion), with A_k dh read as the transposed support.  For the
+// adaptive support the gram's operands t2 = W_2^T dh and t1 = W_1^T dh + W_2^T (A dh) come from
+// the same accumulators.  Prologue (BN backward) and epilogue (gate backward / dxg) as the chain
+// kernel's.
+template <int MAXT>
+__global__ __launch_bounds__(MAXT, 4) void gcn_bwd_pow_kernel(const FusedBwd a, const PowSup p) {
   extern __shared__ float lds[];
+  __shared__ int last_unit;
+  Unit un;
+  if (!unit_of(a, un)) return;
   const int n = a.n;
-  const int nkb = (n + 31) >> 5;
+  const int nkb = (int)(blockDim.x >> 6);
   const int np = nkb * 32;
   float* dhs = lds;
-  float* buf = lds + np * LDR;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long row0 = (long)blockIdx.x * n;
-  int w0[TPW];
-  bool tv[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    w0[i] = 32 * (wv + 4 * i);
-    tv[i] = wv + 4 * i < nkb;
-  }
+  const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
+  const long row0 = (long)un.slice * n;
 
-  GBatch2 g0 = (a.nsup > 0) ? g_first2(slice_sup(a, a.supT[0]), a.ld_sup, nkb, w0, lane) : GBatch2{};
-  bwd_prologue<EPT4>(a, dhs, row0, n, np);
+  GPairSrc src = gp_src(a.supT[un.k0 < un.k1 ? un.k0 : 0], p.g2[un.k0 < un.k1 ? un.k0 : 0], a.ld_sup, np, w0, lane);
+  GPair g0 = (un.k1 > un.k0) ? gp_load(src, 0) : GPair{};
+  bwd_prologue<EPT>(a, dhs, row0, n, np, un.k0 == 0, un.slice == 0 && un.k0 == 0);
   __syncthreads();
-  f32x16 dx[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) dx[i] = zero16();
-  mlpT_from_lds2(a.w_mlp, a.ld_w, 0, dhs, w0, lane, dx);
-  for (int k = 0; k < a.nsup; ++k) {
-    const float* GT = slice_sup(a, a.supT[k]);
-    {
-      f32x16 u[TPW];
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) u[i] = zero16();
-      mlpT_from_lds2(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, w0, lane, u);
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < TPW; ++i)
-        if (tv[i]) acc_to_lds(buf, u[i], w0[i], lane);
-      if (k == a.adp_index) {
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) acc_to_global(a.t2 + row0 * a.ld_t, a.ld_t, u[i], w0[i], lane, n);
-      }
+  f32x16 dx = (un.k0 == 0) ? mlpT_from_lds(a.w_mlp, a.ld_w, 0, dhs, w0, lane, zero16()) : zero16();
+  for (int k = un.k0; k < un.k1; ++k) {
+    f32x16 e1 = zero16(), e2 = zero16();
+    diffuse_pair(dhs, src, n, lane, e1, e2, g0);
+    if (k + 1 < un.k1) {
+      src = gp_src(a.supT[k + 1], p.g2[k + 1], a.ld_sup, np, w0, lane);
+      g0 = gp_load(src, 0);
     }
-    __syncthreads();
-    f32x16 t[TPW];
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) t[i] = zero16();
-    mlpT_from_lds2(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, w0, lane, t);
-    diffuse2(buf, GT, a.ld_sup, nkb, w0, lane, t, g0);  // dx1 = dP_x1 + A dP_x2
-    g0 = g_first2(GT, a.ld_sup, nkb, w0, lane);
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < TPW; ++i)
-      if (tv[i]) acc_to_lds(buf, t[i], w0[i], lane);
+    dx = mlpT_from_acc(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, e1, lane, dx);
+    dx = mlpT_from_acc(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, e2, lane, dx);
     if (k == a.adp_index) {
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) acc_to_global(a.t1 + row0 * a.ld_t, a.ld_t, t[i], w0[i], lane, n);
+      const f32x16 t2 = mlpT_from_lds(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, w0, lane, zero16());
+      acc_to_global(a.t2 + row0 * a.ld_t, a.ld_t, t2, w0, lane, n);
+      f32x16 t1 = mlpT_from_lds(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, w0, lane, zero16());
+      t1 = mlpT_from_acc(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, e1, lane, t1);
+      acc_to_global(a.t1 + row0 * a.ld_t, a.ld_t, t1, w0, lane, n);
     }
-    __syncthreads();
-    diffuse2(buf, GT, a.ld_sup, nkb, w0, lane, dx, g0);  // dxg += A dx1
-    if (k + 1 < a.nsup) g0 = g_first2(slice_sup(a, a.supT[k + 1]), a.ld_sup, nkb, w0, lane);
   }
-  if (!a.dfg) {
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx[i], w0[i], lane, n);
+  if (a.ksplit > 1) {  // partial input gradient of this support; the slice's last unit finishes
+    float* part = a.kws + (long)un.slice * a.ksplit * np * CH;
+    acc_to_part(part + (long)un.k0 * np * CH, n, dx, w0, lane);
+    if (!split_arrive(a.kcnt + un.slice, a.ksplit, &last_unit)) return;
+    __syncthreads();  // every wave of the last unit is done with the dh image
+    split_sum_to_lds(part, a.ksplit, n, np, dhs);
+    __syncthreads();
+    if (a.dfg) {
+      bwd_gate_epilogue<EPT>(a, dhs, row0, n);
+    } else {
+      for (int e = threadIdx.x; e < n * CH; e += blockDim.x)
+        a.dxg[(row0 + (e >> 5)) * a.ld_dxg + (e & 31)] = dhs[(e >> 5) * LDR + (e & 31)];
+    }
     return;
   }
-  __syncthreads();  // every wave finished reading buf
-#pragma unroll
-  for (int i = 0; i < TPW; ++i)
-    if (tv[i]) acc_to_lds(buf, dx[i], w0[i], lane);
-  __syncthreads();
-  bwd_gate_epilogue<EPT4>(a, buf, row0, n);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Balanced layout (v_mfma_f32_16x16x4_f32), n <= 256: four waves, one per SIMD, equal work.
-//
-// The 32x32 tile-wave layout lands 7 node tiles (n = 207) on the 4 SIMDs as 2,2,2,1, so the busiest
-// SIMD carries 2/7 of the slice instead of 1/4, and a lone workgroup (the last round of a layer,
-// or the small T = 1 layers) leaves three SIMDs mostly idle.  Here every product D'[c][w] of the
-// slice is cut in four equal quarters: wave (hc, hw) owns channels 16hc..16hc+15 of the 16*NKB
-// nodes from hw*16*NKB (NKB 16x16 tiles; np = 32*NKB).  The costs: a support fragment feeds one
-// channel half (each G element is loaded twice per slice, ~32 B/clk/CU of L2 at full MFMA rate),
-// and the forward mlp's contraction over channels is split between the two channel-half waves,
-// whose partial outputs are summed once per slice, in a fixed order, before the epilogue.
-// LDS images are channel-half planes [2][np][16] (img_idx<true>): the A fragment of a k-step
-// (4 rows x 16 channels) is 256 contiguous bytes, and an accumulator tile (4 consecutive channels
-// of 16 rows per lane group) is written back as one ds_write_b128 per lane.
-//
-// 16x16x4 f32 operand layout (lane l = 16 g + i, i = l & 15, g = l >> 4):
-//   A[m = i][k = g], B[k = g][n = i], D register r: D[m = 4 g + r][n = i].
-// The mlp contracts over channels straight from the accumulator: k-slot g of MFMA step j is channel
-// 4g + j of the half (register j of the accumulator), with the weights indexed to match.
-//
-// Measured (tools/bench_gcn.py, n = 207, round 2): 5 % slower than the tile-wave layout at T = 12
-// and 11-27 % slower at T = 7 / T = 1 (forward and backward), although its busiest SIMD carries
-// 13 % fewer MFMA cycles.  Each 32-cycle 16x16x4 MFMA needs a 4-row x 64-B support fragment (four
-// cache lines) where the 64-cycle 32x32x2 needs two: four times the L1 line rate per MFMA cycle,
-// and a single wave per SIMD when one workgroup per CU is left.  Selectable (layout 3), never
-// auto-selected; parity-tested with the other layouts.
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f32x4 zero4() {
-  f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-  return z;
-}
-
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-// acc[t][c][w] += sum_v img[v][c] * G[v][w] over the wave's quarter, v < 16 * nb16
-template <int NKB>
-__device__ __forceinline__ void bal_diffuse(const float* img, const float* G, int ld, int np, int nb16, int hc,
-                                            int hw, int lane, f32x4 (&acc)[NKB]) {
-  const int g = lane >> 4, i = lane & 15;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, np * ld * 4, 0x00020000);
-  const int voff = (g * ld + hw * 16 * NKB + i) * 4;
-  const float* ap = img + (hc * np + g) * 16 + i;
-  // batch b = nodes 16b..16b+15 = 4 k-steps; two register sets, batch b+1 loads issued before
-  // batch b's MFMAs (a third set, two batches ahead, measured 25 % slower: register pressure)
-  float ga[4][NKB], gb[4][NKB];
-  auto gload = [&](int b, float (&gr)[4][NKB]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int t = 0; t < NKB; ++t) gr[j][t] = bload(rs, voff + 64 * t, (16 * b + 4 * j) * ld * 4);
-  };
-  auto step = [&](int b, float (&gr)[4][NKB]) {
-    float av[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) av[j] = ap[(16 * b + 4 * j) * 16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int t = 0; t < NKB; ++t) acc[t] = mfma4(av[j], gr[j][t], acc[t]);
-  };
-  gload(0, ga);
-  int b = 0;
-  for (; b + 2 < nb16; b += 2) {
-    gload(b + 1, gb);
-    step(b, ga);
-    gload(b + 2, ga);
-    step(b + 1, gb);
-  }
-  if (b + 1 < nb16) {
-    gload(b + 1, gb);
-    step(b, ga);
-    step(b + 1, gb);
-  } else {
-    step(b, ga);
-  }
-}
-
-// hacc[hp][t][c'][w] += sum_{c in half hc} W[16hp + c'][off + c] * d[t][c][w]
-template <int NKB>
-__device__ __forceinline__ void bal_mlp(const float* W, int ld_w, int off, int hc, int lane, const f32x4 (&d)[NKB],
-                                        f32x4 (&hacc)[2][NKB]) {
-  const int g = lane >> 4, i = lane & 15;
-  float wf[2][4];
-#pragma unroll
-  for (int hp = 0; hp < 2; ++hp)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wf[hp][j] = W[(long)(16 * hp + i) * ld_w + off + 16 * hc + 4 * g + j];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int hp = 0; hp < 2; ++hp)
-#pragma unroll
-      for (int t = 0; t < NKB; ++t) hacc[hp][t] = mfma4(wf[hp][j], d[t][j], hacc[hp][t]);
-}
-
-// acc[t][c][w] += sum_{c'} W[c'][off + c] * dimg[w][c']     (dP = W^T dh, dimg in planes)
-template <int NKB>
-__device__ __forceinline__ void bal_mlpT(const float* W, int ld_w, int off, const float* dimg, int np, int hc, int hw,
-                                         int lane, f32x4 (&acc)[NKB]) {
-  const int g = lane >> 4, i = lane & 15;
-  float wa[2][4];
-#pragma unroll
-  for (int hp = 0; hp < 2; ++hp)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wa[hp][j] = W[(long)(16 * hp + 4 * g + j) * ld_w + off + 16 * hc + i];
-#pragma unroll
-  for (int hp = 0; hp < 2; ++hp) {
-    f32x4 bv[NKB];
-#pragma unroll
-    for (int t = 0; t < NKB; ++t) bv[t] = *(const f32x4*)(dimg + (hp * np + 16 * (hw * NKB + t) + i) * 16 + 4 * g);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int t = 0; t < NKB; ++t) acc[t] = mfma4(wa[hp][j], bv[t][j], acc[t]);
-  }
-}
-
-// the wave's quarter of D'[c][w] into a plane image / into rows w < n of dst (16-B aligned rows)
-template <int NKB>
-__device__ __forceinline__ void bal_to_img(float* img, const f32x4 (&d)[NKB], int np, int hc, int hw, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-#pragma unroll
-  for (int t = 0; t < NKB; ++t) *(f32x4*)(img + (hc * np + 16 * (hw * NKB + t) + i) * 16 + 4 * g) = d[t];
-}
-
-template <int NKB, bool NT>
-__device__ __forceinline__ void bal_to_global(float* dst, long ld, const f32x4 (&d)[NKB], int hc, int hw, int lane,
-                                              int n) {
-  const int g = lane >> 4, i = lane & 15;
-#pragma unroll
-  for (int t = 0; t < NKB; ++t) {
-    const int w = 16 * (hw * NKB + t) + i;
-    if (w < n) {
-      f32x4* p = (f32x4*)(dst + (long)w * ld + 16 * hc + 4 * g);
-      if (NT) __builtin_nontemporal_store(d[t], p);
-      else *p = d[t];
-    }
-  }
-}
-
-// the wave's quarter of D'[c][w] (c in half hc, or c' = 16hp + ... for the mlp halves) into padded
-// rows S[w][LDR]; ADD: S = d + S
-template <int NKB, bool ADD>
-__device__ __forceinline__ void bal_to_rows(float* S, const f32x4 (&d)[NKB], int c0, int hw, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-#pragma unroll
-  for (int t = 0; t < NKB; ++t) {
-    float* p = S + (16 * (hw * NKB + t) + i) * LDR + c0 + 4 * g;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) p[r] = ADD ? d[t][r] + p[r] : d[t][r];
-  }
-}
-
-template <int NKB>
-__device__ __forceinline__ void bal_zero(f32x4 (&d)[NKB]) {
-#pragma unroll
-  for (int t = 0; t < NKB; ++t) d[t] = zero4();
-}
-
-template <int NKB>
-__global__ __launch_bounds__(256, 2) void gcn_fwd_bal_kernel(const FusedFwd a) {
-  extern __shared__ float lds[];
-  __shared__ float red[2][256];
-  constexpr int np = 32 * NKB;
-  const int n = a.n, nb16 = (n + 15) >> 4;
-  float* xs = lds;            // x (piece 0), planes
-  float* ys = lds + np * CH;  // hop-1 output, planes
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hc = wave & 1, hw = wave >> 1;
-  const long row0 = (long)blockIdx.x * n;
-  float* hs = (float*)a.h + row0 * a.ld_h;
-  for (int e = threadIdx.x; e < np * 8; e += 256) {  // x rows as float4s, rows >= n zero
-    const int w = e >> 3, q = e & 7;
-    f32x4 v = zero4();
-    if (w < n) v = *(const f32x4*)(hs + (long)w * a.ld_h + 4 * q);
-    *(f32x4*)(xs + ((q >> 2) * np + w) * 16 + 4 * (q & 3)) = v;
-  }
-  __syncthreads();
-  f32x4 hacc[2][NKB];
-  bal_zero(hacc[0]);
-  bal_zero(hacc[1]);
-  {
-    f32x4 x[NKB];
-    const int g = lane >> 4, i = lane & 15;
-#pragma unroll
-    for (int t = 0; t < NKB; ++t) x[t] = *(const f32x4*)(xs + (hc * np + 16 * (hw * NKB + t) + i) * 16 + 4 * g);
-    bal_mlp(a.w_mlp, a.ld_w, 0, hc, lane, x, hacc);
-  }
-  for (int k = 0; k < a.nsup; ++k) {
-    const float* G = slice_sup(a, a.sup[k]);
-    f32x4 d[NKB];
-    bal_zero(d);
-    bal_diffuse(xs, G, a.ld_sup, np, nb16, hc, hw, lane, d);
-    bal_mlp(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, hc, lane, d, hacc);
-    if (a.store_pieces) bal_to_global<NKB, true>(hs + (1 + 2 * k) * CH, a.ld_h, d, hc, hw, lane, n);
-    __syncthreads();  // ys is free: every wave finished the previous support's hop 2
-    bal_to_img(ys, d, np, hc, hw, lane);
-    __syncthreads();
-    bal_zero(d);
-    bal_diffuse(ys, G, a.ld_sup, np, nb16, hc, hw, lane, d);
-    bal_mlp(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, hc, lane, d, hacc);
-    if (a.store_pieces) bal_to_global<NKB, true>(hs + (2 + 2 * k) * CH, a.ld_h, d, hc, hw, lane, n);
-  }
-  // mlp output = channel-half-0 partial + channel-half-1 partial (fixed order), rows [np][LDR]
-  float* S = lds;
-  __syncthreads();
-  if (hc == 1) {
-    bal_to_rows<NKB, false>(S, hacc[0], 0, hw, lane);
-    bal_to_rows<NKB, false>(S, hacc[1], 16, hw, lane);
-  }
-  __syncthreads();
-  if (hc == 0) {
-    bal_to_rows<NKB, true>(S, hacc[0], 0, hw, lane);
-    bal_to_rows<NKB, true>(S, hacc[1], 16, hw, lane);
-  }
-  __syncthreads();
-  fwd_epilogue<4 * NKB>(a, S, red[0], red[1], row0, n, blockIdx.x);
-}
-
-template <int NKB>
-__global__ __launch_bounds__(256, 2) void gcn_bwd_bal_kernel(const FusedBwd a) {
-  extern __shared__ float lds[];
-  constexpr int np = 32 * NKB;
-  const int n = a.n, nb16 = (n + 15) >> 4;
-  float* dhs = lds;            // dh, planes
-  float* buf = lds + np * CH;  // dP_x2 / dx1, planes
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hc = wave & 1, hw = wave >> 1;
-  const long row0 = (long)blockIdx.x * n;
-
-  bwd_prologue<4 * NKB, true>(a, dhs, row0, n, np);
-  __syncthreads();
-  f32x4 dx[NKB];
-  bal_zero(dx);
-  bal_mlpT(a.w_mlp, a.ld_w, 0, dhs, np, hc, hw, lane, dx);
-  for (int k = 0; k < a.nsup; ++k) {
-    const float* GT = slice_sup(a, a.supT[k]);
-    {
-      f32x4 u[NKB];
-      bal_zero(u);
-      bal_mlpT(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, np, hc, hw, lane, u);
-      __syncthreads();
-      bal_to_img(buf, u, np, hc, hw, lane);
-      if (k == a.adp_index) bal_to_global<NKB, false>(a.t2 + row0 * a.ld_t, a.ld_t, u, hc, hw, lane, n);
-    }
-    __syncthreads();
-    f32x4 t[NKB];
-    bal_zero(t);
-    bal_mlpT(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, np, hc, hw, lane, t);
-    bal_diffuse(buf, GT, a.ld_sup, np, nb16, hc, hw, lane, t);  // dx1 = dP_x1 + A dP_x2
-    __syncthreads();
-    bal_to_img(buf, t, np, hc, hw, lane);
-    if (k == a.adp_index) bal_to_global<NKB, false>(a.t1 + row0 * a.ld_t, a.ld_t, t, hc, hw, lane, n);
-    __syncthreads();
-    bal_diffuse(buf, GT, a.ld_sup, np, nb16, hc, hw, lane, dx);  // dxg += A dx1
-  }
   if (!a.dfg) {
-    bal_to_global<NKB, false>(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, hc, hw, lane, n);
+    acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
     return;
   }
-  __syncthreads();  // every wave finished reading dhs / buf
-  bal_to_rows<NKB, false>(lds, dx, 16 * hc, hw, lane);
+  __syncthreads();  // every wave finished reading the dh image
+  acc_to_lds(dhs, dx, w0, lane);
   __syncthreads();
-  bwd_gate_epilogue<4 * NKB>(a, lds, row0, n);
+  bwd_gate_epilogue<EPT>(a, dhs, row0, n);
 }
 
-// dst (padded [np][ld_dst], zero outside n x n) = src or src^T
+// C = A A and C^T for a padded support A [np][ld] (zero outside [n][n], so C is too): one wave per
+// 32 x 32 output tile on v_mfma_f32_32x32x2_f32, K = np.  Also A^T when at != nullptr.
+__global__ __launch_bounds__(64) void support_square_kernel(const float* A, int np, int ld, float* C, float* CT,
+                                                            float* AT) {
+  const int ti = blockIdx.y * 32, tj = blockIdx.x * 32;
+  const int lane = threadIdx.x, half = lane >> 5, col = lane & 31;
+  f32x16 acc = zero16();
+  // D[i][j] = sum_k A[ti + i][k] A[k][tj + j]: A operand lane (half, col) = A[ti + col][2s + half]
+  const float* ar = A + (long)(ti + col) * ld + half;
+  const float* br = A + (long)half * ld + tj + col;
+  for (int k = 0; k < np; k += 2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[k], br[(long)k * ld], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = ti + crow(r, half), j = tj + col;
+    C[(long)i * ld + j] = acc[r];
+    CT[(long)j * ld + i] = acc[r];
+  }
+  if (AT) {
+    for (int r = half; r < 32; r += 2) AT[(long)(tj + col) * ld + ti + r] = A[(long)(ti + r) * ld + tj + col];
+  }
+}
+
 __global__ void pad_copy_kernel(const float* src, int n, int ld_src, float* dst, int ld_dst, int np,
                                 int transpose, long src_bstride = 0, long dst_bstride = 0) {
   __shared__ float tile[32][33];
@@ -1258,36 +925,17 @@ size_t fused_lds_bytes(int n) {
   return (size_t)2 * np * LDR * sizeof(float);
 }
 
+// the power schedule keeps one image (node features forward, dh backward)
+size_t pow_lds_bytes(int n) {
+  const int np = (n + 31) / 32 * 32;
+  return (size_t)np * LDR * sizeof(float);
+}
+
 template <typename K>
 void ensure_lds_attr(K kern) {
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)fused_lds_bytes(512));
 }
-
-// layout: 0 = auto, 1 = tile-wave, 2 = 4-wave.  Auto picks the tile-wave layout: measured at
-// METR-LA shape (n = 207, 7 tiles) the 4-wave kernel is 10-23 % slower (fewer waves to hide the
-// operand latency, plus the dead 8th tile slot); it is only auto-selected when all 8 slots are real.
-bool use_4wave(int layout, int nwt) { return layout == 2 || (layout == 0 && nwt == 8); }
-
-inline bool al16(const void* q, long ld) { return ((((uintptr_t)q) & 15) | (ld & 3)) == 0; }
-
-// layout 0 (auto) resolves through GWN_GCN_LAYOUT when set (measurements), else the default below
-int auto_layout() {
-  static int v = [] {
-    const char* e = getenv("GWN_GCN_LAYOUT");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-#define GWN_BAL_CASE(K, N) \
-  case N: K<N><<<slices, 256, lds, s>>>(a); break;
-#define GWN_BAL_SWITCH(K)                                                                    \
-  switch (nwt) {                                                                             \
-    GWN_BAL_CASE(K, 1) GWN_BAL_CASE(K, 2) GWN_BAL_CASE(K, 3) GWN_BAL_CASE(K, 4)             \
-    GWN_BAL_CASE(K, 5) GWN_BAL_CASE(K, 6) GWN_BAL_CASE(K, 7) GWN_BAL_CASE(K, 8)             \
-    default: break;                                                                          \
-  }
 
 // Support split policy.  Measured per layer (round 2, n = 207, B = 64, 256 CUs; fwd / bwd us,
 // whole slices -> split): a unit costs about half a slice, not a third (it still stages the whole
@@ -1330,8 +978,7 @@ int gwn_gcn_bf16_bwd_launch(const gwn_gcn_bwd_args* g, const FusedBwd& a, hipStr
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
   const int nwt = (g->n + 31) / 32;
   GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_fwd (fused): supports must be padded to 32*ceil(n/32)");
-  GWN_REQUIRE(g->layout >= 0 && g->layout <= 3 && !(g->layout >= 2 && nwt > 8),
-              "gcn_fwd (fused): layouts 2 (4-wave) and 3 (balanced) need n <= 256");
+  GWN_REQUIRE(g->layout == 0 || g->layout == 1, "gcn_fwd (fused): layout must be 0 or 1 (one wave per node tile)");
   FusedFwd a;
   a.h = g->h; a.ld_h = g->ld_h;
   for (int k = 0; k < 8; ++k) a.sup[k] = (k < g->nsup) ? g->sup[k] : nullptr;
@@ -1362,28 +1009,30 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
                 "gcn_fwd (split): needs c == 32, an instantiated node-tile count, split supports and weights");
     return gwn_gcn_split_fwd_launch(g, a, s);
   }
-  const size_t lds = fused_lds_bytes(g->n);
   static bool attr_set = false;
   if (!attr_set) {
     ensure_lds_attr(gcn_fwd_fused_kernel<512, false>);
     ensure_lds_attr(gcn_fwd_fused_kernel<512, true>);
     ensure_lds_attr(gcn_fwd_fused_kernel<1024, false>);
     ensure_lds_attr(gcn_fwd_fused_kernel<1024, true>);
-    ensure_lds_attr(gcn_fwd_fused4_kernel);
+    ensure_lds_attr(gcn_fwd_pow_kernel<512>);
+    ensure_lds_attr(gcn_fwd_pow_kernel<1024>);
     attr_set = true;
   }
   const int slices = g->rows / g->n;
-  const int layout = g->layout ? g->layout : auto_layout();
-  if (layout == 3) {
-    GWN_REQUIRE(nwt <= 8 && al16(a.h, a.ld_h), "gcn_fwd (fused): layout 3 (balanced) needs n <= 256 and 16-B rows of h");
-    GWN_BAL_SWITCH(gcn_fwd_bal_kernel)
-  } else if (use_4wave(layout, nwt)) gcn_fwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
-  else {
+  a.ksplit = pick_ksplit(g, slices, nwt);
+  const int grid = a.ksplit > 1 ? (slices + 7) / 8 * 8 * a.ksplit : slices;
+  if (g->sup2 && a.sup_batch <= 1 && g->nsup > 0) {
+    PowSup p;
+    for (int k = 0; k < 8; ++k) p.g2[k] = (k < g->nsup) ? g->sup2[k] : nullptr;
+    const size_t lds = pow_lds_bytes(g->n);
+    if (nwt <= 8) gcn_fwd_pow_kernel<512><<<grid, 64 * nwt, lds, s>>>(a, p);
+    else gcn_fwd_pow_kernel<1024><<<grid, 64 * nwt, lds, s>>>(a, p);
+  } else {
     // + one store wave when hop pieces are stored through LDS rows (h 16-B aligned, ld % 4 == 0)
-    const bool rows_ok = !(GWN_EXP & 32) && ((((uintptr_t)a.h) & 15) | (a.ld_h & 3)) == 0;
+    const size_t lds = fused_lds_bytes(g->n);
+    const bool rows_ok = ((((uintptr_t)a.h) & 15) | (a.ld_h & 3)) == 0;
     const int waves = nwt + ((a.store_pieces && rows_ok && nwt < 16) ? 1 : 0);
-    a.ksplit = pick_ksplit(g, slices, nwt);
-    const int grid = a.ksplit > 1 ? (slices + 7) / 8 * 8 * a.ksplit : slices;
     if (half_last_batch(g->n)) {
       if (waves <= 8) gcn_fwd_fused_kernel<512, true><<<grid, 64 * waves, lds, s>>>(a);
       else gcn_fwd_fused_kernel<1024, true><<<grid, 64 * waves, lds, s>>>(a);
@@ -1400,8 +1049,7 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
                              float* t1, float* t2, long ld_t, hipStream_t s) {
   const int nwt = (g->n + 31) / 32;
   GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_bwd (fused): supports must be padded to 32*ceil(n/32)");
-  GWN_REQUIRE(g->layout >= 0 && g->layout <= 3 && !(g->layout >= 2 && nwt > 8),
-              "gcn_bwd (fused): layouts 2 (4-wave) and 3 (balanced) need n <= 256");
+  GWN_REQUIRE(g->layout == 0 || g->layout == 1, "gcn_bwd (fused): layout must be 0 or 1 (one wave per node tile)");
   FusedBwd a;
   a.dh = g->dh;
   for (int k = 0; k < 8; ++k) a.supT[k] = (k < g->nsup) ? supT[k] : nullptr;
@@ -1435,21 +1083,21 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
     ensure_lds_attr(gcn_bwd_fused_kernel<512, true>);
     ensure_lds_attr(gcn_bwd_fused_kernel<1024, false>);
     ensure_lds_attr(gcn_bwd_fused_kernel<1024, true>);
-    ensure_lds_attr(gcn_bwd_fused4_kernel);
+    ensure_lds_attr(gcn_bwd_pow_kernel<512>);
+    ensure_lds_attr(gcn_bwd_pow_kernel<1024>);
     attr_set = true;
   }
-  const size_t lds = fused_lds_bytes(g->n);
   const int slices = g->rows / g->n;
-  const int layout = g->layout ? g->layout : auto_layout();
-  if (layout == 3) {
-    GWN_REQUIRE(nwt <= 8 && (a.dfg || al16(a.dxg, a.ld_dxg)) &&
-                    (a.adp_index < 0 || (al16(a.t1, a.ld_t) && al16(a.t2, a.ld_t))),
-                "gcn_bwd (fused): layout 3 (balanced) needs n <= 256 and 16-B rows of dxg / t1 / t2");
-    GWN_BAL_SWITCH(gcn_bwd_bal_kernel)
-  } else if (use_4wave(layout, nwt)) gcn_bwd_fused4_kernel<<<slices, 256, lds, s>>>(a);
-  else {
-    a.ksplit = pick_ksplit(g, slices, nwt);
-    const int grid = a.ksplit > 1 ? (slices + 7) / 8 * 8 * a.ksplit : slices;
+  a.ksplit = pick_ksplit(g, slices, nwt);
+  const int grid = a.ksplit > 1 ? (slices + 7) / 8 * 8 * a.ksplit : slices;
+  if (g->sup2_t && a.sup_batch <= 1 && g->nsup > 0) {
+    PowSup p;
+    for (int k = 0; k < 8; ++k) p.g2[k] = (k < g->nsup) ? g->sup2_t[k] : nullptr;
+    const size_t lds = pow_lds_bytes(g->n);
+    if (nwt <= 8) gcn_bwd_pow_kernel<512><<<grid, 64 * nwt, lds, s>>>(a, p);
+    else gcn_bwd_pow_kernel<1024><<<grid, 64 * nwt, lds, s>>>(a, p);
+  } else {
+    const size_t lds = fused_lds_bytes(g->n);
     if (half_last_batch(g->n)) {
       if (nwt <= 8) gcn_bwd_fused_kernel<512, true><<<grid, 64 * nwt, lds, s>>>(a);
       else gcn_bwd_fused_kernel<1024, true><<<grid, 64 * nwt, lds, s>>>(a);
@@ -1462,24 +1110,33 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   return GWN_OK;
 }
 
-// diagnostics: resident workgroups per CU of the fused kernels for n nodes (HIP occupancy API),
-// for the layout the launchers pick by default
-extern "C" int gwn_fused_occupancy(int n, int backward) {
+// diagnostics: resident workgroups per CU of the fused kernels for n nodes (HIP occupancy API):
+// the power schedule the executor uses for shared supports (pow = 1) or the chain schedule
+extern "C" int gwn_fused_occupancy(int n, int backward, int pow) {
   const int nwt = (n + 31) / 32;
-  const size_t lds = fused_lds_bytes(n);
   int blocks = -1;
   hipError_t e;
-  if (use_4wave(0, nwt)) {
-    if (backward) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_fused4_kernel, 256, lds);
-    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_fused4_kernel, 256, lds);
+  if (pow) {
+    const size_t lds = pow_lds_bytes(n);
+    if (backward) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_pow_kernel<1024>, 64 * nwt, lds);
+    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_pow_kernel<1024>, 64 * nwt, lds);
   } else if (backward) {
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_fused_kernel<1024, false>, 64 * nwt, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_bwd_fused_kernel<1024, false>, 64 * nwt,
+                                                     fused_lds_bytes(n));
   } else {
     // training forward: the compute waves plus the store wave
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, gcn_fwd_fused_kernel<1024, false>,
-                                                     64 * (nwt < 16 ? nwt + 1 : nwt), lds);
+                                                     64 * (nwt < 16 ? nwt + 1 : nwt), fused_lds_bytes(n));
   }
   return e == hipSuccess ? blocks : -(int)e;
+}
+
+extern "C" int gwn_support_square(const float* a, int np, int ld, float* a2, float* a2_t, float* a_t, hipStream_t s) {
+  GWN_REQUIRE(a && a2 && a2_t && np > 0 && np % 32 == 0 && ld >= np, "support_square: np must be a multiple of 32");
+  dim3 grid(np / 32, np / 32);
+  support_square_kernel<<<grid, 64, 0, s>>>(a, np, ld, a2, a2_t, a_t);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
 }
 
 extern "C" int gwn_transpose(const float* src, int n, int ld_src, float* dst, int ld_dst, hipStream_t s) {
@@ -1954,8 +1611,7 @@ void launch_split(const FusedFwd& a, const gwn_gcn_args* g, int slices, hipStrea
 
 bool gwn_gcn_split_eligible(int c, int n, int planes) {
   const int nkb = (n + 31) / 32;
-  return c == CH && n > 0 && ((planes == 1 && nkb <= 16) || (planes == 3 && (nkb == 1 || nkb == 7 || nkb == 11)) ||
-                              (planes == 2 && nkb == 7));
+  return c == CH && n > 0 && planes == 1 && nkb <= 16;
 }
 
 // bf16 operands (planes = 1): one instantiation per node-tile count
@@ -1991,12 +1647,8 @@ int gwn_gcn_split_fwd_launch(const gwn_gcn_args* g, const FusedFwd& a, hipStream
       case 15: launch_bf16_fwd<15>(a, g, slices, s); break;
       default: launch_bf16_fwd<16>(a, g, slices, s); break;
     }
-  } else if (g->split_planes == 3) {
-    if (nkb == 7) launch_split<7, 3, 2>(a, g, slices, s);
-    else if (nkb == 11) launch_split<11, 3, 2>(a, g, slices, s);
-    else launch_split<1, 3, 1>(a, g, slices, s);
   } else {
-    launch_split<7, 2, 2>(a, g, slices, s);
+    GWN_REQUIRE(false, "gcn_fwd (split): only bf16 operands (split_planes 1) are built");
   }
   GWN_CHECK_LAUNCH();
   return GWN_OK;
@@ -2040,15 +1692,13 @@ extern "C" long gwn_split_support_elems(int n, int planes) {
 extern "C" int gwn_split_supports(const float* const* sup, int nsup, int n, int ld_sup, int planes, void* dst,
                                   long sup_stride_elems, int ld_dst, hipStream_t s) {
   const int np = (n + 31) / 32 * 32;
-  GWN_REQUIRE(nsup >= 1 && nsup <= 8 && planes >= 1 && planes <= 3 && ld_sup >= np && ld_dst >= np &&
+  GWN_REQUIRE(nsup >= 1 && nsup <= 8 && planes == 1 && ld_sup >= np && ld_dst >= np &&
                   sup_stride_elems >= (long)planes * np * ld_dst,
               "split_supports: bad shape");
   SplitSupArgs sa;
   for (int k = 0; k < 8; ++k) sa.src[k] = k < nsup ? sup[k] : nullptr;
   dim3 grid(np / 32, np / 32, nsup);
-  if (planes == 3) split_supports_kernel<3><<<grid, 256, 0, s>>>(sa, np, ld_sup, (__bf16*)dst, sup_stride_elems, ld_dst);
-  else if (planes == 2) split_supports_kernel<2><<<grid, 256, 0, s>>>(sa, np, ld_sup, (__bf16*)dst, sup_stride_elems, ld_dst);
-  else split_supports_kernel<1><<<grid, 256, 0, s>>>(sa, np, ld_sup, (__bf16*)dst, sup_stride_elems, ld_dst);
+  split_supports_kernel<1><<<grid, 256, 0, s>>>(sa, np, ld_sup, (__bf16*)dst, sup_stride_elems, ld_dst);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -2058,16 +1708,14 @@ extern "C" long gwn_split_mlp_elems(int nsup, int planes) { return (long)(2 * ns
 extern "C" int gwn_split_mlp_weights(const float* const* w, int nlayers, int nsup, int planes, void* dst,
                                      long layer_stride_elems, hipStream_t s) {
   const int width = (2 * nsup + 1) * CH;
-  GWN_REQUIRE(nlayers >= 1 && nlayers <= 16 && nsup >= 0 && planes >= 1 && planes <= 3 &&
+  GWN_REQUIRE(nlayers >= 1 && nlayers <= 16 && nsup >= 0 && planes == 1 &&
                   layer_stride_elems >= gwn_split_mlp_elems(nsup, planes),
               "split_mlp_weights: bad shape");
   SplitWArgs wa;
   for (int l = 0; l < 16; ++l) wa.w[l] = l < nlayers ? w[l] : nullptr;
   const int total = (2 * nsup + 1) * CH * CH;
   dim3 grid((total + 255) / 256, nlayers);
-  if (planes == 3) split_mlp_kernel<3><<<grid, 256, 0, s>>>(wa, width, (__bf16*)dst, layer_stride_elems);
-  else if (planes == 2) split_mlp_kernel<2><<<grid, 256, 0, s>>>(wa, width, (__bf16*)dst, layer_stride_elems);
-  else split_mlp_kernel<1><<<grid, 256, 0, s>>>(wa, width, (__bf16*)dst, layer_stride_elems);
+  split_mlp_kernel<1><<<grid, 256, 0, s>>>(wa, width, (__bf16*)dst, layer_stride_elems);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

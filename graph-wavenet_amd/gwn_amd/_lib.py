@@ -87,6 +87,7 @@ class GcnArgs(ctypes.Structure):
         ("sup_bstride", c_long), ("sup_batch", c_int),
         ("residual_mean", c_void_p), ("residual_scale", c_void_p), ("residual_shift", c_void_p),
         ("ksplit", c_int), ("ksplit_ws", c_void_p), ("ksplit_count", c_void_p),
+        ("sup2", ctypes.POINTER(c_void_p)),
     ]
 
 
@@ -124,6 +125,7 @@ class GcnBwdArgs(ctypes.Structure):
         ("supT_split", c_void_p), ("sup_split_stride", c_long), ("ld_split", c_int),
         ("wT_split", c_void_p),
         ("ksplit", c_int), ("ksplit_ws", c_void_p), ("ksplit_count", c_void_p),
+        ("sup2_t", ctypes.POINTER(c_void_p)),
     ]
 
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time
@@ -191,7 +193,8 @@ _SIGS = [
     ("gwn_batchnorm_fwd_fold", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                        c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_void_p]),
-    ("gwn_fused_occupancy", c_int, [c_int, c_int]),
+    ("gwn_fused_occupancy", c_int, [c_int, c_int, c_int]),
+    ("gwn_support_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gwn_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     ("gwn_pad_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
     ("gwn_pad_square_batched", c_int, [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_int, c_long, c_int,

@@ -192,8 +192,16 @@ class trainer():
             return self._phase_grads(input, real_val, False)
         g = self.optimizer.param_groups[0]
         # everything the captured graph bakes in: shapes, hyper-parameters (kernel arguments), the
-        # flat parameter buffer and the padded supports (device pointers), scaler and BN constants
-        sup_key = tuple((s_.data_ptr(), s_._version) for s_ in (model.supports or []))
+        # flat parameter buffer and the padded supports (device pointers), scaler and BN constants.
+        # The padded supports are rebuilt (new buffers, a new generation) whenever the supports
+        # change: every graph and saved activation set that points at the old ones is dropped
+        model._fixed_supports()
+        sup_key = getattr(model, "_sup_gen", 0)
+        if sup_key != getattr(self, "_sup_gen_seen", sup_key):
+            self._graphs.clear()
+            self._acts.clear()
+            self._eager_runs.clear()
+        self._sup_gen_seen = sup_key
         bn_key = tuple((m.momentum, m.eps) for m in model.bn)
         key = (tuple(input.shape), tuple(real_val.shape), float(g["lr"]), tuple(g["betas"]), float(g["eps"]),
                float(g["weight_decay"]), self.clip, float(model.dropout), model._flat.data_ptr(), sup_key, bn_key,

@@ -299,13 +299,10 @@ class Executor:
         """MFMA operand format of the fused gcn kernels (include/gwn.h gwn_dtype):
         * compute dtype bf16 (gwnet.set_compute_dtype): 1 = bf16 operands, fp32 accumulation,
           forward AND backward (the mixed-precision path of configs[2]);
-        * else GWN_SPLIT=3: the split-bf16 forward at fp32 accuracy (3 pieces; measurements only:
-          at METR-LA shape it holds one workgroup per CU and measured 223 vs 213 us per T=12
-          launch, tools/bench_gcn.py);
         * else 0: the f32-MFMA kernels (the default: the reference's fp32 arithmetic).
         0 when the shape has no such instantiation (c != 32, n > 512, no supports)."""
         cfg = self.cfg
-        planes = 1 if self.compute_dtype == "bf16" else int(os.environ.get("GWN_SPLIT", "0"))
+        planes = 1 if self.compute_dtype == "bf16" else 0
         if planes == 0 or not cfg.use_gcn or cfg.nsup < 1:
             return 0
         return planes if _lib.load().gwn_gcn_split_supported(cfg.C, cfg.N, planes) else 0
@@ -499,14 +496,35 @@ class Executor:
         acts.supT_arr = None
         acts.sup_batch = sup_batch
         sq = cfg.NP * cfg.NP
+        # power schedule of the fused gcn kernels: squared supports (and their transposes); the
+        # adaptive one's square launch also writes its transpose for the backward
+        pw = self._pow_ok(sup_batch)
+        acts.sup2_arr = acts.sup2t_arr = None
+        adp_t_done = False
+        if pw:
+            sq2, sq2t = self._fixed_squares(fixed_sups)
+            if cfg.adp_params:
+                if getattr(acts, "adp2", None) is None:
+                    acts.adp2 = torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32)
+                    acts.adp2_t = torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32)
+                adp_t = None
+                if training:
+                    if getattr(acts, "supT", None) is None or len(acts.supT) != len(sups) or acts.supT[0].numel() != sq:
+                        acts.supT = [torch.empty(sq, device=self.device, dtype=F32) for _ in sups]
+                    adp_t, adp_t_done = acts.supT[-1], True
+                lib.call("gwn_support_square", ptr(acts.adp), cfg.NP, cfg.NP, ptr(acts.adp2), ptr(acts.adp2_t),
+                         ptr(adp_t), st)
+                sq2, sq2t = sq2 + [acts.adp2], sq2t + [acts.adp2_t]
+            acts.sup2_arr = (ctypes.c_void_p * len(sq2))(*[t_.data_ptr() for t_ in sq2])
+            acts.sup2t_arr = (ctypes.c_void_p * len(sq2t))(*[t_.data_ptr() for t_ in sq2t])
         if training and sups:
             # transposed supports: the fused backward computes A·x as (A^T)^T·x on the forward kernel path
             if getattr(acts, "supT", None) is None or len(acts.supT) != len(sups) or acts.supT[0].numel() != sq * sup_batch:
                 acts.supT = [torch.empty(sup_batch * sq, device=self.device, dtype=F32) for _ in sups]
             nfix = len(fixed_t) if (fixed_t is not None and sup_batch <= 1 and cfg.use_gcn) else 0
             for k, (s_, t_) in enumerate(zip(sups, acts.supT)):
-                if k < nfix:
-                    continue  # the caller's cached transpose (below)
+                if k < nfix or (adp_t_done and k == len(sups) - 1):
+                    continue  # the caller's cached transpose (below) / written by gwn_support_square
                 if sup_batch > 1:
                     lib.call("gwn_pad_square_batched", ptr(s_), sup_batch, sq, N, cfg.NP, ptr(t_), cfg.NP, cfg.NP, sq,
                              1, st)
@@ -570,6 +588,7 @@ class Executor:
                               no_pieces=1 if i == L - 1 and self._fused_gcn() else 0,
                               sup_bstride=sq if sup_batch > 1 else 0, sup_batch=sup_batch,
                               residual_mean=raff[0], residual_scale=raff[1], residual_shift=raff[2],
+                              sup2=self._arr_field(acts.sup2_arr),
                               **self.split_fields(sp, i), **self.ksplit_fields(scr))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
@@ -603,6 +622,37 @@ class Executor:
         if tail_done is not None:
             main.wait_event(tail_done)
         return out, acts
+
+    @staticmethod
+    def _arr_field(arr):
+        return ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)) if arr is not None else None
+
+    def _pow_ok(self, sup_batch):
+        """Power schedule of the fused gcn kernels (both hops of a support against A and A^2 in one
+        pass; include/gwn.h sup2 / sup2_t): shared supports, f32 operands.  GWN_GCN_POW=0 selects
+        the chained hops (A/B measurements)."""
+        cfg = self.cfg
+        return (os.environ.get("GWN_GCN_POW", "1") != "0" and self._fused_gcn() and cfg.use_gcn and cfg.nsup >= 1
+                and sup_batch <= 1 and self.split_planes() == 0)
+
+    def _fixed_squares(self, fixed_sups):
+        """(A_k^2, (A_k^2)^T) of the padded fixed supports, cached while they stay the same tensors
+        (the cache keeps them referenced, so their addresses cannot be reused meanwhile)."""
+        fixed_sups = list(fixed_sups) if self.cfg.use_gcn else []
+        key = tuple(s_.data_ptr() for s_ in fixed_sups)
+        c = getattr(self, "_sq_cache", None)
+        if c is None or c[0] != key:
+            NP = self.cfg.NP
+            sq, sqt = [], []
+            for s_ in fixed_sups:
+                a2 = torch.empty(NP, NP, device=self.device, dtype=F32)
+                a2t = torch.empty(NP, NP, device=self.device, dtype=F32)
+                _lib.call("gwn_support_square", ptr(s_), NP, NP, ptr(a2), ptr(a2t), None, _lib.stream())
+                sq.append(a2)
+                sqt.append(a2t)
+            c = (key, fixed_sups, sq, sqt)
+            self._sq_cache = c
+        return list(c[2]), list(c[3])
 
     @staticmethod
     def ksplit_fields(scr):
@@ -707,6 +757,17 @@ class Executor:
                       cfg.NP, st)
             sups.append(bf["adp"])
         sup_arr = (ctypes.c_void_p * max(len(sups), 1))(*[s_.data_ptr() for s_ in sups])
+        bf["sup2_arr"] = None
+        if self._pow_ok(1):
+            sq2, _ = self._fixed_squares(fixed_sups)
+            if cfg.adp_params:
+                if "adp2" not in bf:
+                    bf["adp2"] = torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32)
+                    bf["adp2_t"] = torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32)
+                _lib.call("gwn_support_square", ptr(bf["adp"]), cfg.NP, cfg.NP, ptr(bf["adp2"]), ptr(bf["adp2_t"]),
+                          None, st)
+                sq2 = sq2 + [bf["adp2"]]
+            bf["sup2_arr"] = (ctypes.c_void_p * len(sq2))(*[t_.data_ptr() for t_ in sq2])
         planes = self.split_planes()
         sp = self.split_operands(sup_arr, len(sups), planes) if planes else None
         sx = x.stride()
@@ -733,7 +794,8 @@ class Executor:
                               seed_ptr=ptr(self.seed), salt=i, drop_p=0.0, bn_partials=None,
                               no_pieces=1, bn_running_mean=ptr(rm), bn_running_var=ptr(rv),
                               bn_weight=ptr(self.pk("bn_g%d" % i)), bn_bias=ptr(self.pk("bn_b%d" % i)),
-                              bn_eps=eps, bn_out=ptr(xnext), **self.split_fields(sp, i))
+                              bn_eps=eps, bn_out=ptr(xnext), sup2=self._arr_field(bf["sup2_arr"]),
+                              **self.split_fields(sp, i))
             _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             xcur = xnext
         self._head_fwd(bf["skipcat"], bf["skr"], bf["e1"], bf["y"], tf * P, None)
@@ -844,6 +906,7 @@ class Executor:
                                      sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
                                      if acts.supT_arr is not None else None,
                                      skip_weight_grads=1 if (overlap or defer) else 0,
+                                     sup2_t=self._arr_field(getattr(acts, "sup2t_arr", None)),
                                      **self.ksplit_fields(sc))
                 sb = getattr(acts, "sup_batch", 1)
                 if sb > 1:

@@ -385,7 +385,11 @@ class gwnet(nn.Module):
                 dst_t = torch.empty(np_, np_, device=dev, dtype=F32)
                 _lib.call("gwn_pad_square", src.data_ptr(), n, n, dst_t.data_ptr(), np_, np_, 1, _lib.stream())
                 padded_t.append(dst_t)
-            self._sup_cache = (key, padded, padded_t)
+            # the source tensors stay referenced by the cache, so no other tensor can take their
+            # addresses while the key is live; the generation tells captured graphs (engine.py) that
+            # the padded buffers they baked in are gone
+            self._sup_cache = (key, padded, padded_t, tuple(self.supports))
+            self._sup_gen = getattr(self, "_sup_gen", 0) + 1
         return self._sup_cache[1]
 
     def _fixed_supports_t(self):

@@ -244,18 +244,15 @@ typedef struct gwn_gcn_args {
    * eval BatchNorm (model.py:236 with the module in eval mode) folded into the epilogue: with
    *   bn_out != NULL, bn_out[r][j] = (z - running_mean[j]) / sqrt(running_var[j] + bn_eps) *
    *   weight[j] + bias[j] is written instead of z (z may be NULL, bn_partials must be NULL).
-   * layout: wave layout of the fused kernels, 0 = auto (4-wave only when n fills 8 node tiles,
-   *   225..256; GWN_GCN_LAYOUT overrides auto), 1 = one wave per 32-node tile, 2 = 4-wave
-   *   (n <= 256), 3 = balanced 16x16 quarters (n <= 256, 16-B aligned rows; measured slower). */
+   * layout: wave layout of the fused kernels, 0 or 1: one wave per 32-node tile (the only layout
+   *   built; other values are rejected). */
   int no_pieces;
   const float* bn_running_mean; const float* bn_running_var; const float* bn_weight; const float* bn_bias;
   float bn_eps; float* bn_out;
   int layout;
   /* operand precision of the products (gwn_dtype; 0 = GWN_DTYPE_F32, the f32-MFMA kernels):
    *   GWN_DTYPE_BF16 (1): bf16 operands, fp32 accumulation (v_mfma_f32_32x32x16_bf16), any
-   *     n <= 512 (the mixed-precision path of configs[2]);
-   *   GWN_DTYPE_BF16X3 (3): every fp32 operand as 3 bf16 pieces, 6 piece products = fp32
-   *     accuracy; 32*ceil(n/32) in {32, 224, 352} (2 pieces: 224 only, measurements only).
+   *     n <= 512 (the mixed-precision path of configs[2]).
    * Needs c == 32, nsup >= 1, sup_split = gwn_split_supports output with planes = split_planes
    * (support k at sup_split + k*sup_split_stride elements, rows ld_split), w_split =
    * gwn_split_mlp_weights output for this layer.  The fp32 supports `sup` are not read. */
@@ -281,6 +278,12 @@ typedef struct gwn_gcn_args {
    * 1 = off, nsup = always.  ksplit_ws: gwn_gcn_ksplit_ws_floats(rows, n, nsup) floats,
    * ksplit_count: rows / n ints; NULL = no split. */
   int ksplit; float* ksplit_ws; int* ksplit_count;
+  /* sup2 [nsup] (optional, f32 fused path with shared supports): the squared supports A_k A_k in
+   * the same padded layout (gwn_support_square).  Given, hop piece 2 + 2k is computed as
+   * (A_k^2)^T xg in the same pass over the node features as piece 1 + 2k (no hop-to-hop
+   * dependency inside a slice) -- equal to A_k^T (A_k^T xg) up to fp32 reassociation.  NULL = the
+   * chained hops. */
+  const float* const* sup2;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -363,6 +366,11 @@ typedef struct gwn_gcn_bwd_args {
   /* support split of the fused f32 backward, as gwn_gcn_args (partial input gradients, the last
    * workgroup of a slice adds them in support order and runs the store / gate epilogue) */
   int ksplit; float* ksplit_ws; int* ksplit_count;
+  /* sup2_t [nsup] (optional, f32 fused path, shared supports): the transposed squared supports
+   * (A_k^2)^T (gwn_support_square).  Given, the input gradient is computed as
+   * W0^T dh + sum_k W_{1+2k}^T (A_k dh) + W_{2+2k}^T (A_k^2 dh) with every diffusion reading dh
+   * (no hop-to-hop dependency).  NULL = the chained (Horner) backward. */
+  const float* const* sup2_t;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);
@@ -451,8 +459,13 @@ int gwn_batchnorm_fwd_fold(const float* partials, int nparts, int c, const float
                            float* b_fold, hipStream_t stream);
 /* dst[j][i] = src[i][j] for an n x n matrix (supports for the fused backward) */
 int gwn_transpose(const float* src, int n, int ld_src, float* dst, int ld_dst, hipStream_t stream);
-/* diagnostics: resident workgroups per CU of the fused gcn kernel (forward, or backward != 0) */
-int gwn_fused_occupancy(int n, int backward);
+/* diagnostics: resident workgroups per CU of the fused gcn kernel (forward, or backward != 0;
+ * pow != 0: the power schedule of shared supports, else the chained one) */
+int gwn_fused_occupancy(int n, int backward, int pow);
+/* Squared support for the power schedule of gwn_gcn_fwd / gwn_gcn_bwd (sup2 / sup2_t):
+ * a2 = a a, a2_t = (a a)^T, and a_t = a^T when a_t != NULL, all [np][ld] like a (a padded support,
+ * zero outside [n][n]; np a multiple of 32).  One launch (f32 MFMA). */
+int gwn_support_square(const float* a, int np, int ld, float* a2, float* a2_t, float* a_t, hipStream_t stream);
 /* dst [np][ld_dst] = src (or src^T if transpose) inside [n][n], zero elsewhere (np >= n) */
 int gwn_pad_square(const float* src, int n, int ld_src, float* dst, int np, int ld_dst, int transpose,
                    hipStream_t stream);

@@ -143,10 +143,11 @@ def _relu(x, masks, key):
     return x * masks[key].to(x.dtype)
 
 
-def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, masks=None):
+def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, masks=None, record=None):
     """gwnet forward.  p: dict of parameter tensors (state_dict names); supports: list of [N,N]
     fixed supports; x: [B, Cin, N, T]; bn_state: dict name->buffer updated in train mode;
-    masks: optional ReLU branches {"skip": [B,S,N,T_f], "e1": [B,E,N,T_f]} (module docstring)."""
+    masks: optional ReLU branches {"skip": [B,S,N,T_f], "e1": [B,E,N,T_f]} (module docstring);
+    record: optional dict that receives the head's pre-activations "skip" and "e1" (detached)."""
     t = x.shape[-1]
     if t < cfg.receptive_field:
         x = torch.nn.functional.pad(x, (cfg.receptive_field - t, 0, 0, 0))
@@ -179,8 +180,10 @@ def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, ma
         rm = bn_state["bn.%d.running_mean" % i] if bn_state is not None else None
         rv = bn_state["bn.%d.running_var" % i] if bn_state is not None else None
         h = batchnorm(h, p["bn.%d.weight" % i], p["bn.%d.bias" % i], rm, rv, training)
-    y = _relu(pointwise(_relu(skip, masks, "skip"), p["end_conv_1.weight"], p["end_conv_1.bias"]), masks, "e1")
-    return pointwise(y, p["end_conv_2.weight"], p["end_conv_2.bias"])
+    e1 = pointwise(_relu(skip, masks, "skip"), p["end_conv_1.weight"], p["end_conv_1.bias"])
+    if record is not None:
+        record["skip"], record["e1"] = skip.detach(), e1.detach()
+    return pointwise(_relu(e1, masks, "e1"), p["end_conv_2.weight"], p["end_conv_2.bias"])
 
 
 def masked_metrics(pred, real, null_val=0.0, sign=None):
@@ -201,18 +204,19 @@ def masked_metrics(pred, real, null_val=0.0, sign=None):
     return mae, mape, rmse
 
 
-def engine_loss(p, supports, x, real_val, cfg, scaler_mean, scaler_std, bn_state=None, training=True, masks=None):
+def engine_loss(p, supports, x, real_val, cfg, scaler_mean, scaler_std, bn_state=None, training=True, masks=None,
+                record=None):
     """engine.py:41-51 up to the loss: pad 1, forward, inverse scale, masked MAE.
     masks: optional branches (module docstring; "sign": [B,1,N,T_out] of pred - real)."""
     x = torch.nn.functional.pad(x, (1, 0, 0, 0))
-    out = forward(p, supports, x, cfg, training, bn_state, masks=masks)
+    out = forward(p, supports, x, cfg, training, bn_state, masks=masks, record=record)
     pred = out.transpose(1, 3) * scaler_std + scaler_mean
     real = real_val.unsqueeze(1)
     mae, mape, rmse = masked_metrics(pred, real, sign=None if masks is None else masks.get("sign"))
     return out, mae, mape, rmse
 
 
-def grads(sd, supports, x, real_val, cfg, scaler_mean, scaler_std, dtype=F64, masks=None):
+def grads(sd, supports, x, real_val, cfg, scaler_mean, scaler_std, dtype=F64, masks=None, record=None):
     """Per-parameter gradients of the engine loss (train mode); params that do not reach the
     output get no entry (the reference leaves their .grad None).  masks: optional branch pinning
     (module docstring)."""
@@ -221,7 +225,7 @@ def grads(sd, supports, x, real_val, cfg, scaler_mean, scaler_std, dtype=F64, ma
     bn = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in sd.items() if "running" in k}
     sups = [torch.tensor(np.asarray(a), dtype=dtype) for a in supports]
     out, mae, mape, rmse = engine_loss(p, sups, torch.tensor(x, dtype=dtype), torch.tensor(real_val, dtype=dtype),
-                                       cfg, scaler_mean, scaler_std, bn, masks=masks)
+                                       cfg, scaler_mean, scaler_std, bn, masks=masks, record=record)
     names = list(p.keys())
     gs = torch.autograd.grad(mae, [p[n] for n in names], allow_unused=True)
     g = {n: gi for n, gi in zip(names, gs) if gi is not None}

@@ -3,12 +3,19 @@ with its own HIP trainer on cuda:0, joined by a gloo process group (RCCL refuses
 device; the product launches one rank per GPU with the "nccl" backend = RCCL over xGMI, and the
 trainer code path is the same).
 
-Each rank trains its G7 shard (B=2, N=16).  Step 1 runs eagerly; steps 2 and 3 take the captured
-path of engine.trainer._capture: graph 1 (forward, loss, backward) -> eager all-reduce of the flat
-gradient -> graph 2 (clip + Adam).  Checks: step-1 gradients = the mean of the per-shard f64
-reference gradients (g7, norm-rel <= 1e-4), step-1 parameters = clip + Adam on those mean
-gradients (norm-rel <= 1e-4; BN-cancelled biases, analytically 0, within 2 lr), and the parameters
-of both ranks bitwise equal after the captured steps."""
+Step 1 runs eagerly; steps 2 and 3 take the captured path of engine.trainer._capture: graph g0
+(forward + loss) -> graph g1 (backward) -> eager all-reduce of the flat gradient -> graph g2 (clip +
+Adam; g2 exists only when distributed).
+
+* G7 (B=2 per rank, N=16, C=16): step-1 gradients = the mean of the per-shard f64 reference
+  gradients (g7, norm-rel <= 1e-4), step-1 parameters = clip + Adam on those mean gradients
+  (norm-rel <= 1e-4; BN-cancelled biases, analytically 0, within 2 lr), and the parameters of both
+  ranks bitwise equal after the captured steps.
+* Headline shape (B=64 per rank, N=207, C=32: the fused GCN kernels of the bench): the data-parallel
+  step-1 gradients equal the mean of two single-process HIP trainer runs on the same shards (each
+  of which tests/test_gpu_headline.py pins to the fp64 oracle), and both ranks' parameters are
+  bitwise equal after the captured steps.
+* ``bench.py --gpus 2`` (self-launched ranks; gloo, both on cuda:0) prints one line with n_gpus 2."""
 import math
 import os
 import socket
@@ -58,11 +65,19 @@ def _worker(rank, world, port, out_q):
         for _ in range(2):
             eng.train(x, y)
         torch.cuda.synchronize()
-        captured = len(eng._graphs) == 1 and list(eng._graphs.values())[0][1] is not None
+        captured = _captured_dp(eng)
         p3 = eng.model._flat.detach().cpu().numpy().copy()
         out_q.put((rank, grads, p1, p3, captured))
     finally:
         torch.distributed.destroy_process_group()
+
+
+def _captured_dp(eng):
+    """Steps 2.. replayed the data-parallel graphs: one entry (g0, g1, g2, ...) with g2 present."""
+    if len(eng._graphs) != 1:
+        return False
+    g0, g1, g2 = list(eng._graphs.values())[0][:3]
+    return g0 is not None and g1 is not None and g2 is not None
 
 
 def _expected_step1(sd, gmean, lr=1e-3, wd=1e-4, clip=5.0, b1=0.9, b2=0.999, eps=1e-8):
@@ -118,3 +133,98 @@ def test_gpu_ddp_two_ranks_captured_step(gpu):
     np.testing.assert_array_equal(res[0][1]["start_conv.weight"], res[1][1]["start_conv.weight"])
     np.testing.assert_array_equal(res[0][2], res[1][2])
     assert np.all(np.isfinite(res[0][2]))
+
+
+HB, HN = 64, 207  # headline shape per rank
+
+
+def _headline_setup(dev, seed_x):
+    from gwn_amd import synthetic, util
+    from gwn_amd.engine import trainer
+    adj = synthetic.random_sensor_graph(HN, seed=0)
+    sups = [torch.tensor(a, device=dev) for a in synthetic.double_transition(adj)]
+    torch.manual_seed(999)
+    eng = trainer(util.StandardScaler(synthetic.SCALER_MEAN, synthetic.SCALER_STD), 2, 12, HN, 32, 0.0, 1e-3, 1e-4,
+                  dev, sups, True, True, None, 4, 2)
+    eng.clip = None  # compare raw gradients (clip_grad_norm_ scales grad_flat in place by a norm
+    #                  that differs between a shard and the mean)
+    x, y = synthetic.synthetic_batch(HB, HN, 12, seed=seed_x)
+    return eng, torch.tensor(x, device=dev), torch.tensor(y, device=dev)
+
+
+def _headline_worker(rank, world, port, out_q):
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng, x, y = _headline_setup(torch.device("cuda:0"), 700 + rank)
+        eng.broadcast_parameters(0)
+        eng.train(x, y)
+        torch.cuda.synchronize()
+        g1 = eng.optimizer.grad_flat.detach().cpu().numpy().copy()
+        for _ in range(2):
+            eng.train(x, y)
+        torch.cuda.synchronize()
+        out_q.put((rank, g1, eng.model._flat.detach().cpu().numpy().copy(), _captured_dp(eng)))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_gpu_ddp_headline_shape_equals_mean_of_single_runs(gpu):
+    # the two shards trained by single-process HIP trainers (no process group in this process)
+    singles = []
+    for r in range(2):
+        eng, x, y = _headline_setup(gpu, 700 + r)
+        eng.train(x, y)
+        torch.cuda.synchronize()
+        singles.append(eng.optimizer.grad_flat.detach().cpu().numpy().copy())
+        del eng
+    mean = (singles[0] + singles[1]) / np.float32(2.0)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_headline_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, g1, p3, captured = q.get(timeout=240)
+            res[r] = (g1, p3, captured)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for p in procs:
+        assert p.exitcode == 0
+    scale = float(np.max(np.abs(mean)))
+    for r in range(world):
+        g1, p3, captured = res[r]
+        assert captured, "steps 2-3 did not take the g0 -> g1 -> all-reduce -> g2 path"
+        diff = float(np.max(np.abs(g1.astype(np.float64) - mean)))
+        assert diff <= 1e-6 * scale, (r, diff, scale)
+        assert np.all(np.isfinite(p3))
+    print("DP grads vs mean of single runs: max |diff| %.3g (bitwise %s)"
+          % (float(np.max(np.abs(res[0][0] - mean))), bool(np.array_equal(res[0][0], mean))))
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+def test_bench_gpus_2_self_launch(gpu):
+    """bench.py --gpus 2 with no launcher: two ranks (gloo, both on cuda:0 -- RCCL refuses two ranks
+    on one device) and one JSON line with n_gpus 2 and global_batch 128."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(GWN_DIST_BACKEND="gloo", GWN_SHARE_DEVICE="1", OMP_NUM_THREADS="8")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                          "--warmup", "2", "--no-cpu-baseline"], env=env, capture_output=True, text=True,
+                         timeout=110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = lines[0]
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 128 and rec["config"]["parallelism"] == "dp2"
+    assert rec["value"] > 0 and rec["mae12_delta"] <= 1e-4

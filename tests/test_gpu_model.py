@@ -343,18 +343,19 @@ def test_fused_layer_backward_matches_unfused(gpu, monkeypatch, dropout):
             assert float(a.abs().max()) <= 1e-6, k
 
 
-def test_split_forward_matches_f32_forward(gpu, monkeypatch):
-    """A training step with the split-bf16 gcn forward (GWN_SPLIT=3) against the f32-MFMA
-    forward (GWN_SPLIT=0, the default) on the same inputs and dropout masks: loss and every
-    gradient agree to fp32 rounding."""
+def test_power_schedule_matches_chained_hops(gpu, monkeypatch):
+    """A training step on the power schedule of the fused gcn kernels (GWN_GCN_POW=1, the default:
+    x2 = (A^2)^T x, backward W^T after the diffusions) against the chained hops (GWN_GCN_POW=0:
+    x2 = A^T (A^T x), the reference's order) on the same inputs and dropout masks: loss and every
+    gradient agree to fp32 rounding (the two differ only by reassociation)."""
     from gwn_amd import synthetic, util
     from gwn_amd.engine import trainer
     adj = synthetic.random_sensor_graph(207, seed=0)
     sups = [torch.tensor(a, device=gpu) for a in synthetic.double_transition(adj)]
     x, y = synthetic.synthetic_batch(8, 207, 12, seed=5)
     grads, losses = [], []
-    for split in ("3", "0"):
-        monkeypatch.setenv("GWN_SPLIT", split)
+    for pw in ("1", "0"):
+        monkeypatch.setenv("GWN_GCN_POW", pw)
         monkeypatch.setenv("GWN_GRAPHS", "0")
         torch.manual_seed(999)
         eng = trainer(util.StandardScaler(54.4, 19.5), 2, 12, 207, 32, 0.3, 0.0, 0.0, gpu, sups, True, True,

@@ -164,3 +164,23 @@ def test_workspace_queries_are_monotone_in_rows():
             assert g >= prev_g and b >= prev_b and a >= prev_a, (n, slices)
             assert b >= g
             prev_g, prev_b, prev_a = g, b, a
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` with no launcher around it starts 2 ranks itself (a child
+    torch.distributed.run, before any GPU call) and every rank sees WORLD_SIZE = 2; under a launcher
+    whose WORLD_SIZE differs from --gpus it refuses to run (no mislabelled one-GPU line)."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--plan-only"],
+                         env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert sorted(r["rank"] for r in lines) == [0, 1]
+    assert all(r["world"] == 2 and r["master"].startswith("127.0.0.1:") for r in lines)
+    bad = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--plan-only"],
+                         env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), capture_output=True, text=True,
+                         timeout=120)
+    assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr

@@ -1,0 +1,23 @@
+#!/usr/bin/env bash
+# Experiment builds of libgwn (never the product): copy csrc, apply a sed script to gcn_fused.hip,
+# build into graph-wavenet_amd/gwn_amd/exp/libgwn_<name>.so (git-ignored; select with GWN_LIB).
+#   tools/exp_build.sh <name> '<sed expression>'
+set -euo pipefail
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+name=$1; expr=$2
+D=$(mktemp -d)
+mkdir -p "$D/g"
+cp -r "$ROOT/graph-wavenet_amd/csrc" "$D/g/csrc"
+ln -s "$ROOT/include" "$D/include"   # csrc includes ../../include/gwn.h
+sed -i -e "$expr" "$D/g/csrc/gcn_fused.hip"
+mkdir -p "$ROOT/graph-wavenet_amd/gwn_amd/exp"
+HIPCC=/opt/rocm/bin/hipcc
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I$ROOT/include"
+pids=()
+for f in gemm gemm_nt ops gcn_fused rowgemm gram wgrad infer bigdiff; do
+  $HIPCC $FLAGS -c -o "$D/$f.o" "$D/g/csrc/$f.hip" & pids+=($!)
+done
+for p in "${pids[@]}"; do wait "$p"; done
+$HIPCC --offload-arch=gfx950 -shared -fPIC -o "$ROOT/graph-wavenet_amd/gwn_amd/exp/libgwn_$name.so" "$D"/*.o
+rm -rf "$D"
+echo "built exp/libgwn_$name.so"
