@@ -28,6 +28,7 @@
 // Contract on the supports: [np][ld] with np = 32*ceil(n/32) <= ld, ZERO outside [n][n]
 // (the executor keeps padded copies), so the K loop runs whole 32-node batches unguarded.
 #include "gwn_internal.h"
+#include <type_traits>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -42,6 +43,7 @@ struct FusedFwd {
   const float* h; long ld_h;
   const float* sup[8]; int nsup, ld_sup;
   const float* w_mlp; int ld_w; const float* b_mlp;
+  const float* w_t;  // w_mlp transposed [ld_w][32] (power forward: coalesced fragment rows)
   const float* residual; float* z; float* bn_part;
   const unsigned long long* seed_ptr; unsigned long long salt; float drop_p;
   int n;
@@ -313,6 +315,20 @@ __device__ __forceinline__ void acc_to_global(float* dst, long ld, const f32x16&
   } else {
 #pragma unroll
     for (int r = 0; r < 16; ++r) p[crow(r, half)] = d[r];
+  }
+}
+
+// the same as 4 non-temporal 16-B stores per lane (hop pieces: written once, read by the backward
+// after the whole forward -- kept out of the L2 the supports live in); dst 16-B aligned, ld % 4 == 0
+__device__ __forceinline__ void acc_to_global_nt(float* dst, long ld, const f32x16& d, int w0, int lane, int n) {
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  const int half = lane >> 5, col = lane & 31;
+  if (w0 + col >= n) return;
+  float* p = dst + (long)(w0 + col) * ld;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4_t v = {d[4 * g], d[4 * g + 1], d[4 * g + 2], d[4 * g + 3]};
+    __builtin_nontemporal_store(v, (f32x4_t*)(p + crow(4 * g, half)));
   }
 }
 
@@ -669,16 +685,21 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_bwd_fused_kernel(const FusedBwd a
 }
 
 // ---------------------------------------------------------------------------------------------
-// "power" schedule: both hops of a support in one pass over the LDS image.
+// "power" schedule: both hops of a support in one pass over the LDS image, and every wave on its
+// own from the staging barrier to its end.
 //
 // D1'[c][w] = sum_v img[v][c] G1[v][w],  D2'[c][w] = sum_v img[v][c] G2[v][w]   (G2 = G1^2)
-// K runs in 16-node batches of KP = 8 k-steps (k-step j of batch b: nodes 16 b + 2 j + {0, 1}, the
+// K runs in 8-node batches of KP = 4 k-steps (k-step j of batch b: nodes 8 b + 2 j + {0, 1}, the
 // lane half picks one); one LDS A-operand read feeds the two MFMAs of a k-step (two independent
-// accumulator chains).  The B fragments of batch b + 1 (both supports) are issued before batch b's
-// 16 MFMAs; loads past the padded support (np rows) return zeros (buffer range), so the loop body
-// has no branch around a load and the waits stay counted.  nb = ceil(n / 16) batches: a last
-// 32-node tile with at most 16 real nodes costs half a tile (n = 207: 104 of 112 k-steps).
-constexpr int KP = 8;
+// accumulator chains).  The B fragments of both supports run RING - 1 = 3 batches (24 MFMAs) ahead
+// of their MFMAs in a 4-deep register ring, and the A operands of the next batch are read before
+// the current batch's MFMAs: a wave alone on its SIMD otherwise waits for its operands (per-wave
+// stamps of the one-batch look-ahead form: 68k cycles for 47k cycles of MFMA work).  Loads past the
+// padded support (np rows) return zeros (buffer range) and the LDS image carries 16 spare rows, so
+// the loop has no branch around a load.  nb = ceil(n / 8) batches: the MFMAs stop at the last
+// 8-node group holding a real node (n = 207: 104 of 112 k-steps).
+constexpr int KP = 4;
+constexpr int RING = 4;
 
 struct GPair {
   float a[KP], b[KP];
@@ -708,46 +729,225 @@ __device__ __forceinline__ GPair gp_load(const GPairSrc& s, int batch) {
   return g;
 }
 
-// acc1 += img * G1, acc2 += img * G2 over n nodes; g0 = gp_load(src, 0) (issued by the caller a
-// phase ahead)
-__device__ __forceinline__ void diffuse_pair(const float* img, const GPairSrc& src, int n, int lane, f32x16& acc1,
-                                             f32x16& acc2, const GPair& g0) {
-  const int nb = (n + 15) >> 4;
-  const float* bp = img + (lane >> 5) * LDR + (lane & 31);
-  auto mfma_batch = [&](int b, const GPair& g) {
-    float av[KP];
-#pragma unroll
-    for (int j = 0; j < KP; ++j) av[j] = bp[(16 * b + 2 * j) * LDR];
-#pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], g.a[j], acc1, 0, 0, 0);
-      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], g.b[j], acc2, 0, 0, 0);
-    }
-  };
-  GPair ga = g0, gb;
-  int b = 0;
-  for (; b + 1 < nb; b += 2) {
-    gb = gp_load(src, b + 1);
-    mfma_batch(b, ga);
-    ga = gp_load(src, b + 2);  // past the last batch: zeros or zero rows, never used
-    mfma_batch(b + 1, gb);
-  }
-  if (b < nb) mfma_batch(b, ga);
-}
+// rows of the LDS image of the power kernels: np + 16 (the A operands of one batch past the last
+// are read ahead)
+__host__ __device__ constexpr int pow_img_rows(int np) { return np + 16; }
 
-// acc[c][v] += sum_c' W[c'][off + c] * E[c'][v]  (transposed mlp on an accumulator: MFMA s takes
-// its K pair from accumulator row crow(s, half), the A fragment is W's row of that channel)
-__device__ __forceinline__ f32x16 mlpT_from_acc(const float* W, int ld_w, int off, const f32x16& e, int lane,
-                                                f32x16 acc) {
+// the W fragments of an mlp product on a diffusion accumulator (forward: W[c'][off + crow(s)],
+// the channel contraction W D; backward: W[crow(s)][off + c], the transposed W^T E)
+struct WFrag {
+  float v[16];
+};
+
+template <bool TRANSPOSED>
+__device__ __forceinline__ WFrag wfrag_load(const float* W, int ld_w, int off, int lane) {
   const int half = lane >> 5, col = lane & 31;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, CH * ld_w * 4, 0x00020000);
-  const int voff = (4 * half * ld_w + off + col) * 4;
-  float wf[16];
+  WFrag w;
 #pragma unroll
-  for (int s = 0; s < 16; ++s) wf[s] = bload(rs, voff, ((s & 3) + 8 * (s >> 2)) * ld_w * 4);
+  for (int s = 0; s < 16; ++s) {
+    const int c = crow(s, half);
+    w.v[s] = TRANSPOSED ? bload(rs, (c * ld_w + off + col) * 4, 0) : bload(rs, (col * ld_w + off + c) * 4, 0);
+  }
+  return w;
+}
+
+__device__ __forceinline__ f32x16 mlp_frag(const WFrag& w, const f32x16& d, f32x16 acc) {
 #pragma unroll
-  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[s], e[s], acc, 0, 0, 0);
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w.v[s], d[s], acc, 0, 0, 0);
   return acc;
+}
+
+// acc1 += img * G1, acc2 += img * G2 over n nodes; q0 = gp_load(src, 0), issued by the caller a
+// phase ahead (batches 1 .. RING - 2 are issued here).  The first mlp product's W fragments
+// (offset off1 of W [32][ld_w]) are issued after the last support batch, ahead of the tail's MFMAs.
+template <bool TRANSPOSED>
+__device__ __forceinline__ void diffuse_pair(const float* img, const GPairSrc& src, int n, int lane, f32x16& acc1,
+                                             f32x16& acc2, const GPair& q0, const float* W, int ld_w, int off1,
+                                             WFrag& w1, const float* tail_rows = nullptr, float4* tail = nullptr) {
+  const int nb = (n + 7) >> 3;
+  const float* bp = img + (lane >> 5) * LDR + (lane & 31);
+  auto lds = [&](int b, float* v) {
+#pragma unroll
+    for (int j = 0; j < KP; ++j) v[j] = bp[(8 * b + 2 * j) * LDR];
+  };
+  auto mfma = [&](const float* v, const GPair& g) {
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[j], g.a[j], acc1, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[j], g.b[j], acc2, 0, 0, 0);
+    }
+  };
+  GPair q[RING];
+  q[0] = q0;
+#pragma unroll
+  for (int r = 1; r < RING - 1; ++r) q[r] = gp_load(src, r);
+  float av[KP];
+  lds(0, av);
+  int b = 0;
+  for (; b + RING <= nb; b += RING) {
+#pragma unroll
+    for (int r = 0; r < RING; ++r) {
+      // batch b + r: issue batch b + r + RING - 1 into the slot batch b + r - 1 freed, read batch
+      // b + r + 1's A operands, then b + r's MFMAs.  sched_barrier pins that order: left alone, the
+      // machine scheduler sinks the loads next to their first use and the waits then expose the
+      // full L2 latency every batch (seen in the ISA: vmcnt(3..5) waits inside the loop)
+      q[(r + RING - 1) % RING] = gp_load(src, b + r + RING - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      float an[KP];
+      lds(b + r + 1, an);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma(av, q[r]);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) av[j] = an[j];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  w1 = wfrag_load<TRANSPOSED>(W, ld_w, off1, lane);
+  if (tail_rows) {  // the epilogue's rows (4 x 16 B per lane), behind the last support batch
+#pragma unroll
+    for (int g = 0; g < 4; ++g) tail[g] = *(const float4*)(tail_rows + 8 * g);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // fewer than RING batches left, all already in flight
+#pragma unroll
+  for (int r = 0; r < RING - 1; ++r) {
+    if (b + r < nb) {
+      float an[KP];
+      lds(b + r + 1, an);
+      mfma(av, q[r]);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) av[j] = an[j];
+    }
+  }
+}
+
+// x[r] <- sum of x[r] over the 32 lanes of this lane's half, for 16 registers at once: within each
+// 16-lane row by DPP (xor 1, xor 2 by quad_perm, then row rotations by 4 and 8), across the two
+// rows of the half by one ds_swizzle (xor 16).  Fixed order: deterministic (the lanes of a row may
+// differ in the last bit; callers take lane 0's).
+__device__ __forceinline__ float dpp_add(float x, int ctrl) {
+  int v = __builtin_bit_cast(int, x);
+  int y;
+  switch (ctrl) {  // (the dpp control must be a compile-time constant)
+    case 0: y = __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); break;   // quad_perm [1,0,3,2]
+    case 1: y = __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false); break;   // quad_perm [2,3,0,1]
+    case 2: y = __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false); break;  // row_ror 4
+    default: y = __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false); break; // row_ror 8
+  }
+  return x + __builtin_bit_cast(float, y);
+}
+
+__device__ __forceinline__ void half_sums16(float* x) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = dpp_add(x[r], c);
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    x[r] += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, x[r]), 0x401F));
+}
+
+// Forward epilogue of one wave's 32-node tile, straight from the mlp accumulator (lane = node
+// w0 + col, register r = channel crow(r, half)): bias, dropout (the chain kernel's counter hash,
+// index m*32 + c), residual (optionally BatchNorm-on-load), z (4 x 16-B stores per lane), and the
+// tile's BN partial (count, mean, M2 per channel; butterfly sums over the lanes of a half) in slot
+// (slice, tile) -- or, eval mode, bn(z) to x_out.  `res` = the residual rows, loaded ahead.
+__device__ __forceinline__ void fwd_tile_epilogue(const FusedFwd& a, const f32x16& hacc, const float4* res,
+                                                  long row0, int w0, int lane, int n, int slice, int tile, int nkb,
+                                                  float* tpart, int* tiles_done) {
+  const int half = lane >> 5, col = lane & 31;
+  const int w = w0 + col;
+  const bool valid = w < n;
+  const long m = row0 + min(w, n - 1);
+  const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
+  const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  float* dst = a.x_out ? a.x_out : a.z;
+  float v[16];
+  // channels 8g + 4 half + e of group g: per-channel vectors as float4s, one group at a time
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int c0 = 8 * g + 4 * half;
+    const float4 bq = *(const float4*)(a.b_mlp + c0);
+    const float* bias = (const float*)&bq;
+    const float* rv = (const float*)&res[g];
+    float4 mq, sq, hq;
+    if (a.res_scale) {
+      mq = *(const float4*)(a.res_mean + c0);
+      sq = *(const float4*)(a.res_scale + c0);
+      hq = *(const float4*)(a.res_shift + c0);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = 4 * g + e;
+      float x = hacc[r] + bias[e];
+      if (a.drop_p > 0.0f) {
+        const float u = gwn_uniform(seed, a.salt, (unsigned long long)m * CH + c0 + e);
+        x = (u >= a.drop_p) ? x * keep_scale : 0.0f;
+      }
+      // residual, or bn(z_prev) applied on load: (z - mean) * scale + shift
+      x += a.res_scale ? fmaf(rv[e] - ((const float*)&mq)[e], ((const float*)&sq)[e], ((const float*)&hq)[e]) : rv[e];
+      v[r] = x;
+    }
+    if (a.x_out) {  // eval BatchNorm, the arithmetic of bn_apply_kernel (ops.hip)
+      const float4 rm = *(const float4*)(a.bn_rm + c0), rvv = *(const float4*)(a.bn_rv + c0);
+      const float4 gq = *(const float4*)(a.bn_g + c0), bb = *(const float4*)(a.bn_b + c0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[4 * g + e] = (v[4 * g + e] - ((const float*)&rm)[e]) * (1.0f / sqrtf(((const float*)&rvv)[e] + a.bn_eps)) *
+                           ((const float*)&gq)[e] + ((const float*)&bb)[e];
+    }
+    if (valid) *(float4*)(dst + m * CH + c0) = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+  }
+  if (a.bn_part == nullptr || a.x_out) return;
+  // the tile's BN partial: count, mean and M2 per channel over its real nodes (two butterfly sums)
+  const int cnt = min(32, n - w0);
+  const float inv = 1.0f / (float)cnt;
+  float* pp = tpart + tile * 3 * CH;
+  float sm[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) sm[r] = valid ? v[r] : 0.0f;
+  half_sums16(sm);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    sm[r] *= inv;  // mean
+    const float d = valid ? v[r] - sm[r] : 0.0f;
+    v[r] = d * d;
+  }
+  half_sums16(v);
+  if (col == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = crow(r, half);
+      pp[c] = (float)cnt;
+      pp[CH + c] = sm[r];
+      pp[2 * CH + c] = v[r];
+    }
+  }
+  // the slice's partial: the last wave of the workgroup to get here merges the tiles' partials in
+  // tile order (Chan's formula; LDS counter, no barrier) -- one partial per slice for the finalize
+  __threadfence_block();
+  int last = 0;
+  if (lane == 0) last = atomicAdd(tiles_done, 1) == nkb - 1;
+  last = __shfl(last, 0, 64);
+  if (!last) return;
+  __threadfence_block();
+  if (lane < CH) {
+    float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
+    for (int t = 0; t < nkb; ++t) {
+      const float nb = tpart[t * 3 * CH + lane], mb = tpart[t * 3 * CH + CH + lane];
+      const float qb = tpart[t * 3 * CH + 2 * CH + lane];
+      const float tot = nn + nb;
+      const float d = mb - mean;
+      mean += d * (nb / tot);
+      m2 += qb + d * d * (nn * nb / tot);
+      nn = tot;
+    }
+    float* sp = a.bn_part + (long)slice * 3 * CH;
+    sp[lane] = nn;
+    sp[CH + lane] = mean;
+    sp[2 * CH + lane] = m2;
+  }
 }
 
 struct PowSup {
@@ -755,66 +955,139 @@ struct PowSup {
 };
 
 // Forward: h pieces 1 + 2k, 2 + 2k = A_k^T-diffused xg and (A_k^2)^T-diffused xg (the reference's
-// x1 = nconv(x, A), x2 = nconv(x1, A) up to fp32 reassociation), mlp, then the chain kernel's
-// epilogue (bias, dropout, residual, z, BN partials) on the whole slice.  The only barriers are
-// the staging one and the two around the epilogue: each wave runs its tile's 6 diffusions and
-// mlp on its own.  Hop pieces leave straight from the accumulators (4 x 16-B stores per lane).
+// x1 = nconv(x, A), x2 = nconv(x1, A) up to fp32 reassociation), mlp, epilogue per wave
+// (fwd_tile_epilogue).  One barrier: the staging one.  Hop pieces leave straight from the
+// accumulators (4 x 16-B stores per lane).  The support split (ksplit > 1) keeps the chain
+// kernel's whole-slice epilogue after the in-launch combine.
 template <int MAXT>
 __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_pow_kernel(const FusedFwd a, const PowSup p) {
   extern __shared__ float lds[];
-  __shared__ float red[2][MAXT];
+  __shared__ float red[2][MAXT];  // whole-slice epilogue (support split); tile partials otherwise
   __shared__ int last_unit;
+  __shared__ int tiles_done;
   Unit u;
   if (!unit_of(a, u)) return;
   const int n = a.n;
   const int nkb = (n + 31) >> 5;
   const int np = nkb * 32;
   float* xs = lds;
-  const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, w0 = wave * 32;
   const long row0 = (long)u.slice * n;
   const long ldh = a.ld_h;
   float* hs = (float*)a.h + row0 * ldh;
 
-  GPairSrc src = gp_src(a.sup[u.k0 < u.k1 ? u.k0 : 0], p.g2[u.k0 < u.k1 ? u.k0 : 0], a.ld_sup, np, w0, lane);
-  GPair g0 = (u.k1 > u.k0) ? gp_load(src, 0) : GPair{};
-  global_to_lds(hs, ldh, n, np, xs);
+  const int k0 = u.k0 < u.k1 ? u.k0 : 0;
+  GPairSrc src = gp_src(a.sup[k0], p.g2[k0], a.ld_sup, np, w0, lane);
+  GPair q0 = (u.k1 > u.k0) ? gp_load(src, 0) : GPair{};
+  // piece 0's W fragments (A operand W[c'][c] = W^T[c][c'], K pairs in natural order; rows of W^T
+  // are coalesced) land during the staging
+  float w0f[16];
+  if (u.k0 == 0) {
+    const float* wp = a.w_t + (lane >> 5) * CH + (lane & 31);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) w0f[s] = wp[2 * s * CH];
+  }
+  if (threadIdx.x == 0) tiles_done = 0;
+  global_to_lds(hs, ldh, n, pow_img_rows(np), xs);
   __syncthreads();
   f32x16 hacc = zero16();
-  if (u.k0 == 0) hacc = mlp_from_lds(a.w_mlp, a.ld_w, 0, xs, w0, lane, zero16());
-  for (int k = u.k0; k < u.k1; ++k) {
+  if (u.k0 == 0) {
+    const float* bp = xs + (w0 + (lane & 31)) * LDR + (lane >> 5);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) hacc = __builtin_amdgcn_mfma_f32_32x32x2f32(w0f[s], bp[2 * s], hacc, 0, 0, 0);
+  }
+  // the epilogue's residual rows: prefetched in the last support's tail
+  const bool tile_epi = a.ksplit <= 1;
+  float4 res[4];
+  const float* res_rows = a.residual + (row0 + min(w0 + (lane & 31), n - 1)) * CH + 4 * (lane >> 5);
+  const bool nt_ok = ((((uintptr_t)hs) & 15) | (ldh & 3)) == 0;
+  // one support: both hops, the two mlp products, the hop pieces; LAST (the residual prefetch of
+  // the epilogue rides in its tail) is a separate instantiation so that the residual registers are
+  // not live through the other supports
+  auto support = [&](int k, auto last_tag) {
+    constexpr bool LAST = decltype(last_tag)::value;
     f32x16 d1 = zero16(), d2 = zero16();
-    diffuse_pair(xs, src, n, lane, d1, d2, g0);
-    if (k + 1 < u.k1) {
+    WFrag w1;
+    // W[c'][off + c] = W^T[off + c][c']: the transposed-read form on W^T's piece block
+    diffuse_pair<true>(xs, src, n, lane, d1, d2, q0, a.w_t + (1 + 2 * k) * CH * CH, CH, 0, w1,
+                       LAST ? res_rows : nullptr, res);
+    if (!LAST && k + 1 < u.k1) {
       src = gp_src(a.sup[k + 1], p.g2[k + 1], a.ld_sup, np, w0, lane);
-      g0 = gp_load(src, 0);
+      q0 = gp_load(src, 0);
     }
-    GBatch wf = w_frags(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, lane);
-    hacc = mlp_from_acc(wf, d1, hacc);
-    wf = w_frags(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
-    hacc = mlp_from_acc(wf, d2, hacc);
+    const WFrag w2 = wfrag_load<true>(a.w_t + (2 + 2 * k) * CH * CH, CH, 0, lane);
+    hacc = mlp_frag(w1, d1, hacc);
+    hacc = mlp_frag(w2, d2, hacc);
     if (a.store_pieces) {
-      acc_to_global(hs + (1 + 2 * k) * CH, ldh, d1, w0, lane, n);
-      acc_to_global(hs + (2 + 2 * k) * CH, ldh, d2, w0, lane, n);
+      if (nt_ok) {
+        acc_to_global_nt(hs + (1 + 2 * k) * CH, ldh, d1, w0, lane, n);
+        acc_to_global_nt(hs + (2 + 2 * k) * CH, ldh, d2, w0, lane, n);
+      } else {
+        acc_to_global(hs + (1 + 2 * k) * CH, ldh, d1, w0, lane, n);
+        acc_to_global(hs + (2 + 2 * k) * CH, ldh, d2, w0, lane, n);
+      }
     }
+  };
+  if (u.k1 > u.k0) {
+    for (int k = u.k0; k + 1 < u.k1; ++k) support(k, std::false_type());
+    if (tile_epi) support(u.k1 - 1, std::true_type());
+    else support(u.k1 - 1, std::integral_constant<bool, false>());
   }
-  __syncthreads();  // every wave is done with the node image: it stages the mlp output now
-  if (a.ksplit > 1) {
-    float* part = a.kws + (long)u.slice * a.ksplit * np * CH;
-    acc_to_part(part + (long)u.k0 * np * CH, n, hacc, w0, lane);
-    if (!split_arrive(a.kcnt + u.slice, a.ksplit, &last_unit)) return;
-    split_sum_to_lds(part, a.ksplit, n, np, xs);
-  } else {
-    acc_to_lds(xs, hacc, w0, lane);
+  if (tile_epi) {
+    fwd_tile_epilogue(a, hacc, res, row0, w0, lane, n, u.slice, wave, nkb, &red[0][0], &tiles_done);
+    return;
   }
+  __syncthreads();  // every wave is done with the node image: it stages the combined mlp output now
+  float* part = a.kws + (long)u.slice * a.ksplit * np * CH;
+  acc_to_part(part + (long)u.k0 * np * CH, n, hacc, w0, lane);
+  if (!split_arrive(a.kcnt + u.slice, a.ksplit, &last_unit)) return;
+  split_sum_to_lds(part, a.ksplit, n, np, xs);
   __syncthreads();
   fwd_epilogue<EPT>(a, xs, red[0], red[1], row0, n, u.slice);
+}
+
+// Backward gate epilogue of one wave's tile from the input-gradient accumulator (lane = node,
+// register r = channel crow(r, half)): g = dxg (+ dskip) -> dfg through the saved (tanh f,
+// sigmoid s) pairs (gate_bwd_kernel's arithmetic), 16-B loads / stores.
+__device__ __forceinline__ void bwd_gate_tile(const FusedBwd& a, const f32x16& dx, long row0, int w0, int lane, int n) {
+  const int half = lane >> 5, col = lane & 31;
+  const int w = w0 + col;
+  if (w >= n) return;
+  const long m = row0 + w;
+  float4 fs[8], ds[4];
+  const float* fp = a.fg + m * 2 * CH + 8 * half;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    fs[2 * g] = *(const float4*)(fp + 16 * g);
+    fs[2 * g + 1] = *(const float4*)(fp + 16 * g + 4);
+  }
+  const bool sk = a.dskip && m >= a.skip_row0;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    ds[g] = sk ? *(const float4*)(a.dskip + (m - a.skip_row0) * a.ld_dskip + 8 * g + 4 * half) : make_float4(0, 0, 0, 0);
+  float* op = a.dfg + m * 2 * CH + 8 * half;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float* f8 = (const float*)&fs[2 * g];  // (f, s) of channels 8g + 4h + 0..3
+    const float* d4 = (const float*)&ds[g];
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gv = dx[4 * g + e] + d4[e];
+      const float f = f8[2 * e], sg = f8[2 * e + 1];
+      o[2 * e] = gv * sg * (1.0f - f * f);
+      o[2 * e + 1] = gv * f * sg * (1.0f - sg);
+    }
+    *(float4*)(op + 16 * g) = make_float4(o[0], o[1], o[2], o[3]);
+    *(float4*)(op + 16 * g + 4) = make_float4(o[4], o[5], o[6], o[7]);
+  }
 }
 
 // Backward: dx = W0^T dh + sum_k [W_{1+2k}^T (A_k dh) + W_{2+2k}^T (A_k^2 dh)] (node-wise mlp
 // commutes with the node diffusion), with A_k dh read as the transposed support.  For the
 // adaptive support the gram's operands t2 = W_2^T dh and t1 = W_1^T dh + W_2^T (A dh) come from
-// the same accumulators.  Prologue (BN backward) and epilogue (gate backward / dxg) as the chain
-// kernel's.
+// the same accumulators.  Prologue (BN backward, whole slice) as the chain kernel's; the gate
+// epilogue (or the dxg store) runs per wave from the accumulator.
 template <int MAXT>
 __global__ __launch_bounds__(MAXT, 4) void gcn_bwd_pow_kernel(const FusedBwd a, const PowSup p) {
   extern __shared__ float lds[];
@@ -828,33 +1101,37 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_bwd_pow_kernel(const FusedBwd a, 
   const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
   const long row0 = (long)un.slice * n;
 
-  GPairSrc src = gp_src(a.supT[un.k0 < un.k1 ? un.k0 : 0], p.g2[un.k0 < un.k1 ? un.k0 : 0], a.ld_sup, np, w0, lane);
-  GPair g0 = (un.k1 > un.k0) ? gp_load(src, 0) : GPair{};
-  bwd_prologue<EPT>(a, dhs, row0, n, np, un.k0 == 0, un.slice == 0 && un.k0 == 0);
+  const int k0 = un.k0 < un.k1 ? un.k0 : 0;
+  GPairSrc src = gp_src(a.supT[k0], p.g2[k0], a.ld_sup, np, w0, lane);
+  GPair q0 = (un.k1 > un.k0) ? gp_load(src, 0) : GPair{};
+  bwd_prologue<EPT>(a, dhs, row0, n, pow_img_rows(np), un.k0 == 0, un.slice == 0 && un.k0 == 0);
   __syncthreads();
   f32x16 dx = (un.k0 == 0) ? mlpT_from_lds(a.w_mlp, a.ld_w, 0, dhs, w0, lane, zero16()) : zero16();
   for (int k = un.k0; k < un.k1; ++k) {
     f32x16 e1 = zero16(), e2 = zero16();
-    diffuse_pair(dhs, src, n, lane, e1, e2, g0);
+    WFrag w1;
+    diffuse_pair<true>(dhs, src, n, lane, e1, e2, q0, a.w_mlp, a.ld_w, (1 + 2 * k) * CH, w1);
     if (k + 1 < un.k1) {
       src = gp_src(a.supT[k + 1], p.g2[k + 1], a.ld_sup, np, w0, lane);
-      g0 = gp_load(src, 0);
+      q0 = gp_load(src, 0);
     }
-    dx = mlpT_from_acc(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, e1, lane, dx);
-    dx = mlpT_from_acc(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, e2, lane, dx);
+    const WFrag w2 = wfrag_load<true>(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, lane);
+    dx = mlp_frag(w1, e1, dx);
+    dx = mlp_frag(w2, e2, dx);
     if (k == a.adp_index) {
+      __builtin_amdgcn_sched_barrier(0);  // (register pressure: keep the gram operands after dx)
+      f32x16 t1 = mlpT_from_lds(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, w0, lane, zero16());
+      t1 = mlp_frag(w2, e1, t1);
+      acc_to_global(a.t1 + row0 * a.ld_t, a.ld_t, t1, w0, lane, n);
+      __builtin_amdgcn_sched_barrier(0);
       const f32x16 t2 = mlpT_from_lds(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, dhs, w0, lane, zero16());
       acc_to_global(a.t2 + row0 * a.ld_t, a.ld_t, t2, w0, lane, n);
-      f32x16 t1 = mlpT_from_lds(a.w_mlp, a.ld_w, (1 + 2 * k) * CH, dhs, w0, lane, zero16());
-      t1 = mlpT_from_acc(a.w_mlp, a.ld_w, (2 + 2 * k) * CH, e1, lane, t1);
-      acc_to_global(a.t1 + row0 * a.ld_t, a.ld_t, t1, w0, lane, n);
     }
   }
   if (a.ksplit > 1) {  // partial input gradient of this support; the slice's last unit finishes
     float* part = a.kws + (long)un.slice * a.ksplit * np * CH;
     acc_to_part(part + (long)un.k0 * np * CH, n, dx, w0, lane);
     if (!split_arrive(a.kcnt + un.slice, a.ksplit, &last_unit)) return;
-    __syncthreads();  // every wave of the last unit is done with the dh image
     split_sum_to_lds(part, a.ksplit, n, np, dhs);
     __syncthreads();
     if (a.dfg) {
@@ -865,35 +1142,48 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_bwd_pow_kernel(const FusedBwd a, 
     }
     return;
   }
-  if (!a.dfg) {
-    acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
-    return;
-  }
-  __syncthreads();  // every wave finished reading the dh image
-  acc_to_lds(dhs, dx, w0, lane);
-  __syncthreads();
-  bwd_gate_epilogue<EPT>(a, dhs, row0, n);
+  if (a.dfg) bwd_gate_tile(a, dx, row0, w0, lane, n);
+  else acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
 }
 
-// C = A A and C^T for a padded support A [np][ld] (zero outside [n][n], so C is too): one wave per
-// 32 x 32 output tile on v_mfma_f32_32x32x2_f32, K = np.  Also A^T when at != nullptr.
-__global__ __launch_bounds__(64) void support_square_kernel(const float* A, int np, int ld, float* C, float* CT,
-                                                            float* AT) {
+// C = A A and C^T for a padded support A [np][ld] (zero outside [n][n], so C is too): one
+// 4-wave workgroup per 32 x 32 output tile on v_mfma_f32_32x32x2_f32, each wave a quarter of K
+// (np / 2 k-steps, a multiple of 16) with its operands loaded four k-steps ahead; the four partial
+// tiles are added in wave order through LDS.  Also A^T when at != nullptr.
+__global__ __launch_bounds__(256) void support_square_kernel(const float* A, int np, int ld, float* C, float* CT,
+                                                             float* AT) {
+  __shared__ float red[4][32][33];
   const int ti = blockIdx.y * 32, tj = blockIdx.x * 32;
-  const int lane = threadIdx.x, half = lane >> 5, col = lane & 31;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
+  const int per = np / 8;  // k-steps per wave (np / 2 in all), a multiple of 4
   f32x16 acc = zero16();
-  // D[i][j] = sum_k A[ti + i][k] A[k][tj + j]: A operand lane (half, col) = A[ti + col][2s + half]
+  // D[i][j] = sum_k A[ti + i][k] A[k][tj + j]: A operand lane (half, col) = A[ti + col][2 ks + half]
   const float* ar = A + (long)(ti + col) * ld + half;
   const float* br = A + (long)half * ld + tj + col;
-  for (int k = 0; k < np; k += 2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[k], br[(long)k * ld], acc, 0, 0, 0);
+  for (int ks = wave * per; ks < (wave + 1) * per; ks += 4) {
+    float a[4], b[4];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int i = ti + crow(r, half), j = tj + col;
-    C[(long)i * ld + j] = acc[r];
-    CT[(long)j * ld + i] = acc[r];
+    for (int j = 0; j < 4; ++j) {
+      a[j] = ar[2 * (ks + j)];
+      b[j] = br[(long)2 * (ks + j) * ld];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wave][crow(r, half)][col] = acc[r];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 1024; e += 256) {
+    const int i = e >> 5, j = e & 31;  // C row-major: coalesced rows
+    C[(long)(ti + i) * ld + tj + j] = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
+    const int jt = e >> 5, it = e & 31;  // C^T rows: C[. ][jt] down the column
+    CT[(long)(tj + jt) * ld + ti + it] = ((red[0][it][jt] + red[1][it][jt]) + red[2][it][jt]) + red[3][it][jt];
   }
   if (AT) {
-    for (int r = half; r < 32; r += 2) AT[(long)(tj + col) * ld + ti + r] = A[(long)(ti + r) * ld + tj + col];
+    __syncthreads();
+    for (int e = threadIdx.x; e < 1024; e += 256) red[0][e >> 5][e & 31] = A[(long)(ti + (e >> 5)) * ld + tj + (e & 31)];
+    __syncthreads();
+    for (int e = threadIdx.x; e < 1024; e += 256) AT[(long)(tj + (e >> 5)) * ld + ti + (e & 31)] = red[0][e & 31][e >> 5];
   }
 }
 
@@ -925,10 +1215,10 @@ size_t fused_lds_bytes(int n) {
   return (size_t)2 * np * LDR * sizeof(float);
 }
 
-// the power schedule keeps one image (node features forward, dh backward)
+// the power schedule keeps one image (node features forward, dh backward) of np + 16 rows
 size_t pow_lds_bytes(int n) {
   const int np = (n + 31) / 32 * 32;
-  return (size_t)np * LDR * sizeof(float);
+  return (size_t)pow_img_rows(np) * LDR * sizeof(float);
 }
 
 template <typename K>
@@ -983,7 +1273,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.h = g->h; a.ld_h = g->ld_h;
   for (int k = 0; k < 8; ++k) a.sup[k] = (k < g->nsup) ? g->sup[k] : nullptr;
   a.nsup = g->nsup; a.ld_sup = g->ld_sup;
-  a.w_mlp = g->w_mlp; a.ld_w = (2 * g->nsup + 1) * CH; a.b_mlp = g->b_mlp;
+  a.w_mlp = g->w_mlp; a.ld_w = (2 * g->nsup + 1) * CH; a.b_mlp = g->b_mlp; a.w_t = g->w_mlp_t;
   a.residual = g->residual; a.z = g->z; a.bn_part = bn_part;
   a.seed_ptr = g->seed_ptr; a.salt = g->salt; a.drop_p = g->drop_p;
   a.n = g->n;
@@ -1023,6 +1313,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.ksplit = pick_ksplit(g, slices, nwt);
   const int grid = a.ksplit > 1 ? (slices + 7) / 8 * 8 * a.ksplit : slices;
   if (g->sup2 && a.sup_batch <= 1 && g->nsup > 0) {
+    GWN_REQUIRE(g->w_mlp_t, "gcn_fwd (power schedule): w_mlp_t (the transposed mlp weights) is required with sup2");
     PowSup p;
     for (int k = 0; k < 8; ++k) p.g2[k] = (k < g->nsup) ? g->sup2[k] : nullptr;
     const size_t lds = pow_lds_bytes(g->n);
@@ -1131,10 +1422,16 @@ extern "C" int gwn_fused_occupancy(int n, int backward, int pow) {
   return e == hipSuccess ? blocks : -(int)e;
 }
 
+extern "C" long gwn_gcn_bn_partial_count(int rows, int n, int c, int nsup, int ld_sup) {
+  (void)c; (void)nsup; (void)ld_sup;
+  if (rows <= 0 || n <= 0 || rows % n) return 0;
+  return rows / n;  // one per slice on every path (the power forward merges its tiles in-kernel)
+}
+
 extern "C" int gwn_support_square(const float* a, int np, int ld, float* a2, float* a2_t, float* a_t, hipStream_t s) {
   GWN_REQUIRE(a && a2 && a2_t && np > 0 && np % 32 == 0 && ld >= np, "support_square: np must be a multiple of 32");
   dim3 grid(np / 32, np / 32);
-  support_square_kernel<<<grid, 64, 0, s>>>(a, np, ld, a2, a2_t, a_t);
+  support_square_kernel<<<grid, 256, 0, s>>>(a, np, ld, a2, a2_t, a_t);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

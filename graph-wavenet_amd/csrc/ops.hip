@@ -568,11 +568,20 @@ __global__ void bn_bwd_apply_kernel(const float* dy, const float* z, long rows, 
 // masked metrics (util.py:510-552, null_val = 0).  ws layout: [0] nonzero count,
 // [1 .. 1+3*RED_BLOCKS) partial (mae, mape, mse) sums, [LOSS_CNT ..) partial nonzero-label counts
 constexpr int LOSS_CNT_BLOCKS = 128;
+// loss_terms blocks: few enough that the last-arriver count costs little (one same-address atomic
+// per block is ~6-7 ns of serialised L2 work), enough to cover the [B][o][n][tf] output
+constexpr int LOSS_TERM_BLOCKS = 128;
+// adam_clipped blocks (grid-stride; same reasoning as LOSS_TERM_BLOCKS)
+constexpr int ADAM_BLOCKS = 256;
 constexpr int LOSS_CNT = 1 + 3 * RED_BLOCKS;
+
+// arrival counter of loss_terms_kernel (reset by loss_count_kernel, which always runs first)
+constexpr int LOSS_ARRIVE = LOSS_CNT + LOSS_CNT_BLOCKS;
 
 __global__ void loss_count_kernel(const float* real, long rsb, long rsn, long rso, int B, int n,
                                   int o, float* ws) {
   __shared__ float sh[256];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *(int*)(ws + LOSS_ARRIVE) = 0;
   const long total = (long)B * n * o;
   float cnt = 0.0f;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += 256L * gridDim.x) {
@@ -588,7 +597,7 @@ __global__ void loss_count_kernel(const float* real, long rsb, long rsn, long rs
 
 __global__ void loss_terms_kernel(const float* out, const float* real, long rsb, long rsn, long rso,
                                   int B, int o, int n, int tf, float mean, float std, float* dout,
-                                  float* ws) {
+                                  float* ws, float* metrics) {
   __shared__ float sh[256];
   const long total = (long)B * o * n * tf;  // out is [B][o][n][tf]
   // every block re-derives the (exact, integer-valued) label count from the count partials
@@ -628,20 +637,25 @@ __global__ void loss_terms_kernel(const float* out, const float* real, long rsb,
   s_mae = block_sum<256>(s_mae, sh);
   s_mape = block_sum<256>(s_mape, sh);
   s_mse = block_sum<256>(s_mse, sh);
+  // hand-off to the last block to arrive (MI355X_MICROARCH.md, inter-workgroup visibility, the
+  // one-lane-per-workgroup row: sc1 (write-through) partial stores, drained, one agent-scope add;
+  // the last arriver reads every partial with sc1 loads)
+  __shared__ int last;
   if (threadIdx.x == 0) {
-    ws[1 + blockIdx.x * 3] = s_mae;
-    ws[2 + blockIdx.x * 3] = s_mape;
-    ws[3 + blockIdx.x * 3] = s_mse;
+    __hip_atomic_store(ws + 1 + blockIdx.x * 3, s_mae, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ws + 2 + blockIdx.x * 3, s_mape, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ws + 3 + blockIdx.x * 3, s_mse, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = atomicAdd((int*)(ws + LOSS_ARRIVE), 1) == (int)gridDim.x - 1;
   }
-}
-
-__global__ void loss_final_kernel(const float* ws, int nblocks, long total, float* metrics) {
-  __shared__ float sh[256];
+  __syncthreads();
+  if (!last) return;
+  // the final sums, in block order per thread then the fixed block_sum tree (deterministic)
   float a = 0.0f, b = 0.0f, c = 0.0f;
-  for (int i = threadIdx.x; i < nblocks; i += 256) {
-    a += ws[1 + i * 3];
-    b += ws[2 + i * 3];
-    c += ws[3 + i * 3];
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) {
+    a += __hip_atomic_load(ws + 1 + i * 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b += __hip_atomic_load(ws + 2 + i * 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c += __hip_atomic_load(ws + 3 + i * 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   a = block_sum<256>(a, sh);
   b = block_sum<256>(b, sh);
@@ -668,6 +682,7 @@ __device__ __forceinline__ bool range_index(const long* lo, const long* hi, int 
 __global__ void sqnorm_partial_kernel(const float* g, const long* lo, const long* hi, int nr,
                                       long active, float* ws) {
   __shared__ float sh[256];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *(int*)(ws + RED_BLOCKS + 1) = 0;  // adam_clipped's counter
   float s = 0.0f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < active;
        i += (long)gridDim.x * blockDim.x) {
@@ -678,31 +693,34 @@ __global__ void sqnorm_partial_kernel(const float* g, const long* lo, const long
   if (threadIdx.x == 0) ws[blockIdx.x] = s;
 }
 
-__global__ void clip_coef_kernel(float* ws, int nparts, float max_norm, long long* step,
-                                 float* total_norm_out) {
+// Adam with the clip coefficient computed in every block from the RED_BLOCKS sq-sum partials in
+// ws (fixed order: every block derives the same coefficient), the step read before use (t = *step
+// + 1) and advanced by the last block to finish (arrival counter at ws[RED_BLOCKS + 1], zeroed by
+// the sq-sum kernel that precedes this launch), which also advances the dropout counter
+// (seed_inc != 0) -- one launch for clip_coef + adam + the two counters.
+__global__ void adam_clipped_kernel(float* p, float* g, float* m, float* v, const long* lo, const long* hi, int nr,
+                                    long active, float* ws, long long* step, float max_norm, float lr, float beta1,
+                                    float beta2, float eps, float wd, float* total_norm_out,
+                                    unsigned long long* seed, unsigned long long seed_inc) {
   __shared__ float sh[256];
+  __shared__ float s_coef;
   float part = 0.0f;
-  for (int i = threadIdx.x; i < nparts; i += 256) part += ws[i];
-  const float s = block_sum<256>(part, sh);
-  if (threadIdx.x != 0) return;
-  const float norm = sqrtf(s);
-  const float coef = max_norm / (norm + 1e-6f);
-  ws[RED_BLOCKS] = coef < 1.0f ? coef : 1.0f;
-  if (total_norm_out) *total_norm_out = norm;
-  *step += 1;
-}
-
-__global__ void adam_kernel(float* p, float* g, float* m, float* v, const long* lo, const long* hi,
-                            int nr, long active, const float* ws, const long long* step, float lr,
-                            float beta1, float beta2, float eps, float wd) {
-  const float coef = ws[RED_BLOCKS];
-  const double t = (double)(*step);
+  for (int i = threadIdx.x; i < RED_BLOCKS; i += 256) part += ws[i];
+  const float sq = block_sum<256>(part, sh);
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(sq);
+    const float coef = max_norm / (norm + 1e-6f);
+    s_coef = coef < 1.0f ? coef : 1.0f;
+    if (blockIdx.x == 0 && total_norm_out) *total_norm_out = norm;
+  }
+  __syncthreads();
+  const float coef = s_coef;
+  const double t = (double)(*step + 1);
   const double bc1 = 1.0 - pow((double)beta1, t);
   const double bc2 = 1.0 - pow((double)beta2, t);
   const float step_size = (float)((double)lr / bc1);
   const float bc2_sqrt = (float)sqrt(bc2);
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < active;
-       i += (long)gridDim.x * blockDim.x) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < active; i += (long)gridDim.x * blockDim.x) {
     long k;
     if (!range_index(lo, hi, nr, i, &k)) continue;
     float gr = g[k] * coef;
@@ -711,12 +729,37 @@ __global__ void adam_kernel(float* p, float* g, float* m, float* v, const long* 
     if (wd != 0.0f) gr = gr + wd * pv;
     float mv = m[k];
     mv = mv + (1.0f - beta1) * (gr - mv);
-    float vv = v[k] * beta2 + (1.0f - beta2) * gr * gr;
+    const float vv = v[k] * beta2 + (1.0f - beta2) * gr * gr;
     m[k] = mv;
     v[k] = vv;
     const float denom = sqrtf(vv) / bc2_sqrt + eps;
     p[k] = pv - step_size * (mv / denom);
   }
+  // every block has read *step above: the last one to arrive advances it (and the dropout counter)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* cnt = (int*)(ws + RED_BLOCKS + 1);
+    if (atomicAdd(cnt, 1) == (int)gridDim.x - 1) {
+      *step += 1;
+      if (seed) *seed += seed_inc;
+      atomicExch(cnt, 0);
+    }
+  }
+}
+
+// dst[i] = src[idx[i]] and the RED_BLOCKS partial sums of dst[i]^2 (the clip norm of a flat
+// gradient whose inactive entries gather the zero slot) in one pass
+__global__ void gather_sqnorm_kernel(const float* src, const int* idx, float* dst, long count, float* ws) {
+  __shared__ float sh[256];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *(int*)(ws + RED_BLOCKS + 1) = 0;  // adam_clipped's counter
+  float s = 0.0f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
+    const float v = src[idx[i]];
+    dst[i] = v;
+    s += v * v;
+  }
+  s = block_sum<256>(s, sh);
+  if (threadIdx.x == 0) ws[blockIdx.x] = s;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1311,7 +1354,7 @@ int gwn_colsum(const float* dy, int rows, int ncol, long ld, float* out, int acc
 // ---------------------------------------------------------------------------------------------
 long gwn_masked_loss_workspace_floats(int B, int o, int n, int tf) {
   (void)B; (void)o; (void)n; (void)tf;
-  return LOSS_CNT + LOSS_CNT_BLOCKS;
+  return LOSS_ARRIVE + 1;
 }
 
 int gwn_masked_loss(const float* out, const float* real, long rsb, long rsn, long rso, int B, int o,
@@ -1320,9 +1363,7 @@ int gwn_masked_loss(const float* out, const float* real, long rsb, long rsn, lon
   GWN_REQUIRE(B > 0 && o > 0 && n > 0 && tf > 0, "masked_loss: bad shape");
   loss_count_kernel<<<LOSS_CNT_BLOCKS, 256, 0, s>>>(real, rsb, rsn, rso, B, n, o, ws);
   GWN_CHECK_LAUNCH();
-  loss_terms_kernel<<<RED_BLOCKS, 256, 0, s>>>(out, real, rsb, rsn, rso, B, o, n, tf, mean, std, dout, ws);
-  GWN_CHECK_LAUNCH();
-  loss_final_kernel<<<1, 256, 0, s>>>(ws, RED_BLOCKS, (long)B * o * n * tf, metrics);
+  loss_terms_kernel<<<LOSS_TERM_BLOCKS, 256, 0, s>>>(out, real, rsb, rsn, rso, B, o, n, tf, mean, std, dout, ws, metrics);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -1330,7 +1371,21 @@ int gwn_masked_loss(const float* out, const float* real, long rsb, long rsn, lon
 // ---------------------------------------------------------------------------------------------
 long gwn_clip_adam_workspace_floats(long total) {
   (void)total;
-  return RED_BLOCKS + 1;
+  return RED_BLOCKS + 2;  // sq-sum partials, (unused), arrival counter
+}
+
+int gwn_adam_clipped(float* params, float* grads, float* exp_avg, float* exp_avg_sq, const long* lo,
+                     const long* hi, int nranges, long active, float max_norm, float lr, float beta1,
+                     float beta2, float eps, float wd, long long* step_ptr, float* ws, float* total_norm_out,
+                     unsigned long long* seed, unsigned long long seed_inc, hipStream_t s) {
+  GWN_REQUIRE(nranges > 0 && active > 0, "adam_clipped: empty");
+  const long want = (active + 255) / 256;
+  const int blocks = (int)(want < ADAM_BLOCKS ? want : ADAM_BLOCKS);
+  adam_clipped_kernel<<<blocks, 256, 0, s>>>(params, grads, exp_avg, exp_avg_sq, lo, hi, nranges, active,
+                                                       ws, step_ptr, max_norm, lr, beta1, beta2, eps, wd,
+                                                       total_norm_out, seed, seed_inc);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
 }
 
 int gwn_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, const long* lo,
@@ -1340,10 +1395,21 @@ int gwn_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq
   GWN_REQUIRE(nranges > 0 && active > 0, "clip_adam: empty");
   sqnorm_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(grads, lo, hi, nranges, active, ws);
   GWN_CHECK_LAUNCH();
-  clip_coef_kernel<<<1, 256, 0, s>>>(ws, RED_BLOCKS, max_norm, step_ptr, total_norm_out);
+  return gwn_adam_clipped(params, grads, exp_avg, exp_avg_sq, lo, hi, nranges, active, max_norm, lr, beta1, beta2,
+                          eps, wd, step_ptr, ws, total_norm_out, nullptr, 0, s);
+}
+
+int gwn_sqnorm_partials(const float* grads, const long* lo, const long* hi, int nranges, long active, float* ws,
+                        hipStream_t s) {
+  GWN_REQUIRE(nranges > 0 && active > 0, "sqnorm_partials: empty");
+  sqnorm_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(grads, lo, hi, nranges, active, ws);
   GWN_CHECK_LAUNCH();
-  adam_kernel<<<grid_for(active), 256, 0, s>>>(params, grads, exp_avg, exp_avg_sq, lo, hi, nranges, active,
-                                               ws, step_ptr, lr, beta1, beta2, eps, wd);
+  return GWN_OK;
+}
+
+int gwn_gather_sqnorm(const float* src, const int* idx, float* dst, long count, float* ws, hipStream_t s) {
+  GWN_REQUIRE(count > 0, "gather_sqnorm: empty");
+  gather_sqnorm_kernel<<<RED_BLOCKS, 256, 0, s>>>(src, idx, dst, count, ws);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

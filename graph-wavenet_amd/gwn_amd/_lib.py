@@ -88,6 +88,7 @@ class GcnArgs(ctypes.Structure):
         ("residual_mean", c_void_p), ("residual_scale", c_void_p), ("residual_shift", c_void_p),
         ("ksplit", c_int), ("ksplit_ws", c_void_p), ("ksplit_count", c_void_p),
         ("sup2", ctypes.POINTER(c_void_p)),
+        ("w_mlp_t", c_void_p),
     ]
 
 
@@ -161,6 +162,7 @@ _SIGS = [
     ("gwn_nconv2_adj_grad", c_int, [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                     c_long, c_int, c_void_p]),
     ("gwn_gcn_fwd", c_int, [ctypes.POINTER(GcnArgs), c_void_p]),
+    ("gwn_gcn_bn_partial_count", c_long, [c_int, c_int, c_int, c_int, c_int]),
     ("gwn_gcn_split_supported", c_int, [c_int, c_int, c_int]),
     ("gwn_split_support_elems", c_long, [c_int, c_int]),
     ("gwn_split_supports", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_long, c_int, c_void_p]),
@@ -213,6 +215,11 @@ _SIGS = [
                               c_float, c_float, c_float, c_float, c_float, c_float, c_void_p, c_void_p,
                               c_void_p, c_void_p]),
     ("gwn_clip_adam_workspace_floats", c_long, [c_long]),
+    ("gwn_adam_clipped", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_long,
+                                 c_float, c_float, c_float, c_float, c_float, c_float, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_u64, c_void_p]),
+    ("gwn_gather_sqnorm", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
+    ("gwn_sqnorm_partials", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_long, c_void_p, c_void_p]),
     ("gwn_gather", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p]),
     ("gwn_to_nchw", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("gwn_from_nchw", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),

@@ -19,7 +19,7 @@ _NO_CLIP = 3.0e38
 
 class FlatAdam(torch.optim.Optimizer):
     """``torch.optim.Adam`` semantics (L2 weight decay, bias correction, amsgrad=False) over the
-    model's flat parameter buffer, executed by ``gwn_clip_adam`` in one pass."""
+    model's flat parameter buffer, executed by ``gwn_adam_clipped`` in one launch."""
 
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         super().__init__(model.parameters(), dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
@@ -31,7 +31,7 @@ class FlatAdam(torch.optim.Optimizer):
         self.step_t = torch.zeros(1, device=flat.device, dtype=torch.long)
         self.total_norm = torch.zeros(1, device=flat.device, dtype=F32)
         self._ranges_key = None
-        self._ws = torch.empty(_lib.load().gwn_clip_adam_workspace_floats(flat.numel()) + 16,
+        self._ws = torch.zeros(_lib.load().gwn_clip_adam_workspace_floats(flat.numel()) + 16,
                                device=flat.device, dtype=F32)
 
     def _ranges(self, names):
@@ -56,14 +56,20 @@ class FlatAdam(torch.optim.Optimizer):
             self._ranges_key = key
         return self._lo, self._hi, self._nr, self._active
 
-    def apply(self, names, max_norm):
-        """clip (max_norm; huge = off) + Adam over the flat ranges of ``names``; grads in grad_flat."""
+    def apply(self, names, max_norm, norm_ready=False, seed=None):
+        """clip (max_norm; huge = off) + Adam over the flat ranges of ``names``; grads in grad_flat.
+        norm_ready: the clip-norm partials are already in the workspace (gwn_gather_sqnorm wrote them
+        while unpacking the gradient): one launch.  seed: a device counter advanced by 1 by the same
+        launch (the dropout counter of the step)."""
         g = self.param_groups[0]
         lo, hi, nr, active = self._ranges(names)
-        _lib.call("gwn_clip_adam", ptr(self.model._flat), ptr(self.grad_flat), ptr(self.exp_avg),
-                  ptr(self.exp_avg_sq), ptr(lo), ptr(hi), nr, active, float(max_norm), float(g["lr"]),
-                  float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), float(g["weight_decay"]),
-                  ptr(self.step_t), ptr(self._ws), ptr(self.total_norm), _lib.stream())
+        args = (ptr(self.model._flat), ptr(self.grad_flat), ptr(self.exp_avg), ptr(self.exp_avg_sq), ptr(lo), ptr(hi),
+                nr, active, float(max_norm), float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]),
+                float(g["eps"]), float(g["weight_decay"]), ptr(self.step_t), ptr(self._ws), ptr(self.total_norm))
+        if not norm_ready:
+            _lib.call("gwn_sqnorm_partials", ptr(self.grad_flat), ptr(lo), ptr(hi), nr, active, ptr(self._ws),
+                      _lib.stream())
+        _lib.call("gwn_adam_clipped", *args, ptr(seed), 1 if seed is not None else 0, _lib.stream())
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -130,7 +136,10 @@ class trainer():
     def _phase_backward(self, acts, dout):
         ex = self.model._executor
         ex.backward(acts, dout)
-        ex.unpack_grads(self.optimizer.grad_flat)
+        # single process: the unpack also leaves the clip-norm partials for the update; data
+        # parallel: the norm is taken after the all-reduce
+        self._norm_ready = not self._distributed()
+        ex.unpack_grads(self.optimizer.grad_flat, self.optimizer._ws if self._norm_ready else None)
 
     def _phase_loss(self, input, real_val, training):
         """pad -> forward -> masked loss (+ its gradient); returns (metrics, saved state, dout)."""
@@ -172,9 +181,10 @@ class trainer():
         model = self.model
         ex = model._executor
         clip = self.clip if self.clip is not None else _NO_CLIP
-        self.optimizer.apply(ex.layout.active, clip)
-        if model.dropout > 0:
-            _lib.call("gwn_increment_u64", ptr(ex.seed), 1, _lib.stream())
+        # one launch: clip + Adam, the step counter and the dropout counter
+        self.optimizer.apply(ex.layout.active, clip, norm_ready=getattr(self, "_norm_ready", False),
+                             seed=ex.seed if model.dropout > 0 else None)
+        self._norm_ready = False
 
     def _distributed(self):
         dist = torch.distributed

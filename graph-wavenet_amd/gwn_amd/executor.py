@@ -106,6 +106,8 @@ class PackedLayout:
                 wname, bname = "residual_convs.%d.weight" % i, "residual_convs.%d.bias" % i
             W = cfg.W
             gather_seg("mlp_w%d" % i, flat_range(wname).reshape(-1))
+            # transposed copy [W][C] for the power-schedule gcn forward (coalesced fragment rows)
+            gather_seg("mlp_wT%d" % i, flat_range(wname).reshape(C, W).t().contiguous().reshape(-1))
             gather_seg("mlp_b%d" % i, flat_range(bname))
             gather_seg("bn_g%d" % i, flat_range("bn.%d.weight" % i))
             gather_seg("bn_b%d" % i, flat_range("bn.%d.bias" % i))
@@ -588,14 +590,14 @@ class Executor:
                               no_pieces=1 if i == L - 1 and self._fused_gcn() else 0,
                               sup_bstride=sq if sup_batch > 1 else 0, sup_batch=sup_batch,
                               residual_mean=raff[0], residual_scale=raff[1], residual_shift=raff[2],
-                              sup2=self._arr_field(acts.sup2_arr),
+                              sup2=self._arr_field(acts.sup2_arr), w_mlp_t=ptr(self.pk("mlp_wT%d" % i)),
                               **self.split_fields(sp, i), **self.ksplit_fields(scr))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
             rm, rv, mom, eps = bn_bufs[i]
             if fold:
                 nxt = i + 1 < L
-                lib.call("gwn_batchnorm_fwd_fold", ptr(bnpart), rows // N, C, ptr(self.pk("bn_g%d" % i)),
+                lib.call("gwn_batchnorm_fwd_fold", ptr(bnpart), self._bn_parts(rows), C, ptr(self.pk("bn_g%d" % i)),
                          ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps, ptr(acts.mean[i]), ptr(acts.rstd[i]),
                          acts.bn_scale[i].data_ptr(),
                          ptr(self.pk("fg_w%d" % (i + 1))) if nxt else None,
@@ -603,7 +605,7 @@ class Executor:
                          acts.w_fold[i + 1].data_ptr() if nxt else None,
                          acts.b_fold[i + 1].data_ptr() if nxt else None, st)
             elif training:
-                lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnpart), rows // N,
+                lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnpart), self._bn_parts(rows),
                          ptr(self.pk("bn_g%d" % i)), ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps,
                          ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), st)
             else:
@@ -622,6 +624,10 @@ class Executor:
         if tail_done is not None:
             main.wait_event(tail_done)
         return out, acts
+
+    def _bn_parts(self, rows):
+        cfg = self.cfg
+        return int(_lib.load().gwn_gcn_bn_partial_count(rows, cfg.N, cfg.C, cfg.nsup if cfg.use_gcn else 0, cfg.NP))
 
     @staticmethod
     def _arr_field(arr):
@@ -795,6 +801,7 @@ class Executor:
                               no_pieces=1, bn_running_mean=ptr(rm), bn_running_var=ptr(rv),
                               bn_weight=ptr(self.pk("bn_g%d" % i)), bn_bias=ptr(self.pk("bn_b%d" % i)),
                               bn_eps=eps, bn_out=ptr(xnext), sup2=self._arr_field(bf["sup2_arr"]),
+                              w_mlp_t=ptr(self.pk("mlp_wT%d" % i)),
                               **self.split_fields(sp, i))
             _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             xcur = xnext
@@ -906,7 +913,8 @@ class Executor:
                                      sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
                                      if acts.supT_arr is not None else None,
                                      skip_weight_grads=1 if (overlap or defer) else 0,
-                                     sup2_t=self._arr_field(getattr(acts, "sup2t_arr", None)),
+                                     sup2_t=self._arr_field(getattr(acts, "sup2t_arr", None))
+                                     if os.environ.get("GWN_GCN_POW_BWD", "1") != "0" else None,
                                      **self.ksplit_fields(sc))
                 sb = getattr(acts, "sup_batch", 1)
                 if sb > 1:
@@ -1073,9 +1081,15 @@ class Executor:
         done.record(side)
         return done
 
-    def unpack_grads(self, gflat):
-        _lib.call("gwn_gather", ptr(self.gpacked), ptr(self.uidx), ptr(gflat), self.layout.flat_total,
-                  _lib.stream())
+    def unpack_grads(self, gflat, norm_ws=None):
+        """Kernel-layout gradients -> the flat buffer; with norm_ws also the clip-norm partials (the
+        optimizer's workspace, gwn_gather_sqnorm)."""
+        if norm_ws is not None:
+            _lib.call("gwn_gather_sqnorm", ptr(self.gpacked), ptr(self.uidx), ptr(gflat), self.layout.flat_total,
+                      ptr(norm_ws), _lib.stream())
+        else:
+            _lib.call("gwn_gather", ptr(self.gpacked), ptr(self.uidx), ptr(gflat), self.layout.flat_total,
+                      _lib.stream())
 
 
 def _ksplit_thin(M, N, K):

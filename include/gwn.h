@@ -35,8 +35,7 @@ int gwn_version(void);
  * every mode (activations, weights, gradients, optimizer state); accumulation is always fp32. */
 typedef enum gwn_dtype {
   GWN_DTYPE_F32 = 0,     /* v_mfma_f32_32x32x2_f32: exact fp32 products (the reference's arithmetic) */
-  GWN_DTYPE_BF16 = 1,    /* bf16 operands, fp32 accumulation (mixed precision, configs[2]) */
-  GWN_DTYPE_BF16X3 = 3   /* 3-piece split bf16 = fp32 accuracy on the bf16 MFMA (forward only) */
+  GWN_DTYPE_BF16 = 1     /* bf16 operands, fp32 accumulation (mixed precision, configs[2]) */
 } gwn_dtype;
 /* debugging aid: 1 = synchronise the device after every kernel launch and report a fault at the
  * kernel's source line (also enabled by GWN_SYNC_CHECK=1 in the environment), 2 = suspended (while
@@ -234,9 +233,9 @@ typedef struct gwn_gcn_args {
   const float* residual;
   float* z;
   const unsigned long long* seed_ptr; unsigned long long salt; float drop_p;
-  /* optional: per-slice BatchNorm partials [rows/n][3][c] (count, mean, M2) of z, written by the
-   * fused path (c == 32, n <= 512) for gwn_batchnorm_fwd_partials; NULL = not wanted.  When the
-   * generic path runs instead, they are computed from z by a separate pass. */
+  /* optional: per-slice BatchNorm partials [rows/n][3][c] (count, mean, M2) of z,
+   * written by the fused path (c == 32, n <= 512) for gwn_batchnorm_fwd_partials / _fold; NULL =
+   * not wanted.  When the generic path runs instead, they are computed from z by a separate pass. */
   float* bn_partials;
   /* --- optional (zero / NULL = off), fused path only ---
    * no_pieces: the hop outputs (pieces 1..2K of h) are not stored: an inference forward that no
@@ -284,6 +283,9 @@ typedef struct gwn_gcn_args {
    * dependency inside a slice) -- equal to A_k^T (A_k^T xg) up to fp32 reassociation.  NULL = the
    * chained hops. */
   const float* const* sup2;
+  /* w_mlp_t: w_mlp transposed, [(2*nsup+1)*c][c] (required with sup2: the power forward reads the
+   * mlp's MFMA fragments as coalesced rows of it) */
+  const float* w_mlp_t;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -291,6 +293,10 @@ typedef struct gwn_gcn_args {
  * must be [np][ld_sup] and ZERO outside [n][n] (gwn_pad_square makes such copies).
  * Otherwise: 2K nconv GEMMs + one mlp GEMM. */
 int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t stream);
+/* number of BatchNorm partial slots gwn_gcn_fwd writes to bn_partials ([slots][3][c]): one per
+ * slice, rows/n (the power forward reduces each wave's tile in registers and merges the tiles of a
+ * slice in-kernel).  The consumer (gwn_batchnorm_fwd_fold / _partials) takes this as nparts. */
+long gwn_gcn_bn_partial_count(int rows, int n, int c, int nsup, int ld_sup);
 
 /* bf16 piece planes for the split path of gwn_gcn_fwd.
  * gwn_split_supports: for each of the nsup padded supports sup[k] ([np][ld_sup], zero outside
@@ -512,7 +518,25 @@ int gwn_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq
                   float max_norm, float lr, float beta1, float beta2, float eps,
                   float weight_decay, long long* step_ptr, float* workspace,
                   float* total_norm_out, hipStream_t stream);
+/* workspace floats of gwn_clip_adam / gwn_adam_clipped (the 512 partials and an arrival counter that
+ * the partial-sum pass -- gwn_sqnorm_partials / gwn_gather_sqnorm / gwn_clip_adam's own -- resets) */
 long gwn_clip_adam_workspace_floats(long total);
+/* The same update in ONE launch when the clip norm's partial sums are already in workspace[0 ..
+ * 512) (gwn_gather_sqnorm): every block derives the clip coefficient from them, reads the step, and
+ * the last block to finish advances *step_ptr and, when seed != NULL, the dropout counter
+ * (*seed += seed_inc) -- clip_grad_norm_ + Adam + the step's counter bookkeeping (engine.py:53-55). */
+int gwn_adam_clipped(float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                     const long* range_lo, const long* range_hi, int nranges, long total,
+                     float max_norm, float lr, float beta1, float beta2, float eps, float weight_decay,
+                     long long* step_ptr, float* workspace, float* total_norm_out,
+                     unsigned long long* seed, unsigned long long seed_inc, hipStream_t stream);
+/* the 512 partial sums of grads^2 over the ranges into workspace[0 .. 512) (for gwn_adam_clipped) */
+int gwn_sqnorm_partials(const float* grads, const long* range_lo, const long* range_hi, int nranges, long total,
+                        float* workspace, hipStream_t stream);
+/* gwn_gather plus the 512 partial sums of dst[i]^2 into workspace[0 .. 512) (the flat gradient's
+ * unpack and its clip-norm partials in one pass; entries gathered from a zero slot add nothing) */
+int gwn_gather_sqnorm(const float* src, const int* idx, float* dst, long count, float* workspace,
+                      hipStream_t stream);
 
 /* dst[i] = src[idx[i]] (parameter repacking into kernel layouts and back). */
 int gwn_gather(const float* src, const int* idx, float* dst, long count, hipStream_t stream);

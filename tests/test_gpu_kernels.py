@@ -454,6 +454,24 @@ def test_gemm_nt(gpu, M, N, K, epi):
     assert float((got[:, :N] - ref).abs().max()) / scale <= 2e-6
 
 
+def _merge_bn(bnp, S, nkb, C):
+    """Per-slice (count, mean, M2) [S][3][C] (fp64) from the per-(slice, tile) BN partial slots the
+    fused forward writes (gwn_gcn_bn_partial_count; count-0 slots carry nothing), Chan's merge."""
+    p = bnp.double().cpu().view(S, nkb, 3, C)
+    n = torch.zeros(S, C, dtype=torch.float64)
+    mean = torch.zeros(S, C, dtype=torch.float64)
+    m2 = torch.zeros(S, C, dtype=torch.float64)
+    for t in range(nkb):
+        nb, mb, qb = p[:, t, 0], p[:, t, 1], p[:, t, 2]
+        nn = n + nb
+        safe = torch.where(nn > 0, nn, torch.ones_like(nn))
+        d = mb - mean
+        mean = torch.where(nb > 0, mean + d * nb / safe, mean)
+        m2 = torch.where(nb > 0, m2 + qb + d * d * n * nb / safe, m2)
+        n = nn
+    return torch.stack([n, mean, m2], dim=1)
+
+
 def _squares(gpu, sups, transposes=False):
     """gwn_support_square of each padded support: (A^2, (A^2)^T[, A^T])."""
     from gwn_amd import _lib
@@ -515,6 +533,7 @@ def test_gcn_fused_schedules_agree(gpu, n):
     arr2T = (ctypes.c_void_p * K)(*[q[1].data_ptr() for q in sq])
     P = ctypes.POINTER(ctypes.c_void_p)
     wm = torch.randn(C, W, device=gpu) * 0.1
+    wmt = wm.t().contiguous()
     bm = torch.randn(C, device=gpu)
     res = torch.randn(rows, C, device=gpu)
     xg = torch.randn(rows, C, device=gpu)
@@ -528,11 +547,11 @@ def test_gcn_fused_schedules_agree(gpu, n):
         h = torch.zeros(rows, W, device=gpu)
         h[:, :C] = xg
         z = torch.empty(rows, C, device=gpu)
-        bnp = torch.empty(S * 3 * C, device=gpu)
+        bnp = torch.full((S * (NP // 32) * 3 * C,), float("nan"), device=gpu)
         ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, P),
                           ld_sup=NP, h=h.data_ptr(), ld_h=W, w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(),
                           residual=res.data_ptr(), z=z.data_ptr(), seed_ptr=seed.data_ptr(), salt=0, drop_p=0.0,
-                          bn_partials=bnp.data_ptr(), sup2=ctypes.cast(arr2, P) if pw else None, **kf)
+                          bn_partials=bnp.data_ptr(), sup2=ctypes.cast(arr2, P) if pw else None, w_mlp_t=wmt.data_ptr(), **kf)
         _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
         dhc = torch.zeros(rows, W, device=gpu)
         gb = _lib.GcnBwdArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, P),
@@ -542,7 +561,7 @@ def test_gcn_fused_schedules_agree(gpu, n):
                              sup2_t=ctypes.cast(arr2T, P) if pw else None, **kf)
         _lib.call("gwn_gcn_bwd", ctypes.byref(gb), _lib.stream())
         torch.cuda.synchronize()
-        outs.append((h.clone(), z.clone(), bnp.clone(), dhc.clone()))
+        outs.append((h.clone(), z.clone(), _merge_bn(bnp, S, 1, C), dhc.clone()))
         assert int(kcnt.abs().sum()) == 0  # the split leaves its counters zero
     # fp64 truth
     X = xg.double().cpu().view(S, n, C)
@@ -564,14 +583,16 @@ def test_gcn_fused_schedules_agree(gpu, n):
         t1, t2 = dx1, dx2
     # fp32 rounding floor (max-abs error / max-abs value): the support split adds the partial
     # sums in another order than the MFMA chains (measured 2.02e-6 on dxg at n = 207)
-    for h, z, bnp, dhc in outs:
+    for h, z, st, dhc in outs:
         assert rel_err(h.cpu().numpy(), H.numpy()) <= 4e-6
         assert rel_err(z.cpu().numpy(), Z.numpy()) <= 4e-6
         assert rel_err(dhc[:, :C].cpu().numpy(), dxg.reshape(rows, C).numpy()) <= 4e-6
         assert rel_err(dhc[:, C:2 * C].cpu().numpy(), t1.reshape(rows, C).numpy()) <= 4e-6
         assert rel_err(dhc[:, 2 * C:3 * C].cpu().numpy(), t2.reshape(rows, C).numpy()) <= 4e-6
-        means = bnp.view(S, 3, C)[:, 1].cpu().double()
-        assert rel_err(means.numpy(), Z.view(S, n, C).mean(1).numpy()) <= 1e-5
+        assert torch.all(st[:, 0] == n)
+        assert rel_err(st[:, 1].numpy(), Z.view(S, n, C).mean(1).numpy()) <= 1e-5
+        m2 = ((Z.view(S, n, C) - Z.view(S, n, C).mean(1, keepdim=True)) ** 2).sum(1)
+        assert rel_err(st[:, 2].numpy(), m2.numpy()) <= 1e-5
     # the split against the whole slice, per schedule: the same products, summed in another order
     for a_i, b_i in ((0, 1), (2, 3)):
         for a_, b_ in zip(outs[a_i], outs[b_i]):
@@ -605,6 +626,7 @@ def test_gcn_split_many_slices_bn_prologue_gate_epilogue(gpu, pw):
     arr2 = (ctypes.c_void_p * K)(*[q[0].data_ptr() for q in sq])
     arr2T = (ctypes.c_void_p * K)(*[q[1].data_ptr() for q in sq])
     wm = torch.randn(C, W, device=gpu) * 0.1
+    wmt = wm.t().contiguous()
     bm = torch.randn(C, device=gpu)
     res = torch.randn(rows, C, device=gpu) * 2 + 1
     rmean, rscale, rshift = torch.randn(C, device=gpu), torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu)
@@ -624,12 +646,12 @@ def test_gcn_split_many_slices_bn_prologue_gate_epilogue(gpu, pw):
         h = torch.zeros(rows, W, device=gpu)
         h[:, :C] = xg
         z = torch.empty(rows, C, device=gpu)
-        bnp = torch.empty(S * 3 * C, device=gpu)
+        bnp = torch.full((S * (NP // 32) * 3 * C,), float("nan"), device=gpu)
         ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, P), ld_sup=NP, h=h.data_ptr(), ld_h=W,
                           w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(), residual=res.data_ptr(), z=z.data_ptr(),
                           seed_ptr=seed.data_ptr(), salt=2, drop_p=0.3, bn_partials=bnp.data_ptr(),
                           residual_mean=rmean.data_ptr(), residual_scale=rscale.data_ptr(),
-                          residual_shift=rshift.data_ptr(), sup2=ctypes.cast(arr2, P) if pw else None, **kf)
+                          residual_shift=rshift.data_ptr(), sup2=ctypes.cast(arr2, P) if pw else None, w_mlp_t=wmt.data_ptr(), **kf)
         _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
         dhc = torch.zeros(rows, W, device=gpu)
         dres = torch.zeros(rows, C, device=gpu)
@@ -648,8 +670,8 @@ def test_gcn_split_many_slices_bn_prologue_gate_epilogue(gpu, pw):
         _lib.call("gwn_gcn_bwd", ctypes.byref(gb), _lib.stream())
         torch.cuda.synchronize()
         assert int(kcnt.abs().sum()) == 0
-        outs.append((h.clone(), z.clone(), bnp.clone(), dres.clone(), dh_out.clone(), dfg.clone(), dhc[:, C:3 * C].clone(),
-                     dg.clone(), db.clone()))
+        outs.append((h.clone(), z.clone(), _merge_bn(bnp, S, 1, C), dres.clone(), dh_out.clone(), dfg.clone(),
+                     dhc[:, C:3 * C].clone(), dg.clone(), db.clone()))
     for a_, b_ in zip(*outs):
         assert rel_err(b_.cpu().numpy(), a_.cpu().numpy()) <= 2e-6
     # dfg really is the gate backward of dxg + dskip (fp64 from the whole-slice run's pieces)
@@ -680,6 +702,7 @@ def test_gcn_pow_forward_modes(gpu, n):
     arr = (ctypes.c_void_p * K)(*[s.data_ptr() for s in sups])
     arr2 = (ctypes.c_void_p * K)(*[q[0].data_ptr() for q in sq])
     wm = torch.randn(C, W, device=gpu) * 0.1
+    wmt = wm.t().contiguous()
     bm = torch.randn(C, device=gpu)
     res = torch.randn(rows, C, device=gpu)
     xg = torch.randn(rows, C, device=gpu)
@@ -689,7 +712,7 @@ def test_gcn_pow_forward_modes(gpu, n):
         h = torch.zeros(rows, W, device=gpu)
         h[:, :C] = xg
         z = torch.full((rows, C), 7.0, device=gpu)
-        bnp = torch.empty(S * 3 * C, device=gpu)
+        bnp = torch.empty(S * (NP // 32) * 3 * C, device=gpu)
         kw = {}
         if eval_bn is not None:
             rm, rv, g_, b_, xo = eval_bn
@@ -700,7 +723,7 @@ def test_gcn_pow_forward_modes(gpu, n):
                           residual=res.data_ptr(), z=None if eval_bn is not None else z.data_ptr(),
                           seed_ptr=seed.data_ptr(), salt=3, drop_p=drop,
                           bn_partials=None if eval_bn is not None else bnp.data_ptr(),
-                          sup2=ctypes.cast(arr2, P) if pw else None, **kw)
+                          sup2=ctypes.cast(arr2, P) if pw else None, w_mlp_t=wmt.data_ptr(), **kw)
         _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
         torch.cuda.synchronize()
         return h, z, bnp
@@ -831,6 +854,7 @@ def test_gcn_fused_per_sample_supports(gpu, n, layout):
     arr = (ctypes.c_void_p * K)(*[sup[k].data_ptr() for k in range(K)])
     arrT = (ctypes.c_void_p * K)(*[supT[k].data_ptr() for k in range(K)])
     wm = torch.randn(C, W, device=gpu) * 0.1
+    wmt = wm.t().contiguous()
     bm = torch.randn(C, device=gpu)
     res = torch.randn(rows, C, device=gpu)
     xg = torch.randn(rows, C, device=gpu)

@@ -9,7 +9,11 @@ D=$(mktemp -d)
 mkdir -p "$D/g"
 cp -r "$ROOT/graph-wavenet_amd/csrc" "$D/g/csrc"
 ln -s "$ROOT/include" "$D/include"   # csrc includes ../../include/gwn.h
-sed -i -e "$expr" "$D/g/csrc/gcn_fused.hip"
+if [[ "$expr" == *.py ]]; then
+  python "$expr" "$D/g/csrc/gcn_fused.hip"   # a transform script edits the copy in place
+else
+  sed -i -e "$expr" "$D/g/csrc/gcn_fused.hip"
+fi
 mkdir -p "$ROOT/graph-wavenet_amd/gwn_amd/exp"
 HIPCC=/opt/rocm/bin/hipcc
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I$ROOT/include"

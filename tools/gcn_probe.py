@@ -24,6 +24,10 @@ def main():
     ap.add_argument("--chain", action="store_true")
     ap.add_argument("--no-pieces", action="store_true")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--no-bn", action="store_true", help="no BN partials (forward)")
+    ap.add_argument("--drop", type=float, default=0.3)
+    ap.add_argument("--stamps", default=None, help="with an experiment build that writes per-wave stamps "
+                    "past the BN partials (tools/exp/stamp_pow.py): save them to this .npy (forward, first T)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     N, C, K, B = args.nodes, 32, 3, args.batch
@@ -48,6 +52,7 @@ def main():
     arr2 = (ctypes.c_void_p * K)(*[s.data_ptr() for s in sq])
     arr2T = (ctypes.c_void_p * K)(*[s.data_ptr() for s in sqt])
     wm = torch.randn(C, W, device=dev) * 0.05
+    wmt = wm.t().contiguous()
     bm = torch.randn(C, device=dev)
     seed = torch.zeros(1, device=dev, dtype=torch.int64)
     lib = _lib.load()
@@ -57,12 +62,15 @@ def main():
         h = torch.randn(rows, W, device=dev)
         res = torch.randn(rows, C, device=dev)
         z = torch.empty(rows, C, device=dev)
-        bnp = torch.empty(T * B * 3 * C, device=dev)
+        nwaves = T * B * ((N + 31) // 32)
+        # BN partial slots (gwn_gcn_bn_partial_count) + room for experiment-build stamps
+        bnp = torch.zeros(lib.gwn_gcn_bn_partial_count(rows, N, C, K, NP) * 3 * C + 8 * nwaves, device=dev)
         ga = _lib.GcnArgs(rows=rows, n=N, c=C, nsup=K, sup=ctypes.cast(arr, P), ld_sup=NP, h=h.data_ptr(), ld_h=W,
                           w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(), residual=res.data_ptr(), z=z.data_ptr(),
-                          seed_ptr=seed.data_ptr(), salt=0, drop_p=0.3, bn_partials=bnp.data_ptr(),
+                          seed_ptr=seed.data_ptr(), salt=0, drop_p=args.drop,
+                          bn_partials=None if args.no_bn else bnp.data_ptr(),
                           no_pieces=1 if args.no_pieces else 0,
-                          sup2=None if args.chain else ctypes.cast(arr2, P), ksplit=1)
+                          sup2=None if args.chain else ctypes.cast(arr2, P), w_mlp_t=wmt.data_ptr(), ksplit=1)
         dh = torch.randn(rows, C, device=dev)
         dhc = torch.empty(rows, W, device=dev)
         gb = _lib.GcnBwdArgs(rows=rows, n=N, c=C, nsup=K, sup=ctypes.cast(arr, P), ld_sup=NP, h=h.data_ptr(),
@@ -83,6 +91,10 @@ def main():
             us = 1000.0 * e0.elapsed_time(e1) / args.reps
             print("%s T=%2d slices=%4d %s %8.1f us  %6.1f TFLOP/s (%.3f of 157.3)"
                   % (args.tag, T, T * B, name, us, flop / us / 1e6, flop / us / 1e6 / 157.3), flush=True)
+            if args.stamps and name == "fwd":
+                import numpy as np
+                st_ = bnp[lib.gwn_gcn_bn_partial_count(rows, N, C, K, NP) * 3 * C:].view(torch.int32).view(nwaves, 8).cpu().numpy()
+                np.save(args.stamps.replace(".npy", "_T%d.npy" % T), st_)
     del lib
 
 
