@@ -441,9 +441,10 @@ __device__ void bn_merge_channel(const float* part, int nparts, int c, int j, do
 
 __global__ void bn_finalize_kernel(const float* part, int nparts, int c, float momentum, float eps,
                                    float* running_mean, float* running_var, float* save_mean,
-                                   float* save_rstd) {
+                                   float* save_rstd, long long* nbt) {
   // one block per channel
   const int j = blockIdx.x;
+  if (nbt && j == 0 && threadIdx.x == 0) *nbt += 1;  // BatchNorm2d.num_batches_tracked
   double n, mean, m2;
   bn_merge_channel(part, nparts, c, j, n, mean, m2);
   if (threadIdx.x != 0) return;
@@ -476,10 +477,12 @@ __global__ void bn_apply_kernel(const float* z, long rows, int c, const float* m
 __global__ void bn_finalize_fold_kernel(const float* part, int nparts, int c, float momentum, float eps,
                                         const float* gamma, const float* beta, float* running_mean,
                                         float* running_var, float* save_mean, float* save_rstd, float* scale,
-                                        const float* w_next, const float* b_next, float* w_fold, float* b_fold) {
+                                        const float* w_next, const float* b_next, float* w_fold, float* b_fold,
+                                        long long* nbt) {
   __shared__ float ssc;
   __shared__ float bp[256];
   const int j = blockIdx.x;
+  if (nbt && j == 0 && threadIdx.x == 0) *nbt += 1;  // BatchNorm2d.num_batches_tracked
   // the weight operands do not depend on the statistics: loaded before the merge (latency hidden)
   const bool wcol = w_next && (int)threadIdx.x < 4 * c;  // (row, tap) pairs of column j
   const long we = (long)(threadIdx.x >> 1) * 2 * c + (threadIdx.x & 1) * c + j;
@@ -570,7 +573,7 @@ __global__ void bn_bwd_apply_kernel(const float* dy, const float* z, long rows, 
 constexpr int LOSS_CNT_BLOCKS = 128;
 // loss_terms blocks: few enough that the last-arriver count costs little (one same-address atomic
 // per block is ~6-7 ns of serialised L2 work), enough to cover the [B][o][n][tf] output
-constexpr int LOSS_TERM_BLOCKS = 128;
+constexpr int LOSS_TERM_BLOCKS = 256;
 // adam_clipped blocks (grid-stride; same reasoning as LOSS_TERM_BLOCKS)
 constexpr int ADAM_BLOCKS = 256;
 constexpr int LOSS_CNT = 1 + 3 * RED_BLOCKS;
@@ -595,11 +598,34 @@ __global__ void loss_count_kernel(const float* real, long rsb, long rsn, long rs
   if (threadIdx.x == 0) ws[LOSS_CNT + blockIdx.x] = cnt;
 }
 
+// one prediction's masked terms (util.py:510-552) and its loss gradient (d mae / d out)
+__device__ __forceinline__ float loss_term(float out, float y, float mean, float std, float mask_scale,
+                                          float inv_total, float& s_mae, float& s_mape, float& s_mse) {
+  const float pred = out * std + mean;
+  const float mask = (y != 0.0f) ? mask_scale : 0.0f;
+  const float diff = pred - y;
+  float mae = fabsf(diff) * mask;
+  if (isnan(mae)) mae = 0.0f;
+  float mape = fabsf(diff) / y * mask;
+  if (isnan(mape)) mape = 0.0f;
+  float mse = diff * diff * mask;
+  if (isnan(mse)) mse = 0.0f;
+  s_mae += mae;
+  s_mape += mape;
+  s_mse += mse;
+  const float sg = (diff > 0.0f) ? 1.0f : ((diff < 0.0f) ? -1.0f : 0.0f);
+  const float g = fabsf(diff) * mask;
+  return isnan(g) ? 0.0f : sg * mask * inv_total * std;
+}
+
+// ROWS = false: out / dout are the reference's [B][o][n][tf]; ROWS = true: the head's slab rows,
+// out[((t*B + b)*n + v)*ld_out + oo], dout alike with ld_dout (its columns o..ld_dout zeroed)
+template <bool ROWS>
 __global__ void loss_terms_kernel(const float* out, const float* real, long rsb, long rsn, long rso,
                                   int B, int o, int n, int tf, float mean, float std, float* dout,
-                                  float* ws, float* metrics) {
+                                  float* ws, float* metrics, int ld_out, int ld_dout) {
   __shared__ float sh[256];
-  const long total = (long)B * o * n * tf;  // out is [B][o][n][tf]
+  const long total = (long)B * o * n * tf;
   // every block re-derives the (exact, integer-valued) label count from the count partials
   const float cnt = block_sum<256>((threadIdx.x < LOSS_CNT_BLOCKS) ? ws[LOSS_CNT + threadIdx.x] : 0.0f, sh);
   const float label_total = (float)((long)B * n * o);
@@ -608,30 +634,28 @@ __global__ void loss_terms_kernel(const float* out, const float* real, long rsb,
   float s_mae = 0.0f, s_mape = 0.0f, s_mse = 0.0f;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
        idx += (long)gridDim.x * blockDim.x) {
-    const int t = (int)(idx % tf);
-    const long r1 = idx / tf;
-    const int v = (int)(r1 % n);
-    const long r2 = r1 / n;
-    const int oo = (int)(r2 % o);
-    const int b = (int)(r2 / o);
-    const float y = real[b * rsb + v * rsn + oo * rso];
-    const float pred = out[idx] * std + mean;
-    const float mask = (y != 0.0f) ? mask_scale : 0.0f;
-    const float diff = pred - y;
-    float mae = fabsf(diff) * mask;
-    if (isnan(mae)) mae = 0.0f;
-    float mape = fabsf(diff) / y * mask;
-    if (isnan(mape)) mape = 0.0f;
-    float mse = diff * diff * mask;
-    if (isnan(mse)) mse = 0.0f;
-    s_mae += mae;
-    s_mape += mape;
-    s_mse += mse;
-    (void)t;
-    if (dout) {
-      const float sg = (diff > 0.0f) ? 1.0f : ((diff < 0.0f) ? -1.0f : 0.0f);
-      const float g = fabsf(diff) * mask;
-      dout[idx] = isnan(g) ? 0.0f : sg * mask * inv_total * std;
+    if (ROWS) {
+      const long r = idx / o;
+      const int oo = (int)(idx - r * o);
+      const int v = (int)(r % n);
+      const int b = (int)((r / n) % B);
+      const float gr = loss_term(out[r * ld_out + oo], real[b * rsb + v * rsn + oo * rso], mean, std, mask_scale,
+                                 inv_total, s_mae, s_mape, s_mse);
+      if (dout) {
+        float* row = dout + r * ld_dout;
+        row[oo] = gr;
+        if (oo == 0)
+          for (int c = o; c < ld_dout; ++c) row[c] = 0.0f;
+      }
+    } else {
+      const long r1 = idx / tf;
+      const int v = (int)(r1 % n);
+      const long r2 = r1 / n;
+      const int oo = (int)(r2 % o);
+      const int b = (int)(r2 / o);
+      const float gr = loss_term(out[idx], real[b * rsb + v * rsn + oo * rso], mean, std, mask_scale, inv_total,
+                                 s_mae, s_mape, s_mse);
+      if (dout) dout[idx] = gr;
     }
   }
   s_mae = block_sum<256>(s_mae, sh);
@@ -767,6 +791,23 @@ __global__ void gather_kernel(const float* src, const int* idx, float* dst, long
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count;
        i += (long)gridDim.x * blockDim.x)
     dst[i] = src[idx[i]];
+}
+
+// gather_kernel plus one computed segment: dst[sum_dst + j] = sum_v src[idx[sum_src + v*len + j]]
+// (v in order, the same sums as sum_vectors_kernel over the gathered vectors)
+__global__ void gather_sum_kernel(const float* src, const int* idx, float* dst, long count, long sum_src, int nvec,
+                                  int len, long sum_dst) {
+  const long total = count + len;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    if (i < count) {
+      if (i < sum_dst || i >= sum_dst + len) dst[i] = src[idx[i]];
+    } else {
+      const long j = i - count;
+      float s = 0.0f;
+      for (int v = 0; v < nvec; ++v) s += src[idx[sum_src + (long)v * len + j]];
+      dst[sum_dst + j] = s;
+    }
+  }
 }
 
 __global__ void to_nchw_kernel(const float* y, int B, int o, int n, int t, float* out) {
@@ -1020,46 +1061,64 @@ int gwn_start_conv_fwd(const float* x, long sb, long sc, long sn, long st, int B
 
 // ---------------------------------------------------------------------------------------------
 int gwn_gated_tcn_fwd(const gwn_tcn_args* a, hipStream_t s) {
-  GWN_REQUIRE(a && a->t_in > a->dilation && a->c > 0 && a->P > 0, "gated_tcn_fwd: bad shape");
-  GWN_REQUIRE(a->c % 16 == 0, "gated_tcn_fwd: channels must be a multiple of 16");
-  const int c = a->c, P = a->P, t_out = a->t_in - a->dilation;
-  if (c == 32 && aligned16(a->x) && aligned16(a->fg)) return gwn_rowgemm_tcn_fwd(a, s);
+  GWN_REQUIRE(a && a->c > 0 && a->P > 0 && a->ntaps >= 0 && a->c_out >= 0, "gated_tcn_fwd: bad shape");
+  const int taps = a->ntaps > 0 ? a->ntaps : 2, co = a->c_out > 0 ? a->c_out : a->c;
+  GWN_REQUIRE(a->t_in > a->dilation * (taps - 1), "gated_tcn_fwd: input shorter than the receptive field");
+  GWN_REQUIRE(a->c % 16 == 0 && co % 16 == 0, "gated_tcn_fwd: channels must be multiples of 16");
+  const int c = a->c, P = a->P, t_out = a->t_in - a->dilation * (taps - 1);
+  if (c == 32 && taps == 2 && co == c && aligned16(a->x) && aligned16(a->fg)) return gwn_rowgemm_tcn_fwd(a, s);
   GWN_REQUIRE(a->fg != nullptr && !a->x_mean, "gated_tcn_fwd: fg may only be NULL (and x_mean set) on the c == 32 path");
   gwn_gemm_desc d = gemm_zero();
   d.A = a->x; d.lda_m = c; d.lda_k = 1; d.a_kin = c; d.a_row_shift = a->dilation * P;
   d.a_rows = a->t_in * P;
-  d.B = a->w_fg; d.ldb_k = 1; d.ldb_n = 2 * c;
+  d.B = a->w_fg; d.ldb_k = 1; d.ldb_n = taps * c;
   d.C = a->xg; d.ldc_m = a->ld_xg; d.ldc_n = 1;
   d.bias_n = a->b_fg;
   d.epi = EPI_GATE;
-  d.aux = a->fg; d.ld_aux = 2 * c;
+  d.aux = a->fg; d.ld_aux = 2 * co;
   d.aux2 = a->skipcat; d.ld_aux2 = a->ld_skip; d.aux2_row0 = a->skip_row0;
-  d.M = t_out * P; d.N = 2 * c; d.K = 2 * c;
+  d.M = t_out * P; d.N = 2 * co; d.K = taps * c;
   return gwn_gemm_launch(d, s);
 }
 
-static int tcn_w_ksplit(int rows, int c) { return pick_ksplit(2 * c, 2 * c, rows); }
+static int tcn_w_ksplit(int rows, int c, int taps, int co) { return pick_ksplit(2 * co, taps * c, rows); }
 
-long gwn_gated_tcn_bwd_workspace_floats(int t_in, int P, int c, int dilation) {
-  const int rows = (t_in - dilation) * P;
-  const long g = gwn_gemm_workspace_floats(2 * c, 2 * c, tcn_w_ksplit(rows, c));
-  const long w = gwn_wgrad_workspace_floats(rows, 2 * c, 2 * c);
+// the weight gradient of the TCN runs on the row-reduction kernel when its tiles fit (gwn_wgrad)
+static bool tcn_wgrad_rows(int c, int taps, int co) {
+  return (2 * co) % 32 == 0 && c % 32 == 0 && (2 * co / 32) * (taps * c / 32) <= 16;
+}
+
+long gwn_gated_tcn_bwd_workspace_floats_ex(int t_in, int P, int c, int dilation, int ntaps, int c_out) {
+  const int taps = ntaps > 0 ? ntaps : 2, co = c_out > 0 ? c_out : c;
+  const int rows = (t_in - dilation * (taps - 1)) * P;
+  if (rows <= 0 || c <= 0) return 0;
+  const long g = gwn_gemm_workspace_floats(2 * co, taps * c, tcn_w_ksplit(rows, c, taps, co));
+  const long w = tcn_wgrad_rows(c, taps, co) ? gwn_wgrad_workspace_floats(rows, 2 * co, taps * c) : 0;
   long m = g > w ? g : w;
   // BN statistics partials of the fused rowgemm epilogue, or of the generic fallback pass
   const long b = (long)(GWN_ROWGEMM_MAX_PARTS > RED_BLOCKS ? GWN_ROWGEMM_MAX_PARTS : RED_BLOCKS) * 2 * c;
   return m > b ? m : b;
 }
 
+long gwn_gated_tcn_bwd_workspace_floats(int t_in, int P, int c, int dilation) {
+  return gwn_gated_tcn_bwd_workspace_floats_ex(t_in, P, c, dilation, 2, c);
+}
+
 int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
-  GWN_REQUIRE(a && a->t_in > a->dilation && a->c % 16 == 0, "gated_tcn_bwd: bad shape");
-  const int c = a->c, P = a->P, t_out = a->t_in - a->dilation;
+  GWN_REQUIRE(a && a->c % 16 == 0 && a->ntaps >= 0 && a->c_out >= 0, "gated_tcn_bwd: bad shape");
+  const int taps = a->ntaps > 0 ? a->ntaps : 2, co = a->c_out > 0 ? a->c_out : a->c;
+  GWN_REQUIRE(a->t_in > a->dilation * (taps - 1) && co % 16 == 0, "gated_tcn_bwd: bad shape");
+  const bool square = taps == 2 && co == a->c;  // the row-GEMM fusions' shape
+  GWN_REQUIRE(square || (!a->dfg_ready && !a->x_mean && !a->x_scale && !a->x_shift),
+              "gated_tcn_bwd: dfg_ready / x_mean fusions need ntaps 2 and c_out == c");
+  const int c = a->c, P = a->P, t_out = a->t_in - a->dilation * (taps - 1);
   const long rows = (long)t_out * P;
   GWN_REQUIRE(a->acc_row0 >= 0 && a->acc_row0 <= (long)a->t_in * P, "gated_tcn_bwd: bad acc_row0");
   if (a->bn_sums) GWN_REQUIRE(a->bn_z && a->bn_mean && a->bn_rstd && c <= 256 && 256 % c == 0,
                               "gated_tcn_bwd: BN statistics need bn_z, bn_mean, bn_rstd");
   if (!a->dfg_ready) {
-    gate_bwd_kernel<<<grid_for(rows * c), 256, 0, s>>>(a->dxg, a->ld_dxg, a->dskip, a->ld_dskip,
-                                                       a->skip_row0, a->fg, rows, c, a->dfg);
+    gate_bwd_kernel<<<grid_for(rows * co), 256, 0, s>>>(a->dxg, a->ld_dxg, a->dskip, a->ld_dskip,
+                                                        a->skip_row0, a->fg, rows, co, a->dfg);
     GWN_CHECK_LAUNCH();
   }
   // dW_fg[j][tap*c + ci] = sum_r dfg[r][j] * x[r + tap*d*P][ci];  db_fg[j] = sum_r dfg[r][j]
@@ -1067,23 +1126,23 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
   gwn_gemm_desc d = gemm_zero();
   if (a->skip_weight_grads) {
     // caller computes dW_fg / db_fg itself (gwn_wgrad)
-  } else if (c % 32 == 0) {
-    rc = gwn_wgrad_bn(a->dfg, 2 * c, 2 * c, a->x, c, (long)a->t_in * P, c, 2, (long)a->dilation * P, (int)rows,
-                      a->x_mean, a->x_scale, a->x_shift, a->dw_fg, 2 * c, a->db_fg, a->workspace, s);
+  } else if (tcn_wgrad_rows(c, taps, co)) {
+    rc = gwn_wgrad_bn(a->dfg, 2 * co, 2 * co, a->x, c, (long)a->t_in * P, c, taps, (long)a->dilation * P, (int)rows,
+                      a->x_mean, a->x_scale, a->x_shift, a->dw_fg, taps * c, a->db_fg, a->workspace, s);
   } else {
     GWN_REQUIRE(!a->x_mean && !a->x_scale && !a->x_shift, "gated_tcn_bwd: x_mean / x_scale / x_shift need c % 32 == 0");
-    d.A = a->dfg; d.lda_m = 1; d.lda_k = 2 * c;
+    d.A = a->dfg; d.lda_m = 1; d.lda_k = 2 * co;
     d.B = a->x; d.ldb_k = c; d.ldb_n = 1; d.b_nin = c; d.b_no_stride = (long)a->dilation * P * c;
-    d.C = a->dw_fg; d.ldc_m = 2 * c; d.ldc_n = 1;
+    d.C = a->dw_fg; d.ldc_m = taps * c; d.ldc_n = 1;
     d.ones_out = a->db_fg;
-    d.M = 2 * c; d.N = 2 * c; d.K = (int)rows;
-    d.ksplit = tcn_w_ksplit((int)rows, c);
+    d.M = 2 * co; d.N = taps * c; d.K = (int)rows;
+    d.ksplit = tcn_w_ksplit((int)rows, c, taps, co);
     d.part = a->workspace;
     rc = gwn_gemm_launch(d, s);
   }
   if (rc) return rc;
   // dx[r'][ci] (+)= sum_tap sum_j dfg[r' - tap*d*P][j] * Wfg[j][tap*c + ci]
-  if (c == 32 && aligned16(a->dfg) && aligned16(a->dx)) {
+  if (c == 32 && square && aligned16(a->dfg) && aligned16(a->dx)) {
     rc = gwn_rowgemm_tcn_bwd_data(a, s);
     if (rc || !a->bn_sums) return rc;
     colsum_final_wide_kernel<<<2 * c, 256, 0, s>>>(a->workspace, gwn_rowgemm_tcn_bwd_nparts(a), 2 * c,
@@ -1096,12 +1155,12 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
       return gwn_set_error(GWN_ERR_HIP, "gated_tcn_bwd: memset failed");
   }
   d = gemm_zero();
-  d.A = a->dfg; d.lda_m = 2 * c; d.lda_k = 1; d.a_kin = 2 * c; d.a_row_shift = -a->dilation * P;
+  d.A = a->dfg; d.lda_m = 2 * co; d.lda_k = 1; d.a_kin = 2 * co; d.a_row_shift = -a->dilation * P;
   d.a_rows = (int)rows;
-  d.B = a->w_fg; d.ldb_k = 2 * c; d.ldb_n = 1; d.b_kin = 2 * c; d.b_ko_stride = c;
+  d.B = a->w_fg; d.ldb_k = taps * c; d.ldb_n = 1; d.b_kin = 2 * co; d.b_ko_stride = c;
   d.C = a->dx; d.ldc_m = c; d.ldc_n = 1;
   if (a->accumulate_dx) { d.C0 = a->dx; d.ldc0_m = c; d.ldc0_n = 1; d.beta = 1.0f; }
-  d.M = a->t_in * P; d.N = c; d.K = 4 * c;
+  d.M = a->t_in * P; d.N = c; d.K = taps * 2 * co;
   rc = gwn_gemm_launch(d, s);
   if (rc || !a->bn_sums) return rc;
   const long rows_in = (long)a->t_in * P;
@@ -1117,7 +1176,9 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
 int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_fwd: rows must be slices*n");
   const int c = a->c, n = a->n, slices = a->rows / n;
-  if (gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup)) return gwn_gcn_fused_fwd_launch(a, a->bn_partials, s);
+  GWN_REQUIRE(a->c_out >= 0, "gcn_fwd: bad c_out");
+  const int co = a->c_out > 0 ? a->c_out : c;
+  if (co == c && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup)) return gwn_gcn_fused_fwd_launch(a, a->bn_partials, s);
   GWN_REQUIRE(a->sup_batch <= 1, "gcn_fwd: per-sample supports need the fused path (c == 32, n <= 512)");
   GWN_REQUIRE(!a->no_pieces && !a->bn_out && !a->residual_scale && !a->residual_mean,
               "gcn_fwd: no_pieces / bn_out / residual_scale need the fused path (c == 32, n <= 512)");
@@ -1133,15 +1194,15 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   gwn_gemm_desc d = gemm_zero();
   d.A = a->h; d.lda_m = a->ld_h; d.lda_k = 1;
   d.B = a->w_mlp; d.ldb_k = 1; d.ldb_n = width;
-  d.C = a->z; d.ldc_m = c; d.ldc_n = 1;
+  d.C = a->z; d.ldc_m = co; d.ldc_n = 1;
   d.bias_n = a->b_mlp;
-  d.C0 = a->residual; d.ldc0_m = c; d.ldc0_n = 1; d.beta = 1.0f;
+  d.C0 = a->residual; d.ldc0_m = co; d.ldc0_n = 1; d.beta = 1.0f;
   d.seed_ptr = a->seed_ptr; d.seed_salt = a->salt; d.drop_p = a->drop_p;
-  d.M = a->rows; d.N = c; d.K = width;
+  d.M = a->rows; d.N = co; d.K = width;
   int rc = gwn_gemm_launch(d, s);
   if (rc || !a->bn_partials) return rc;
-  GWN_REQUIRE(c <= 256 && 256 % c == 0, "gcn_fwd: BN partials need c | 256");
-  bn_partial_kernel<<<slices, 256, 0, s>>>(a->z, a->rows, c, a->bn_partials);  // one chunk per slice
+  GWN_REQUIRE(co <= 256 && 256 % co == 0, "gcn_fwd: BN partials need c_out | 256");
+  bn_partial_kernel<<<slices, 256, 0, s>>>(a->z, a->rows, co, a->bn_partials);  // one chunk per slice
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -1149,10 +1210,15 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
 static int gcn_w_ksplit(int rows, int c, int width) { return pick_ksplit(c, width, rows); }
 
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup) {
+  return gwn_gcn_bwd_workspace_floats_ex(rows, n, c, nsup, c);
+}
+
+long gwn_gcn_bwd_workspace_floats_ex(int rows, int n, int c, int nsup, int c_out) {
+  const int co = c_out > 0 ? c_out : c;
   const int width = (2 * nsup + 1) * c;
-  long w = gwn_gemm_workspace_floats(c, width, gcn_w_ksplit(rows, c, width));
+  long w = gwn_gemm_workspace_floats(co, width, gcn_w_ksplit(rows, co, width));
   const long g = gwn_nconv_adj_grad_workspace_floats(n, c, rows / n);
-  const long v = gwn_wgrad_workspace_floats(rows, c, width);
+  const long v = gwn_wgrad_workspace_floats(rows, co, width);
   const long gr = gwn_gram_workspace_floats(n, rows / n);  // any slice count up to rows / n
   if (v > w) w = v;
   if (gr > w) w = gr;
@@ -1167,8 +1233,10 @@ long gwn_gcn_ksplit_ws_floats(int rows, int n, int nsup) {
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_bwd: rows must be slices*n");
   const int c = a->c, n = a->n, slices = a->rows / n;
+  GWN_REQUIRE(a->c_out >= 0, "gcn_bwd: bad c_out");
+  const int co = a->c_out > 0 ? a->c_out : c;
   const int width = (2 * a->nsup + 1) * c;
-  const bool fused = a->sup_t && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup);
+  const bool fused = co == c && a->sup_t && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup);
   GWN_REQUIRE(fused || (!a->bn_dy && !a->dfg && a->sup_batch <= 1),
               "gcn_bwd: the BN / gate fusions and per-sample supports need the fused path "
               "(sup_t given, c == 32, n <= 512)");
@@ -1186,16 +1254,16 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   // dW_mlp[j][k] = sum_r dh[r][j] h[r][k];  db_mlp[j] = sum_r dh[r][j]
   gwn_gemm_desc d = gemm_zero();
   if (!wgrads) {
-  } else if (c % 32 == 0 && width % 32 == 0) {
-    rc = gwn_wgrad(dh, c, c, a->h, a->ld_h, a->rows, width, 1, 0, a->rows, a->dw_mlp, width, a->db_mlp,
+  } else if (co % 32 == 0 && width % 32 == 0 && (co / 32) * (width / 32) <= 16) {
+    rc = gwn_wgrad(dh, co, co, a->h, a->ld_h, a->rows, width, 1, 0, a->rows, a->dw_mlp, width, a->db_mlp,
                    a->workspace, s);
   } else {
-    d.A = dh; d.lda_m = 1; d.lda_k = c;
+    d.A = dh; d.lda_m = 1; d.lda_k = co;
     d.B = a->h; d.ldb_k = a->ld_h; d.ldb_n = 1;
     d.C = a->dw_mlp; d.ldc_m = width; d.ldc_n = 1;
     d.ones_out = a->db_mlp;
-    d.M = c; d.N = width; d.K = a->rows;
-    d.ksplit = gcn_w_ksplit(a->rows, c, width);
+    d.M = co; d.N = width; d.K = a->rows;
+    d.ksplit = gcn_w_ksplit(a->rows, co, width);
     d.part = a->workspace;
     rc = gwn_gemm_launch(d, s);
   }
@@ -1220,10 +1288,10 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   }
   // dhcat[r][k] = sum_j dh[r][j] W[j][k]
   d = gemm_zero();
-  d.A = a->dh; d.lda_m = c; d.lda_k = 1;
+  d.A = a->dh; d.lda_m = co; d.lda_k = 1;
   d.B = a->w_mlp; d.ldb_k = width; d.ldb_n = 1;
   d.C = a->dhcat; d.ldc_m = a->ld_dhcat; d.ldc_n = 1;
-  d.M = a->rows; d.N = width; d.K = c;
+  d.M = a->rows; d.N = width; d.K = co;
   rc = gwn_gemm_launch(d, s);
   if (rc) return rc;
   // A x = (A^T)^T x: with the transposed supports the products run on the transpose_a = 1 kernels
@@ -1268,7 +1336,7 @@ int gwn_batchnorm_fwd(const float* z, int rows, int c, const float* gamma, const
     bn_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(z, rows, c, ws);
     GWN_CHECK_LAUNCH();
     bn_finalize_kernel<<<c, 256, 0, s>>>(ws, RED_BLOCKS, c, momentum, eps, running_mean, running_var,
-                                         save_mean, save_rstd);
+                                         save_mean, save_rstd, nullptr);
     GWN_CHECK_LAUNCH();
     bn_apply_kernel<<<grid_for(total), 256, 0, s>>>(z, rows, c, save_mean, save_rstd, nullptr, eps,
                                                     gamma, beta, out);
@@ -1289,10 +1357,10 @@ int gwn_batchnorm_fwd(const float* z, int rows, int c, const float* gamma, const
 int gwn_batchnorm_fwd_partials(const float* z, int rows, int c, const float* partials, int nparts,
                                const float* gamma, const float* beta, float* running_mean, float* running_var,
                                float momentum, float eps, float* out, float* save_mean, float* save_rstd,
-                               hipStream_t s) {
+                               long long* num_batches_tracked, hipStream_t s) {
   GWN_REQUIRE(rows > 0 && c > 0 && nparts > 0, "batchnorm_fwd_partials: bad shape");
   bn_finalize_kernel<<<c, 256, 0, s>>>(partials, nparts, c, momentum, eps, running_mean, running_var,
-                                       save_mean, save_rstd);
+                                       save_mean, save_rstd, num_batches_tracked);
   GWN_CHECK_LAUNCH();
   const long total = (long)rows * c;
   bn_apply_kernel<<<grid_for(total), 256, 0, s>>>(z, rows, c, save_mean, save_rstd, nullptr, eps, gamma,
@@ -1304,13 +1372,14 @@ int gwn_batchnorm_fwd_partials(const float* z, int rows, int c, const float* par
 int gwn_batchnorm_fwd_fold(const float* partials, int nparts, int c, const float* gamma, const float* beta,
                            float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
                            float* save_rstd, float* scale, const float* w_next, const float* b_next, float* w_fold,
-                           float* b_fold, hipStream_t s) {
+                           float* b_fold, long long* num_batches_tracked, hipStream_t s) {
   GWN_REQUIRE(c == 32 && nparts > 0 && partials && gamma && beta && save_mean && save_rstd && scale,
               "batchnorm_fwd_fold: needs c == 32, the partials, gamma / beta and the outputs");
   GWN_REQUIRE(!w_next || (b_next && w_fold && b_fold && w_fold != w_next),
               "batchnorm_fwd_fold: w_next needs b_next, w_fold, b_fold (w_fold not aliasing w_next)");
   bn_finalize_fold_kernel<<<c, 256, 0, s>>>(partials, nparts, c, momentum, eps, gamma, beta, running_mean,
-                                            running_var, save_mean, save_rstd, scale, w_next, b_next, w_fold, b_fold);
+                                            running_var, save_mean, save_rstd, scale, w_next, b_next, w_fold, b_fold,
+                                            num_batches_tracked);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -1363,7 +1432,20 @@ int gwn_masked_loss(const float* out, const float* real, long rsb, long rsn, lon
   GWN_REQUIRE(B > 0 && o > 0 && n > 0 && tf > 0, "masked_loss: bad shape");
   loss_count_kernel<<<LOSS_CNT_BLOCKS, 256, 0, s>>>(real, rsb, rsn, rso, B, n, o, ws);
   GWN_CHECK_LAUNCH();
-  loss_terms_kernel<<<LOSS_TERM_BLOCKS, 256, 0, s>>>(out, real, rsb, rsn, rso, B, o, n, tf, mean, std, dout, ws, metrics);
+  loss_terms_kernel<false><<<LOSS_TERM_BLOCKS, 256, 0, s>>>(out, real, rsb, rsn, rso, B, o, n, tf, mean, std, dout,
+                                                             ws, metrics, 0, 0);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_masked_loss_rows(const float* y, int ld_y, const float* real, long rsb, long rsn, long rso, int B, int o,
+                         int n, int tf, float mean, float std, float* metrics, float* dy, int ld_dy, float* ws,
+                         hipStream_t s) {
+  GWN_REQUIRE(B > 0 && o > 0 && n > 0 && tf > 0 && ld_y >= o && (!dy || ld_dy >= o), "masked_loss_rows: bad shape");
+  loss_count_kernel<<<LOSS_CNT_BLOCKS, 256, 0, s>>>(real, rsb, rsn, rso, B, n, o, ws);
+  GWN_CHECK_LAUNCH();
+  loss_terms_kernel<true><<<LOSS_TERM_BLOCKS, 256, 0, s>>>(y, real, rsb, rsn, rso, B, o, n, tf, mean, std, dy, ws,
+                                                           metrics, ld_y, ld_dy);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -1417,6 +1499,16 @@ int gwn_gather_sqnorm(const float* src, const int* idx, float* dst, long count, 
 int gwn_gather(const float* src, const int* idx, float* dst, long count, hipStream_t s) {
   if (count <= 0) return GWN_OK;
   gather_kernel<<<grid_for(count), 256, 0, s>>>(src, idx, dst, count);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+int gwn_gather_sum(const float* src, const int* idx, float* dst, long count, long sum_src, int nvec, int len,
+                   long sum_dst, hipStream_t s) {
+  GWN_REQUIRE(count > 0 && nvec >= 0 && len >= 0 && sum_src >= 0 && sum_src + (long)nvec * len <= count &&
+                  sum_dst >= 0 && sum_dst + len <= count,
+              "gather_sum: segments outside [0, count)");
+  gather_sum_kernel<<<grid_for(count + len), 256, 0, s>>>(src, idx, dst, count, sum_src, nvec, len, sum_dst);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

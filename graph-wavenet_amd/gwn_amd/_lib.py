@@ -47,6 +47,7 @@ class TcnArgs(ctypes.Structure):
         ("fg", c_void_p),
         ("skipcat", c_void_p), ("ld_skip", c_long), ("skip_row0", c_int),
         ("x_mean", c_void_p),
+        ("ntaps", c_int), ("c_out", c_int),
     ]
 
 
@@ -64,6 +65,7 @@ class TcnBwdArgs(ctypes.Structure):
         ("dfg_ready", c_int), ("acc_row0", c_long),
         ("bn_z", c_void_p), ("bn_mean", c_void_p), ("bn_rstd", c_void_p), ("bn_sums", c_void_p),
         ("x_mean", c_void_p), ("x_scale", c_void_p), ("x_shift", c_void_p),
+        ("ntaps", c_int), ("c_out", c_int),
     ]
 
 
@@ -89,6 +91,7 @@ class GcnArgs(ctypes.Structure):
         ("ksplit", c_int), ("ksplit_ws", c_void_p), ("ksplit_count", c_void_p),
         ("sup2", ctypes.POINTER(c_void_p)),
         ("w_mlp_t", c_void_p),
+        ("c_out", c_int),
     ]
 
 
@@ -127,6 +130,7 @@ class GcnBwdArgs(ctypes.Structure):
         ("wT_split", c_void_p),
         ("ksplit", c_int), ("ksplit_ws", c_void_p), ("ksplit_count", c_void_p),
         ("sup2_t", ctypes.POINTER(c_void_p)),
+        ("c_out", c_int),
     ]
 
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time
@@ -157,6 +161,7 @@ _SIGS = [
     ("gwn_gated_tcn_fwd", c_int, [ctypes.POINTER(TcnArgs), c_void_p]),
     ("gwn_gated_tcn_bwd", c_int, [ctypes.POINTER(TcnBwdArgs), c_void_p]),
     ("gwn_gated_tcn_bwd_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
+    ("gwn_gated_tcn_bwd_workspace_floats_ex", c_long, [c_int, c_int, c_int, c_int, c_int, c_int]),
     ("gwn_nconv2", c_int, [c_void_p, c_int, c_long, c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int,
                            c_int, c_void_p]),
     ("gwn_nconv2_adj_grad", c_int, [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int,
@@ -172,6 +177,7 @@ _SIGS = [
     ("gwn_bf16_mlpT_weights", c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p]),
     ("gwn_gcn_bwd", c_int, [ctypes.POINTER(GcnBwdArgs), c_void_p]),
     ("gwn_gcn_bwd_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
+    ("gwn_gcn_bwd_workspace_floats_ex", c_long, [c_int, c_int, c_int, c_int, c_int]),
     ("gwn_gcn_ksplit_ws_floats", c_long, [c_int, c_int, c_int]),
     ("gwn_wgrad", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,
                           c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
@@ -184,6 +190,9 @@ _SIGS = [
                              c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     ("gwn_gram", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_int,
                          c_int, c_void_p, c_void_p]),
+    ("gwn_masked_loss_rows", c_int, [c_void_p, c_int, c_void_p, c_long, c_long, c_long, c_int, c_int, c_int, c_int,
+                                     c_float, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    ("gwn_gather_sum", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_long, c_void_p]),
     ("gwn_gram_workspace_floats", c_long, [c_int, c_int]),
     ("gwn_gram_bf16", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_int,
                               c_int, c_void_p, c_void_p]),
@@ -191,10 +200,11 @@ _SIGS = [
                                   c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gwn_batchnorm_workspace_floats", c_long, [c_int, c_int]),
     ("gwn_batchnorm_fwd_partials", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
-                                           c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                           c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p]),
     ("gwn_batchnorm_fwd_fold", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                        c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                       c_void_p, c_void_p]),
+                                       c_void_p, c_void_p, c_void_p]),
     ("gwn_fused_occupancy", c_int, [c_int, c_int, c_int]),
     ("gwn_support_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gwn_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),

@@ -151,17 +151,17 @@ class trainer():
         acts = self._acts.get(key)
         out, acts = ex.forward(model._flat, model._fixed_supports(), input, training, model._bn_bufs(),
                                fixed_t=model._fixed_supports_t(),
-                               acts=acts, lead_pad=1)
+                               acts=acts, lead_pad=1, want_out=False)
         self._acts[key] = acts
-        if training:
-            model._nbt.add_(1)
         sc = ex.scratch(B, ts)
-        dout = torch.empty_like(out) if training else None
         rs = real_val.stride()
-        _lib.call("gwn_masked_loss", ptr(out), ptr(real_val), rs[0], rs[1], rs[2], B, ex.cfg.O, ex.cfg.N,
-                  ts[-1], float(self.scaler.mean), float(self.scaler.std), ptr(sc["metrics"]), ptr(dout),
-                  ptr(sc["ws"]), _lib.stream())
-        return sc["metrics"], acts, dout
+        # the loss reads the head's rows and writes the output gradient in the backward's row layout
+        # (no NCHW round trip; the gradient stays in scratch "dy")
+        cfg = ex.cfg
+        _lib.call("gwn_masked_loss_rows", ptr(acts.y), cfg.O, ptr(real_val), rs[0], rs[1], rs[2], B, cfg.O, cfg.N,
+                  ts[-1], float(self.scaler.mean), float(self.scaler.std), ptr(sc["metrics"]),
+                  ptr(sc["dy"]) if training else None, cfg.OP, ptr(sc["ws"]), _lib.stream())
+        return sc["metrics"], acts, None
 
     def _eval_lean(self, input, real_val):
         """engine.py:119-130 on the lean inference schedule: pad 1, eval forward (no saved state),
@@ -248,7 +248,7 @@ class trainer():
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2, pool=g0.pool()):
                 self._phase_update()
-        # dout lives in g0's pool and is read by g1: the entry keeps it (and acts) referenced
+        # acts (and the scratch dy the loss wrote) live on; the entry keeps them referenced
         self._graphs[key] = (g0, g1, g2, sx, sy, m, (acts, dout))
 
     def _replay(self, key, input, real_val):

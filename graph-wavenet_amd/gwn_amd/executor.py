@@ -35,8 +35,7 @@ class PackedLayout:
 
     def __init__(self, model, cfg=None):
         cfg = cfg if cfg is not None else Config(model)
-        C, Cin, S, E, O, L = cfg.C, cfg.Cin, cfg.S, cfg.E, cfg.O, cfg.L
-        offs = {}
+        C, D, K, Cin, S, E, O, L = cfg.C, cfg.D, cfg.K, cfg.Cin, cfg.S, cfg.E, cfg.O, cfg.L
         names = [n for n, _ in model.named_parameters()]
         flat_off = {}
         o = 0
@@ -85,19 +84,19 @@ class PackedLayout:
                 map_grad("nodevec1", seg_index("nv1", tuple(flat_off["nodevec1"][1])))
                 map_grad("nodevec2", seg_index("nv2", tuple(flat_off["nodevec2"][1])))
         for i in range(L):
-            fw = flat_range("filter_convs.%d.weight" % i).reshape(C, C, 2)   # [co][ci][tap]
-            gw = flat_range("gate_convs.%d.weight" % i).reshape(C, C, 2)
-            # packed [2C rows j=2co+g][2C cols k=tap*C+ci]
+            fw = flat_range("filter_convs.%d.weight" % i).reshape(D, C, K)   # [co][ci][tap]
+            gw = flat_range("gate_convs.%d.weight" % i).reshape(D, C, K)
+            # packed [2D rows j=2co+g][K*C cols k=tap*C+ci]
             both = torch.stack([fw, gw], dim=1)  # [co][g][ci][tap]
-            packed = both.permute(0, 1, 3, 2).reshape(2 * C, 2 * C)
+            packed = both.permute(0, 1, 3, 2).reshape(2 * D, K * C)
             gather_seg("fg_w%d" % i, packed.reshape(-1))
-            idx = seg_index("fg_w%d" % i, (C, 2, 2, C))  # [co][g][tap][ci]
-            map_grad("filter_convs.%d.weight" % i, idx[:, 0].permute(0, 2, 1).reshape(C, C, 1, 2))
-            map_grad("gate_convs.%d.weight" % i, idx[:, 1].permute(0, 2, 1).reshape(C, C, 1, 2))
+            idx = seg_index("fg_w%d" % i, (D, 2, K, C))  # [co][g][tap][ci]
+            map_grad("filter_convs.%d.weight" % i, idx[:, 0].permute(0, 2, 1).reshape(D, C, 1, K))
+            map_grad("gate_convs.%d.weight" % i, idx[:, 1].permute(0, 2, 1).reshape(D, C, 1, K))
             fb = flat_range("filter_convs.%d.bias" % i)
             gb = flat_range("gate_convs.%d.bias" % i)
             gather_seg("fg_b%d" % i, torch.stack([fb, gb], dim=1).reshape(-1))
-            bidx = seg_index("fg_b%d" % i, (C, 2))
+            bidx = seg_index("fg_b%d" % i, (D, 2))
             map_grad("filter_convs.%d.bias" % i, bidx[:, 0].clone())
             map_grad("gate_convs.%d.bias" % i, bidx[:, 1].clone())
             if cfg.use_gcn:
@@ -117,12 +116,12 @@ class PackedLayout:
                 map_grad("bn.%d.weight" % i, seg_index("bn_g%d" % i, (C,)))
                 map_grad("bn.%d.bias" % i, seg_index("bn_b%d" % i, (C,)))
             assert flat_off[wname][1][1] == W
-        # skip convs concatenated along K: [S][L*C]
-        sk = torch.stack([flat_range("skip_convs.%d.weight" % i).reshape(S, C) for i in range(L)], dim=1)
+        # skip convs concatenated along K: [S][L*D]
+        sk = torch.stack([flat_range("skip_convs.%d.weight" % i).reshape(S, D) for i in range(L)], dim=1)
         gather_seg("skip_w", sk.reshape(-1))
-        skidx = seg_index("skip_w", (S, L, C))
+        skidx = seg_index("skip_w", (S, L, D))
         for i in range(L):
-            map_grad("skip_convs.%d.weight" % i, skidx[:, i].reshape(S, C, 1, 1).clone())
+            map_grad("skip_convs.%d.weight" % i, skidx[:, i].reshape(S, D, 1, 1).clone())
         gather_seg("skip_b", torch.cat([flat_range("skip_convs.%d.bias" % i) for i in range(L)]))
         # computed slot: sum_i skip bias (and, for grads, the shared bias gradient)
         segs["skip_bsum"] = (len(pidx), S)
@@ -138,7 +137,7 @@ class PackedLayout:
         gather_seg("e2_b", flat_range("end_conv_2.bias"))
         map_grad("end_conv_2.bias", seg_index("e2_b", (O,)))
         # transposed copies of the head weights for the input gradients (NT GEMMs, no grads)
-        gather_seg("skip_wT", sk.reshape(S, L * C).t().contiguous().reshape(-1))
+        gather_seg("skip_wT", sk.reshape(S, L * D).t().contiguous().reshape(-1))
         gather_seg("e1_wT", flat_range("end_conv_1.weight").reshape(E, S).t().contiguous().reshape(-1))
         gather_seg("e2_wT", flat_range("end_conv_2.weight").reshape(O, E).t().contiguous().reshape(-1))
         self.zero_slot = len(pidx)
@@ -180,9 +179,11 @@ class PackedLayout:
 class Config:
     """Static model configuration (mirrors the gwnet ctor, model.py:83-171)."""
 
-    def __init__(self, model):
+    def __init__(self, model, residual_only=False):
         self.N = model.num_nodes
-        self.C = model.residual_channels
+        self.C = model.residual_channels   # residual / BatchNorm / gcn-output channels
+        self.D = model.dilation_channels   # gated-TCN output, gcn input and skip-conv input channels
+        self.K = model.kernel_size         # taps of the dilated convs (model.py:135-141)
         self.Cin = model.in_dim
         self.S = model.skip_channels
         self.E = model.end_channels
@@ -203,7 +204,9 @@ class Config:
         # [B][N][N] input of the call; the adaptive embeddings are not parameters
         self.per_sample = bool(getattr(model, "per_sample_graphs", False))
         if self.per_sample:
-            self.use_gcn = bool(model.gcn_bool)
+            # residual_only: gwnet_diff_G called without supports (model.py:391-398 takes the
+            # residual_convs branch whenever the gcn does not run)
+            self.use_gcn = bool(model.gcn_bool) and not residual_only
             self.nsup = model.supports_len if self.use_gcn else 0
             self.nfixed = self.nsup
             self.adp_params = False
@@ -212,23 +215,31 @@ class Config:
             self.nfixed = len(model.supports) if (self.use_gcn and model.supports is not None) else 0
             self.nsup = self.nfixed + (1 if (self.use_gcn and self.adaptive) else 0)
             self.adp_params = bool(self.use_gcn and self.adaptive)  # trained nodevec1 / nodevec2
-        self.W = (2 * self.nsup + 1) * self.C if self.use_gcn else self.C
+        self.W = (2 * self.nsup + 1) * self.D if self.use_gcn else self.D
         # the adaptive support reaches the output only through a gcn of a non-final layer (the
         # last layer's gcn output is dead, model.py:225-236): otherwise nodevec1/2 keep grad None
         self.adp_live = bool(self.adp_params and self.L > 1)
         self.NP = (self.N + 31) // 32 * 32  # padded support side (zero outside N x N)
-        if model.residual_channels != model.dilation_channels:
-            raise ValueError("gwn_amd: residual_channels must equal dilation_channels")
-        if model.kernel_size != 2:
-            raise ValueError("gwn_amd: only kernel_size=2 (the reference default) is implemented")
         if self.C % 16 != 0 or 256 % self.C != 0:
             raise ValueError("gwn_amd: residual channels must be 16, 32, 64, 128 or 256")
+        if self.D % 16 != 0 or self.D > 1024:
+            raise ValueError("gwn_amd: dilation channels must be a multiple of 16 (<= 1024)")
+        if self.K < 1:
+            raise ValueError("gwn_amd: kernel_size must be >= 1")
+        # the shape of the fused kernels (fused gcn, row-GEMM TCN, BatchNorm fold): the reference
+        # default's square layers; any other (residual != dilation channels, kernel_size != 2)
+        # runs the generic MFMA GEMM path
+        self.square = self.C == self.D and self.K == 2
+
+    def shift(self, i):
+        """Steps layer i's dilated conv consumes: T_out = T_in - (kernel_size - 1) * dilation."""
+        return (self.K - 1) * self.dilations[i]
 
     def times(self, t_in):
         t0 = max(t_in, self.R)
         ts = [t0]
-        for d in self.dilations:
-            ts.append(ts[-1] - d)
+        for i in range(len(self.dilations)):
+            ts.append(ts[-1] - self.shift(i))
         return ts
 
 
@@ -236,7 +247,7 @@ class Acts:
     """Activations of one forward (kept for its backward)."""
 
     def __init__(self, cfg, B, ts, device, training):
-        C, N, L = cfg.C, cfg.N, cfg.L
+        C, D, N, L = cfg.C, cfg.D, cfg.N, cfg.L
         P = B * N
         self.B, self.ts, self.P = B, ts, P
         tf = ts[-1]
@@ -246,13 +257,13 @@ class Acts:
         self.FG, self.H, self.Z, self.mean, self.rstd = [], [], [], [], []
         for i in range(L):
             rows = ts[i + 1] * P
-            self.FG.append(e(rows, 2 * C))
+            self.FG.append(e(rows, 2 * D))
             self.H.append(e(rows, cfg.W))
             self.Z.append(e(rows, C))
             self.X.append(e(rows, C))
             self.mean.append(e(C))
             self.rstd.append(e(C))
-        self.skipcat = e(tf * P, L * C)
+        self.skipcat = e(tf * P, L * D)
         self.skr = e(tf * P, cfg.S)
         self.e1 = e(tf * P, cfg.E)
         self.y = e(tf * P, cfg.O)
@@ -272,8 +283,8 @@ class _HeadBufs:
 
 
 class Executor:
-    def __init__(self, model):
-        self.cfg = Config(model)
+    def __init__(self, model, residual_only=False):
+        self.cfg = Config(model, residual_only)
         self.layout = PackedLayout(model, self.cfg)
         self.dropout = model.dropout
         self.compute_dtype = getattr(model, "compute_dtype", "fp32")
@@ -305,7 +316,7 @@ class Executor:
         0 when the shape has no such instantiation (c != 32, n > 512, no supports)."""
         cfg = self.cfg
         planes = 1 if self.compute_dtype == "bf16" else 0
-        if planes == 0 or not cfg.use_gcn or cfg.nsup < 1:
+        if planes == 0 or not cfg.use_gcn or cfg.nsup < 1 or not cfg.square:
             return 0
         return planes if _lib.load().gwn_gcn_split_supported(cfg.C, cfg.N, planes) else 0
 
@@ -369,7 +380,7 @@ class Executor:
         if s is not None:
             return s
         cfg = self.cfg
-        C, N, L = cfg.C, cfg.N, cfg.L
+        C, D, N, L = cfg.C, cfg.D, cfg.N, cfg.L
         P = B * N
         tf = ts[-1]
         e = lambda *s_: torch.empty(*s_, device=self.device, dtype=F32)  # noqa: E731
@@ -378,14 +389,14 @@ class Executor:
             "dy": e(tf * P, cfg.OP),  # the output gradient, rows padded to 32 columns (zeros)
             "de1": e(tf * P, cfg.E),
             "dsk": e(tf * P, cfg.S),
-            "dskipcat": e(tf * P, L * C),
+            "dskipcat": e(tf * P, L * D),
             "dxa": e(ts[0] * P, C),
             "dxb": e(ts[0] * P, C),
-            "dfg": e(maxrows, 2 * C),
+            "dfg": e(maxrows, 2 * D),
             "dh": e(maxrows, C),
             "dhc": e(maxrows, cfg.W),
             # second-parity buffers for the side-stream weight gradients (backward overlap)
-            "dfg2": e(maxrows, 2 * C),
+            "dfg2": e(maxrows, 2 * D),
             "dh2": e(maxrows, C),
             "dhc2": e(maxrows, cfg.W),
             "dadp": torch.zeros(cfg.NP, cfg.NP, device=self.device, dtype=F32),
@@ -395,23 +406,24 @@ class Executor:
         }
         lib = _lib.load()
         need = [
-            lib.gwn_gated_tcn_bwd_workspace_floats(ts[0], P, C, 1),
-            lib.gwn_gcn_bwd_workspace_floats(maxrows, N, C, max(cfg.nsup, 0)),
+            lib.gwn_gcn_bwd_workspace_floats_ex(maxrows, N, D, max(cfg.nsup, 0), C),
             lib.gwn_batchnorm_workspace_floats(maxrows, C),
-            lib.gwn_colsum_workspace_floats(maxrows, max(cfg.E, cfg.S, cfg.L * C)),
+            lib.gwn_colsum_workspace_floats(maxrows, max(cfg.E, cfg.S, cfg.L * D)),
             lib.gwn_masked_loss_workspace_floats(B, cfg.O, N, tf),
             lib.gwn_clip_adam_workspace_floats(self.layout.flat_total),
             cfg.NP * cfg.NP,
         ]
+        # every layer's TCN backward (the largest workspace need may sit at any dilation)
+        need += [lib.gwn_gated_tcn_bwd_workspace_floats_ex(ts[i], P, C, cfg.dilations[i], cfg.K, D) for i in range(L)]
         # split-K partials of the head / start weight grads
-        for (M_, N_, K_) in ((cfg.O, cfg.E, tf * P), (cfg.E, cfg.S, tf * P), (cfg.S, L * C, tf * P),
+        for (M_, N_, K_) in ((cfg.O, cfg.E, tf * P), (cfg.E, cfg.S, tf * P), (cfg.S, L * D, tf * P),
                              (C, cfg.Cin, ts[0] * P)):
             need.append(lib.gwn_gemm_workspace_floats(M_, N_, _ksplit(M_, N_, K_)))
         need.append(lib.gwn_gemm_workspace_floats(tf * P, cfg.O, _ksplit_thin(tf * P, cfg.O, cfg.E)))
         s["ws"] = e(int(max(need)) + 16)
         # deferred weight gradients (_defer_ok): per-layer wgrad partials, reduced by one launch at
         # the end of the backward
-        if cfg.C % 32 == 0 and cfg.W % 32 == 0:
+        if cfg.C == 32 and cfg.square and cfg.W % 32 == 0:
             pm, pt = [], []
             for i in range(L):
                 rows = ts[i + 1] * P
@@ -426,7 +438,7 @@ class Executor:
         side_need = [lib.gwn_wgrad_workspace_floats(maxrows, C, cfg.W),
                      lib.gwn_wgrad_workspace_floats(maxrows, 2 * C, 2 * C),
                      lib.gwn_gram_workspace_floats(N, maxrows // N)]
-        for (M_, N_, K_) in ((cfg.O, cfg.E, tf * P), (cfg.E, cfg.S, tf * P), (cfg.S, L * C, tf * P)):
+        for (M_, N_, K_) in ((cfg.O, cfg.E, tf * P), (cfg.E, cfg.S, tf * P), (cfg.S, L * D, tf * P)):
             side_need.append(lib.gwn_gemm_workspace_floats(M_, N_, _ksplit(M_, N_, K_)))
         s["ws_side"] = e(int(max(side_need)) + 16)
         # support split of the fused gcn kernels (gwn_gcn_args.ksplit): partial sums + per-slice
@@ -441,10 +453,10 @@ class Executor:
     def pack_params(self, flat):
         st = _lib.stream()
         lay = self.layout
-        _lib.call("gwn_gather", ptr(flat), ptr(self.pidx), ptr(self.packed), lay.total, st)
         cfg = self.cfg
-        _lib.call("gwn_sum_vectors", ptr(self.pk("skip_b")), cfg.L, cfg.S, cfg.S,
-                  ptr(self.pk("skip_bsum")), st)
+        # one launch: the packing and the summed skip bias (slot skip_bsum)
+        _lib.call("gwn_gather_sum", ptr(flat), ptr(self.pidx), ptr(self.packed), lay.total, lay.segs["skip_b"][0],
+                  cfg.L, cfg.S, lay.segs["skip_bsum"][0], st)
 
     def supports(self, fixed, acts):
         sups = list(fixed) if self.cfg.use_gcn else []
@@ -454,7 +466,7 @@ class Executor:
         return sups, arr
 
     def forward(self, flat, fixed_sups, x, training, bn_bufs, acts=None, lead_pad=0, seed=None, sup_batch=1,
-                fixed_t=None):
+                fixed_t=None, want_out=True):
         """x: reference NCHW input [B, Cin, N, T] (any strides).  ``lead_pad`` extra zero steps
         are prepended (engine.py:44) before the receptive-field pad (model.py:176-178).
         ``seed``: the dropout counter this forward (and its backward) draws its masks from
@@ -463,6 +475,8 @@ class Executor:
         [B][NP][NP] buffer, sample b of slice (t, b) diffusing with matrix b.
         ``fixed_t``: padded transposes of ``fixed_sups`` kept by the caller (they change only with the
         supports); the backward's transposes of the others are built here.
+        ``want_out`` False: the NCHW copy of the output is not made (the fused training step reads
+        the head's rows, acts.y, through gwn_masked_loss_rows); out is then None.
         Returns (out [B, O, N, T_f], acts)."""
         cfg = self.cfg
         C, N, L = cfg.C, cfg.N, cfg.L
@@ -558,13 +572,13 @@ class Executor:
         fold = training and self._bn_fold_ok(sup_batch)
         acts.bn_fold = fold
         for i in range(L):
-            d = cfg.dilations[i]
+            d, sh = cfg.dilations[i], cfg.shift(i)
             rows = ts[i + 1] * P
             xin, wfg, bfg, raff = self.layer_input(acts, i)
             ta = _lib.TcnArgs(x=xin, x_mean=raff[0], t_in=ts[i], P=P, c=C, dilation=d, w_fg=wfg, b_fg=bfg,
                               xg=ptr(acts.H[i]), ld_xg=cfg.W, fg=ptr(acts.FG[i]),
-                              skipcat=acts.skipcat.data_ptr() + 4 * i * C, ld_skip=L * C,
-                              skip_row0=(ts[i + 1] - tf) * P)
+                              skipcat=acts.skipcat.data_ptr() + 4 * i * cfg.D, ld_skip=L * cfg.D,
+                              skip_row0=(ts[i + 1] - tf) * P, ntaps=cfg.K, c_out=cfg.D)
             lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), st)
             if i == L - 1 and not training:
                 continue  # the last gcn / bn output is dead in eval (only skip reaches the output)
@@ -578,11 +592,11 @@ class Executor:
                 side_ctx.__enter__()
                 st = _lib.stream()
             drop = float(self.dropout) if (training and cfg.use_gcn) else 0.0
-            ga = _lib.GcnArgs(rows=rows, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
+            ga = _lib.GcnArgs(rows=rows, n=N, c=cfg.D, c_out=C, nsup=cfg.nsup if cfg.use_gcn else 0,
                               sup=ctypes.cast(sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=cfg.NP,
                               h=ptr(acts.H[i]), ld_h=cfg.W,
                               w_mlp=ptr(self.pk("mlp_w%d" % i)), b_mlp=ptr(self.pk("mlp_b%d" % i)),
-                              residual=xin + 4 * d * P * C, z=ptr(acts.Z[i]),
+                              residual=xin + 4 * sh * P * C, z=ptr(acts.Z[i]),
                               seed_ptr=ptr(acts.seed), salt=i, drop_p=drop,
                               bn_partials=ptr(bnpart) if training else None,
                               # the last layer's gcn output only feeds bn[L-1]'s running statistics:
@@ -594,7 +608,7 @@ class Executor:
                               **self.split_fields(sp, i), **self.ksplit_fields(scr))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
-            rm, rv, mom, eps = bn_bufs[i]
+            rm, rv, mom, eps, nbt = bn_bufs[i]
             if fold:
                 nxt = i + 1 < L
                 lib.call("gwn_batchnorm_fwd_fold", ptr(bnpart), self._bn_parts(rows), C, ptr(self.pk("bn_g%d" % i)),
@@ -603,11 +617,11 @@ class Executor:
                          ptr(self.pk("fg_w%d" % (i + 1))) if nxt else None,
                          ptr(self.pk("fg_b%d" % (i + 1))) if nxt else None,
                          acts.w_fold[i + 1].data_ptr() if nxt else None,
-                         acts.b_fold[i + 1].data_ptr() if nxt else None, st)
+                         acts.b_fold[i + 1].data_ptr() if nxt else None, ptr(nbt), st)
             elif training:
                 lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnpart), self._bn_parts(rows),
                          ptr(self.pk("bn_g%d" % i)), ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps,
-                         ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), st)
+                         ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(nbt), st)
             else:
                 lib.call("gwn_batchnorm_fwd", ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
                          ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps, 0,
@@ -619,8 +633,10 @@ class Executor:
                 st = _lib.stream()
         rows_f = tf * P
         self._head_fwd(acts.skipcat, acts.skr, acts.e1, acts.y, rows_f, ws)
-        out = torch.empty(B, cfg.O, N, tf, device=self.device, dtype=F32)
-        lib.call("gwn_to_nchw", ptr(acts.y), B, cfg.O, N, tf, ptr(out), st)
+        out = None
+        if want_out:
+            out = torch.empty(B, cfg.O, N, tf, device=self.device, dtype=F32)
+            lib.call("gwn_to_nchw", ptr(acts.y), B, cfg.O, N, tf, ptr(out), st)
         if tail_done is not None:
             main.wait_event(tail_done)
         return out, acts
@@ -670,7 +686,7 @@ class Executor:
     def _fused_gcn(self):
         """gwn_gcn_fwd takes the fused path (c == 32, n <= 512, nsup <= 8; include/gwn.h)."""
         cfg = self.cfg
-        return cfg.C == 32 and cfg.N <= 512 and (not cfg.use_gcn or cfg.nsup <= 8)
+        return cfg.C == 32 and cfg.square and cfg.N <= 512 and (not cfg.use_gcn or cfg.nsup <= 8)
 
     def _bn_fold_ok(self, sup_batch):
         """BatchNorm on load needs the fused gcn forward (its epilogue applies the residual affine)
@@ -691,7 +707,7 @@ class Executor:
     def _head_fwd(self, skipcat, skr, e1, y, rows_f, ws):
         """skip sum (relu'd) -> end_conv_1 (+relu) -> end_conv_2 (model.py:216-222, 238-240)."""
         cfg = self.cfg
-        L, C = cfg.L, cfg.C
+        L, C = cfg.L, cfg.D  # the skip convs read the gated (dilation-channel) outputs
         acts = _HeadBufs(skipcat, skr, e1, y)
         if self._head_nt():
             gemm_nt(acts.skipcat, L * C, self.pk("skip_w"), L * C, acts.skr, cfg.S, rows_f, cfg.S, L * C,
@@ -713,7 +729,7 @@ class Executor:
     def infer_ok(self):
         """The lean inference schedule needs the fused GCN path and the NT head GEMMs."""
         cfg = self.cfg
-        return (os.environ.get("GWN_LEAN_EVAL", "1") != "0" and cfg.C == 32 and cfg.N <= 512
+        return (os.environ.get("GWN_LEAN_EVAL", "1") != "0" and cfg.C == 32 and cfg.square and cfg.N <= 512
                 and cfg.nsup <= 8 and self._head_nt() and not cfg.per_sample)
 
     def _infer_bufs(self, B, ts):
@@ -786,12 +802,12 @@ class Executor:
                               w_fg=ptr(self.pk("fg_w%d" % i)), b_fg=ptr(self.pk("fg_b%d" % i)),
                               xg=ptr(bf["xg"]), ld_xg=C, fg=None,
                               skipcat=bf["skipcat"].data_ptr() + 4 * i * C, ld_skip=L * C,
-                              skip_row0=(ts[i + 1] - tf) * P)
+                              skip_row0=(ts[i + 1] - tf) * P, ntaps=cfg.K, c_out=cfg.D)
             _lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), st)
             if i == L - 1:
                 break  # the last gcn / bn output never reaches the output
             xnext = bf["xa"] if xcur is not bf["xa"] else bf["xb"]
-            rm, rv, _, eps = bn_bufs[i]
+            rm, rv, _, eps, _ = bn_bufs[i]
             ga = _lib.GcnArgs(rows=ts[i + 1] * P, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
                               sup=ctypes.cast(sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=cfg.NP,
                               h=ptr(bf["xg"]), ld_h=C,
@@ -812,9 +828,11 @@ class Executor:
 
     # ---------------------------------------------------------------------------------------
     def backward(self, acts, dout):
-        """Gradients of every active parameter into self.gpacked (kernel layout)."""
+        """Gradients of every active parameter into self.gpacked (kernel layout).  dout: the output
+        gradient [B, O, N, T_f], or None when scratch "dy" already holds it in row layout
+        (gwn_masked_loss_rows)."""
         cfg = self.cfg
-        C, N, L, S, E, O = cfg.C, cfg.N, cfg.L, cfg.S, cfg.E, cfg.O
+        C, D, N, L, S, E, O = cfg.C, cfg.D, cfg.N, cfg.L, cfg.S, cfg.E, cfg.O
         B, ts, P = acts.B, acts.ts, acts.P
         tf = ts[-1]
         rows_f = tf * P
@@ -822,9 +840,10 @@ class Executor:
         ws = sc["ws"]
         st = _lib.stream()
         lib = _lib
-        dout = dout.contiguous()
         OP = cfg.OP
-        lib.call("gwn_from_nchw_ld", ptr(dout), B, O, N, tf, ptr(sc["dy"]), OP, st)
+        if dout is not None:
+            dout = dout.contiguous()
+            lib.call("gwn_from_nchw_ld", ptr(dout), B, O, N, tf, ptr(sc["dy"]), OP, st)
         # Weight / adjacency gradients (head wgrads, gwn_wgrad, gwn_gram: off the critical path)
         # run on a second stream when the fused data path is on (C = 32), overlapping the input
         # gradients that follow; in the layers the buffers they read (dh, dhcat, dfg) alternate by
@@ -876,18 +895,18 @@ class Executor:
             gemm(sc["de1"], E, 1, self.pk("e1_w"), S, 1, sc["dsk"], S, 1, M=rows_f, N=S, K=E,
                  epi=2, mask=acts.skr, ldmask=S)
         # skip convs
-        head_wgrad(sc["dsk"], S, acts.skipcat, L * C, self.gk("skip_w"), self.gk("skip_bsum"))
+        head_wgrad(sc["dsk"], S, acts.skipcat, L * D, self.gk("skip_w"), self.gk("skip_bsum"))
         if nt:
-            gemm_nt(sc["dsk"], S, self.pk("skip_wT"), S, sc["dskipcat"], L * C, rows_f, L * C, S)
+            gemm_nt(sc["dsk"], S, self.pk("skip_wT"), S, sc["dskipcat"], L * D, rows_f, L * D, S)
         else:
-            gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * C, 1, sc["dskipcat"], L * C, 1, M=rows_f, N=L * C, K=S)
+            gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * D, 1, sc["dskipcat"], L * D, 1, M=rows_f, N=L * D, K=S)
         side_done = {}
         dnext = None
         bufs = [sc["dxa"], sc["dxb"]]
         first_adp = True
         adp_index = cfg.nsup - 1 if cfg.adp_params else -1
         for i in range(L - 1, -1, -1):
-            d = cfg.dilations[i]
+            d, sh = cfg.dilations[i], cfg.shift(i)
             rows = ts[i + 1] * P
             dx = bufs[i % 2]
             par = "" if (i % 2 == 0 or not overlap) else "2"
@@ -900,9 +919,9 @@ class Executor:
                 if not fuse:
                     lib.call("gwn_batchnorm_bwd", ptr(dnext), ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
                              ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(self.gk("bn_g%d" % i)),
-                             ptr(self.gk("bn_b%d" % i)), ptr(dx), d * P, ptr(dh), ptr(acts.seed), i,
+                             ptr(self.gk("bn_b%d" % i)), ptr(dx), sh * P, ptr(dh), ptr(acts.seed), i,
                              drop, 1 if acts.training else 0, ptr(ws), st)
-                gb = _lib.GcnBwdArgs(rows=rows, n=N, c=C, nsup=cfg.nsup if cfg.use_gcn else 0,
+                gb = _lib.GcnBwdArgs(rows=rows, n=N, c=D, c_out=C, nsup=cfg.nsup if cfg.use_gcn else 0,
                                      sup=ctypes.cast(acts.sup_arr, ctypes.POINTER(ctypes.c_void_p)),
                                      ld_sup=cfg.NP,
                                      h=ptr(acts.H[i]), ld_h=cfg.W, w_mlp=ptr(self.pk("mlp_w%d" % i)),
@@ -913,8 +932,11 @@ class Executor:
                                      sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
                                      if acts.supT_arr is not None else None,
                                      skip_weight_grads=1 if (overlap or defer) else 0,
+                                     # the power-schedule backward measured slower than the
+                                     # chained one (131.5 vs 125.8 us per launch, 19,263 vs 19,517
+                                     # samples/s): GWN_GCN_POW_BWD=1 selects it
                                      sup2_t=self._arr_field(getattr(acts, "sup2t_arr", None))
-                                     if os.environ.get("GWN_GCN_POW_BWD", "1") != "0" else None,
+                                     if os.environ.get("GWN_GCN_POW_BWD", "0") != "0" else None,
                                      **self.ksplit_fields(sc))
                 sb = getattr(acts, "sup_batch", 1)
                 if sb > 1:
@@ -928,9 +950,9 @@ class Executor:
                     gb.bn_dy, gb.bn_z = ptr(dnext), ptr(acts.Z[i])
                     gb.bn_gamma, gb.bn_mean, gb.bn_rstd = ptr(self.pk("bn_g%d" % i)), ptr(acts.mean[i]), ptr(acts.rstd[i])
                     gb.bn_sums, gb.bn_dgamma, gb.bn_dbeta = ptr(sc["bnsums"]), ptr(self.gk("bn_g%d" % i)), ptr(self.gk("bn_b%d" % i))
-                    gb.dres, gb.dh_out = dx.data_ptr() + 4 * d * P * C, ptr(dh)
+                    gb.dres, gb.dh_out = dx.data_ptr() + 4 * sh * P * C, ptr(dh)
                     gb.seed_ptr, gb.salt, gb.drop_p = ptr(acts.seed), i, drop
-                    gb.fg, gb.dskip, gb.ld_dskip = ptr(acts.FG[i]), sc["dskipcat"].data_ptr() + 4 * i * C, L * C
+                    gb.fg, gb.dskip, gb.ld_dskip = ptr(acts.FG[i]), sc["dskipcat"].data_ptr() + 4 * i * D, L * D
                     gb.skip_row0, gb.dfg = (ts[i + 1] - tf) * P, ptr(dfg)
                 lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)
                 if overlap:
@@ -944,17 +966,17 @@ class Executor:
                 dxg, ld_dxg, acc = dhc, cfg.W, 1
             xin, _, _, raff = self.layer_input(acts, i)
             tb = _lib.TcnBwdArgs(x=xin, x_mean=raff[0], x_scale=raff[1], x_shift=raff[2], t_in=ts[i], P=P, c=C,
-                                 dilation=d,
+                                 dilation=d, ntaps=cfg.K, c_out=D,
                                  w_fg=ptr(self.pk("fg_w%d" % i)), fg=ptr(acts.FG[i]),
                                  dxg=ptr(dxg), ld_dxg=ld_dxg,
-                                 dskip=sc["dskipcat"].data_ptr() + 4 * i * C, ld_dskip=L * C,
+                                 dskip=sc["dskipcat"].data_ptr() + 4 * i * D, ld_dskip=L * D,
                                  skip_row0=(ts[i + 1] - tf) * P, dfg=ptr(dfg),
                                  dw_fg=ptr(self.gk("fg_w%d" % i)), db_fg=ptr(self.gk("fg_b%d" % i)),
                                  dx=ptr(dx), accumulate_dx=acc, workspace=ptr(ws),
                                  skip_weight_grads=1 if (overlap or defer) else 0)
             if fuse:
                 if dnext is not None:
-                    tb.dfg_ready, tb.acc_row0 = 1, d * P
+                    tb.dfg_ready, tb.acc_row0 = 1, sh * P
                 if i >= 1:  # statistics of bn[i-1], whose output gradient is this dx
                     tb.bn_z, tb.bn_mean, tb.bn_rstd = ptr(acts.Z[i - 1]), ptr(acts.mean[i - 1]), ptr(acts.rstd[i - 1])
                     tb.bn_sums = ptr(sc["bnsums"])
@@ -1000,18 +1022,18 @@ class Executor:
         layer backward the main-stream kernels fill the chip, and the side stream's wgrad / gram
         launches only contend with them (measured 16.62k vs 16.72k samples/s, round 1)."""
         cfg = self.cfg
-        return (os.environ.get("GWN_OVERLAP", "0") != "0" and cfg.C == 32 and cfg.W % 32 == 0
+        return (os.environ.get("GWN_OVERLAP", "0") != "0" and cfg.C == 32 and cfg.square and cfg.W % 32 == 0
                 and acts.supT_arr is not None)
 
     def _head_nt(self):
         """Row-tile NT GEMMs for the head (K dims / leading dims multiples of 4)."""
         cfg = self.cfg
         return (os.environ.get("GWN_HEAD_NT", "1") != "0"
-                and all(v % 4 == 0 for v in (cfg.O, cfg.S, cfg.E, cfg.L * cfg.C)))
+                and all(v % 4 == 0 for v in (cfg.O, cfg.S, cfg.E, cfg.L * cfg.D)))
 
     def _fuse_ok(self, acts):
         cfg = self.cfg
-        return (os.environ.get("GWN_FUSE_BWD", "1") != "0" and cfg.use_gcn and cfg.C == 32
+        return (os.environ.get("GWN_FUSE_BWD", "1") != "0" and cfg.use_gcn and cfg.C == 32 and cfg.square
                 and cfg.W % 32 == 0 and cfg.N <= 512 and acts.supT_arr is not None)
 
     def _side_stream(self):

@@ -405,7 +405,9 @@ class gwnet(nn.Module):
         out = []
         for m in self.bn:
             mom = 0.1 if m.momentum is None else m.momentum
-            out.append((m.running_mean, m.running_var, float(mom), float(m.eps)))
+            # num_batches_tracked: a view into the model's counter vector, advanced on the device by
+            # the train-mode BatchNorm launch itself
+            out.append((m.running_mean, m.running_var, float(mom), float(m.eps), m.num_batches_tracked))
         return out
 
     def forward(self, input):
@@ -431,7 +433,10 @@ class gwnet_diff_G(gwnet):
     per-sample softmax(relu(E1_b E2_b)) on the GPU (gwn_adaptive_adj_fwd_batched), appended as the
     last support, and no gradient through it.  ``aptinit`` must be None: the reference stops at an
     ``ipdb.set_trace()`` there (model.py:331, "fix this").  The diffusion runs in the fused kernels
-    with per-sample supports (sup_batch = B), so it needs residual_channels = 32 and N <= 512."""
+    with per-sample supports (sup_batch = B), so it needs residual_channels = 32 and N <= 512.
+    Without a graph convolution (gcn_bool False, or supports None without addaptadj) every layer
+    takes the residual_convs 1x1 branch (model.py:391-398), on a second executor whose packed
+    layout maps residual_convs instead of the gcn mlps."""
 
     def __init__(self, device, num_nodes, dropout=0.3, supports_len=0, gcn_bool=True, addaptadj=True, in_dim=2,
                  out_dim=12, residual_channels=32, dilation_channels=32, skip_channels=256, end_channels=512,
@@ -480,10 +485,22 @@ class gwnet_diff_G(gwnet):
         self._nbt = None
         self._sup_cache = (None, None, None)
         self._call = None
+        self._res_executor = None
         self._place(device)
 
     def _call_supports(self):
-        return self._call
+        return self._call[:2]
+
+    def residual_executor(self):
+        """Executor of the no-graph-convolution branch (model.py:391-398)."""
+        self.executor()  # (re)places the flat buffer first
+        if self._res_executor is None or self._res_executor.layout.flat_total != self._flat.numel():
+            self._res_executor = Executor(self, residual_only=True)
+        ex = self._res_executor
+        ex.dropout = self.dropout
+        ex.compute_dtype = self.compute_dtype
+        ex.bind(self._flat.device)
+        return ex
 
     def forward(self, input, supports, aptinit):
         ex = self.executor()
@@ -502,8 +519,12 @@ class gwnet_diff_G(gwnet):
             nv2 = torch.randn(B, 10, N)
             adp = (nv1, nv2)
         if not self.gcn_bool or sups is None:
-            raise NotImplementedError("gwnet_diff_G: only the graph-convolution path (gcn_bool with supports or "
-                                      "addaptadj) is built on libgwn")
+            # model.py:391-398: x = residual_convs[i](x) in every layer; no supports are read
+            self._call = ([], 1, self.residual_executor())
+            try:
+                return _GwnetFn.apply(self, input, *self.parameters())
+            finally:
+                self._call = None
         nsup = len(sups) + (1 if adp is not None else 0)
         if nsup != self.supports_len:
             raise RuntimeError("gwnet_diff_G: built for %d supports, got %d" % (self.supports_len, nsup))
@@ -526,7 +547,7 @@ class gwnet_diff_G(gwnet):
             _lib.call("gwn_adaptive_adj_fwd_batched", e1.data_ptr(), e2.data_ptr(), B, N, 10, dst.data_ptr(), np_,
                       sq, st)
             padded.append(dst)
-        self._call = (padded, B)
+        self._call = (padded, B, ex)
         try:
             return _GwnetFn.apply(self, input, *self.parameters())
         finally:
@@ -540,7 +561,8 @@ class _GwnetFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, model, x, *params):
-        ex = model._executor
+        call = getattr(model, "_call", None)
+        ex = call[2] if call is not None else model._executor
         training = model.training
         seed = None
         if training and model.dropout > 0:
@@ -552,16 +574,15 @@ class _GwnetFn(torch.autograd.Function):
         fixed_t = model._fixed_supports_t() if sup_batch <= 1 else None
         out, acts = ex.forward(model._flat, sups, x, training, model._bn_bufs(), seed=seed, sup_batch=sup_batch,
                                fixed_t=fixed_t)
-        if training:
-            model._nbt.add_(1)
         ctx.model = model
+        ctx.ex = ex
         ctx.acts = acts
         return out
 
     @staticmethod
     def backward(ctx, dout):
         model = ctx.model
-        ex = model._executor
+        ex = ctx.ex
         ex.backward(ctx.acts, dout)
         gflat = torch.zeros_like(model._flat)
         ex.unpack_grads(gflat)

@@ -175,6 +175,12 @@ typedef struct gwn_tcn_args {
    * input used is x - x_mean; w_fg / b_fg are then the folded weights of gwn_batchnorm_fwd_fold
    * (BatchNorm applied on load, centred before any product). */
   const float* x_mean;
+  /* kernel taps and output (dilation) channels (model.py:135-141 kernel_size, dilation_channels):
+   * ntaps taps t, t+d, ..., t+(ntaps-1)d, so t_out = t_in - (ntaps-1)*dilation; w_fg is then
+   * [2*c_out][ntaps*c] (row 2co+gate, column tap*c+ci), b_fg [2*c_out], xg / fg / skipcat carry
+   * c_out (resp. 2*c_out) channels.  0 = the defaults ntaps 2, c_out c.  Non-default values run
+   * the generic GEMM path (no x_mean fold). */
+  int ntaps, c_out;
 } gwn_tcn_args;
 /* fg may be NULL when no backward follows (inference; c == 32 row-GEMM path): the (tanh, sigmoid)
  * pairs are then not stored. */
@@ -211,9 +217,14 @@ typedef struct gwn_tcn_bwd_args {
    * input is (z - x_mean[ci]) * x_scale[ci] + x_shift[ci] (gwn_batchnorm_fwd_fold; the weight
    * gradient applies it on load).  c % 32 == 0 path only. */
   const float* x_mean; const float* x_scale; const float* x_shift;
+  /* taps / output channels as gwn_tcn_args (0 = 2 / c): dfg, fg [rows][2*c_out], dxg c_out
+   * channels, dW_fg [2*c_out][ntaps*c], dx [t_in*P][c] */
+  int ntaps, c_out;
 } gwn_tcn_bwd_args;
 int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t stream);
 long gwn_gated_tcn_bwd_workspace_floats(int t_in, int P, int c, int dilation);
+/* the same for ntaps taps and c_out output channels (gwn_tcn_bwd_args.ntaps / .c_out) */
+long gwn_gated_tcn_bwd_workspace_floats_ex(int t_in, int P, int c, int dilation, int ntaps, int c_out);
 
 /* ---------------------------------------------------------------------------------------------
  * Graph convolution + residual (gcn.forward model.py:41-55 and model.py:234):
@@ -286,6 +297,10 @@ typedef struct gwn_gcn_args {
   /* w_mlp_t: w_mlp transposed, [(2*nsup+1)*c][c] (required with sup2: the power forward reads the
    * mlp's MFMA fragments as coalesced rows of it) */
   const float* w_mlp_t;
+  /* c_out: output channels (model.py:152 gcn(dilation_channels, residual_channels)): the pieces
+   * of h carry c channels, w_mlp is [c_out][(2K+1)c], b_mlp / residual / z / bn_partials carry
+   * c_out.  0 = c.  c_out != c runs the generic path. */
+  int c_out;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -377,9 +392,12 @@ typedef struct gwn_gcn_bwd_args {
    * W0^T dh + sum_k W_{1+2k}^T (A_k dh) + W_{2+2k}^T (A_k^2 dh) with every diffusion reading dh
    * (no hop-to-hop dependency).  NULL = the chained (Horner) backward. */
   const float* const* sup2_t;
+  /* output channels as gwn_gcn_args.c_out (0 = c): dh [rows][c_out], dW_mlp [c_out][(2K+1)c] */
+  int c_out;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);
+long gwn_gcn_bwd_workspace_floats_ex(int rows, int n, int c, int nsup, int c_out);
 /* partial-sum floats of the support split (gwn_gcn_args.ksplit_ws / gwn_gcn_bwd_args.ksplit_ws):
  * (rows / n) * nsup * 32*ceil(n/32) * 32 */
 long gwn_gcn_ksplit_ws_floats(int rows, int n, int nsup);
@@ -449,7 +467,10 @@ long gwn_batchnorm_workspace_floats(int rows, int c);
 int gwn_batchnorm_fwd_partials(const float* z, int rows, int c, const float* partials, int nparts,
                                const float* gamma, const float* beta, float* running_mean,
                                float* running_var, float momentum, float eps, float* out,
-                               float* save_mean, float* save_rstd, hipStream_t stream);
+                               float* save_mean, float* save_rstd, long long* num_batches_tracked,
+                               hipStream_t stream);
+/* num_batches_tracked (here and in gwn_batchnorm_fwd_fold; NULL = none): the module's counter,
+ * advanced by one by the same launch (BatchNorm2d's train-mode forward, model.py:236) */
 /* BatchNorm applied on load instead of a normalised copy (train mode, c == 32): merge the partials
  * and update the running statistics as gwn_batchnorm_fwd_partials; instead of writing bn(z), emit
  * scale[j] = gamma[j] * rstd[j] (bn(z) = (z - mean) * scale + beta) and fold it into the NEXT
@@ -462,7 +483,7 @@ int gwn_batchnorm_fwd_partials(const float* z, int rows, int c, const float* par
 int gwn_batchnorm_fwd_fold(const float* partials, int nparts, int c, const float* gamma, const float* beta,
                            float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
                            float* save_rstd, float* scale, const float* w_next, const float* b_next, float* w_fold,
-                           float* b_fold, hipStream_t stream);
+                           float* b_fold, long long* num_batches_tracked, hipStream_t stream);
 /* dst[j][i] = src[i][j] for an n x n matrix (supports for the fused backward) */
 int gwn_transpose(const float* src, int n, int ld_src, float* dst, int ld_dst, hipStream_t stream);
 /* diagnostics: resident workgroups per CU of the fused gcn kernel (forward, or backward != 0;
@@ -506,6 +527,13 @@ int gwn_masked_loss(const float* out, const float* real, long rsb, long rsn, lon
                     int o, int n, int tf, float mean, float std, float* metrics, float* dout,
                     float* workspace, hipStream_t stream);
 long gwn_masked_loss_workspace_floats(int B, int o, int n, int tf);
+/* gwn_masked_loss on the head's own row layout (the fused training step: no NCHW copy of the
+ * output and none of its gradient): prediction (b, oo, v, t) at y[((t*B + b)*n + v)*ld_y + oo],
+ * its gradient written to dy[((t*B + b)*n + v)*ld_dy + oo] (columns o .. ld_dy zeroed; dy NULL =
+ * metrics only).  Same metrics (summed in another order), same workspace. */
+int gwn_masked_loss_rows(const float* y, int ld_y, const float* real, long rsb, long rsn, long rso, int B, int o,
+                         int n, int tf, float mean, float std, float* metrics, float* dy, int ld_dy,
+                         float* workspace, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Optimiser tail (engine.py:53-55): clip_grad_norm_(max_norm) over the listed ranges of the flat
@@ -540,6 +568,11 @@ int gwn_gather_sqnorm(const float* src, const int* idx, float* dst, long count, 
 
 /* dst[i] = src[idx[i]] (parameter repacking into kernel layouts and back). */
 int gwn_gather(const float* src, const int* idx, float* dst, long count, hipStream_t stream);
+/* gwn_gather, except that dst[sum_dst .. sum_dst + len) receives the sum of the nvec gathered
+ * vectors at sum_src + v*len (v in order): the parameter packing with the skip convs' summed bias
+ * (model.py:216-222 adds every layer's skip bias into one sum) in one launch */
+int gwn_gather_sum(const float* src, const int* idx, float* dst, long count, long sum_src, int nvec, int len,
+                   long sum_dst, hipStream_t stream);
 /* out[b][o][v][t] = y[(t*B + b)*n + v][o]  (head output back to the reference NCHW layout) */
 int gwn_to_nchw(const float* y, int B, int o, int n, int t, float* out, hipStream_t stream);
 /* dy[(t*B + b)*n + v][o] = dout[b][o][v][t] */

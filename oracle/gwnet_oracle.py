@@ -40,15 +40,22 @@ class Cfg:
     """Hyper-parameters of one gwnet (reference ctor, model.py:83-86)."""
 
     def __init__(self, num_nodes, nfixed=2, gcn_bool=True, addaptadj=True, in_dim=2, out_dim=12, nhid=32,
-                 skip=None, end=None, blocks=4, layers=2, dropout=0.0):
+                 skip=None, end=None, blocks=4, layers=2, dropout=0.0, kernel_size=2, dilation_channels=None,
+                 first_dilation=1):
         self.N, self.nfixed = num_nodes, nfixed
         self.gcn_bool, self.addaptadj = gcn_bool, addaptadj
         self.Cin, self.O, self.C = in_dim, out_dim, nhid
+        self.D = dilation_channels if dilation_channels is not None else nhid  # gated-TCN / gcn width
         self.S = skip if skip is not None else 8 * nhid
         self.E = end if end is not None else 16 * nhid
         self.blocks, self.layers, self.dropout = blocks, layers, dropout
-        self.dilations = [2 ** j for _ in range(blocks) for j in range(layers)]
-        self.receptive_field = 1 + sum(self.dilations)   # kernel 2: each layer adds its dilation
+        self.kernel_size = kernel_size
+        # gwnet_diff_G starts every block at dilation 4 (model.py:291)
+        self.dilations = [first_dilation * 2 ** j for _ in range(blocks) for j in range(layers)]
+        # model.py:130-157: every layer adds (kernel_size - 1) * 2^j -- the reference counts from
+        # dilation 1 in both models, so for gwnet_diff_G this under-counts (the input must then be
+        # long enough by itself)
+        self.receptive_field = 1 + (kernel_size - 1) * sum(2 ** j for _ in range(blocks) for j in range(layers))
         self.adaptive = gcn_bool and addaptadj
         # model.py:110-128 + 225: the gcn path runs iff gcn_bool and supports is not None (the
         # adaptive branch turns supports=None into [])
@@ -115,10 +122,15 @@ def pointwise(x, w, bias=None):
     return y if bias is None else y + bias.view(1, -1, 1, 1)
 
 
-def dilated_pair(x, w, bias, d):
-    """Conv with kernel (1,2), dilation d, no padding: taps at t and t+d."""
-    w0, w1 = w[:, :, 0, 0], w[:, :, 0, 1]
-    return pointwise(x[..., :-d], w0) + pointwise(x[..., d:], w1) + bias.view(1, -1, 1, 1)
+def dilated_conv(x, w, bias, d):
+    """Conv with kernel (1,k), dilation d, no padding (model.py:135-141): output step t reads taps
+    t, t+d, ..., t+(k-1)d."""
+    k = w.shape[-1]
+    t_out = x.shape[-1] - (k - 1) * d
+    y = bias.view(1, -1, 1, 1)
+    for j in range(k):
+        y = y + pointwise(x[..., j * d:j * d + t_out], w[:, :, 0, j])
+    return y
 
 
 def batchnorm(x, gamma, beta, rmean, rvar, training, momentum=0.1, eps=1e-5):
@@ -158,8 +170,8 @@ def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, ma
     skip = None
     for i, d in enumerate(cfg.dilations):
         res = h
-        filt = torch.tanh(dilated_pair(res, p["filter_convs.%d.weight" % i], p["filter_convs.%d.bias" % i], d))
-        gate = torch.sigmoid(dilated_pair(res, p["gate_convs.%d.weight" % i], p["gate_convs.%d.bias" % i], d))
+        filt = torch.tanh(dilated_conv(res, p["filter_convs.%d.weight" % i], p["filter_convs.%d.bias" % i], d))
+        gate = torch.sigmoid(dilated_conv(res, p["gate_convs.%d.weight" % i], p["gate_convs.%d.bias" % i], d))
         g = filt * gate
         s = pointwise(g, p["skip_convs.%d.weight" % i], p["skip_convs.%d.bias" % i])
         skip = s if skip is None else s + skip[..., -s.shape[-1]:]

@@ -245,15 +245,17 @@ def test_batchnorm_fold_vs_materialised(gpu):
     wfg = torch.randn(2 * C, 2 * C, device=gpu) * 0.2
     bfg = torch.randn(2 * C, device=gpu)
     wfold, bfold = torch.empty_like(wfg), torch.empty_like(bfg)
+    nbt = torch.full((1,), 41, device=gpu, dtype=torch.int64)
     _lib.call("gwn_batchnorm_fwd_fold", part.data_ptr(), len(chunks), C, gamma.data_ptr(), beta.data_ptr(),
               rm.data_ptr(), rv.data_ptr(), 0.1, 1e-5, mean.data_ptr(), rstd.data_ptr(), scale.data_ptr(),
-              wfg.data_ptr(), bfg.data_ptr(), wfold.data_ptr(), bfold.data_ptr(), _lib.stream())
+              wfg.data_ptr(), bfg.data_ptr(), wfold.data_ptr(), bfold.data_ptr(), nbt.data_ptr(), _lib.stream())
     zd = z.double()
     mu, var = zd.mean(0), zd.var(0, unbiased=False)
     torch.cuda.synchronize()
     assert rel_err(mean.cpu().numpy(), mu.numpy()) < 1e-6
     assert rel_err(rstd.cpu().numpy(), (1 / torch.sqrt(var + 1e-5)).numpy()) < 1e-6
     assert rel_err(rm.cpu().numpy(), (0.1 * mu).numpy()) < 1e-6
+    assert int(nbt.item()) == 42  # num_batches_tracked advanced by the same launch
     assert rel_err(rv.cpu().numpy(), (0.9 + 0.1 * zd.var(0, unbiased=True)).numpy()) < 1e-6
     assert rel_err(scale.cpu().numpy(), (gamma.double().cpu() * rstd.double().cpu()).numpy()) < 1e-6
     # the TCN on z (folded, centred) = the TCN on bn(z)
@@ -455,9 +457,9 @@ def test_gemm_nt(gpu, M, N, K, epi):
 
 
 def _merge_bn(bnp, S, nkb, C):
-    """Per-slice (count, mean, M2) [S][3][C] (fp64) from the per-(slice, tile) BN partial slots the
-    fused forward writes (gwn_gcn_bn_partial_count; count-0 slots carry nothing), Chan's merge."""
-    p = bnp.double().cpu().view(S, nkb, 3, C)
+    """Per-slice (count, mean, M2) [S][3][C] (fp64) from BN partial slots [S][nkb][3][C] (count-0
+    slots carry nothing), Chan's merge; the fused forward writes one slot per slice (nkb = 1)."""
+    p = bnp.double().cpu()[:S * nkb * 3 * C].view(S, nkb, 3, C)
     n = torch.zeros(S, C, dtype=torch.float64)
     mean = torch.zeros(S, C, dtype=torch.float64)
     m2 = torch.zeros(S, C, dtype=torch.float64)
@@ -758,8 +760,7 @@ def test_gcn_pow_forward_modes(gpu, n):
 def test_gram_vs_fp64(gpu, n, slices, pairs, ld, accumulate):
     """gwn_gram (the adaptive-support gradient, the backward of model.py:13 w.r.t. A over all slices of
     a layer, both hop pairs) against an fp64 einsum: odd tile counts (n = 207: 7 tiles, 325: 11), a
-    single tile, one slice, padded row strides, accumulation into dA.  Bound: an fp32 FMA chain over
-    K = slices*32*pairs terms, |err| <= 2^-22 K sum|x||t|."""
+    single tile, one slice, padded row strides, accumulation into dA.  Bound: an fp32 FMA chain over K = slices*32*pairs terms, |err| <= 2^-22 K sum|x||t|."""
     from gwn_amd import _lib
     lib = _lib.load()
     torch.manual_seed(n + slices)

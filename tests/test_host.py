@@ -143,10 +143,16 @@ def test_packed_layout_roundtrip():
 def test_config_rejects_unsupported():
     from gwn_amd.executor import Config
     from gwn_amd.model import gwnet
-    m = gwnet("cpu", 8, 0.0, supports=None, residual_channels=16, dilation_channels=32, skip_channels=64,
+    m = gwnet("cpu", 8, 0.0, supports=None, residual_channels=24, dilation_channels=32, skip_channels=64,
               end_channels=64)
     with pytest.raises(ValueError):
-        Config(m)
+        Config(m)  # residual channels feed the BatchNorm kernels: 16..256, dividing 256
+    # residual != dilation channels and kernel_size 3 (model.py:83-86) are accepted: generic GEMM path
+    m = gwnet("cpu", 8, 0.0, supports=None, residual_channels=16, dilation_channels=32, skip_channels=64,
+              end_channels=64, kernel_size=3)
+    cfg = Config(m)
+    assert (cfg.C, cfg.D, cfg.K, cfg.square) == (16, 32, 3, False)
+    assert cfg.R == 25 and cfg.times(13) == [25, 23, 19, 17, 13, 11, 7, 5, 1]
 
 
 def test_workspace_queries_are_monotone_in_rows():
