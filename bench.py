@@ -261,8 +261,10 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
             rec = json.load(f).get("gcn_fwd_fused_kernel", {})
         traffic, mfma_busy = rec.get("hbm_bytes_per_dispatch"), rec.get("mfma_busy_frac")
     if fused:
-        kname = ("gcn_fwd_pow_kernel<512> (fused diffusion GCN forward, power schedule, 8 launches/step)"
-                 if ex._pow_ok(1) else "gcn_fwd_fused_kernel<512, true> (fused diffusion GCN forward, chained hops, "
+        t16 = os.environ.get("GWN_GCN_T16", "1") != "0"
+        kname = (("gcn_fwd_t16_kernel<1024> (fused diffusion GCN forward, power schedule, 16-node tile waves"
+                  if t16 else "gcn_fwd_pow_kernel<512> (fused diffusion GCN forward, power schedule")
+                 + ", 8 launches/step)" if ex._pow_ok(1) else "gcn_fwd_fused_kernel<512, true> (fused diffusion GCN forward, chained hops, "
                                        "8 launches/step)")
     else:
         kname = "gwn_gcn_fwd large-graph schedule (batched diffusion GEMMs + mlp, 8 calls/step)"

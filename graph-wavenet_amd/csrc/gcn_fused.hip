@@ -1046,6 +1046,453 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_pow_kernel(const FusedFwd a, 
   fwd_epilogue<EPT>(a, xs, red[0], red[1], row0, n, u.slice);
 }
 
+// ---------------------------------------------------------------------------------------------
+// 16-node tiles (v_mfma_f32_16x16x4_f32): the power-schedule forward with one wave per 16-node
+// tile.  Against the 32-node tile waves it pads 207 nodes to 208 rows instead of 224 (7 % fewer
+// MFMAs), gives a slice 13 equal waves instead of 7 (the SIMD imbalance of 7 waves on 4 SIMDs:
+// 2,2,2,1), and needs fewer registers per wave (4-register accumulators), so two workgroups share
+// a CU at 6-7 waves per SIMD.
+//   diffusion (piece p of support k, channel half hf): D[c][w] = sum_v x[v][c] * G[v][w] with
+//     A operand x[v0 + lane/16][16 hf + lane%16] (LDS image, row stride LDR16: conflict-free),
+//     B operand G[v0 + lane/16][w0 + lane%16] (support row segments, L2-resident), and
+//     lane l holding D[16 hf + 4 (l/16) + r][w0 + l%16] in register r;
+//   mlp: z[w][o] += sum_c W[o][c] piece[c][w] with the contraction PERMUTED so that the pieces
+//     feed the B operand straight from the accumulators: step s of half hf takes, in lane group
+//     g = l/16, channel 16 hf + 4 g + s (register s), and the A operand W^T[that channel][o] from
+//     the transposed weights (16 consecutive floats per lane group);
+//   z tile: lane l holds z[w0 + l%16][16 oh + 4 (l/16) + r]: 16-B epilogue rows per lane.
+// ---------------------------------------------------------------------------------------------
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+constexpr int LDR16 = 48;  // LDS row stride: lanes (g, j) of a 32-lane half hit banks 16 g + j
+constexpr int T16_RING = 4;  // k-steps (4 support rows each) of support fragments in flight
+
+__host__ __device__ inline int t16_img_rows(int n) {
+  const int nt16 = (n + 15) / 16;
+  const int nk = (n + 3) / 4, nkp = (nk + T16_RING - 1) / T16_RING * T16_RING;
+  // (+4: the diffusion loop reads one k-step ahead)
+  return 16 * nt16 > 4 * nkp + 4 ? 16 * nt16 : 4 * nkp + 4;
+}
+
+constexpr int LDW16 = 36;  // LDS row stride of the staged channel maps: lane groups g hit banks 16 g + j
+
+// image + the channel maps of all 2K+1 pieces (32 x LDW16 floats each) + the tiles' BN partials
+size_t t16_lds_bytes(int n, int nsup) {
+  return (size_t)(t16_img_rows(n) * LDR16 + (2 * nsup + 1) * CH * LDW16 + ((n + 15) / 16) * 3 * CH) * sizeof(float);
+}
+
+// the channel maps M_p[out][in] of pieces p < npieces into LDS as m[(p*32 + in)*LDW16 + out]:
+// forward M_p = W[:, p-block] read from W^T rows (w_t + (p*32 + in)*32); backward M_p = W[:, p-block]^T
+// read from W rows (w + in*ld_w + p*32: in = output channel of the mlp)
+__device__ __forceinline__ void t16_stage_maps(const float* src, int ld_w, bool backward, int npieces, float* dst) {
+  const int total = npieces * CH * 8;  // float4s
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    const int r = e >> 3, q = e & 7;
+    const float* row = backward ? src + (long)(r & 31) * ld_w + (r >> 5) * CH : src + (long)r * CH;
+    *(float4*)(dst + r * LDW16 + 4 * q) = *(const float4*)(row + 4 * q);
+  }
+}
+
+// rows [0, rows) of the slice's node features (rows >= n zero) into LDS rows of LDR16 floats
+__device__ __forceinline__ void global_to_lds16(const float* src, long ld, int n, int rows, float* buf) {
+  if ((((uintptr_t)src) & 15) == 0 && (ld & 3) == 0) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((long)n * ld * 4), 0x00020000);
+    const int total = rows * 8;
+    for (int e0 = 0; e0 < total; e0 += 4 * (int)blockDim.x) {
+      float4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = e0 + threadIdx.x + i * blockDim.x;
+        const int off = e < total ? (int)(((long)(e >> 3) * ld + 4 * (e & 7)) * 4) : 0x7ffffff0;
+        v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = e0 + threadIdx.x + i * blockDim.x;
+        if (e < total) *(float4*)(buf + (e >> 3) * LDR16 + 4 * (e & 7)) = v[i];
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < rows * CH; e += blockDim.x) {
+      const int w = e / CH, c = e % CH;
+      buf[w * LDR16 + c] = w < n ? src[(long)w * ld + c] : 0.0f;
+    }
+  }
+}
+
+// x += (x rotated by 8, 4, 2, 1 lanes within its 16-lane row): the row sum in every lane (each lane
+// in its own order; callers take lane 0 of the row: deterministic)
+__device__ __forceinline__ float row16_sum(float x) {
+  int v = __builtin_bit_cast(int, x);
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false));
+  v = __builtin_bit_cast(int, x);
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false));
+  v = __builtin_bit_cast(int, x);
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x122, 0xF, 0xF, false));
+  v = __builtin_bit_cast(int, x);
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x121, 0xF, 0xF, false));
+  return x;
+}
+
+// z tile epilogue (fwd_tile_epilogue's arithmetic on the 16-node tile layout) and the tile's BN
+// partial, merged per slice by the workgroup's last tile
+__device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* hacc, long row0, int w0, int lane,
+                                             int n, int slice, int tile, int ntiles, float* tpart, int* tiles_done) {
+  const int g = lane >> 4, j = lane & 15;
+  const int w = w0 + j;
+  const bool valid = w < n;
+  const long m = row0 + min(w, n - 1);
+  const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
+  const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  float* dst = a.x_out ? a.x_out : a.z;
+  float v[8];
+#pragma unroll
+  for (int oh = 0; oh < 2; ++oh) {
+    const int c0 = 16 * oh + 4 * g;
+    const float4 bq = *(const float4*)(a.b_mlp + c0);
+    const float4 rq = *(const float4*)(a.residual + m * CH + c0);
+    const float* bias = (const float*)&bq;
+    const float* rv = (const float*)&rq;
+    float4 mq, sq, hq;
+    if (a.res_scale) {
+      mq = *(const float4*)(a.res_mean + c0);
+      sq = *(const float4*)(a.res_scale + c0);
+      hq = *(const float4*)(a.res_shift + c0);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = hacc[oh][e] + bias[e];
+      if (a.drop_p > 0.0f) {
+        const float u = gwn_uniform(seed, a.salt, (unsigned long long)m * CH + c0 + e);
+        x = (u >= a.drop_p) ? x * keep_scale : 0.0f;
+      }
+      x += a.res_scale ? fmaf(rv[e] - ((const float*)&mq)[e], ((const float*)&sq)[e], ((const float*)&hq)[e]) : rv[e];
+      v[4 * oh + e] = x;
+    }
+    if (a.x_out) {  // eval BatchNorm, the arithmetic of bn_apply_kernel (ops.hip)
+      const float4 rm = *(const float4*)(a.bn_rm + c0), rvv = *(const float4*)(a.bn_rv + c0);
+      const float4 gq = *(const float4*)(a.bn_g + c0), bb = *(const float4*)(a.bn_b + c0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[4 * oh + e] = (v[4 * oh + e] - ((const float*)&rm)[e]) *
+                            (1.0f / sqrtf(((const float*)&rvv)[e] + a.bn_eps)) * ((const float*)&gq)[e] +
+                        ((const float*)&bb)[e];
+    }
+    if (valid) *(float4*)(dst + m * CH + c0) = make_float4(v[4 * oh], v[4 * oh + 1], v[4 * oh + 2], v[4 * oh + 3]);
+  }
+  if (a.bn_part == nullptr || a.x_out) return;
+  const int cnt = min(16, n - w0);
+  const float inv = 1.0f / (float)cnt;
+  float* pp = tpart + tile * 3 * CH;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float mean = row16_sum(valid ? v[q] : 0.0f) * inv;
+    const float d = valid ? v[q] - mean : 0.0f;
+    const float m2 = row16_sum(d * d);
+    if (j == 0) {
+      const int c = 16 * (q >> 2) + 4 * g + (q & 3);
+      pp[c] = (float)cnt;
+      pp[CH + c] = mean;
+      pp[2 * CH + c] = m2;
+    }
+  }
+  // the slice's partial: the last tile to get here merges the tiles' partials in tile order
+  __threadfence_block();
+  int last = 0;
+  if (lane == 0) last = atomicAdd(tiles_done, 1) == ntiles - 1;
+  last = __shfl(last, 0, 64);
+  if (!last) return;
+  __threadfence_block();
+  if (lane < CH) {
+    float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
+    for (int t = 0; t < ntiles; ++t) {
+      const float nb = tpart[t * 3 * CH + lane], mb = tpart[t * 3 * CH + CH + lane];
+      const float qb = tpart[t * 3 * CH + 2 * CH + lane];
+      const float tot = nn + nb;
+      const float d = mb - mean;
+      mean += d * (nb / tot);
+      m2 += qb + d * d * (nn * nb / tot);
+      nn = tot;
+    }
+    float* sp = a.bn_part + (long)slice * 3 * CH;
+    sp[lane] = nn;
+    sp[CH + lane] = mean;
+    sp[2 * CH + lane] = m2;
+  }
+}
+
+// the channel map of one piece held in accumulators acc[hf] (register s = input channel
+// 16 hf + 4 g + s): hacc[oh] (output channel 16 oh + 4 g + r) += M x piece with the A operand
+// M[out][in] read as m[in * ld_m + out] -- forward: the piece's block of W^T (ld_m = 32);
+// backward: the piece's column block of W itself (ld_m = ld_w), i.e. W^T applied to dh
+__device__ __forceinline__ void t16_mlp(const float* m, int ld_m, const f32x4v* acc, int lane, f32x4v* hacc) {
+  const int g = lane >> 4, j = lane & 15;
+  float wf[2][2][4];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int oh = 0; oh < 2; ++oh) wf[hf][oh][s] = m[(16 * hf + 4 * g + s) * ld_m + 16 * oh + j];
+  // all 16 fragment reads in flight before the first product (one LDS latency, not sixteen)
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int oh = 0; oh < 2; ++oh)
+        hacc[oh] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[hf][oh][s], acc[hf][s], hacc[oh], 0, 0, 0);
+}
+
+// both powers of one support for the wave's 16-node tile: acc[q][hf] (q = 0: G1, 1: G2) holds
+// D[16 hf + 4 g + r][w0 + j] = sum_v img[v][16 hf + 4 g + r] G_q[v][w0 + j]
+__device__ __forceinline__ void t16_diffuse(const float* img, const float* G1, const float* G2, int ld_sup, int np,
+                                            int n, int w0, int lane, f32x4v (*acc)[2]) {
+  const int g = lane >> 4, j = lane & 15;
+  const int nk = (n + 3) >> 2;
+  const int nkp = (nk + T16_RING - 1) / T16_RING * T16_RING;
+  const __amdgpu_buffer_rsrc_t r1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)G1, (short)0, (int)((long)np * ld_sup * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t r2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)G2, (short)0, (int)((long)np * ld_sup * 4), 0x00020000);
+  // support fragment of k-step ks: G[4 ks + g][w0 + j] (rows >= np out of range: zero)
+  auto off = [&](int ks) { return (int)(((long)(4 * ks + g) * ld_sup + w0 + j) * 4); };
+  float s1[T16_RING], s2[T16_RING];
+#pragma unroll
+  for (int r = 0; r < T16_RING - 1; ++r) {
+    s1[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, off(r), 0, 0));
+    s2[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, off(r), 0, 0));
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) acc[q][0] = acc[q][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  const float* xp = img + g * LDR16 + j;
+  // image operands one k-step ahead: the LDS latency hides behind the current step's products
+  float xa = xp[0], xb = xp[16];
+  for (int ks0 = 0; ks0 < nkp; ks0 += T16_RING) {
+#pragma unroll
+    for (int r = 0; r < T16_RING; ++r) {
+      const int ks = ks0 + r;
+      const int nx = (r + T16_RING - 1) % T16_RING;
+      s1[nx] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, off(ks + T16_RING - 1), 0, 0));
+      s2[nx] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, off(ks + T16_RING - 1), 0, 0));
+      // the image has 4 * nkp + 4 rows (t16_img_rows): step nkp's read stays inside
+      const float na = xp[4 * (ks + 1) * LDR16], nb = xp[4 * (ks + 1) * LDR16 + 16];
+      __builtin_amdgcn_sched_barrier(0);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, s1[r], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb, s1[r], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, s2[r], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb, s2[r], acc[1][1], 0, 0, 0);
+      xa = na;
+      xb = nb;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// the image rows of the wave's tile as B operands in the permuted channel order of t16_mlp
+__device__ __forceinline__ void t16_rows(const float* img, int w0, int lane, f32x4v* x) {
+  const int g = lane >> 4, j = lane & 15;
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const float4 q = *(const float4*)(img + (w0 + j) * LDR16 + 16 * hf + 4 * g);
+    x[hf] = f32x4v{q.x, q.y, q.z, q.w};
+  }
+}
+
+template <int MAXT>
+__global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(8))) void gcn_fwd_t16_kernel(const FusedFwd a,
+                                                                                                 const PowSup p) {
+  extern __shared__ float lds[];
+  __shared__ int tiles_done;
+  const int n = a.n;
+  const int ntiles = (n + 15) >> 4;
+  const int rows_img = t16_img_rows(n);
+  float* xs = lds;
+  float* ws = lds + rows_img * LDR16;
+  float* tpart = ws + (2 * a.nsup + 1) * CH * LDW16;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  const int nwaves = blockDim.x >> 6;
+  const int slice = blockIdx.x;
+  const long row0 = (long)slice * n;
+  const long ldh = a.ld_h;
+  float* hs = (float*)a.h + row0 * ldh;
+  const int np = (n + 31) / 32 * 32;
+  const bool nt_ok = ((((uintptr_t)hs) & 15) | (ldh & 3)) == 0;
+  if (threadIdx.x == 0) tiles_done = 0;
+  t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
+  global_to_lds16(hs, ldh, n, rows_img, xs);
+  __syncthreads();
+  for (int tile = wave; tile < ntiles; tile += nwaves) {
+    const int w0 = 16 * tile;
+    f32x4v hacc[2];
+    hacc[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    hacc[1] = hacc[0];
+    {  // piece 0: the node features themselves
+      f32x4v x0[2];
+      t16_rows(xs, w0, lane, x0);
+      t16_mlp(ws, LDW16, x0, lane, hacc);
+    }
+    for (int k = 0; k < a.nsup; ++k) {
+      f32x4v acc[2][2];  // [power][channel half]
+      t16_diffuse(xs, a.sup[k], p.g2[k], a.ld_sup, np, n, w0, lane, acc);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        t16_mlp(ws + (1 + 2 * k + q) * CH * LDW16, LDW16, acc[q], lane, hacc);
+        if (a.store_pieces && w0 + j < n) {
+          float* dp = hs + (long)(w0 + j) * ldh + (1 + 2 * k + q) * CH + 4 * g;
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            if (nt_ok) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
+            else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) dp[16 * hf + e] = acc[q][hf][e];
+            }
+          }
+        }
+      }
+    }
+    t16_epilogue(a, hacc, row0, w0, lane, n, slice, tile, ntiles, tpart, &tiles_done);
+  }
+}
+
+// Backward on 16-node tiles: the forward's structure with the dh image (BN-backward prologue),
+// the transposed supports A_k^T and (A_k^2)^T (so D = A dh, A^2 dh) and the channel map W^T:
+//   dxg = W_0^T dh + sum_k W_{1+2k}^T (A_k dh) + W_{2+2k}^T (A_k^2 dh)
+// (gcn_bwd_pow_kernel's schedule), t1 / t2 of the adaptive support, and the dxg store or the gate
+// backward in the epilogue.
+__device__ __forceinline__ void t16_bwd_prologue(const FusedBwd& a, float* img, long row0, int n, int rows) {
+  if (!a.bn_dy) {
+    global_to_lds16(a.dh + row0 * CH, CH, n, rows, img);
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < CH) {
+    if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
+    if (a.bn_dgamma) a.bn_dgamma[threadIdx.x] = a.bn_sums[CH + threadIdx.x];
+  }
+  const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
+  const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  const int c = threadIdx.x & 31;  // blockDim is a multiple of 64: every element of a thread has channel c
+  const float mu = a.bn_mean[c], rs = a.bn_rstd[c], gm = a.bn_gamma[c];
+  const float k1 = a.bn_sums[c] * a.inv_rows, k2 = a.bn_sums[CH + c] * a.inv_rows;
+  const int total = rows * CH;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 4 * (int)blockDim.x) {
+    float dy[4], zv[4];  // all loads before the first store
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int w = min((e0 + i * (int)blockDim.x) >> 5, n - 1);
+      dy[i] = a.bn_dy[(row0 + w) * CH + c];
+      zv[i] = a.bn_z[(row0 + w) * CH + c];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = e0 + i * (int)blockDim.x;
+      if (e >= total) break;
+      const int w = e >> 5;
+      float v = 0.0f;
+      if (w < n) {
+        const long idx = (row0 + w) * CH + c;
+        const float xhat = (zv[i] - mu) * rs;
+        const float dz = gm * rs * (dy[i] - k1 - xhat * k2);
+        a.dres[idx] = dz;
+        v = dz;
+        if (a.drop_p > 0.0f) {
+          const float u = gwn_uniform(seed, a.salt, (unsigned long long)idx);
+          v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
+        }
+        a.dh_out[idx] = v;
+      }
+      img[w * LDR16 + c] = v;
+    }
+  }
+}
+
+// rows of a [rows][ld] output from the t16 accumulator layout (lane: node w0 + j, channels
+// 16 oh + 4 g .. + 3)
+__device__ __forceinline__ void t16_store(float* out, long ld, const f32x4v* acc, int w0, int lane, int n) {
+  const int g = lane >> 4, j = lane & 15;
+  if (w0 + j >= n) return;
+  float* p = out + (long)(w0 + j) * ld + 4 * g;
+#pragma unroll
+  for (int oh = 0; oh < 2; ++oh) *(float4*)(p + 16 * oh) = make_float4(acc[oh][0], acc[oh][1], acc[oh][2], acc[oh][3]);
+}
+
+template <int MAXT>
+__global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(8))) void gcn_bwd_t16_kernel(const FusedBwd a,
+                                                                                                 const PowSup p) {
+  extern __shared__ float lds[];
+  const int n = a.n;
+  const int ntiles = (n + 15) >> 4;
+  const int rows_img = t16_img_rows(n);
+  float* dhs = lds;
+  float* ws = lds + rows_img * LDR16;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  const int nwaves = blockDim.x >> 6;
+  const long row0 = (long)blockIdx.x * n;
+  const int np = (n + 31) / 32 * 32;
+  t16_stage_maps(a.w_mlp, a.ld_w, true, 2 * a.nsup + 1, ws);
+  t16_bwd_prologue(a, dhs, row0, n, rows_img);
+  __syncthreads();
+  for (int tile = wave; tile < ntiles; tile += nwaves) {
+    const int w0 = 16 * tile;
+    f32x4v dx[2];
+    dx[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    dx[1] = dx[0];
+    {
+      f32x4v d0[2];
+      t16_rows(dhs, w0, lane, d0);
+      t16_mlp(ws, LDW16, d0, lane, dx);
+    }
+    for (int k = 0; k < a.nsup; ++k) {
+      f32x4v e[2][2];
+      t16_diffuse(dhs, a.supT[k], p.g2[k], a.ld_sup, np, n, w0, lane, e);
+      t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, e[0], lane, dx);
+      t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[1], lane, dx);
+      if (k == a.adp_index) {  // t1 = W1^T dh + W2^T (A dh), t2 = W2^T dh
+        f32x4v d0[2], t[2];
+        t16_rows(dhs, w0, lane, d0);
+        t[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+        t[1] = t[0];
+        t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, d0, lane, t);
+        t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[0], lane, t);
+        t16_store(a.t1 + row0 * a.ld_t, a.ld_t, t, w0, lane, n);
+        t[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+        t[1] = t[0];
+        t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, d0, lane, t);
+        t16_store(a.t2 + row0 * a.ld_t, a.ld_t, t, w0, lane, n);
+      }
+    }
+    if (!a.dfg) {
+      t16_store(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
+      continue;
+    }
+    // gate backward (gate_bwd_kernel's arithmetic): g = dxg (+ dskip) -> dfg via (tanh f, sigmoid s)
+    const int w = w0 + j;
+    if (w >= n) continue;
+    const long m = row0 + w;
+    const bool sk = a.dskip && m >= a.skip_row0;
+#pragma unroll
+    for (int oh = 0; oh < 2; ++oh) {
+      const int c0 = 16 * oh + 4 * g;
+      const float4 f0 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0);
+      const float4 f1 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0 + 4);
+      const float4 dq = sk ? *(const float4*)(a.dskip + (m - a.skip_row0) * a.ld_dskip + c0) : make_float4(0, 0, 0, 0);
+      const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      const float dv[4] = {dq.x, dq.y, dq.z, dq.w};
+      float o[8];
+#pragma unroll
+      for (int e2 = 0; e2 < 4; ++e2) {
+        const float gv = dx[oh][e2] + dv[e2];
+        const float f = fv[2 * e2], sg = fv[2 * e2 + 1];
+        o[2 * e2] = gv * sg * (1.0f - f * f);
+        o[2 * e2 + 1] = gv * f * sg * (1.0f - sg);
+      }
+      *(float4*)(a.dfg + m * 2 * CH + 2 * c0) = make_float4(o[0], o[1], o[2], o[3]);
+      *(float4*)(a.dfg + m * 2 * CH + 2 * c0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    }
+  }
+}
+
 // Backward gate epilogue of one wave's tile from the input-gradient accumulator (lane = node,
 // register r = channel crow(r, half)): g = dxg (+ dskip) -> dfg through the saved (tanh f,
 // sigmoid s) pairs (gate_bwd_kernel's arithmetic), 16-B loads / stores.
@@ -1265,6 +1712,14 @@ bool gwn_gcn_split_eligible(int c, int n, int planes);
 int gwn_gcn_split_fwd_launch(const gwn_gcn_args* g, const FusedFwd& a, hipStream_t s);
 int gwn_gcn_bf16_bwd_launch(const gwn_gcn_bwd_args* g, const FusedBwd& a, hipStream_t s);
 
+// the 16-node tile forward (GWN_GCN_T16=0 selects the 32-node tile power kernel)
+constexpr int T16_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS of a t16 workgroup (static: a counter)
+
+static bool t16_enabled() {
+  const char* e = getenv("GWN_GCN_T16");  // read per launch (tests switch it within one process)
+  return !(e && e[0] == '0');
+}
+
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
   const int nwt = (g->n + 31) / 32;
   GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_fwd (fused): supports must be padded to 32*ceil(n/32)");
@@ -1307,6 +1762,8 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
     ensure_lds_attr(gcn_fwd_fused_kernel<1024, true>);
     ensure_lds_attr(gcn_fwd_pow_kernel<512>);
     ensure_lds_attr(gcn_fwd_pow_kernel<1024>);
+    (void)hipFuncSetAttribute((const void*)gcn_fwd_t16_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              T16_LDS_MAX);
     attr_set = true;
   }
   const int slices = g->rows / g->n;
@@ -1316,6 +1773,14 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
     GWN_REQUIRE(g->w_mlp_t, "gcn_fwd (power schedule): w_mlp_t (the transposed mlp weights) is required with sup2");
     PowSup p;
     for (int k = 0; k < 8; ++k) p.g2[k] = (k < g->nsup) ? g->sup2[k] : nullptr;
+    if (a.ksplit <= 1 && g->layout == 0 && t16_enabled() && t16_lds_bytes(g->n, g->nsup) <= T16_LDS_MAX) {
+      // 16-node tile waves (one per tile up to 16, then two tiles per wave)
+      const int nt16 = (g->n + 15) / 16;
+      const int waves = nt16 <= 16 ? nt16 : (nt16 + 1) / 2;
+      gcn_fwd_t16_kernel<1024><<<grid, 64 * waves, t16_lds_bytes(g->n, g->nsup), s>>>(a, p);
+      GWN_CHECK_LAUNCH();
+      return GWN_OK;
+    }
     const size_t lds = pow_lds_bytes(g->n);
     if (nwt <= 8) gcn_fwd_pow_kernel<512><<<grid, 64 * nwt, lds, s>>>(a, p);
     else gcn_fwd_pow_kernel<1024><<<grid, 64 * nwt, lds, s>>>(a, p);
@@ -1376,6 +1841,8 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
     ensure_lds_attr(gcn_bwd_fused_kernel<1024, true>);
     ensure_lds_attr(gcn_bwd_pow_kernel<512>);
     ensure_lds_attr(gcn_bwd_pow_kernel<1024>);
+    (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              T16_LDS_MAX);
     attr_set = true;
   }
   const int slices = g->rows / g->n;
@@ -1384,6 +1851,13 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   if (g->sup2_t && a.sup_batch <= 1 && g->nsup > 0) {
     PowSup p;
     for (int k = 0; k < 8; ++k) p.g2[k] = (k < g->nsup) ? g->sup2_t[k] : nullptr;
+    if (a.ksplit <= 1 && g->layout == 0 && t16_enabled() && t16_lds_bytes(g->n, g->nsup) <= T16_LDS_MAX) {
+      const int nt16 = (g->n + 15) / 16;
+      const int waves = nt16 <= 16 ? nt16 : (nt16 + 1) / 2;
+      gcn_bwd_t16_kernel<1024><<<grid, 64 * waves, t16_lds_bytes(g->n, g->nsup), s>>>(a, p);
+      GWN_CHECK_LAUNCH();
+      return GWN_OK;
+    }
     const size_t lds = pow_lds_bytes(g->n);
     if (nwt <= 8) gcn_bwd_pow_kernel<512><<<grid, 64 * nwt, lds, s>>>(a, p);
     else gcn_bwd_pow_kernel<1024><<<grid, 64 * nwt, lds, s>>>(a, p);

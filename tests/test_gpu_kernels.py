@@ -509,12 +509,13 @@ def test_support_square(gpu, n):
 
 
 @pytest.mark.parametrize("n", [16, 96, 207, 256, 325])
-def test_gcn_fused_schedules_agree(gpu, n):
+def test_gcn_fused_schedules_agree(gpu, n, monkeypatch):
     """The two schedules of the fused gcn forward / backward -- chained hops (hop 2 diffuses hop 1
     through LDS) and the power schedule (A and A^2 against the node features in one pass, backward
     W^T-after-diffusion) -- each whole-slice and with the support split (one workgroup per (slice,
-    support), partial sums combined by the slice's last workgroup), against fp64 (model.py:41-55):
-    hop pieces, z, BN partials, dxg and the adaptive-support pieces t1 / t2."""
+    support), partial sums combined by the slice's last workgroup), the power forward on 16-node
+    tiles (default) and on 32-node tiles (GWN_GCN_T16=0), against fp64 (model.py:41-55): hop
+    pieces, z, BN partials, dxg and the adaptive-support pieces t1 / t2."""
     import ctypes
     from gwn_amd import _lib
     torch.manual_seed(n)
@@ -544,7 +545,8 @@ def test_gcn_fused_schedules_agree(gpu, n):
     outs = []
     kws = torch.empty(_lib.load().gwn_gcn_ksplit_ws_floats(rows, n, K), device=gpu)
     kcnt = torch.zeros(S, device=gpu, dtype=torch.int32)
-    for pw, ksplit in ((False, 1), (False, K), (True, 1), (True, K)):
+    for pw, ksplit, t16 in ((False, 1, "1"), (False, K, "1"), (True, 1, "1"), (True, K, "1"), (True, 1, "0")):
+        monkeypatch.setenv("GWN_GCN_T16", t16)
         kf = dict(ksplit=ksplit, ksplit_ws=kws.data_ptr(), ksplit_count=kcnt.data_ptr())
         h = torch.zeros(rows, W, device=gpu)
         h[:, :C] = xg
