@@ -222,17 +222,19 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
     C, N, K = cfg.C, cfg.N, cfg.nsup
     st = _lib.stream()
     launches = [acts.gcn_args[i] for i in sorted(acts.gcn_args)]
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in launches]
+    # one event pair around each round of the 8 back-to-back launches (an event pair per launch
+    # added ~10 us of event overhead to every 100 us launch); the inter-launch gaps stay inside
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     total_ms, total_flop, total_bytes, count = 0.0, 0.0, 0.0, 0
     for _ in range(rounds):
-        for ga, (e0, e1) in zip(launches, evs):
-            e0.record()
+        e0.record()
+        for ga in launches:
             _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
-            e1.record()
+        e1.record()
         torch.cuda.synchronize()
-        for ga, (e0, e1) in zip(launches, evs):
+        total_ms += e0.elapsed_time(e1)
+        for ga in launches:
             slices = ga.rows // N
-            total_ms += e0.elapsed_time(e1)
             total_flop += slices * (K * 2 * 2.0 * C * N * N + 2.0 * (2 * K + 1) * C * C * N)
             # compulsory bytes: xg + residual in, 2K hop outputs + z out; the
             # last layer (output dead but for BN running stats) stores no hop pieces
@@ -241,29 +243,36 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
     avg_us = 1000.0 * total_ms / count
     achieved = total_flop / (total_ms / 1000.0) / 1e12
     fused = N <= 512
+    def pmc(name, key):
+        # HBM bytes per launch and MFMA busy fraction from the committed PMC passes of this kernel
+        # over this bench (tools/gpu_pmc_r3.sh + tools/pmc_summary.py: separate --pmc runs for
+        # FETCH_SIZE, WRITE_SIZE and the SQ counters; FETCH x2 per the gfx950 correction)
+        path = os.path.join(ROOT, "profiles", "r03", name)
+        if not os.path.exists(path):
+            return None, None, None
+        with open(path) as f:
+            rec = json.load(f).get(key, {})
+        return rec.get("hbm_bytes_per_dispatch"), rec.get("mfma_busy_frac"), "profiles/r03/" + name
+
     if bf16:
         # bf16 operands: arithmetic intensity (~80 FLOP/B algorithmic) sits far below the bf16
         # ridge (2.5 PF / 8 TB/s = 312 FLOP/B): the kernel is bounded by HBM, priced in bytes
         gbs = total_bytes / (total_ms / 1000.0) / 1e9
-        return {"kernel": "gcn_fwd_split_kernel<%d, 1, 2> (fused diffusion GCN forward, bf16 operands, "
-                          "8 launches/step)" % ((N + 31) // 32),
+        traffic, mfma_busy, src = pmc("pmc_bench_pems.json", "gcn_fwd_split_kernel") if N == 325 else (None,) * 3
+        return {"kernel": "gcn_fwd_split_kernel<%d, 1, %d> (fused diffusion GCN forward, bf16 operands, "
+                          "8 launches/step)" % ((N + 31) // 32, (N + 31) // 32),
                 "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
+                "pmc_mfma_busy_frac": mfma_busy,
                 "mfma_tflops": round(achieved, 3), "mfma_peak_bf16": BF16_PEAK_TFLOPS,
                 "avg_launch_us": round(avg_us, 3), "flop_per_launch_avg": round(total_flop / count, 1),
                 "algorithmic_bytes_per_launch": round(total_bytes / count), "launches_timed": count}
-    # HBM bytes per launch and MFMA busy fraction from the committed PMC passes of this kernel over
-    # this bench (tools/pmc.sh + tools/pmc_summary.py: separate --pmc runs for FETCH_SIZE,
-    # WRITE_SIZE and the SQ counters; FETCH x2 per the gfx950 correction)
-    traffic, mfma_busy, pmc = None, None, os.path.join(ROOT, "profiles", "r02", "pmc_bench_metr.json")
-    if fused and N == 207 and os.path.exists(pmc):
-        with open(pmc) as f:
-            rec = json.load(f).get("gcn_fwd_fused_kernel", {})
-        traffic, mfma_busy = rec.get("hbm_bytes_per_dispatch"), rec.get("mfma_busy_frac")
+    t16 = fused and ex._pow_ok(1) and os.environ.get("GWN_GCN_T16", "1") != "0"
+    traffic, mfma_busy, src = pmc("pmc_bench_metr.json", "gcn_fwd_t16_kernel") if t16 and N == 207 else (None,) * 3
     if fused:
-        t16 = os.environ.get("GWN_GCN_T16", "1") != "0"
-        kname = (("gcn_fwd_t16_kernel<1024> (fused diffusion GCN forward, power schedule, 16-node tile waves"
-                  if t16 else "gcn_fwd_pow_kernel<512> (fused diffusion GCN forward, power schedule")
+        kname = (("gcn_fwd_t16_kernel<1024> (fused diffusion GCN forward, power schedule, persistent 16-node "
+                  "tile waves: one workgroup per CU over an equal tile range" if t16 else
+                  "gcn_fwd_pow_kernel<512> (fused diffusion GCN forward, power schedule")
                  + ", 8 launches/step)" if ex._pow_ok(1) else "gcn_fwd_fused_kernel<512, true> (fused diffusion GCN forward, chained hops, "
                                        "8 launches/step)")
     else:
@@ -271,7 +280,7 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
     return {"kernel": kname,
             "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-            "traffic_source": "profiles/r02/pmc_bench_metr.json" if traffic else None,
+            "traffic_source": src,
             "pmc_mfma_busy_frac": mfma_busy,
             "avg_launch_us": round(avg_us, 3), "flop_per_launch_avg": round(total_flop / count, 1),
             "algorithmic_bytes_per_launch": round(total_bytes / count),

@@ -53,6 +53,7 @@ struct FusedFwd {
   long sup_bstride; int sup_batch;  // per-sample supports (sup_batch > 1): sample b = slice % sup_batch
   const float* res_mean; const float* res_scale; const float* res_shift;  // (residual - mean) * scale + shift
   int ksplit, slices; float* kws; int* kcnt;  // support split (ksplit > 1): see unit_of()
+  int bn_slots;  // t16 kernels: BN partial slots to write (those past the grid get count 0)
 };
 
 struct FusedBwd {
@@ -1063,21 +1064,27 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_pow_kernel(const FusedFwd a, 
 //   z tile: lane l holds z[w0 + l%16][16 oh + 4 (l/16) + r]: 16-B epilogue rows per lane.
 // ---------------------------------------------------------------------------------------------
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-constexpr int LDR16 = 48;  // LDS row stride: lanes (g, j) of a 32-lane half hit banks 16 g + j
-constexpr int T16_RING = 4;  // k-steps (4 support rows each) of support fragments in flight
+constexpr int T16_RING = 4;   // k-steps (4 support rows each) of support fragments in flight
+constexpr int T16_WAVES = 16; // waves of a t16 workgroup (one workgroup per CU, persistent over a tile range)
+constexpr int T16_MAXIMG = 4; // slice images a workgroup holds at once (LDS permitting)
 
+// rows of a slice image: the tiles' rows, and the diffusion loop's reads (4 rows per k-step, one
+// k-step ahead, whole rings of T16_RING k-steps); rows >= n are zero
 __host__ __device__ inline int t16_img_rows(int n) {
   const int nt16 = (n + 15) / 16;
   const int nk = (n + 3) / 4, nkp = (nk + T16_RING - 1) / T16_RING * T16_RING;
-  // (+4: the diffusion loop reads one k-step ahead)
   return 16 * nt16 > 4 * nkp + 4 ? 16 * nt16 : 4 * nkp + 4;
 }
 
+// Slice image in LDS: two channel halves, each [rows][16] (no padding): lane (g, j) of the
+// diffusion's A-operand read (row 4 ks + g, channel 16 hf + j) hits bank 16 g + j of 64.  The
+// half stride hs = rows * 16 floats is a multiple of 64 (ds_read2st64 pairs the two halves).
 constexpr int LDW16 = 36;  // LDS row stride of the staged channel maps: lane groups g hit banks 16 g + j
 
-// image + the channel maps of all 2K+1 pieces (32 x LDW16 floats each) + the tiles' BN partials
-size_t t16_lds_bytes(int n, int nsup) {
-  return (size_t)(t16_img_rows(n) * LDR16 + (2 * nsup + 1) * CH * LDW16 + ((n + 15) / 16) * 3 * CH) * sizeof(float);
+// LDS of a t16 workgroup: the channel maps of all 2K+1 pieces (32 x LDW16 floats each), the waves'
+// BN partials [16][3][32], and maximg slice images
+size_t t16_lds_bytes(int n, int nsup, int maximg) {
+  return (size_t)((2 * nsup + 1) * CH * LDW16 + T16_WAVES * 3 * CH + maximg * t16_img_rows(n) * CH) * sizeof(float);
 }
 
 // the channel maps M_p[out][in] of pieces p < npieces into LDS as m[(p*32 + in)*LDW16 + out]:
@@ -1092,8 +1099,9 @@ __device__ __forceinline__ void t16_stage_maps(const float* src, int ld_w, bool 
   }
 }
 
-// rows [0, rows) of the slice's node features (rows >= n zero) into LDS rows of LDR16 floats
+// rows [0, rows) of a slice's node features (rows >= n zero) into the two-half LDS image
 __device__ __forceinline__ void global_to_lds16(const float* src, long ld, int n, int rows, float* buf) {
+  const int hs = rows * 16;
   if ((((uintptr_t)src) & 15) == 0 && (ld & 3) == 0) {
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((long)n * ld * 4), 0x00020000);
@@ -1109,13 +1117,13 @@ __device__ __forceinline__ void global_to_lds16(const float* src, long ld, int n
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int e = e0 + threadIdx.x + i * blockDim.x;
-        if (e < total) *(float4*)(buf + (e >> 3) * LDR16 + 4 * (e & 7)) = v[i];
+        if (e < total) *(float4*)(buf + ((e >> 2) & 1) * hs + (e >> 3) * 16 + 4 * (e & 3)) = v[i];
       }
     }
   } else {
     for (int e = threadIdx.x; e < rows * CH; e += blockDim.x) {
       const int w = e / CH, c = e % CH;
-      buf[w * LDR16 + c] = w < n ? src[(long)w * ld + c] : 0.0f;
+      buf[(c >> 4) * hs + w * 16 + (c & 15)] = w < n ? src[(long)w * ld + c] : 0.0f;
     }
   }
 }
@@ -1134,10 +1142,17 @@ __device__ __forceinline__ float row16_sum(float x) {
   return x;
 }
 
-// z tile epilogue (fwd_tile_epilogue's arithmetic on the 16-node tile layout) and the tile's BN
-// partial, merged per slice by the workgroup's last tile
+// A wave's running BatchNorm partial over its tiles (Chan merge in tile order): lane (g, j) keeps
+// the 8 channels 16 (q >> 2) + 4 g + (q & 3) of its row group (lane j = 0 of a group is the one read)
+struct BnRun {
+  float n, mean[8], m2[8];
+};
+
+// z tile epilogue (fwd_tile_epilogue's arithmetic on the 16-node tile layout): bias, dropout,
+// residual (BN of the layer below applied on load), z or eval-BN output store; the tile's BN
+// partial merged into the wave's running one
 __device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* hacc, long row0, int w0, int lane,
-                                             int n, int slice, int tile, int ntiles, float* tpart, int* tiles_done) {
+                                             int n, BnRun& bn) {
   const int g = lane >> 4, j = lane & 15;
   const int w = w0 + j;
   const bool valid = w < n;
@@ -1181,44 +1196,57 @@ __device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* ha
     if (valid) *(float4*)(dst + m * CH + c0) = make_float4(v[4 * oh], v[4 * oh + 1], v[4 * oh + 2], v[4 * oh + 3]);
   }
   if (a.bn_part == nullptr || a.x_out) return;
-  const int cnt = min(16, n - w0);
-  const float inv = 1.0f / (float)cnt;
-  float* pp = tpart + tile * 3 * CH;
+  const float cnt = (float)min(16, n - w0);
+  const float inv = 1.0f / cnt;
+  const float tot = bn.n + cnt;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const float mean = row16_sum(valid ? v[q] : 0.0f) * inv;
     const float d = valid ? v[q] - mean : 0.0f;
     const float m2 = row16_sum(d * d);
-    if (j == 0) {
+    const float dm = mean - bn.mean[q];
+    bn.mean[q] += dm * (cnt / tot);
+    bn.m2[q] += m2 + dm * dm * (bn.n * cnt / tot);
+  }
+  bn.n = tot;
+}
+
+// the waves' running partials (wave order) -> the workgroup's BN partial, slot blockIdx.x
+__device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn, float* wpart) {
+  if (a.bn_part == nullptr || a.x_out) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  if (j == 0) {
+    float* wp = wpart + wave * 3 * CH;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
       const int c = 16 * (q >> 2) + 4 * g + (q & 3);
-      pp[c] = (float)cnt;
-      pp[CH + c] = mean;
-      pp[2 * CH + c] = m2;
+      wp[c] = bn.n;
+      wp[CH + c] = bn.mean[q];
+      wp[2 * CH + c] = bn.m2[q];
     }
   }
-  // the slice's partial: the last tile to get here merges the tiles' partials in tile order
-  __threadfence_block();
-  int last = 0;
-  if (lane == 0) last = atomicAdd(tiles_done, 1) == ntiles - 1;
-  last = __shfl(last, 0, 64);
-  if (!last) return;
-  __threadfence_block();
-  if (lane < CH) {
+  __syncthreads();
+  if (threadIdx.x < CH) {
+    const int c = threadIdx.x;
     float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
-    for (int t = 0; t < ntiles; ++t) {
-      const float nb = tpart[t * 3 * CH + lane], mb = tpart[t * 3 * CH + CH + lane];
-      const float qb = tpart[t * 3 * CH + 2 * CH + lane];
+    for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) {
+      const float nb = wpart[wv * 3 * CH + c];
+      if (nb <= 0.0f) continue;
+      const float mb = wpart[wv * 3 * CH + CH + c], qb = wpart[wv * 3 * CH + 2 * CH + c];
       const float tot = nn + nb;
       const float d = mb - mean;
       mean += d * (nb / tot);
       m2 += qb + d * d * (nn * nb / tot);
       nn = tot;
     }
-    float* sp = a.bn_part + (long)slice * 3 * CH;
-    sp[lane] = nn;
-    sp[CH + lane] = mean;
-    sp[2 * CH + lane] = m2;
+    float* sp = a.bn_part + (long)blockIdx.x * 3 * CH;
+    sp[c] = nn;
+    sp[CH + c] = mean;
+    sp[2 * CH + c] = m2;
   }
+  // the slots past the grid (gwn_bn_part_slots: at least one per slice) hold no rows
+  for (long slot = blockIdx.x + gridDim.x; slot < a.bn_slots; slot += gridDim.x)
+    if (threadIdx.x < 3 * CH) a.bn_part[slot * 3 * CH + threadIdx.x] = 0.0f;
 }
 
 // the channel map of one piece held in accumulators acc[hf] (register s = input channel
@@ -1247,8 +1275,8 @@ __device__ __forceinline__ void t16_mlp(const float* m, int ld_m, const f32x4v* 
 
 // both powers of one support for the wave's 16-node tile: acc[q][hf] (q = 0: G1, 1: G2) holds
 // D[16 hf + 4 g + r][w0 + j] = sum_v img[v][16 hf + 4 g + r] G_q[v][w0 + j]
-__device__ __forceinline__ void t16_diffuse(const float* img, const float* G1, const float* G2, int ld_sup, int np,
-                                            int n, int w0, int lane, f32x4v (*acc)[2]) {
+__device__ __forceinline__ void t16_diffuse(const float* img, int hs, const float* G1, const float* G2, int ld_sup,
+                                            int np, int n, int w0, int lane, f32x4v (*acc)[2]) {
   const int g = lane >> 4, j = lane & 15;
   const int nk = (n + 3) >> 2;
   const int nkp = (nk + T16_RING - 1) / T16_RING * T16_RING;
@@ -1266,9 +1294,9 @@ __device__ __forceinline__ void t16_diffuse(const float* img, const float* G1, c
   }
 #pragma unroll
   for (int q = 0; q < 2; ++q) acc[q][0] = acc[q][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-  const float* xp = img + g * LDR16 + j;
+  const float* xp = img + g * 16 + j;
   // image operands one k-step ahead: the LDS latency hides behind the current step's products
-  float xa = xp[0], xb = xp[16];
+  float xa = xp[0], xb = xp[hs];
   for (int ks0 = 0; ks0 < nkp; ks0 += T16_RING) {
 #pragma unroll
     for (int r = 0; r < T16_RING; ++r) {
@@ -1277,7 +1305,7 @@ __device__ __forceinline__ void t16_diffuse(const float* img, const float* G1, c
       s1[nx] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, off(ks + T16_RING - 1), 0, 0));
       s2[nx] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, off(ks + T16_RING - 1), 0, 0));
       // the image has 4 * nkp + 4 rows (t16_img_rows): step nkp's read stays inside
-      const float na = xp[4 * (ks + 1) * LDR16], nb = xp[4 * (ks + 1) * LDR16 + 16];
+      const float na = xp[4 * (ks + 1) * 16], nb = xp[hs + 4 * (ks + 1) * 16];
       __builtin_amdgcn_sched_barrier(0);
       acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, s1[r], acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb, s1[r], acc[0][1], 0, 0, 0);
@@ -1291,84 +1319,107 @@ __device__ __forceinline__ void t16_diffuse(const float* img, const float* G1, c
 }
 
 // the image rows of the wave's tile as B operands in the permuted channel order of t16_mlp
-__device__ __forceinline__ void t16_rows(const float* img, int w0, int lane, f32x4v* x) {
+__device__ __forceinline__ void t16_rows(const float* img, int hs, int w0, int lane, f32x4v* x) {
   const int g = lane >> 4, j = lane & 15;
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
-    const float4 q = *(const float4*)(img + (w0 + j) * LDR16 + 16 * hf + 4 * g);
+    const float4 q = *(const float4*)(img + hf * hs + (w0 + j) * 16 + 4 * g);
     x[hf] = f32x4v{q.x, q.y, q.z, q.w};
   }
 }
 
+// Tile range of a t16 workgroup: the launch's slices x nt tiles in slice-major order, cut into
+// gridDim.x equal contiguous ranges (one workgroup per CU: every CU gets the same number of tiles,
+// whatever the slice count -- no partial last round of whole slices).  The range is worked in
+// phases of at most maximg slices: their images staged, one barrier, then wave w takes the
+// phase's tiles t with t % nwaves == w (the 16 waves of a CU spread over its 4 SIMDs evenly).
+struct T16Range {
+  long tb, te;
+};
+__device__ __forceinline__ T16Range t16_range(int slices, int nt) {
+  const long total = (long)slices * nt;
+  return {total * blockIdx.x / gridDim.x, total * (blockIdx.x + 1) / gridDim.x};
+}
+
 template <int MAXT>
-__global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(8))) void gcn_fwd_t16_kernel(const FusedFwd a,
-                                                                                                 const PowSup p) {
+__global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, const PowSup p, const int maximg) {
   extern __shared__ float lds[];
-  __shared__ int tiles_done;
   const int n = a.n;
-  const int ntiles = (n + 15) >> 4;
-  const int rows_img = t16_img_rows(n);
-  float* xs = lds;
-  float* ws = lds + rows_img * LDR16;
-  float* tpart = ws + (2 * a.nsup + 1) * CH * LDW16;
+  const int nt = (n + 15) >> 4;
+  const int rows_img = t16_img_rows(n), hs = rows_img * 16, imgf = rows_img * CH;
+  float* ws = lds;
+  float* wpart = ws + (2 * a.nsup + 1) * CH * LDW16;
+  float* imgs = wpart + T16_WAVES * 3 * CH;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int nwaves = blockDim.x >> 6;
-  const int slice = blockIdx.x;
-  const long row0 = (long)slice * n;
   const long ldh = a.ld_h;
-  float* hs = (float*)a.h + row0 * ldh;
   const int np = (n + 31) / 32 * 32;
-  const bool nt_ok = ((((uintptr_t)hs) & 15) | (ldh & 3)) == 0;
-  if (threadIdx.x == 0) tiles_done = 0;
+  const T16Range rg = t16_range(a.slices, nt);
+  BnRun bn;
+  bn.n = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bn.mean[q] = bn.m2[q] = 0.0f;
   t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
-  global_to_lds16(hs, ldh, n, rows_img, xs);
-  __syncthreads();
-  for (int tile = wave; tile < ntiles; tile += nwaves) {
-    const int w0 = 16 * tile;
-    f32x4v hacc[2];
-    hacc[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-    hacc[1] = hacc[0];
-    {  // piece 0: the node features themselves
-      f32x4v x0[2];
-      t16_rows(xs, w0, lane, x0);
-      t16_mlp(ws, LDW16, x0, lane, hacc);
-    }
-    for (int k = 0; k < a.nsup; ++k) {
-      f32x4v acc[2][2];  // [power][channel half]
-      t16_diffuse(xs, a.sup[k], p.g2[k], a.ld_sup, np, n, w0, lane, acc);
+  for (long p0 = rg.tb; p0 < rg.te;) {
+    const int s0 = (int)(p0 / nt);
+    const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
+    const int s1 = (int)((p1 - 1) / nt);
+    if (p0 != rg.tb) __syncthreads();  // the previous phase's images are released
+    for (int s = s0; s <= s1; ++s) global_to_lds16(a.h + (long)s * n * ldh, ldh, n, rows_img, imgs + (s - s0) * imgf);
+    __syncthreads();
+    for (long t = p0 + ((wave - p0 % nwaves) + nwaves) % nwaves; t < p1; t += nwaves) {
+      const int s = (int)(t / nt), tile = (int)(t - (long)s * nt);
+      const float* xs = imgs + (s - s0) * imgf;
+      const long row0 = (long)s * n;
+      float* hs_out = (float*)a.h + row0 * ldh;
+      const bool nt_ok = ((((uintptr_t)hs_out) & 15) | (ldh & 3)) == 0;
+      const int w0 = 16 * tile;
+      f32x4v hacc[2];
+      hacc[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      hacc[1] = hacc[0];
+      {  // piece 0: the node features themselves
+        f32x4v x0[2];
+        t16_rows(xs, hs, w0, lane, x0);
+        t16_mlp(ws, LDW16, x0, lane, hacc);
+      }
+      for (int k = 0; k < a.nsup; ++k) {
+        f32x4v acc[2][2];  // [power][channel half]
+        t16_diffuse(xs, hs, a.sup[k], p.g2[k], a.ld_sup, np, n, w0, lane, acc);
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        t16_mlp(ws + (1 + 2 * k + q) * CH * LDW16, LDW16, acc[q], lane, hacc);
-        if (a.store_pieces && w0 + j < n) {
-          float* dp = hs + (long)(w0 + j) * ldh + (1 + 2 * k + q) * CH + 4 * g;
+        for (int q = 0; q < 2; ++q) {
+          t16_mlp(ws + (1 + 2 * k + q) * CH * LDW16, LDW16, acc[q], lane, hacc);
+          if (a.store_pieces && w0 + j < n) {
+            float* dp = hs_out + (long)(w0 + j) * ldh + (1 + 2 * k + q) * CH + 4 * g;
 #pragma unroll
-          for (int hf = 0; hf < 2; ++hf) {
-            if (nt_ok) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
-            else {
+            for (int hf = 0; hf < 2; ++hf) {
+              if (nt_ok) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
+              else {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) dp[16 * hf + e] = acc[q][hf][e];
+                for (int e = 0; e < 4; ++e) dp[16 * hf + e] = acc[q][hf][e];
+              }
             }
           }
         }
       }
+      t16_epilogue(a, hacc, row0, w0, lane, n, bn);
     }
-    t16_epilogue(a, hacc, row0, w0, lane, n, slice, tile, ntiles, tpart, &tiles_done);
+    p0 = p1;
   }
+  t16_bn_flush(a, bn, wpart);
 }
 
 // Backward on 16-node tiles: the forward's structure with the dh image (BN-backward prologue),
 // the transposed supports A_k^T and (A_k^2)^T (so D = A dh, A^2 dh) and the channel map W^T:
 //   dxg = W_0^T dh + sum_k W_{1+2k}^T (A_k dh) + W_{2+2k}^T (A_k^2 dh)
 // (gcn_bwd_pow_kernel's schedule), t1 / t2 of the adaptive support, and the dxg store or the gate
-// backward in the epilogue.
-__device__ __forceinline__ void t16_bwd_prologue(const FusedBwd& a, float* img, long row0, int n, int rows) {
+// backward in the epilogue.  The prologue stages a whole slice's dh image; dres / dh_out rows are
+// written for the workgroup's own tiles only [r0, r1).
+__device__ __forceinline__ void t16_bwd_prologue(const FusedBwd& a, float* img, long row0, int n, int rows, int r0,
+                                                 int r1) {
+  const int hs = rows * 16;
   if (!a.bn_dy) {
     global_to_lds16(a.dh + row0 * CH, CH, n, rows, img);
     return;
-  }
-  if (blockIdx.x == 0 && threadIdx.x < CH) {
-    if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
-    if (a.bn_dgamma) a.bn_dgamma[threadIdx.x] = a.bn_sums[CH + threadIdx.x];
   }
   const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
   const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
@@ -1376,6 +1427,7 @@ __device__ __forceinline__ void t16_bwd_prologue(const FusedBwd& a, float* img, 
   const float mu = a.bn_mean[c], rs = a.bn_rstd[c], gm = a.bn_gamma[c];
   const float k1 = a.bn_sums[c] * a.inv_rows, k2 = a.bn_sums[CH + c] * a.inv_rows;
   const int total = rows * CH;
+  float* ip = img + (c >> 4) * hs + (c & 15);
   for (int e0 = threadIdx.x; e0 < total; e0 += 4 * (int)blockDim.x) {
     float dy[4], zv[4];  // all loads before the first store
 #pragma unroll
@@ -1394,15 +1446,17 @@ __device__ __forceinline__ void t16_bwd_prologue(const FusedBwd& a, float* img, 
         const long idx = (row0 + w) * CH + c;
         const float xhat = (zv[i] - mu) * rs;
         const float dz = gm * rs * (dy[i] - k1 - xhat * k2);
-        a.dres[idx] = dz;
         v = dz;
         if (a.drop_p > 0.0f) {
           const float u = gwn_uniform(seed, a.salt, (unsigned long long)idx);
           v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
         }
-        a.dh_out[idx] = v;
+        if (w >= r0 && w < r1) {
+          a.dres[idx] = dz;
+          a.dh_out[idx] = v;
+        }
       }
-      img[w * LDR16 + c] = v;
+      ip[w * 16] = v;
     }
   }
 }
@@ -1418,78 +1472,95 @@ __device__ __forceinline__ void t16_store(float* out, long ld, const f32x4v* acc
 }
 
 template <int MAXT>
-__global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(8))) void gcn_bwd_t16_kernel(const FusedBwd a,
-                                                                                                 const PowSup p) {
+__global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, const PowSup p, const int maximg) {
   extern __shared__ float lds[];
   const int n = a.n;
-  const int ntiles = (n + 15) >> 4;
-  const int rows_img = t16_img_rows(n);
-  float* dhs = lds;
-  float* ws = lds + rows_img * LDR16;
+  const int nt = (n + 15) >> 4;
+  const int rows_img = t16_img_rows(n), hs = rows_img * 16, imgf = rows_img * CH;
+  float* ws = lds;
+  float* imgs = ws + (2 * a.nsup + 1) * CH * LDW16 + T16_WAVES * 3 * CH;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int nwaves = blockDim.x >> 6;
-  const long row0 = (long)blockIdx.x * n;
   const int np = (n + 31) / 32 * 32;
+  const T16Range rg = t16_range(a.slices, nt);
+  if (a.bn_dy && blockIdx.x == 0 && threadIdx.x < CH) {
+    if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
+    if (a.bn_dgamma) a.bn_dgamma[threadIdx.x] = a.bn_sums[CH + threadIdx.x];
+  }
   t16_stage_maps(a.w_mlp, a.ld_w, true, 2 * a.nsup + 1, ws);
-  t16_bwd_prologue(a, dhs, row0, n, rows_img);
-  __syncthreads();
-  for (int tile = wave; tile < ntiles; tile += nwaves) {
-    const int w0 = 16 * tile;
-    f32x4v dx[2];
-    dx[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-    dx[1] = dx[0];
-    {
-      f32x4v d0[2];
-      t16_rows(dhs, w0, lane, d0);
-      t16_mlp(ws, LDW16, d0, lane, dx);
+  for (long p0 = rg.tb; p0 < rg.te;) {
+    const int s0 = (int)(p0 / nt);
+    const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
+    const int s1 = (int)((p1 - 1) / nt);
+    if (p0 != rg.tb) __syncthreads();
+    for (int s = s0; s <= s1; ++s) {
+      // this workgroup's rows of slice s
+      const long t0 = max(rg.tb - (long)s * nt, 0l), t1 = min(rg.te - (long)s * nt, (long)nt);
+      t16_bwd_prologue(a, imgs + (s - s0) * imgf, (long)s * n, n, rows_img, 16 * (int)t0, 16 * (int)t1);
     }
-    for (int k = 0; k < a.nsup; ++k) {
-      f32x4v e[2][2];
-      t16_diffuse(dhs, a.supT[k], p.g2[k], a.ld_sup, np, n, w0, lane, e);
-      t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, e[0], lane, dx);
-      t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[1], lane, dx);
-      if (k == a.adp_index) {  // t1 = W1^T dh + W2^T (A dh), t2 = W2^T dh
-        f32x4v d0[2], t[2];
-        t16_rows(dhs, w0, lane, d0);
-        t[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-        t[1] = t[0];
-        t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, d0, lane, t);
-        t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[0], lane, t);
-        t16_store(a.t1 + row0 * a.ld_t, a.ld_t, t, w0, lane, n);
-        t[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-        t[1] = t[0];
-        t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, d0, lane, t);
-        t16_store(a.t2 + row0 * a.ld_t, a.ld_t, t, w0, lane, n);
+    __syncthreads();
+    for (long t = p0 + ((wave - p0 % nwaves) + nwaves) % nwaves; t < p1; t += nwaves) {
+      const int s = (int)(t / nt), tile = (int)(t - (long)s * nt);
+      const float* dhs = imgs + (s - s0) * imgf;
+      const long row0 = (long)s * n;
+      const int w0 = 16 * tile;
+      f32x4v dx[2];
+      dx[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      dx[1] = dx[0];
+      {
+        f32x4v d0[2];
+        t16_rows(dhs, hs, w0, lane, d0);
+        t16_mlp(ws, LDW16, d0, lane, dx);
+      }
+      for (int k = 0; k < a.nsup; ++k) {
+        f32x4v e[2][2];
+        t16_diffuse(dhs, hs, a.supT[k], p.g2[k], a.ld_sup, np, n, w0, lane, e);
+        t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, e[0], lane, dx);
+        t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[1], lane, dx);
+        if (k == a.adp_index) {  // t1 = W1^T dh + W2^T (A dh), t2 = W2^T dh
+          f32x4v d0[2], tt[2];
+          t16_rows(dhs, hs, w0, lane, d0);
+          tt[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+          tt[1] = tt[0];
+          t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, d0, lane, tt);
+          t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[0], lane, tt);
+          t16_store(a.t1 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
+          tt[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+          tt[1] = tt[0];
+          t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, d0, lane, tt);
+          t16_store(a.t2 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
+        }
+      }
+      if (!a.dfg) {
+        t16_store(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
+        continue;
+      }
+      // gate backward (gate_bwd_kernel's arithmetic): g = dxg (+ dskip) -> dfg via (tanh f, sigmoid s)
+      const int w = w0 + j;
+      if (w >= n) continue;
+      const long m = row0 + w;
+      const bool sk = a.dskip && m >= a.skip_row0;
+#pragma unroll
+      for (int oh = 0; oh < 2; ++oh) {
+        const int c0 = 16 * oh + 4 * g;
+        const float4 f0 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0);
+        const float4 f1 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0 + 4);
+        const float4 dq = sk ? *(const float4*)(a.dskip + (m - a.skip_row0) * a.ld_dskip + c0) : make_float4(0, 0, 0, 0);
+        const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+        const float dv[4] = {dq.x, dq.y, dq.z, dq.w};
+        float o[8];
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          const float gv = dx[oh][e2] + dv[e2];
+          const float f = fv[2 * e2], sg = fv[2 * e2 + 1];
+          o[2 * e2] = gv * sg * (1.0f - f * f);
+          o[2 * e2 + 1] = gv * f * sg * (1.0f - sg);
+        }
+        *(float4*)(a.dfg + m * 2 * CH + 2 * c0) = make_float4(o[0], o[1], o[2], o[3]);
+        *(float4*)(a.dfg + m * 2 * CH + 2 * c0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
       }
     }
-    if (!a.dfg) {
-      t16_store(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
-      continue;
-    }
-    // gate backward (gate_bwd_kernel's arithmetic): g = dxg (+ dskip) -> dfg via (tanh f, sigmoid s)
-    const int w = w0 + j;
-    if (w >= n) continue;
-    const long m = row0 + w;
-    const bool sk = a.dskip && m >= a.skip_row0;
-#pragma unroll
-    for (int oh = 0; oh < 2; ++oh) {
-      const int c0 = 16 * oh + 4 * g;
-      const float4 f0 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0);
-      const float4 f1 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0 + 4);
-      const float4 dq = sk ? *(const float4*)(a.dskip + (m - a.skip_row0) * a.ld_dskip + c0) : make_float4(0, 0, 0, 0);
-      const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-      const float dv[4] = {dq.x, dq.y, dq.z, dq.w};
-      float o[8];
-#pragma unroll
-      for (int e2 = 0; e2 < 4; ++e2) {
-        const float gv = dx[oh][e2] + dv[e2];
-        const float f = fv[2 * e2], sg = fv[2 * e2 + 1];
-        o[2 * e2] = gv * sg * (1.0f - f * f);
-        o[2 * e2 + 1] = gv * f * sg * (1.0f - sg);
-      }
-      *(float4*)(a.dfg + m * 2 * CH + 2 * c0) = make_float4(o[0], o[1], o[2], o[3]);
-      *(float4*)(a.dfg + m * 2 * CH + 2 * c0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
-    }
+    p0 = p1;
   }
 }
 
@@ -1712,13 +1783,67 @@ bool gwn_gcn_split_eligible(int c, int n, int planes);
 int gwn_gcn_split_fwd_launch(const gwn_gcn_args* g, const FusedFwd& a, hipStream_t s);
 int gwn_gcn_bf16_bwd_launch(const gwn_gcn_bwd_args* g, const FusedBwd& a, hipStream_t s);
 
-// the 16-node tile forward (GWN_GCN_T16=0 selects the 32-node tile power kernel)
-constexpr int T16_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS of a t16 workgroup (static: a counter)
+// the 16-node tile kernels (GWN_GCN_T16=0 selects the 32-node tile power kernels)
+constexpr int T16_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS of a t16 workgroup
 
 static bool t16_enabled() {
   const char* e = getenv("GWN_GCN_T16");  // read per launch (tests switch it within one process)
   return !(e && e[0] == '0');
 }
+
+int gwn_device_cus() {
+  static int v = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    return cus;
+  }();
+  return v;
+}
+
+long gwn_bn_part_slots(int slices) { return slices > gwn_device_cus() ? slices : gwn_device_cus(); }
+
+namespace {
+
+// Launch plan of the t16 kernels: one 16-wave workgroup per CU (at most one per tile), each over an
+// equal contiguous range of the launch's tiles; the LDS holds the channel maps, the waves' BN
+// partials and maximg slice images (as many as a range can touch, at most T16_MAXIMG and what
+// fits), and never less than half a CU's LDS so that no two of them share a CU.
+struct T16Plan {
+  bool ok;
+  int grid, maximg;
+  size_t lds;
+};
+T16Plan t16_plan(int n, int nsup, int slices) {
+  T16Plan pl{false, 0, 0, 0};
+  const size_t fixed = t16_lds_bytes(n, nsup, 0), img = t16_lds_bytes(n, nsup, 1) - fixed;
+  if (fixed + img > (size_t)T16_LDS_MAX || slices <= 0) return pl;
+  const int nt = (n + 15) / 16;
+  const long tiles = (long)slices * nt;
+  pl.grid = (int)(tiles < gwn_device_cus() ? tiles : gwn_device_cus());
+  const long per = (tiles + pl.grid - 1) / pl.grid;
+  const int span = (int)((per - 1 + nt - 1) / nt) + 1;  // slices a range of `per` tiles can touch
+  int maximg = (int)((T16_LDS_MAX - fixed) / img);
+  maximg = maximg < T16_MAXIMG ? maximg : T16_MAXIMG;
+  pl.maximg = maximg < span ? maximg : span;
+  pl.lds = fixed + pl.maximg * img;
+  if (pl.lds < 81 * 1024) pl.lds = 81 * 1024;
+  pl.ok = true;
+  return pl;
+}
+
+// zero the BN partial slots [written, gwn_bn_part_slots(slices)) that a whole-slice kernel leaves
+int bn_part_tail(float* bn_part, int slices, int c, hipStream_t s) {
+  const long slots = gwn_bn_part_slots(slices);
+  if (!bn_part || slots <= slices) return GWN_OK;
+  return hipMemsetAsync(bn_part + (long)slices * 3 * c, 0, (size_t)(slots - slices) * 3 * c * sizeof(float), s) ==
+                 hipSuccess
+             ? GWN_OK
+             : gwn_set_error(GWN_ERR_HIP, "gcn_fwd: BN partial tail memset failed");
+}
+
+}  // namespace
 
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
   const int nwt = (g->n + 31) / 32;
@@ -1737,7 +1862,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.bn_eps = g->bn_eps; a.x_out = g->bn_out;
   a.sup_bstride = g->sup_bstride; a.sup_batch = g->sup_batch;
   a.res_mean = g->residual_mean; a.res_scale = g->residual_scale; a.res_shift = g->residual_shift;
-  a.ksplit = 1; a.slices = g->rows / g->n; a.kws = g->ksplit_ws; a.kcnt = g->ksplit_count;
+  a.ksplit = 1; a.slices = g->rows / g->n; a.kws = g->ksplit_ws; a.kcnt = g->ksplit_count; a.bn_slots = 0;
   GWN_REQUIRE(g->ksplit == 0 || g->ksplit == 1 || g->ksplit == g->nsup, "gcn_fwd: ksplit must be 0, 1 or nsup");
   GWN_REQUIRE(!a.res_scale == !a.res_shift && !a.res_scale == !a.res_mean,
               "gcn_fwd (fused): residual_mean, residual_scale and residual_shift go together");
@@ -1752,7 +1877,8 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   if (g->split_planes) {
     GWN_REQUIRE(gwn_gcn_split_eligible(g->c, g->n, g->split_planes) && g->sup_split && g->w_split && g->nsup > 0,
                 "gcn_fwd (split): needs c == 32, an instantiated node-tile count, split supports and weights");
-    return gwn_gcn_split_fwd_launch(g, a, s);
+    const int rc = gwn_gcn_split_fwd_launch(g, a, s);
+    return rc ? rc : bn_part_tail(a.x_out ? nullptr : bn_part, g->rows / g->n, CH, s);
   }
   static bool attr_set = false;
   if (!attr_set) {
@@ -1773,11 +1899,14 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
     GWN_REQUIRE(g->w_mlp_t, "gcn_fwd (power schedule): w_mlp_t (the transposed mlp weights) is required with sup2");
     PowSup p;
     for (int k = 0; k < 8; ++k) p.g2[k] = (k < g->nsup) ? g->sup2[k] : nullptr;
-    if (a.ksplit <= 1 && g->layout == 0 && t16_enabled() && t16_lds_bytes(g->n, g->nsup) <= T16_LDS_MAX) {
-      // 16-node tile waves (one per tile up to 16, then two tiles per wave)
-      const int nt16 = (g->n + 15) / 16;
-      const int waves = nt16 <= 16 ? nt16 : (nt16 + 1) / 2;
-      gcn_fwd_t16_kernel<1024><<<grid, 64 * waves, t16_lds_bytes(g->n, g->nsup), s>>>(a, p);
+    const T16Plan pl = t16_plan(g->n, g->nsup, slices);
+    // (the t16 ranges already cut small launches finely: the support split runs only when forced)
+    if ((a.ksplit <= 1 || g->ksplit != g->nsup) && g->layout == 0 && t16_enabled() && pl.ok) {
+      a.ksplit = 1;
+      // 16-node tile waves, one workgroup per CU over an equal tile range; it writes every BN
+      // partial slot (gwn_bn_part_slots)
+      a.bn_slots = (int)gwn_bn_part_slots(slices);
+      gcn_fwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
       GWN_CHECK_LAUNCH();
       return GWN_OK;
     }
@@ -1798,7 +1927,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
     }
   }
   GWN_CHECK_LAUNCH();
-  return GWN_OK;
+  return bn_part_tail(a.x_out ? nullptr : bn_part, slices, CH, s);
 }
 
 int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT, float* dxg, long ld_dxg,
@@ -1851,10 +1980,10 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   if (g->sup2_t && a.sup_batch <= 1 && g->nsup > 0) {
     PowSup p;
     for (int k = 0; k < 8; ++k) p.g2[k] = (k < g->nsup) ? g->sup2_t[k] : nullptr;
-    if (a.ksplit <= 1 && g->layout == 0 && t16_enabled() && t16_lds_bytes(g->n, g->nsup) <= T16_LDS_MAX) {
-      const int nt16 = (g->n + 15) / 16;
-      const int waves = nt16 <= 16 ? nt16 : (nt16 + 1) / 2;
-      gcn_bwd_t16_kernel<1024><<<grid, 64 * waves, t16_lds_bytes(g->n, g->nsup), s>>>(a, p);
+    const T16Plan pl = t16_plan(g->n, g->nsup, slices);
+    if ((a.ksplit <= 1 || g->ksplit != g->nsup) && g->layout == 0 && t16_enabled() && pl.ok) {
+      a.ksplit = 1;
+      gcn_bwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
       GWN_CHECK_LAUNCH();
       return GWN_OK;
     }
@@ -1899,7 +2028,7 @@ extern "C" int gwn_fused_occupancy(int n, int backward, int pow) {
 extern "C" long gwn_gcn_bn_partial_count(int rows, int n, int c, int nsup, int ld_sup) {
   (void)c; (void)nsup; (void)ld_sup;
   if (rows <= 0 || n <= 0 || rows % n) return 0;
-  return rows / n;  // one per slice on every path (the power forward merges its tiles in-kernel)
+  return gwn_bn_part_slots(rows / n);  // max(slices, CUs): every path writes all of them
 }
 
 extern "C" int gwn_support_square(const float* a, int np, int ld, float* a2, float* a2_t, float* a_t, hipStream_t s) {

@@ -1204,6 +1204,10 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   GWN_REQUIRE(co <= 256 && 256 % co == 0, "gcn_fwd: BN partials need c_out | 256");
   bn_partial_kernel<<<slices, 256, 0, s>>>(a->z, a->rows, co, a->bn_partials);  // one chunk per slice
   GWN_CHECK_LAUNCH();
+  const long slots = gwn_bn_part_slots(slices);  // the slots past the slices hold no rows
+  if (slots > slices && hipMemsetAsync(a->bn_partials + (long)slices * 3 * co, 0,
+                                       (size_t)(slots - slices) * 3 * co * sizeof(float), s) != hipSuccess)
+    return gwn_set_error(GWN_ERR_HIP, "gcn_fwd: BN partial tail memset failed");
   return GWN_OK;
 }
 

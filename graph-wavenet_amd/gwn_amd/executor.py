@@ -402,7 +402,8 @@ class Executor:
             "dadp": torch.zeros(cfg.NP, cfg.NP, device=self.device, dtype=F32),
             "metrics": e(4),
             "bnsums": e(2 * C),  # BN-backward statistics handed from a layer's TCN backward to the next
-            "bnpart": e(ts[0] * B * 3 * C),  # per-slice BN partials of one layer
+            # BN partials of one layer: gwn_gcn_bn_partial_count slots (>= one per slice)
+            "bnpart": e(self._bn_parts(ts[0] * B * N) * 3 * C),
         }
         lib = _lib.load()
         need = [
@@ -932,11 +933,11 @@ class Executor:
                                      sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
                                      if acts.supT_arr is not None else None,
                                      skip_weight_grads=1 if (overlap or defer) else 0,
-                                     # the power-schedule backward measured slower than the
-                                     # chained one (131.5 vs 125.8 us per launch, 19,263 vs 19,517
-                                     # samples/s): GWN_GCN_POW_BWD=1 selects it
+                                     # power-schedule backward (the persistent 16-node tile
+                                     # kernel: 750 vs 863 us per step for the chained one, 21.3k
+                                     # vs 20.5k samples/s); GWN_GCN_POW_BWD=0 selects the chain
                                      sup2_t=self._arr_field(getattr(acts, "sup2t_arr", None))
-                                     if os.environ.get("GWN_GCN_POW_BWD", "0") != "0" else None,
+                                     if os.environ.get("GWN_GCN_POW_BWD", "1") != "0" else None,
                                      **self.ksplit_fields(sc))
                 sb = getattr(acts, "sup_batch", 1)
                 if sb > 1:

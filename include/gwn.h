@@ -254,8 +254,9 @@ typedef struct gwn_gcn_args {
    * eval BatchNorm (model.py:236 with the module in eval mode) folded into the epilogue: with
    *   bn_out != NULL, bn_out[r][j] = (z - running_mean[j]) / sqrt(running_var[j] + bn_eps) *
    *   weight[j] + bias[j] is written instead of z (z may be NULL, bn_partials must be NULL).
-   * layout: wave layout of the fused kernels, 0 or 1: one wave per 32-node tile (the only layout
-   *   built; other values are rejected). */
+   * layout: wave layout of the fused kernels: 0 = the persistent 16-node tile kernels where they
+   *   apply (sup2 given, shared supports; GWN_GCN_T16=0 disables them), else one wave per 32-node
+   *   tile; 1 = one wave per 32-node tile always.  Other values are rejected. */
   int no_pieces;
   const float* bn_running_mean; const float* bn_running_var; const float* bn_weight; const float* bn_bias;
   float bn_eps; float* bn_out;
@@ -284,7 +285,8 @@ typedef struct gwn_gcn_args {
    * a device counter that is zero on entry and left zero) adds them in support order and runs the
    * epilogue.  Finer work units for layers with too few slices to occupy the chip (a unit costs
    * about half a slice, so auto splits only when slices * nsup <= CUs; GWN_KSPLIT_SLICES = a slice
-   * threshold overrides).  ksplit: 0 = auto,
+   * threshold overrides; with sup2 given the persistent 16-node tile kernels, which already cut
+   * every launch into equal per-CU tile ranges, take precedence over the auto split).  ksplit: 0 = auto,
    * 1 = off, nsup = always.  ksplit_ws: gwn_gcn_ksplit_ws_floats(rows, n, nsup) floats,
    * ksplit_count: rows / n ints; NULL = no split. */
   int ksplit; float* ksplit_ws; int* ksplit_count;
@@ -308,9 +310,11 @@ typedef struct gwn_gcn_args {
  * must be [np][ld_sup] and ZERO outside [n][n] (gwn_pad_square makes such copies).
  * Otherwise: 2K nconv GEMMs + one mlp GEMM. */
 int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t stream);
-/* number of BatchNorm partial slots gwn_gcn_fwd writes to bn_partials ([slots][3][c]): one per
- * slice, rows/n (the power forward reduces each wave's tile in registers and merges the tiles of a
- * slice in-kernel).  The consumer (gwn_batchnorm_fwd_fold / _partials) takes this as nparts. */
+/* number of BatchNorm partial slots gwn_gcn_fwd writes to bn_partials ([slots][3][c]):
+ * max(rows/n, CUs of the device).  Every path writes all of them (slots that hold no rows get
+ * count 0): the whole-slice kernels one per slice, the persistent 16-node tile kernels one per
+ * workgroup (one workgroup per CU, each over an equal tile range).  The consumer
+ * (gwn_batchnorm_fwd_fold / _partials) takes this as nparts. */
 long gwn_gcn_bn_partial_count(int rows, int n, int c, int nsup, int ld_sup);
 
 /* bf16 piece planes for the split path of gwn_gcn_fwd.

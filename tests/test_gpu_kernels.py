@@ -474,6 +474,13 @@ def _merge_bn(bnp, S, nkb, C):
     return torch.stack([n, mean, m2], dim=1)
 
 
+def _bn_all(bnp, rows, n, C, K, NP):
+    """(count, mean, M2) [1][3][C] of all rows from the gwn_gcn_bn_partial_count slots gwn_gcn_fwd
+    writes (per slice or per workgroup tile range, by kernel; count-0 slots carry nothing)."""
+    from gwn_amd import _lib
+    return _merge_bn(bnp, 1, int(_lib.load().gwn_gcn_bn_partial_count(rows, n, C, K, NP)), C)
+
+
 def _squares(gpu, sups, transposes=False):
     """gwn_support_square of each padded support: (A^2, (A^2)^T[, A^T])."""
     from gwn_amd import _lib
@@ -551,7 +558,7 @@ def test_gcn_fused_schedules_agree(gpu, n, monkeypatch):
         h = torch.zeros(rows, W, device=gpu)
         h[:, :C] = xg
         z = torch.empty(rows, C, device=gpu)
-        bnp = torch.full((S * (NP // 32) * 3 * C,), float("nan"), device=gpu)
+        bnp = torch.full((_lib.load().gwn_gcn_bn_partial_count(rows, n, C, K, NP) * 3 * C,), float("nan"), device=gpu)
         ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, P),
                           ld_sup=NP, h=h.data_ptr(), ld_h=W, w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(),
                           residual=res.data_ptr(), z=z.data_ptr(), seed_ptr=seed.data_ptr(), salt=0, drop_p=0.0,
@@ -565,7 +572,7 @@ def test_gcn_fused_schedules_agree(gpu, n, monkeypatch):
                              sup2_t=ctypes.cast(arr2T, P) if pw else None, **kf)
         _lib.call("gwn_gcn_bwd", ctypes.byref(gb), _lib.stream())
         torch.cuda.synchronize()
-        outs.append((h.clone(), z.clone(), _merge_bn(bnp, S, 1, C), dhc.clone()))
+        outs.append((h.clone(), z.clone(), _bn_all(bnp, rows, n, C, K, NP), dhc.clone()))
         assert int(kcnt.abs().sum()) == 0  # the split leaves its counters zero
     # fp64 truth
     X = xg.double().cpu().view(S, n, C)
@@ -593,9 +600,9 @@ def test_gcn_fused_schedules_agree(gpu, n, monkeypatch):
         assert rel_err(dhc[:, :C].cpu().numpy(), dxg.reshape(rows, C).numpy()) <= 4e-6
         assert rel_err(dhc[:, C:2 * C].cpu().numpy(), t1.reshape(rows, C).numpy()) <= 4e-6
         assert rel_err(dhc[:, 2 * C:3 * C].cpu().numpy(), t2.reshape(rows, C).numpy()) <= 4e-6
-        assert torch.all(st[:, 0] == n)
-        assert rel_err(st[:, 1].numpy(), Z.view(S, n, C).mean(1).numpy()) <= 1e-5
-        m2 = ((Z.view(S, n, C) - Z.view(S, n, C).mean(1, keepdim=True)) ** 2).sum(1)
+        assert torch.all(st[:, 0] == rows)
+        assert rel_err(st[:, 1].numpy(), Z.mean(0, keepdim=True).numpy()) <= 1e-5
+        m2 = ((Z - Z.mean(0, keepdim=True)) ** 2).sum(0, keepdim=True)
         assert rel_err(st[:, 2].numpy(), m2.numpy()) <= 1e-5
     # the split against the whole slice, per schedule: the same products, summed in another order
     for a_i, b_i in ((0, 1), (2, 3)):
@@ -650,7 +657,7 @@ def test_gcn_split_many_slices_bn_prologue_gate_epilogue(gpu, pw):
         h = torch.zeros(rows, W, device=gpu)
         h[:, :C] = xg
         z = torch.empty(rows, C, device=gpu)
-        bnp = torch.full((S * (NP // 32) * 3 * C,), float("nan"), device=gpu)
+        bnp = torch.full((_lib.load().gwn_gcn_bn_partial_count(rows, n, C, K, NP) * 3 * C,), float("nan"), device=gpu)
         ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, P), ld_sup=NP, h=h.data_ptr(), ld_h=W,
                           w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(), residual=res.data_ptr(), z=z.data_ptr(),
                           seed_ptr=seed.data_ptr(), salt=2, drop_p=0.3, bn_partials=bnp.data_ptr(),
@@ -674,7 +681,7 @@ def test_gcn_split_many_slices_bn_prologue_gate_epilogue(gpu, pw):
         _lib.call("gwn_gcn_bwd", ctypes.byref(gb), _lib.stream())
         torch.cuda.synchronize()
         assert int(kcnt.abs().sum()) == 0
-        outs.append((h.clone(), z.clone(), _merge_bn(bnp, S, 1, C), dres.clone(), dh_out.clone(), dfg.clone(),
+        outs.append((h.clone(), z.clone(), _bn_all(bnp, rows, n, C, K, NP), dres.clone(), dh_out.clone(), dfg.clone(),
                      dhc[:, C:3 * C].clone(), dg.clone(), db.clone()))
     for a_, b_ in zip(*outs):
         assert rel_err(b_.cpu().numpy(), a_.cpu().numpy()) <= 2e-6
@@ -716,7 +723,7 @@ def test_gcn_pow_forward_modes(gpu, n):
         h = torch.zeros(rows, W, device=gpu)
         h[:, :C] = xg
         z = torch.full((rows, C), 7.0, device=gpu)
-        bnp = torch.empty(S * (NP // 32) * 3 * C, device=gpu)
+        bnp = torch.empty(_lib.load().gwn_gcn_bn_partial_count(rows, n, C, K, NP) * 3 * C, device=gpu)
         kw = {}
         if eval_bn is not None:
             rm, rv, g_, b_, xo = eval_bn
