@@ -952,7 +952,8 @@ __device__ __forceinline__ void fwd_tile_epilogue(const FusedFwd& a, const f32x1
 }
 
 struct PowSup {
-  const float* g2[8];  // forward: A_k^2; backward: (A_k^2)^T
+  const float* g2[8];   // forward: A_k^2; backward: (A_k^2)^T
+  const float* g4[16];  // t16 kernels: [2k] A_k, [2k + 1] A_k^2 (backward: transposed) in gwn_support_g4's layout
 };
 
 // Forward: h pieces 1 + 2k, 2 + 2k = A_k^T-diffused xg and (A_k^2)^T-diffused xg (the reference's
@@ -1275,47 +1276,56 @@ __device__ __forceinline__ void t16_mlp(const float* m, int ld_m, const f32x4v* 
 
 // both powers of one support for the wave's 16-node tile: acc[q][hf] (q = 0: G1, 1: G2) holds
 // D[16 hf + 4 g + r][w0 + j] = sum_v img[v][16 hf + 4 g + r] G_q[v][w0 + j]
-__device__ __forceinline__ void t16_diffuse(const float* img, int hs, const float* G1, const float* G2, int ld_sup,
-                                            int np, int n, int w0, int lane, f32x4v (*acc)[2]) {
+// The supports come in gwn_support_g4's k-interleaved layout: one 16-B load per lane fetches the
+// fragments of four k-steps (a wave's load is one contiguous KiB).  Per-k-step 4-B fragment loads
+// of the padded [np][ld] supports held the MFMA pipes at ~0.70 busy in the isolated loop
+// (tools/t16_loop_probe.hip, 16 waves per CU: L1 / address processing per load instruction),
+// these at 0.93.  Fragments run one group (4 k-steps) ahead: the group's load pair is issued
+// before the previous group's products, so every wait is vmcnt(2).
+__device__ __forceinline__ void t16_diffuse(const float* img, int hs, const float* G1, const float* G2, int n, int tile,
+                                            int lane, f32x4v (*acc)[2]) {
   const int g = lane >> 4, j = lane & 15;
-  const int nk = (n + 3) >> 2;
-  const int nkp = (nk + T16_RING - 1) / T16_RING * T16_RING;
-  const __amdgpu_buffer_rsrc_t r1 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)G1, (short)0, (int)((long)np * ld_sup * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t r2 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)G2, (short)0, (int)((long)np * ld_sup * 4), 0x00020000);
-  // support fragment of k-step ks: G[4 ks + g][w0 + j] (rows >= np out of range: zero)
-  auto off = [&](int ks) { return (int)(((long)(4 * ks + g) * ld_sup + w0 + j) * 4); };
-  float s1[T16_RING], s2[T16_RING];
-#pragma unroll
-  for (int r = 0; r < T16_RING - 1; ++r) {
-    s1[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, off(r), 0, 0));
-    s2[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, off(r), 0, 0));
-  }
+  const int nt = (n + 15) >> 4, nkg = nt;  // k-groups of 16 rows: ceil(n / 16), as the column tiles
+  const int bytes = nkg * nt * 1024;
+  const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc((void*)G1, (short)0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc((void*)G2, (short)0, bytes, 0x00020000);
+  // group kg of this tile: 1 KiB block kg * nt + tile, lane l's 16 B (k-steps 4 kg .. 4 kg + 3)
+  auto off = [&](int kg) { return ((kg * nt + tile) * 64 + lane) * 16; };
+  f32x4v a1[2], a2[2];
+  a1[0] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r1, off(0), 0, 0));
+  a2[0] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r2, off(0), 0, 0));
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int q = 0; q < 2; ++q) acc[q][0] = acc[q][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
   const float* xp = img + g * 16 + j;
   // image operands one k-step ahead: the LDS latency hides behind the current step's products
   float xa = xp[0], xb = xp[hs];
-  for (int ks0 = 0; ks0 < nkp; ks0 += T16_RING) {
+  // group kg (fragments in buffer kg & 1); the next group's pair is requested first (past the
+  // last group the offsets leave the buffer range: zeros, no traffic)
+  auto group = [&](int kg, int bsel) {
+    a1[bsel ^ 1] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r1, off(kg + 1), 0, 0));
+    a2[bsel ^ 1] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r2, off(kg + 1), 0, 0));
 #pragma unroll
-    for (int r = 0; r < T16_RING; ++r) {
-      const int ks = ks0 + r;
-      const int nx = (r + T16_RING - 1) % T16_RING;
-      s1[nx] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, off(ks + T16_RING - 1), 0, 0));
-      s2[nx] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, off(ks + T16_RING - 1), 0, 0));
+    for (int i = 0; i < 4; ++i) {
+      const int ks = 4 * kg + i;
       // the image has 4 * nkp + 4 rows (t16_img_rows): step nkp's read stays inside
       const float na = xp[4 * (ks + 1) * 16], nb = xp[hs + 4 * (ks + 1) * 16];
       __builtin_amdgcn_sched_barrier(0);
-      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, s1[r], acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb, s1[r], acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, s2[r], acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb, s2[r], acc[1][1], 0, 0, 0);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, a1[bsel][i], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb, a1[bsel][i], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, a2[bsel][i], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb, a2[bsel][i], acc[1][1], 0, 0, 0);
       xa = na;
       xb = nb;
       __builtin_amdgcn_sched_barrier(0);
     }
+  };
+  int kg = 0;
+  for (; kg + 2 <= nkg; kg += 2) {
+    group(kg, 0);
+    group(kg + 1, 1);
   }
+  if (kg < nkg) group(kg, 0);
 }
 
 // the image rows of the wave's tile as B operands in the permuted channel order of t16_mlp
@@ -1353,7 +1363,6 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int nwaves = blockDim.x >> 6;
   const long ldh = a.ld_h;
-  const int np = (n + 31) / 32 * 32;
   const T16Range rg = t16_range(a.slices, nt);
   BnRun bn;
   bn.n = 0.0f;
@@ -1384,7 +1393,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
       }
       for (int k = 0; k < a.nsup; ++k) {
         f32x4v acc[2][2];  // [power][channel half]
-        t16_diffuse(xs, hs, a.sup[k], p.g2[k], a.ld_sup, np, n, w0, lane, acc);
+        t16_diffuse(xs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, acc);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           t16_mlp(ws + (1 + 2 * k + q) * CH * LDW16, LDW16, acc[q], lane, hacc);
@@ -1481,7 +1490,6 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
   float* imgs = ws + (2 * a.nsup + 1) * CH * LDW16 + T16_WAVES * 3 * CH;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int nwaves = blockDim.x >> 6;
-  const int np = (n + 31) / 32 * 32;
   const T16Range rg = t16_range(a.slices, nt);
   if (a.bn_dy && blockIdx.x == 0 && threadIdx.x < CH) {
     if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
@@ -1514,7 +1522,7 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
       }
       for (int k = 0; k < a.nsup; ++k) {
         f32x4v e[2][2];
-        t16_diffuse(dhs, hs, a.supT[k], p.g2[k], a.ld_sup, np, n, w0, lane, e);
+        t16_diffuse(dhs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, e);
         t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, e[0], lane, dx);
         t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[1], lane, dx);
         if (k == a.adp_index) {  // t1 = W1^T dh + W2^T (A dh), t2 = W2^T dh
@@ -1895,21 +1903,25 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   const int slices = g->rows / g->n;
   a.ksplit = pick_ksplit(g, slices, nwt);
   const int grid = a.ksplit > 1 ? (slices + 7) / 8 * 8 * a.ksplit : slices;
+  const T16Plan pl = t16_plan(g->n, g->nsup, slices);
+  // (the t16 ranges already cut small launches finely: the support split runs only when forced)
+  if (g->sup_g4 && a.sup_batch <= 1 && g->nsup > 0 && (a.ksplit <= 1 || g->ksplit != g->nsup) && g->layout == 0 &&
+      t16_enabled() && pl.ok) {
+    GWN_REQUIRE(g->w_mlp_t, "gcn_fwd (16-node tiles): w_mlp_t (the transposed mlp weights) is required with sup_g4");
+    PowSup p = {};
+    for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = g->sup_g4[k];
+    a.ksplit = 1;
+    // 16-node tile waves, one workgroup per CU over an equal tile range; it writes every BN
+    // partial slot (gwn_bn_part_slots)
+    a.bn_slots = (int)gwn_bn_part_slots(slices);
+    gcn_fwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
+    GWN_CHECK_LAUNCH();
+    return GWN_OK;
+  }
   if (g->sup2 && a.sup_batch <= 1 && g->nsup > 0) {
     GWN_REQUIRE(g->w_mlp_t, "gcn_fwd (power schedule): w_mlp_t (the transposed mlp weights) is required with sup2");
-    PowSup p;
+    PowSup p = {};
     for (int k = 0; k < 8; ++k) p.g2[k] = (k < g->nsup) ? g->sup2[k] : nullptr;
-    const T16Plan pl = t16_plan(g->n, g->nsup, slices);
-    // (the t16 ranges already cut small launches finely: the support split runs only when forced)
-    if ((a.ksplit <= 1 || g->ksplit != g->nsup) && g->layout == 0 && t16_enabled() && pl.ok) {
-      a.ksplit = 1;
-      // 16-node tile waves, one workgroup per CU over an equal tile range; it writes every BN
-      // partial slot (gwn_bn_part_slots)
-      a.bn_slots = (int)gwn_bn_part_slots(slices);
-      gcn_fwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
-      GWN_CHECK_LAUNCH();
-      return GWN_OK;
-    }
     const size_t lds = pow_lds_bytes(g->n);
     if (nwt <= 8) gcn_fwd_pow_kernel<512><<<grid, 64 * nwt, lds, s>>>(a, p);
     else gcn_fwd_pow_kernel<1024><<<grid, 64 * nwt, lds, s>>>(a, p);
@@ -1977,16 +1989,19 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   const int slices = g->rows / g->n;
   a.ksplit = pick_ksplit(g, slices, nwt);
   const int grid = a.ksplit > 1 ? (slices + 7) / 8 * 8 * a.ksplit : slices;
+  const T16Plan pl = t16_plan(g->n, g->nsup, slices);
+  if (g->sup_g4_t && a.sup_batch <= 1 && g->nsup > 0 && (a.ksplit <= 1 || g->ksplit != g->nsup) && g->layout == 0 &&
+      t16_enabled() && pl.ok) {
+    PowSup p = {};
+    for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = g->sup_g4_t[k];
+    a.ksplit = 1;
+    gcn_bwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
+    GWN_CHECK_LAUNCH();
+    return GWN_OK;
+  }
   if (g->sup2_t && a.sup_batch <= 1 && g->nsup > 0) {
-    PowSup p;
+    PowSup p = {};
     for (int k = 0; k < 8; ++k) p.g2[k] = (k < g->nsup) ? g->sup2_t[k] : nullptr;
-    const T16Plan pl = t16_plan(g->n, g->nsup, slices);
-    if ((a.ksplit <= 1 || g->ksplit != g->nsup) && g->layout == 0 && t16_enabled() && pl.ok) {
-      a.ksplit = 1;
-      gcn_bwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
-      GWN_CHECK_LAUNCH();
-      return GWN_OK;
-    }
     const size_t lds = pow_lds_bytes(g->n);
     if (nwt <= 8) gcn_bwd_pow_kernel<512><<<grid, 64 * nwt, lds, s>>>(a, p);
     else gcn_bwd_pow_kernel<1024><<<grid, 64 * nwt, lds, s>>>(a, p);
@@ -2035,6 +2050,38 @@ extern "C" int gwn_support_square(const float* a, int np, int ld, float* a2, flo
   GWN_REQUIRE(a && a2 && a2_t && np > 0 && np % 32 == 0 && ld >= np, "support_square: np must be a multiple of 32");
   dim3 grid(np / 32, np / 32);
   support_square_kernel<<<grid, 256, 0, s>>>(a, np, ld, a2, a2_t, a_t);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+namespace {
+struct G4Src {
+  const float* src[32];
+};
+// one 256-thread block per (1-KiB block = (k-group, tile), copy): thread e writes float e of the block
+__global__ __launch_bounds__(256) void support_g4_kernel(G4Src gs, int nt, int ld, float* dst, long dst_stride) {
+  const int blk = blockIdx.x, c = blockIdx.y;
+  const int kg = blk / nt, t = blk - kg * nt;
+  const int e = threadIdx.x, lane = e >> 2, i = e & 3, g = lane >> 4, j = lane & 15;
+  dst[(long)c * dst_stride + (long)blk * 256 + e] = gs.src[c][(long)(16 * kg + 4 * i + g) * ld + 16 * t + j];
+}
+}  // namespace
+
+extern "C" long gwn_support_g4_floats(int n) {
+  const long nt = (n + 15) / 16;
+  return n > 0 ? nt * nt * 256 : 0;
+}
+
+extern "C" int gwn_support_g4(const float* const* src, int count, int n, int ld, float* dst, long dst_stride,
+                              hipStream_t s) {
+  GWN_REQUIRE(src && dst && n > 0 && count > 0 && count <= 32 && ld >= (n + 31) / 32 * 32 &&
+                  dst_stride >= gwn_support_g4_floats(n),
+              "support_g4: needs 1..32 padded [np][ld] supports (ld >= 32*ceil(n/32)) and dst_stride >= "
+              "gwn_support_g4_floats(n)");
+  G4Src gs = {};
+  for (int c = 0; c < count; ++c) gs.src[c] = src[c];
+  const int nt = (n + 15) / 16;
+  support_g4_kernel<<<dim3(nt * nt, count), 256, 0, s>>>(gs, nt, ld, dst, dst_stride);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

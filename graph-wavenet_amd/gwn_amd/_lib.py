@@ -92,6 +92,7 @@ class GcnArgs(ctypes.Structure):
         ("sup2", ctypes.POINTER(c_void_p)),
         ("w_mlp_t", c_void_p),
         ("c_out", c_int),
+        ("sup_g4", ctypes.POINTER(c_void_p)),
     ]
 
 
@@ -131,6 +132,7 @@ class GcnBwdArgs(ctypes.Structure):
         ("ksplit", c_int), ("ksplit_ws", c_void_p), ("ksplit_count", c_void_p),
         ("sup2_t", ctypes.POINTER(c_void_p)),
         ("c_out", c_int),
+        ("sup_g4_t", ctypes.POINTER(c_void_p)),
     ]
 
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time
@@ -207,6 +209,8 @@ _SIGS = [
                                        c_void_p, c_void_p, c_void_p]),
     ("gwn_fused_occupancy", c_int, [c_int, c_int, c_int]),
     ("gwn_support_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("gwn_support_g4_floats", c_long, [c_int]),
+    ("gwn_support_g4", c_int, [ctypes.POINTER(c_void_p), c_int, c_int, c_int, c_void_p, c_long, c_void_p]),
     ("gwn_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     ("gwn_pad_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
     ("gwn_pad_square_batched", c_int, [c_void_p, c_int, c_long, c_int, c_int, c_void_p, c_int, c_int, c_long, c_int,

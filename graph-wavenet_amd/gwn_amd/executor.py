@@ -516,10 +516,12 @@ class Executor:
         # power schedule of the fused gcn kernels: squared supports (and their transposes); the
         # adaptive one's square launch also writes its transpose for the backward
         pw = self._pow_ok(sup_batch)
-        acts.sup2_arr = acts.sup2t_arr = None
+        acts.sup2_arr = acts.sup2t_arr = acts.g4f_arr = acts.g4b_arr = None
         adp_t_done = False
         if pw:
-            sq2, sq2t = self._fixed_squares(fixed_sups)
+            sq2, sq2t, g4f, g4b = self._fixed_squares(fixed_sups)
+            g4f_p = [t_.data_ptr() for t_ in g4f] if g4f is not None else []
+            g4b_p = [t_.data_ptr() for t_ in g4b] if g4b is not None else []
             if cfg.adp_params:
                 if getattr(acts, "adp2", None) is None:
                     acts.adp2 = torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32)
@@ -532,8 +534,20 @@ class Executor:
                 lib.call("gwn_support_square", ptr(acts.adp), cfg.NP, cfg.NP, ptr(acts.adp2), ptr(acts.adp2_t),
                          ptr(adp_t), st)
                 sq2, sq2t = sq2 + [acts.adp2], sq2t + [acts.adp2_t]
+                if self._t16_ok():
+                    # the adaptive support's 16-node tile copies, rewritten every step (one launch)
+                    mats = [acts.adp, acts.adp2] + ([adp_t, acts.adp2_t] if training else [])
+                    fl = int(_lib.load().gwn_support_g4_floats(N))
+                    if getattr(acts, "g4_adp", None) is None or acts.g4_adp.shape[0] < len(mats):
+                        acts.g4_adp = torch.empty(4, fl, device=self.device, dtype=F32)
+                    self._g4_into(mats, acts.g4_adp)
+                    g4f_p += [acts.g4_adp[0].data_ptr(), acts.g4_adp[1].data_ptr()]
+                    g4b_p += [acts.g4_adp[2].data_ptr(), acts.g4_adp[3].data_ptr()]
             acts.sup2_arr = (ctypes.c_void_p * len(sq2))(*[t_.data_ptr() for t_ in sq2])
             acts.sup2t_arr = (ctypes.c_void_p * len(sq2t))(*[t_.data_ptr() for t_ in sq2t])
+            if self._t16_ok() and len(g4f_p) == 2 * len(sups):
+                acts.g4f_arr = (ctypes.c_void_p * len(g4f_p))(*g4f_p)
+                acts.g4b_arr = (ctypes.c_void_p * len(g4b_p))(*g4b_p)
         if training and sups:
             # transposed supports: the fused backward computes A·x as (A^T)^T·x on the forward kernel path
             if getattr(acts, "supT", None) is None or len(acts.supT) != len(sups) or acts.supT[0].numel() != sq * sup_batch:
@@ -606,6 +620,7 @@ class Executor:
                               sup_bstride=sq if sup_batch > 1 else 0, sup_batch=sup_batch,
                               residual_mean=raff[0], residual_scale=raff[1], residual_shift=raff[2],
                               sup2=self._arr_field(acts.sup2_arr), w_mlp_t=ptr(self.pk("mlp_wT%d" % i)),
+                              sup_g4=self._arr_field(acts.g4f_arr),
                               **self.split_fields(sp, i), **self.ksplit_fields(scr))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
@@ -658,24 +673,50 @@ class Executor:
         return (os.environ.get("GWN_GCN_POW", "1") != "0" and self._fused_gcn() and cfg.use_gcn and cfg.nsup >= 1
                 and sup_batch <= 1 and self.split_planes() == 0)
 
+    def _t16_ok(self):
+        """The persistent 16-node tile gcn kernels (include/gwn.h sup_g4 / sup_g4_t) with the power
+        schedule; GWN_GCN_T16=0 selects the 32-node tile power kernels."""
+        return os.environ.get("GWN_GCN_T16", "1") != "0"
+
+    def _g4(self, mats):
+        """gwn_support_g4 copies of padded supports (one launch): a [len(mats)][floats] tensor."""
+        cfg = self.cfg
+        fl = int(_lib.load().gwn_support_g4_floats(cfg.N))
+        out = torch.empty(len(mats), fl, device=self.device, dtype=F32)
+        self._g4_into(mats, out)
+        return out
+
+    def _g4_into(self, mats, out):
+        cfg = self.cfg
+        arr = (ctypes.c_void_p * len(mats))(*[ptr(m_) for m_ in mats])
+        _lib.call("gwn_support_g4", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), len(mats), cfg.N, cfg.NP,
+                  ptr(out), out.shape[1], _lib.stream())
+
     def _fixed_squares(self, fixed_sups):
-        """(A_k^2, (A_k^2)^T) of the padded fixed supports, cached while they stay the same tensors
-        (the cache keeps them referenced, so their addresses cannot be reused meanwhile)."""
+        """(A_k^2, (A_k^2)^T) of the padded fixed supports, and the gwn_support_g4 copies of
+        (A_k, A_k^2) and (A_k^T, (A_k^2)^T) for the 16-node tile kernels, cached while the supports
+        stay the same tensors (the cache keeps them referenced, so their addresses cannot be reused
+        meanwhile).  Returns (sq, sqt, g4f, g4b) with g4f / g4b [2 * nfixed][floats]."""
         fixed_sups = list(fixed_sups) if self.cfg.use_gcn else []
         key = tuple(s_.data_ptr() for s_ in fixed_sups)
         c = getattr(self, "_sq_cache", None)
         if c is None or c[0] != key:
             NP = self.cfg.NP
-            sq, sqt = [], []
+            sq, sqt, fw, bw = [], [], [], []
             for s_ in fixed_sups:
                 a2 = torch.empty(NP, NP, device=self.device, dtype=F32)
                 a2t = torch.empty(NP, NP, device=self.device, dtype=F32)
-                _lib.call("gwn_support_square", ptr(s_), NP, NP, ptr(a2), ptr(a2t), None, _lib.stream())
+                at = torch.empty(NP, NP, device=self.device, dtype=F32)
+                _lib.call("gwn_support_square", ptr(s_), NP, NP, ptr(a2), ptr(a2t), ptr(at), _lib.stream())
                 sq.append(a2)
                 sqt.append(a2t)
-            c = (key, fixed_sups, sq, sqt)
+                fw += [s_, a2]
+                bw += [at, a2t]
+            g4f = self._g4(fw) if fw else None
+            g4b = self._g4(bw) if bw else None
+            c = (key, fixed_sups, sq, sqt, g4f, g4b)
             self._sq_cache = c
-        return list(c[2]), list(c[3])
+        return list(c[2]), list(c[3]), c[4], c[5]
 
     @staticmethod
     def ksplit_fields(scr):
@@ -780,9 +821,10 @@ class Executor:
                       cfg.NP, st)
             sups.append(bf["adp"])
         sup_arr = (ctypes.c_void_p * max(len(sups), 1))(*[s_.data_ptr() for s_ in sups])
-        bf["sup2_arr"] = None
+        bf["sup2_arr"] = bf["g4f_arr"] = None
         if self._pow_ok(1):
-            sq2, _ = self._fixed_squares(fixed_sups)
+            sq2, _, g4f, _ = self._fixed_squares(fixed_sups)
+            g4f_p = [t_.data_ptr() for t_ in g4f] if g4f is not None else []
             if cfg.adp_params:
                 if "adp2" not in bf:
                     bf["adp2"] = torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32)
@@ -790,7 +832,15 @@ class Executor:
                 _lib.call("gwn_support_square", ptr(bf["adp"]), cfg.NP, cfg.NP, ptr(bf["adp2"]), ptr(bf["adp2_t"]),
                           None, st)
                 sq2 = sq2 + [bf["adp2"]]
+                if self._t16_ok():
+                    if "g4_adp" not in bf:
+                        bf["g4_adp"] = torch.empty(2, int(_lib.load().gwn_support_g4_floats(N)), device=self.device,
+                                                   dtype=F32)
+                    self._g4_into([bf["adp"], bf["adp2"]], bf["g4_adp"])
+                    g4f_p += [bf["g4_adp"][0].data_ptr(), bf["g4_adp"][1].data_ptr()]
             bf["sup2_arr"] = (ctypes.c_void_p * len(sq2))(*[t_.data_ptr() for t_ in sq2])
+            if self._t16_ok() and len(g4f_p) == 2 * len(sups):
+                bf["g4f_arr"] = (ctypes.c_void_p * len(g4f_p))(*g4f_p)
         planes = self.split_planes()
         sp = self.split_operands(sup_arr, len(sups), planes) if planes else None
         sx = x.stride()
@@ -818,6 +868,7 @@ class Executor:
                               no_pieces=1, bn_running_mean=ptr(rm), bn_running_var=ptr(rv),
                               bn_weight=ptr(self.pk("bn_g%d" % i)), bn_bias=ptr(self.pk("bn_b%d" % i)),
                               bn_eps=eps, bn_out=ptr(xnext), sup2=self._arr_field(bf["sup2_arr"]),
+                              sup_g4=self._arr_field(bf["g4f_arr"]),
                               w_mlp_t=ptr(self.pk("mlp_wT%d" % i)),
                               **self.split_fields(sp, i))
             _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
@@ -937,6 +988,8 @@ class Executor:
                                      # kernel: 750 vs 863 us per step for the chained one, 21.3k
                                      # vs 20.5k samples/s); GWN_GCN_POW_BWD=0 selects the chain
                                      sup2_t=self._arr_field(getattr(acts, "sup2t_arr", None))
+                                     if os.environ.get("GWN_GCN_POW_BWD", "1") != "0" else None,
+                                     sup_g4_t=self._arr_field(getattr(acts, "g4b_arr", None))
                                      if os.environ.get("GWN_GCN_POW_BWD", "1") != "0" else None,
                                      **self.ksplit_fields(sc))
                 sb = getattr(acts, "sup_batch", 1)

@@ -255,8 +255,8 @@ typedef struct gwn_gcn_args {
    *   bn_out != NULL, bn_out[r][j] = (z - running_mean[j]) / sqrt(running_var[j] + bn_eps) *
    *   weight[j] + bias[j] is written instead of z (z may be NULL, bn_partials must be NULL).
    * layout: wave layout of the fused kernels: 0 = the persistent 16-node tile kernels where they
-   *   apply (sup2 given, shared supports; GWN_GCN_T16=0 disables them), else one wave per 32-node
-   *   tile; 1 = one wave per 32-node tile always.  Other values are rejected. */
+   *   apply (sup_g4 given, shared supports; GWN_GCN_T16=0 disables them), else one wave per
+   *   32-node tile; 1 = one wave per 32-node tile always.  Other values are rejected. */
   int no_pieces;
   const float* bn_running_mean; const float* bn_running_var; const float* bn_weight; const float* bn_bias;
   float bn_eps; float* bn_out;
@@ -285,7 +285,7 @@ typedef struct gwn_gcn_args {
    * a device counter that is zero on entry and left zero) adds them in support order and runs the
    * epilogue.  Finer work units for layers with too few slices to occupy the chip (a unit costs
    * about half a slice, so auto splits only when slices * nsup <= CUs; GWN_KSPLIT_SLICES = a slice
-   * threshold overrides; with sup2 given the persistent 16-node tile kernels, which already cut
+   * threshold overrides; with sup_g4 given the persistent 16-node tile kernels, which already cut
    * every launch into equal per-CU tile ranges, take precedence over the auto split).  ksplit: 0 = auto,
    * 1 = off, nsup = always.  ksplit_ws: gwn_gcn_ksplit_ws_floats(rows, n, nsup) floats,
    * ksplit_count: rows / n ints; NULL = no split. */
@@ -303,6 +303,11 @@ typedef struct gwn_gcn_args {
    * of h carry c channels, w_mlp is [c_out][(2K+1)c], b_mlp / residual / z / bn_partials carry
    * c_out.  0 = c.  c_out != c runs the generic path. */
   int c_out;
+  /* sup_g4 [2*nsup] (optional, f32 fused path, shared supports): A_k (index 2k) and A_k^2 (2k+1) in
+   * the 16-node k-interleaved layout of gwn_support_g4.  Given (layout 0, GWN_GCN_T16 not 0), the
+   * persistent 16-node tile kernels run: one 16-wave workgroup per CU over an equal range of the
+   * launch's 16-node tiles, each support fragment a 16-B load of four k-steps. */
+  const float* const* sup_g4;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -398,6 +403,9 @@ typedef struct gwn_gcn_bwd_args {
   const float* const* sup2_t;
   /* output channels as gwn_gcn_args.c_out (0 = c): dh [rows][c_out], dW_mlp [c_out][(2K+1)c] */
   int c_out;
+  /* sup_g4_t [2*nsup] (optional): A_k^T (index 2k) and (A_k^2)^T (2k+1) in the layout of
+   * gwn_support_g4: the persistent 16-node tile backward, as gwn_gcn_args.sup_g4 */
+  const float* const* sup_g4_t;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);
@@ -497,6 +505,15 @@ int gwn_fused_occupancy(int n, int backward, int pow);
  * a2 = a a, a2_t = (a a)^T, and a_t = a^T when a_t != NULL, all [np][ld] like a (a padded support,
  * zero outside [n][n]; np a multiple of 32).  One launch (f32 MFMA). */
 int gwn_support_square(const float* a, int np, int ld, float* a2, float* a2_t, float* a_t, hipStream_t stream);
+/* 16-node k-interleaved copies of `count` padded [np][ld] supports src[c] (zero outside [n][n]) for
+ * the 16-node tile kernels (gwn_gcn_args.sup_g4): with nt = ceil(n/16) column tiles and
+ * nkg = ceil(n/16) groups of four 4-row k-steps,
+ *   dst[c*dst_stride + ((kg*nt + t)*64 + 16*g + j)*4 + i] = src[c][16*kg + 4*i + g][16*t + j]
+ * (one 1-KiB block per (k-group, tile): a wave's 16-B load per lane holds four k-steps).
+ * gwn_support_g4_floats(n) = nkg*nt*256, the floats of one copy (dst_stride >= it). */
+long gwn_support_g4_floats(int n);
+int gwn_support_g4(const float* const* src, int count, int n, int ld, float* dst, long dst_stride,
+                   hipStream_t stream);
 /* dst [np][ld_dst] = src (or src^T if transpose) inside [n][n], zero elsewhere (np >= n) */
 int gwn_pad_square(const float* src, int n, int ld_src, float* dst, int np, int ld_dst, int transpose,
                    hipStream_t stream);

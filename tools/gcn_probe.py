@@ -51,6 +51,14 @@ def main():
     arrT = (ctypes.c_void_p * K)(*[s.data_ptr() for s in supT])
     arr2 = (ctypes.c_void_p * K)(*[s.data_ptr() for s in sq])
     arr2T = (ctypes.c_void_p * K)(*[s.data_ptr() for s in sqt])
+    # gwn_support_g4 copies (the 16-node tile kernels): forward [A_k, A_k^2], backward [A_k^T, (A_k^2)^T]
+    fl = _lib.load().gwn_support_g4_floats(N)
+    g4 = []
+    for mats in ([m for a_, b_ in zip(sups, sq) for m in (a_, b_)], [m for a_, b_ in zip(supT, sqt) for m in (a_, b_)]):
+        buf = torch.empty(len(mats), fl, device=dev)
+        src = (ctypes.c_void_p * len(mats))(*[m.data_ptr() for m in mats])
+        _lib.call("gwn_support_g4", ctypes.cast(src, P), len(mats), N, NP, buf.data_ptr(), fl, _lib.stream())
+        g4.append((buf, (ctypes.c_void_p * len(mats))(*[buf[i].data_ptr() for i in range(len(mats))])))
     wm = torch.randn(C, W, device=dev) * 0.05
     wmt = wm.t().contiguous()
     bm = torch.randn(C, device=dev)
@@ -70,13 +78,15 @@ def main():
                           seed_ptr=seed.data_ptr(), salt=0, drop_p=args.drop,
                           bn_partials=None if args.no_bn else bnp.data_ptr(),
                           no_pieces=1 if args.no_pieces else 0,
-                          sup2=None if args.chain else ctypes.cast(arr2, P), w_mlp_t=wmt.data_ptr(), ksplit=1)
+                          sup2=None if args.chain else ctypes.cast(arr2, P), w_mlp_t=wmt.data_ptr(), ksplit=1,
+                          sup_g4=None if args.chain else ctypes.cast(g4[0][1], P))
         dh = torch.randn(rows, C, device=dev)
         dhc = torch.empty(rows, W, device=dev)
         gb = _lib.GcnBwdArgs(rows=rows, n=N, c=C, nsup=K, sup=ctypes.cast(arr, P), ld_sup=NP, h=h.data_ptr(),
                              ld_h=W, w_mlp=wm.data_ptr(), dh=dh.data_ptr(), dhcat=dhc.data_ptr(), ld_dhcat=W,
                              adp_index=K - 1, accumulate_dadp=0, sup_t=ctypes.cast(arrT, P), skip_weight_grads=1,
-                             sup2_t=None if args.chain else ctypes.cast(arr2T, P), ksplit=1)
+                             sup2_t=None if args.chain else ctypes.cast(arr2T, P), ksplit=1,
+                             sup_g4_t=None if args.chain else ctypes.cast(g4[1][1], P))
         flop = T * B * (K * 2 * 2.0 * C * N * N + 2.0 * (2 * K + 1) * C * C * N)
         for name, fn, a in (("fwd", "gwn_gcn_fwd", ga), ("bwd", "gwn_gcn_bwd", gb)):
             for _ in range(3):
