@@ -209,9 +209,10 @@ def main():
 def measure_dominant(eng, dev, rounds=5, bf16=False):
     """The dominant kernel is the diffusion graph convolution forward (gwn_gcn_fwd: 3 supports x 2
     hops of 'ncvl,vw->ncwl' + the 224->32 mlp + residual + dropout + BN partials, one call per
-    layer, 8 per step; for N <= 512 ONE fused launch, gcn_fwd_fused_kernel<512, true>).  Replay
+    layer, 8 per step; for N <= 512 ONE fused launch, gcn_fwd_t16_kernel).  Replay
     exactly the last training step's 8 calls (same arguments and buffers; the replay is
-    idempotent) with HIP events on the launch stream; achieved = algorithmic FLOP / summed time,
+    idempotent) as one captured HIP graph between HIP events on the launch stream; achieved =
+    algorithmic FLOP / time,
     where the algorithmic FLOP of a call = slices * (K*order*2*C*N^2 + 2*(2K+1)*C*C*N) (SURVEY.md
     Appendix A)."""
     import ctypes
@@ -220,19 +221,31 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
     acts = [a for k, a in eng._acts.items() if k[2]][0]
     cfg = ex.cfg
     C, N, K = cfg.C, cfg.N, cfg.nsup
-    st = _lib.stream()
     launches = [acts.gcn_args[i] for i in sorted(acts.gcn_args)]
-    # one event pair around each round of the 8 back-to-back launches (an event pair per launch
-    # added ~10 us of event overhead to every 100 us launch); the inter-launch gaps stay inside
+    # the 8 launches captured in one HIP graph (as the training step replays them: no host launch
+    # overhead between kernels) and replayed `rounds` times between one event pair on the stream;
+    # per-launch events had added ~10 us of event overhead, and host-issued launches ~12 us of
+    # Python/ctypes issue time, to each ~80-90 us kernel
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for ga in launches:
+            _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for ga in launches:
+            _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     total_ms, total_flop, total_bytes, count = 0.0, 0.0, 0.0, 0
+    e0.record()
     for _ in range(rounds):
-        e0.record()
-        for ga in launches:
-            _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
-        e1.record()
-        torch.cuda.synchronize()
-        total_ms += e0.elapsed_time(e1)
+        graph.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    total_ms = e0.elapsed_time(e1)
+    for _ in range(rounds):
         for ga in launches:
             slices = ga.rows // N
             total_flop += slices * (K * 2 * 2.0 * C * N * N + 2.0 * (2 * K + 1) * C * C * N)
