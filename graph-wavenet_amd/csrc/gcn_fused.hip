@@ -1417,6 +1417,150 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   t16_bn_flush(a, bn, wpart);
 }
 
+// ---------------------------------------------------------------------------------------------
+// bf16 operands (configs[2]'s mixed precision) on the 16-node tile forward: the diffusion on
+// v_mfma_f32_16x16x32_bf16 (32 nodes per MFMA instead of 4), fp32 accumulation; the mlp, the hop
+// pieces, z and the BN partials exactly as the f32 kernel (its accumulator layout is the same:
+// lane l holds D[16 hf + 4 (l >> 4) + r][w0 + (l & 15)]).
+//   A operand: the slice image in bf16, channel-major [32][s16] in LDS (s16 = 32 * nkg + 8: rows
+//     >= n zero; the 8-element pad spreads the channel rows over the banks), lane l reading the 8
+//     nodes 32 kg + 8 (l >> 4) .. of channel 16 hf + (l & 15) with one ds_read_b128;
+//   B operand: gwn_support_g4_bf16's copy of the support, one 16-B load per lane per 32 nodes;
+//   piece 0's mlp takes the tile's fp32 rows straight from HBM / L2 (no fp32 image in LDS).
+typedef __bf16 bf16x8b __attribute__((ext_vector_type(8)));
+
+__host__ __device__ inline int t16b_s16(int n) { return 32 * ((n + 31) / 32) + 8; }
+
+size_t t16b_lds_bytes(int n, int nsup, int maximg) {
+  return (size_t)((2 * nsup + 1) * CH * LDW16 + T16_WAVES * 3 * CH) * sizeof(float) +
+         (size_t)maximg * CH * t16b_s16(n) * 2;
+}
+
+// a slice's node features (rows >= n zero) -> the channel-major bf16 image [32][s16]
+__device__ __forceinline__ void global_to_lds16_bf16(const float* src, long ld, int n, __bf16* img) {
+  const int s16 = t16b_s16(n), rows = s16 - 8;
+  for (int e = threadIdx.x; e < rows * 8; e += blockDim.x) {
+    const int v = e >> 3, q = e & 7;
+    float4 x = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (v < n) x = *(const float4*)(src + (long)v * ld + 4 * q);
+    img[(4 * q) * s16 + v] = (__bf16)x.x;
+    img[(4 * q + 1) * s16 + v] = (__bf16)x.y;
+    img[(4 * q + 2) * s16 + v] = (__bf16)x.z;
+    img[(4 * q + 3) * s16 + v] = (__bf16)x.w;
+  }
+}
+
+// both powers of one support on bf16 operands (acc as t16_diffuse); G1 / G2: gwn_support_g4_bf16
+// copies (block (kg, tile) = 64 lanes x 8 bf16)
+__device__ __forceinline__ void t16b_diffuse(const __bf16* img, const __bf16* G1, const __bf16* G2, int n, int tile,
+                                             int lane, f32x4v (*acc)[2]) {
+  const int g = lane >> 4, j = lane & 15;
+  const int nt = (n + 15) >> 4, nkg = (n + 31) >> 5, s16 = t16b_s16(n);
+  const int bytes = nkg * nt * 1024;
+  const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc((void*)G1, (short)0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc((void*)G2, (short)0, bytes, 0x00020000);
+  auto off = [&](int kg) { return ((kg * nt + tile) * 64 + lane) * 16; };
+  const __bf16* x0 = img + j * s16 + 8 * g;         // channel j (half 0)
+  const __bf16* x1 = img + (16 + j) * s16 + 8 * g;  // channel 16 + j (half 1)
+#pragma unroll
+  for (int q = 0; q < 2; ++q) acc[q][0] = acc[q][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  bf16x8b b1 = __builtin_bit_cast(bf16x8b, __builtin_amdgcn_raw_buffer_load_b128(r1, off(0), 0, 0));
+  bf16x8b b2 = __builtin_bit_cast(bf16x8b, __builtin_amdgcn_raw_buffer_load_b128(r2, off(0), 0, 0));
+  bf16x8b a0 = *(const bf16x8b*)x0, a1 = *(const bf16x8b*)x1;
+  for (int kg = 0; kg < nkg; ++kg) {
+    // the next group's operands first (past the last group: out of range, zeros / the pad)
+    const bf16x8b nb1 = __builtin_bit_cast(bf16x8b, __builtin_amdgcn_raw_buffer_load_b128(r1, off(kg + 1), 0, 0));
+    const bf16x8b nb2 = __builtin_bit_cast(bf16x8b, __builtin_amdgcn_raw_buffer_load_b128(r2, off(kg + 1), 0, 0));
+    const int nx = kg + 1 < nkg ? 32 * (kg + 1) : 32 * kg;
+    const bf16x8b na0 = *(const bf16x8b*)(x0 + nx), na1 = *(const bf16x8b*)(x1 + nx);
+    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b2, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b2, acc[1][1], 0, 0, 0);
+    b1 = nb1;
+    b2 = nb2;
+    a0 = na0;
+    a1 = na1;
+  }
+}
+
+// the tile's fp32 node rows (piece 0 of the mlp) from global memory, in t16_rows' order
+__device__ __forceinline__ void t16_rows_global(const float* src, long ld, int w0, int n, int lane, f32x4v* x) {
+  const int g = lane >> 4, j = lane & 15;
+  const int w = min(w0 + j, n - 1);
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const float4 q = *(const float4*)(src + (long)w * ld + 16 * hf + 4 * g);
+    x[hf] = w0 + j < n ? f32x4v{q.x, q.y, q.z, q.w} : f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  }
+}
+
+template <int MAXT>
+__global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, const PowSup p, const int maximg) {
+  extern __shared__ float lds[];
+  const int n = a.n;
+  const int nt = (n + 15) >> 4;
+  const int s16 = t16b_s16(n), imgb = CH * s16;  // bf16 elements per image
+  float* ws = lds;
+  float* wpart = ws + (2 * a.nsup + 1) * CH * LDW16;
+  __bf16* imgs = (__bf16*)(wpart + T16_WAVES * 3 * CH);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  const int nwaves = blockDim.x >> 6;
+  const long ldh = a.ld_h;
+  const T16Range rg = t16_range(a.slices, nt);
+  BnRun bn;
+  bn.n = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bn.mean[q] = bn.m2[q] = 0.0f;
+  t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
+  for (long p0 = rg.tb; p0 < rg.te;) {
+    const int s0 = (int)(p0 / nt);
+    const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
+    const int s1 = (int)((p1 - 1) / nt);
+    if (p0 != rg.tb) __syncthreads();  // the previous phase's images are released
+    for (int sl = s0; sl <= s1; ++sl) global_to_lds16_bf16(a.h + (long)sl * n * ldh, ldh, n, imgs + (sl - s0) * imgb);
+    __syncthreads();
+    for (long t = p0 + ((wave - p0 % nwaves) + nwaves) % nwaves; t < p1; t += nwaves) {
+      const int sl = (int)(t / nt), tile = (int)(t - (long)sl * nt);
+      const __bf16* xs = imgs + (sl - s0) * imgb;
+      const long row0 = (long)sl * n;
+      float* hs_out = (float*)a.h + row0 * ldh;
+      const bool nt_ok = ((((uintptr_t)hs_out) & 15) | (ldh & 3)) == 0;
+      const int w0 = 16 * tile;
+      f32x4v hacc[2];
+      hacc[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      hacc[1] = hacc[0];
+      {  // piece 0: the node features themselves (fp32)
+        f32x4v x0[2];
+        t16_rows_global(hs_out, ldh, w0, n, lane, x0);
+        t16_mlp(ws, LDW16, x0, lane, hacc);
+      }
+      for (int k = 0; k < a.nsup; ++k) {
+        f32x4v acc[2][2];
+        t16b_diffuse(xs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, acc);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          t16_mlp(ws + (1 + 2 * k + q) * CH * LDW16, LDW16, acc[q], lane, hacc);
+          if (a.store_pieces && w0 + j < n) {
+            float* dp = hs_out + (long)(w0 + j) * ldh + (1 + 2 * k + q) * CH + 4 * g;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+              if (nt_ok) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
+              else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) dp[16 * hf + e] = acc[q][hf][e];
+              }
+            }
+          }
+        }
+      }
+      t16_epilogue(a, hacc, row0, w0, lane, n, bn);
+    }
+    p0 = p1;
+  }
+  t16_bn_flush(a, bn, wpart);
+}
+
 // Backward on 16-node tiles: the forward's structure with the dh image (BN-backward prologue),
 // the transposed supports A_k^T and (A_k^2)^T (so D = A dh, A^2 dh) and the channel map W^T:
 //   dxg = W_0^T dh + sum_k W_{1+2k}^T (A_k dh) + W_{2+2k}^T (A_k^2 dh)
@@ -1882,6 +2026,37 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
                 "gcn_fwd (fused): eval BatchNorm needs running mean / var, weight, bias (and no BN partials)");
   else
     GWN_REQUIRE(a.z != nullptr, "gcn_fwd (fused): z is required");
+  if (g->split_planes == 1 && g->sup_g4b && a.sup_batch <= 1 && g->nsup > 0 && g->layout == 0 && t16_enabled() &&
+      g->ksplit != g->nsup) {
+    const int slices = g->rows / g->n;
+    const size_t fixed = t16b_lds_bytes(g->n, g->nsup, 0), img = t16b_lds_bytes(g->n, g->nsup, 1) - fixed;
+    if (fixed + img <= (size_t)T16_LDS_MAX) {
+      GWN_REQUIRE(g->w_mlp_t, "gcn_fwd (16-node tiles, bf16): w_mlp_t is required with sup_g4b");
+      static bool attr_b = false;
+      if (!attr_b) {
+        (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  T16_LDS_MAX);
+        attr_b = true;
+      }
+      const int nt = (g->n + 15) / 16;
+      const long tiles = (long)slices * nt;
+      const int grid = (int)(tiles < gwn_device_cus() ? tiles : gwn_device_cus());
+      const long per = (tiles + grid - 1) / grid;
+      int maximg = (int)((T16_LDS_MAX - fixed) / img);
+      maximg = maximg < T16_MAXIMG ? maximg : T16_MAXIMG;
+      const int span = (int)((per - 1 + nt - 1) / nt) + 1;
+      maximg = maximg < span ? maximg : span;
+      size_t lds = fixed + maximg * img;
+      if (lds < 81 * 1024) lds = 81 * 1024;
+      PowSup p = {};
+      for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = (const float*)g->sup_g4b[k];
+      a.ksplit = 1;
+      a.bn_slots = (int)gwn_bn_part_slots(slices);
+      gcn_fwd_t16b_kernel<1024><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      GWN_CHECK_LAUNCH();
+      return GWN_OK;
+    }
+  }
   if (g->split_planes) {
     GWN_REQUIRE(gwn_gcn_split_eligible(g->c, g->n, g->split_planes) && g->sup_split && g->w_split && g->nsup > 0,
                 "gcn_fwd (split): needs c == 32, an instantiated node-tile count, split supports and weights");
@@ -2082,6 +2257,37 @@ extern "C" int gwn_support_g4(const float* const* src, int count, int n, int ld,
   for (int c = 0; c < count; ++c) gs.src[c] = src[c];
   const int nt = (n + 15) / 16;
   support_g4_kernel<<<dim3(nt * nt, count), 256, 0, s>>>(gs, nt, ld, dst, dst_stride);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+namespace {
+// bf16 copy: one 512-thread block per (32-row k-group, 16-column tile, copy): thread e writes element
+// e of the block, lane e >> 3's k-step row 8 (lane >> 4) + (e & 7)
+__global__ __launch_bounds__(512) void support_g4_bf16_kernel(G4Src gs, int nt, int ld, __bf16* dst, long dst_stride) {
+  const int blk = blockIdx.x, c = blockIdx.y;
+  const int kg = blk / nt, t = blk - kg * nt;
+  const int e = threadIdx.x, lane = e >> 3, i = e & 7;
+  dst[(long)c * dst_stride + (long)blk * 512 + e] =
+      (__bf16)gs.src[c][(long)(32 * kg + 8 * (lane >> 4) + i) * ld + 16 * t + (lane & 15)];
+}
+}  // namespace
+
+extern "C" long gwn_support_g4_bf16_elems(int n) {
+  const long nt = (n + 15) / 16, nkg = (n + 31) / 32;
+  return n > 0 ? nkg * nt * 512 : 0;
+}
+
+extern "C" int gwn_support_g4_bf16(const float* const* src, int count, int n, int ld, void* dst, long dst_stride,
+                                   hipStream_t s) {
+  GWN_REQUIRE(src && dst && n > 0 && count > 0 && count <= 32 && ld >= (n + 31) / 32 * 32 &&
+                  dst_stride >= gwn_support_g4_bf16_elems(n) && dst_stride % 8 == 0,
+              "support_g4_bf16: needs 1..32 padded [np][ld] supports (ld >= 32*ceil(n/32)) and dst_stride >= "
+              "gwn_support_g4_bf16_elems(n), a multiple of 8");
+  G4Src gs = {};
+  for (int c = 0; c < count; ++c) gs.src[c] = src[c];
+  const int nt = (n + 15) / 16, nkg = (n + 31) / 32;
+  support_g4_bf16_kernel<<<dim3(nkg * nt, count), 512, 0, s>>>(gs, nt, ld, (__bf16*)dst, dst_stride);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

@@ -93,6 +93,7 @@ class GcnArgs(ctypes.Structure):
         ("w_mlp_t", c_void_p),
         ("c_out", c_int),
         ("sup_g4", ctypes.POINTER(c_void_p)),
+        ("sup_g4b", ctypes.POINTER(c_void_p)),
     ]
 
 
@@ -210,6 +211,8 @@ _SIGS = [
     ("gwn_fused_occupancy", c_int, [c_int, c_int, c_int]),
     ("gwn_support_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gwn_support_g4_floats", c_long, [c_int]),
+    ("gwn_support_g4_bf16_elems", c_long, [c_int]),
+    ("gwn_support_g4_bf16", c_int, [ctypes.POINTER(c_void_p), c_int, c_int, c_int, c_void_p, c_long, c_void_p]),
     ("gwn_support_g4", c_int, [ctypes.POINTER(c_void_p), c_int, c_int, c_int, c_void_p, c_long, c_void_p]),
     ("gwn_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     ("gwn_pad_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),

@@ -573,6 +573,7 @@ class Executor:
         sp = self.split_operands(sup_arr, len(sups), planes) if planes else None
         acts.sp_bwd = (self.split_bwd_operands(acts.supT_arr, len(sups))
                        if planes == 1 and training and acts.supT_arr is not None else None)
+        acts.g4b_arr = self._g4_bf16(fixed_sups, acts, st) if planes == 1 and sups else None
         # the last layer's gcn + bn only update bn[L-1]'s running statistics (their output is dead,
         # model.py:225-236): GWN_TAIL_OVERLAP=1 runs them on a second stream beside the head GEMMs
         # (the head needs only the skip sum), joined before the forward returns.  Off by default:
@@ -621,6 +622,7 @@ class Executor:
                               residual_mean=raff[0], residual_scale=raff[1], residual_shift=raff[2],
                               sup2=self._arr_field(acts.sup2_arr), w_mlp_t=ptr(self.pk("mlp_wT%d" % i)),
                               sup_g4=self._arr_field(acts.g4f_arr),
+                              sup_g4b=self._arr_field(acts.g4b_arr),
                               **self.split_fields(sp, i), **self.ksplit_fields(scr))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
@@ -691,6 +693,43 @@ class Executor:
         arr = (ctypes.c_void_p * len(mats))(*[ptr(m_) for m_ in mats])
         _lib.call("gwn_support_g4", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), len(mats), cfg.N, cfg.NP,
                   ptr(out), out.shape[1], _lib.stream())
+
+    def _g4_bf16(self, fixed_sups, acts, st):
+        """bf16 mode: gwn_support_g4_bf16 copies of (A_k, A_k^2) for the bf16 16-node tile forward
+        (include/gwn.h sup_g4b) -- the fixed supports' cached, the adaptive one's (square and copy)
+        rebuilt every step; None where the t16 kernels are off."""
+        cfg = self.cfg
+        if not self._t16_ok() or not cfg.use_gcn:
+            return None
+        lib = _lib.load()
+        el = int(lib.gwn_support_g4_bf16_elems(cfg.N))
+        sq, _, _, _ = self._fixed_squares(fixed_sups)
+        fixed = list(fixed_sups)
+        key = tuple(s_.data_ptr() for s_ in fixed)
+        c = getattr(self, "_g4b_cache", None)
+        if c is None or c[0] != key:
+            mats = [m for s_, q in zip(fixed, sq) for m in (s_, q)]
+            buf = torch.empty(max(len(mats), 1), el // 2, device=self.device, dtype=F32)  # bf16 pairs
+            if mats:
+                arr = (ctypes.c_void_p * len(mats))(*[ptr(m) for m in mats])
+                _lib.call("gwn_support_g4_bf16", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), len(mats), cfg.N,
+                          cfg.NP, ptr(buf), el, st)
+            c = (key, fixed, buf, len(mats))
+            self._g4b_cache = c
+        ptrs = [c[2][i].data_ptr() for i in range(c[3])]
+        if cfg.adp_params:
+            if getattr(acts, "adp2b", None) is None:
+                acts.adp2b = torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32)
+                acts.adp2b_t = torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32)
+                acts.g4b_adp = torch.empty(2, el // 2, device=self.device, dtype=F32)
+            _lib.call("gwn_support_square", ptr(acts.adp), cfg.NP, cfg.NP, ptr(acts.adp2b), ptr(acts.adp2b_t), None, st)
+            arr = (ctypes.c_void_p * 2)(ptr(acts.adp), ptr(acts.adp2b))
+            _lib.call("gwn_support_g4_bf16", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), 2, cfg.N, cfg.NP,
+                      ptr(acts.g4b_adp), el, st)
+            ptrs += [acts.g4b_adp[0].data_ptr(), acts.g4b_adp[1].data_ptr()]
+        if len(ptrs) != 2 * cfg.nsup:
+            return None
+        return (ctypes.c_void_p * len(ptrs))(*ptrs)
 
     def _fixed_squares(self, fixed_sups):
         """(A_k^2, (A_k^2)^T) of the padded fixed supports, and the gwn_support_g4 copies of

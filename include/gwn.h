@@ -308,6 +308,10 @@ typedef struct gwn_gcn_args {
    * persistent 16-node tile kernels run: one 16-wave workgroup per CU over an equal range of the
    * launch's 16-node tiles, each support fragment a 16-B load of four k-steps. */
   const float* const* sup_g4;
+  /* sup_g4b [2*nsup] (optional, bf16 operands: split_planes == 1): A_k and A_k^2 as
+   * gwn_support_g4_bf16 copies.  Given, the 16-node tile forward runs with the diffusion on bf16
+   * MFMA operands (fp32 accumulation; the mlp, hop pieces, z and BN partials in fp32). */
+  const void* const* sup_g4b;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -512,6 +516,12 @@ int gwn_support_square(const float* a, int np, int ld, float* a2, float* a2_t, f
  * (one 1-KiB block per (k-group, tile): a wave's 16-B load per lane holds four k-steps).
  * gwn_support_g4_floats(n) = nkg*nt*256, the floats of one copy (dst_stride >= it). */
 long gwn_support_g4_floats(int n);
+/* the bf16 form for the bf16 16-node tile forward (gwn_gcn_args.sup_g4b): with nkg = ceil(n/32)
+ * groups of 32 rows, dst[c*dst_stride + ((kg*nt + t)*64 + 16*g + j)*8 + i] =
+ * bf16(src[c][32*kg + 8*g + i][16*t + j]); gwn_support_g4_bf16_elems(n) = nkg*nt*512 bf16 per copy */
+long gwn_support_g4_bf16_elems(int n);
+int gwn_support_g4_bf16(const float* const* src, int count, int n, int ld, void* dst, long dst_stride,
+                        hipStream_t stream);
 int gwn_support_g4(const float* const* src, int count, int n, int ld, float* dst, long dst_stride,
                    hipStream_t stream);
 /* dst [np][ld_dst] = src (or src^T if transpose) inside [n][n], zero elsewhere (np >= n) */

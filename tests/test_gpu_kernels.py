@@ -984,3 +984,66 @@ def test_nconv2_errors_and_strided_input(gpu):
     y = nconv2()(xt, A)
     ref = torch.einsum("ncvl,nvw->ncwl", xt.double().cpu(), A.double().cpu())
     assert rel_err(y.cpu().numpy(), ref.numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("n", [16, 207, 325])
+def test_gcn_t16_bf16_forward(gpu, n):
+    """The bf16 16-node tile forward (gwn_gcn_args.sup_g4b, split_planes 1): the diffusion on bf16
+    MFMA operands with fp32 accumulation, the mlp / z / BN partials in fp32, against fp64
+    (model.py:41-55 + residual).  Bound: bf16 rounding of the node features and supports (2^-9
+    relative each) over K = n terms of positive weights -- hop pieces and z within 1e-2 of their
+    max magnitude; the BN statistics of z within 1e-2."""
+    import ctypes
+    from gwn_amd import _lib
+    torch.manual_seed(n + 3)
+    C, K, S = 32, 3, 21
+    NP = (n + 31) // 32 * 32
+    W = (2 * K + 1) * C
+    rows = S * n
+    sups = []
+    for _ in range(K):
+        s_ = torch.zeros(NP, NP, device=gpu)
+        a = torch.rand(n, n, device=gpu)
+        s_[:n, :n] = a / a.sum(1, keepdim=True)
+        sups.append(s_)
+    sq = _squares(gpu, sups)
+    P = ctypes.POINTER(ctypes.c_void_p)
+    el = _lib.load().gwn_support_g4_bf16_elems(n)
+    mats = [m for s_, q in zip(sups, sq) for m in (s_, q[0])]
+    g4b = torch.zeros(len(mats), el // 2, device=gpu)
+    src = (ctypes.c_void_p * len(mats))(*[m.data_ptr() for m in mats])
+    _lib.call("gwn_support_g4_bf16", ctypes.cast(src, P), len(mats), n, NP, g4b.data_ptr(), el, _lib.stream())
+    arrb = (ctypes.c_void_p * len(mats))(*[g4b[i].data_ptr() for i in range(len(mats))])
+    arr = (ctypes.c_void_p * K)(*[s_.data_ptr() for s_ in sups])
+    wm = torch.randn(C, W, device=gpu) * 0.1
+    wmt = wm.t().contiguous()
+    bm = torch.randn(C, device=gpu)
+    res = torch.randn(rows, C, device=gpu)
+    xg = torch.randn(rows, C, device=gpu)
+    seed = torch.zeros(1, device=gpu, dtype=torch.int64)
+    h = torch.zeros(rows, W, device=gpu)
+    h[:, :C] = xg
+    z = torch.empty(rows, C, device=gpu)
+    bnp = torch.full((_lib.load().gwn_gcn_bn_partial_count(rows, n, C, K, NP) * 3 * C,), float("nan"), device=gpu)
+    ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, P), ld_sup=NP, h=h.data_ptr(), ld_h=W,
+                      w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(), residual=res.data_ptr(), z=z.data_ptr(),
+                      seed_ptr=seed.data_ptr(), salt=0, drop_p=0.0, bn_partials=bnp.data_ptr(), w_mlp_t=wmt.data_ptr(),
+                      split_planes=1, sup_g4b=ctypes.cast(arrb, P))
+    _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
+    torch.cuda.synchronize()
+    X = xg.double().cpu().view(S, n, C)
+    pieces = [X]
+    for s_ in sups:
+        a = s_[:n, :n].double().cpu()
+        x1 = torch.einsum("svc,vw->swc", X, a)
+        x2 = torch.einsum("svc,vw->swc", x1, a)
+        pieces += [x1, x2]
+    H = torch.cat(pieces, dim=2).reshape(rows, W)
+    Z = H @ wm.double().cpu().t() + bm.double().cpu() + res.double().cpu()
+    for p_ in range(1, W // C):
+        assert rel_err(h[:, p_ * C:(p_ + 1) * C].cpu().numpy(), H[:, p_ * C:(p_ + 1) * C].numpy()) <= 1e-2, p_
+    assert torch.equal(h[:, :C], xg)
+    assert rel_err(z.cpu().numpy(), Z.numpy()) <= 1e-2
+    st = _bn_all(bnp, rows, n, C, K, NP)
+    assert torch.all(st[:, 0] == rows)
+    assert rel_err(st[:, 1].numpy(), Z.mean(0, keepdim=True).numpy()) <= 1e-2
