@@ -1567,11 +1567,14 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
 // (gcn_bwd_pow_kernel's schedule), t1 / t2 of the adaptive support, and the dxg store or the gate
 // backward in the epilogue.  The prologue stages a whole slice's dh image; dres / dh_out rows are
 // written for the workgroup's own tiles only [r0, r1).
+// BF: the image is the bf16 channel-major one of the bf16 forward ([32][s16], rows = s16 - 8)
+template <bool BF>
 __device__ __forceinline__ void t16_bwd_prologue(const FusedBwd& a, float* img, long row0, int n, int rows, int r0,
                                                  int r1) {
   const int hs = rows * 16;
   if (!a.bn_dy) {
-    global_to_lds16(a.dh + row0 * CH, CH, n, rows, img);
+    if (BF) global_to_lds16_bf16(a.dh + row0 * CH, CH, n, (__bf16*)img);
+    else global_to_lds16(a.dh + row0 * CH, CH, n, rows, img);
     return;
   }
   const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
@@ -1609,7 +1612,8 @@ __device__ __forceinline__ void t16_bwd_prologue(const FusedBwd& a, float* img, 
           a.dh_out[idx] = v;
         }
       }
-      ip[w * 16] = v;
+      if (BF) ((__bf16*)img)[c * (rows + 8) + w] = (__bf16)v;
+      else ip[w * 16] = v;
     }
   }
 }
@@ -1624,12 +1628,16 @@ __device__ __forceinline__ void t16_store(float* out, long ld, const f32x4v* acc
   for (int oh = 0; oh < 2; ++oh) *(float4*)(p + 16 * oh) = make_float4(acc[oh][0], acc[oh][1], acc[oh][2], acc[oh][3]);
 }
 
-template <int MAXT>
+// BF: bf16 operands in the diffusion (the bf16 forward's image / support layouts: sup_g4b_t), the
+// tile's fp32 dh rows for the channel maps of piece 0 and t1 / t2 read back from dh_out (written by
+// this workgroup's prologue for its own rows) or dh
+template <int MAXT, bool BF>
 __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, const PowSup p, const int maximg) {
   extern __shared__ float lds[];
   const int n = a.n;
   const int nt = (n + 15) >> 4;
-  const int rows_img = t16_img_rows(n), hs = rows_img * 16, imgf = rows_img * CH;
+  const int rows_img = BF ? t16b_s16(n) - 8 : t16_img_rows(n), hs = rows_img * 16;
+  const int imgf = BF ? CH * t16b_s16(n) / 2 : rows_img * CH;  // floats per image
   float* ws = lds;
   float* imgs = ws + (2 * a.nsup + 1) * CH * LDW16 + T16_WAVES * 3 * CH;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
@@ -1648,7 +1656,7 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
     for (int s = s0; s <= s1; ++s) {
       // this workgroup's rows of slice s
       const long t0 = max(rg.tb - (long)s * nt, 0l), t1 = min(rg.te - (long)s * nt, (long)nt);
-      t16_bwd_prologue(a, imgs + (s - s0) * imgf, (long)s * n, n, rows_img, 16 * (int)t0, 16 * (int)t1);
+      t16_bwd_prologue<BF>(a, imgs + (s - s0) * imgf, (long)s * n, n, rows_img, 16 * (int)t0, 16 * (int)t1);
     }
     __syncthreads();
     for (long t = p0 + ((wave - p0 % nwaves) + nwaves) % nwaves; t < p1; t += nwaves) {
@@ -1659,19 +1667,23 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
       f32x4v dx[2];
       dx[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
       dx[1] = dx[0];
+      const float* dh_rows = (a.bn_dy ? a.dh_out : a.dh) + row0 * CH;  // (BF: the fp32 rows)
       {
         f32x4v d0[2];
-        t16_rows(dhs, hs, w0, lane, d0);
+        if (BF) t16_rows_global(dh_rows, CH, w0, n, lane, d0);
+        else t16_rows(dhs, hs, w0, lane, d0);
         t16_mlp(ws, LDW16, d0, lane, dx);
       }
       for (int k = 0; k < a.nsup; ++k) {
         f32x4v e[2][2];
-        t16_diffuse(dhs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, e);
+        if (BF) t16b_diffuse((const __bf16*)dhs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, e);
+        else t16_diffuse(dhs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, e);
         t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, e[0], lane, dx);
         t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[1], lane, dx);
         if (k == a.adp_index) {  // t1 = W1^T dh + W2^T (A dh), t2 = W2^T dh
           f32x4v d0[2], tt[2];
-          t16_rows(dhs, hs, w0, lane, d0);
+          if (BF) t16_rows_global(dh_rows, CH, w0, n, lane, d0);
+          else t16_rows(dhs, hs, w0, lane, d0);
           tt[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
           tt[1] = tt[0];
           t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, d0, lane, tt);
@@ -2147,6 +2159,35 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   else
     GWN_REQUIRE(a.dh != nullptr, "gcn_bwd (fused): dh is required without the BN prologue");
   if (a.dfg) GWN_REQUIRE(a.fg != nullptr, "gcn_bwd (fused): the gate epilogue needs fg");
+  if (g->split_planes == 1 && g->sup_g4b_t && a.sup_batch <= 1 && g->nsup > 0 && g->layout == 0 && t16_enabled() &&
+      g->ksplit != g->nsup) {
+    const int slices = g->rows / g->n;
+    const size_t fixed = t16b_lds_bytes(g->n, g->nsup, 0), img = t16b_lds_bytes(g->n, g->nsup, 1) - fixed;
+    if (fixed + img <= (size_t)T16_LDS_MAX) {
+      static bool attr_b = false;
+      if (!attr_b) {
+        (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<1024, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
+        attr_b = true;
+      }
+      const int nt = (g->n + 15) / 16;
+      const long tiles = (long)slices * nt;
+      const int grid = (int)(tiles < gwn_device_cus() ? tiles : gwn_device_cus());
+      const long per = (tiles + grid - 1) / grid;
+      int maximg = (int)((T16_LDS_MAX - fixed) / img);
+      maximg = maximg < T16_MAXIMG ? maximg : T16_MAXIMG;
+      const int span = (int)((per - 1 + nt - 1) / nt) + 1;
+      maximg = maximg < span ? maximg : span;
+      size_t lds = fixed + maximg * img;
+      if (lds < 81 * 1024) lds = 81 * 1024;
+      PowSup p = {};
+      for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = (const float*)g->sup_g4b_t[k];
+      a.ksplit = 1;
+      gcn_bwd_t16_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      GWN_CHECK_LAUNCH();
+      return GWN_OK;
+    }
+  }
   if (g->split_planes == 1) return gwn_gcn_bf16_bwd_launch(g, a, s);
   GWN_REQUIRE(g->split_planes == 0, "gcn_bwd (fused): split_planes must be 0 (f32) or 1 (bf16)");
   static bool attr_set = false;
@@ -2157,7 +2198,9 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
     ensure_lds_attr(gcn_bwd_fused_kernel<1024, true>);
     ensure_lds_attr(gcn_bwd_pow_kernel<512>);
     ensure_lds_attr(gcn_bwd_pow_kernel<1024>);
-    (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              T16_LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<1024, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               T16_LDS_MAX);
     attr_set = true;
   }
@@ -2170,7 +2213,7 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
     PowSup p = {};
     for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = g->sup_g4_t[k];
     a.ksplit = 1;
-    gcn_bwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
+    gcn_bwd_t16_kernel<1024, false><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
     GWN_CHECK_LAUNCH();
     return GWN_OK;
   }

@@ -134,6 +134,7 @@ class GcnBwdArgs(ctypes.Structure):
         ("sup2_t", ctypes.POINTER(c_void_p)),
         ("c_out", c_int),
         ("sup_g4_t", ctypes.POINTER(c_void_p)),
+        ("sup_g4b_t", ctypes.POINTER(c_void_p)),
     ]
 
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time

@@ -573,7 +573,8 @@ class Executor:
         sp = self.split_operands(sup_arr, len(sups), planes) if planes else None
         acts.sp_bwd = (self.split_bwd_operands(acts.supT_arr, len(sups))
                        if planes == 1 and training and acts.supT_arr is not None else None)
-        acts.g4b_arr = self._g4_bf16(fixed_sups, acts, st) if planes == 1 and sups else None
+        acts.g4bt_arr = None
+        acts.g4bf_arr = self._g4_bf16(fixed_sups, acts, st) if planes == 1 and sups else None
         # the last layer's gcn + bn only update bn[L-1]'s running statistics (their output is dead,
         # model.py:225-236): GWN_TAIL_OVERLAP=1 runs them on a second stream beside the head GEMMs
         # (the head needs only the skip sum), joined before the forward returns.  Off by default:
@@ -622,7 +623,7 @@ class Executor:
                               residual_mean=raff[0], residual_scale=raff[1], residual_shift=raff[2],
                               sup2=self._arr_field(acts.sup2_arr), w_mlp_t=ptr(self.pk("mlp_wT%d" % i)),
                               sup_g4=self._arr_field(acts.g4f_arr),
-                              sup_g4b=self._arr_field(acts.g4b_arr),
+                              sup_g4b=self._arr_field(acts.g4bf_arr),
                               **self.split_fields(sp, i), **self.ksplit_fields(scr))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
@@ -703,33 +704,43 @@ class Executor:
             return None
         lib = _lib.load()
         el = int(lib.gwn_support_g4_bf16_elems(cfg.N))
-        sq, _, _, _ = self._fixed_squares(fixed_sups)
+        sq, sqt, _, _ = self._fixed_squares(fixed_sups)
+        at = self._sq_cache[6]
         fixed = list(fixed_sups)
         key = tuple(s_.data_ptr() for s_ in fixed)
         c = getattr(self, "_g4b_cache", None)
         if c is None or c[0] != key:
-            mats = [m for s_, q in zip(fixed, sq) for m in (s_, q)]
+            # rows: [A_k, A_k^2] (forward), then [A_k^T, (A_k^2)^T] (backward)
+            mats = [m for s_, q in zip(fixed, sq) for m in (s_, q)] + [m for t_, q in zip(at, sqt) for m in (t_, q)]
             buf = torch.empty(max(len(mats), 1), el // 2, device=self.device, dtype=F32)  # bf16 pairs
             if mats:
                 arr = (ctypes.c_void_p * len(mats))(*[ptr(m) for m in mats])
                 _lib.call("gwn_support_g4_bf16", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), len(mats), cfg.N,
                           cfg.NP, ptr(buf), el, st)
-            c = (key, fixed, buf, len(mats))
+            c = (key, fixed, buf, len(fixed))
             self._g4b_cache = c
-        ptrs = [c[2][i].data_ptr() for i in range(c[3])]
+        nf = c[3]
+        fw = [c[2][i].data_ptr() for i in range(2 * nf)]
+        bw = [c[2][2 * nf + i].data_ptr() for i in range(2 * nf)]
+        acts.g4bt_arr = None
         if cfg.adp_params:
             if getattr(acts, "adp2b", None) is None:
                 acts.adp2b = torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32)
                 acts.adp2b_t = torch.empty(cfg.NP, cfg.NP, device=self.device, dtype=F32)
-                acts.g4b_adp = torch.empty(2, el // 2, device=self.device, dtype=F32)
+                acts.g4b_adp = torch.empty(4, el // 2, device=self.device, dtype=F32)
             _lib.call("gwn_support_square", ptr(acts.adp), cfg.NP, cfg.NP, ptr(acts.adp2b), ptr(acts.adp2b_t), None, st)
-            arr = (ctypes.c_void_p * 2)(ptr(acts.adp), ptr(acts.adp2b))
-            _lib.call("gwn_support_g4_bf16", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), 2, cfg.N, cfg.NP,
-                      ptr(acts.g4b_adp), el, st)
-            ptrs += [acts.g4b_adp[0].data_ptr(), acts.g4b_adp[1].data_ptr()]
-        if len(ptrs) != 2 * cfg.nsup:
+            adp_t = acts.supT[-1] if getattr(acts, "supT", None) is not None and acts.training else None
+            mats = [acts.adp, acts.adp2b] + ([adp_t, acts.adp2b_t] if adp_t is not None else [])
+            arr = (ctypes.c_void_p * len(mats))(*[ptr(m) for m in mats])
+            _lib.call("gwn_support_g4_bf16", ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), len(mats), cfg.N,
+                      cfg.NP, ptr(acts.g4b_adp), el, st)
+            fw += [acts.g4b_adp[0].data_ptr(), acts.g4b_adp[1].data_ptr()]
+            bw = bw + [acts.g4b_adp[2].data_ptr(), acts.g4b_adp[3].data_ptr()] if adp_t is not None else []
+        if len(fw) != 2 * cfg.nsup:
             return None
-        return (ctypes.c_void_p * len(ptrs))(*ptrs)
+        if len(bw) == 2 * cfg.nsup:
+            acts.g4bt_arr = (ctypes.c_void_p * len(bw))(*bw)
+        return (ctypes.c_void_p * len(fw))(*fw)
 
     def _fixed_squares(self, fixed_sups):
         """(A_k^2, (A_k^2)^T) of the padded fixed supports, and the gwn_support_g4 copies of
@@ -753,7 +764,7 @@ class Executor:
                 bw += [at, a2t]
             g4f = self._g4(fw) if fw else None
             g4b = self._g4(bw) if bw else None
-            c = (key, fixed_sups, sq, sqt, g4f, g4b)
+            c = (key, fixed_sups, sq, sqt, g4f, g4b, [bw[2 * k] for k in range(len(fixed_sups))])
             self._sq_cache = c
         return list(c[2]), list(c[3]), c[4], c[5]
 
@@ -1030,6 +1041,7 @@ class Executor:
                                      if os.environ.get("GWN_GCN_POW_BWD", "1") != "0" else None,
                                      sup_g4_t=self._arr_field(getattr(acts, "g4b_arr", None))
                                      if os.environ.get("GWN_GCN_POW_BWD", "1") != "0" else None,
+                                     sup_g4b_t=self._arr_field(getattr(acts, "g4bt_arr", None)),
                                      **self.ksplit_fields(sc))
                 sb = getattr(acts, "sup_batch", 1)
                 if sb > 1:

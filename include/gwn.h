@@ -410,6 +410,9 @@ typedef struct gwn_gcn_bwd_args {
   /* sup_g4_t [2*nsup] (optional): A_k^T (index 2k) and (A_k^2)^T (2k+1) in the layout of
    * gwn_support_g4: the persistent 16-node tile backward, as gwn_gcn_args.sup_g4 */
   const float* const* sup_g4_t;
+  /* sup_g4b_t [2*nsup] (optional, bf16 operands: split_planes == 1): A_k^T and (A_k^2)^T as
+   * gwn_support_g4_bf16 copies: the bf16 16-node tile backward (as sup_g4b of gwn_gcn_args) */
+  const void* const* sup_g4b_t;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);
