@@ -271,9 +271,14 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
         # bf16 operands: arithmetic intensity (~80 FLOP/B algorithmic) sits far below the bf16
         # ridge (2.5 PF / 8 TB/s = 312 FLOP/B): the kernel is bounded by HBM, priced in bytes
         gbs = total_bytes / (total_ms / 1000.0) / 1e9
-        traffic, mfma_busy, src = pmc("pmc_bench_pems.json", "gcn_fwd_split_kernel") if N == 325 else (None,) * 3
-        return {"kernel": "gcn_fwd_split_kernel<%d, 1, %d> (fused diffusion GCN forward, bf16 operands, "
-                          "8 launches/step)" % ((N + 31) // 32, (N + 31) // 32),
+        t16b = getattr(acts, "g4bf_arr", None) is not None
+        kname = ("gcn_fwd_t16b_kernel<1024> (fused diffusion GCN forward, persistent 16-node tile waves, "
+                 "diffusion on bf16 MFMA operands, fp32 accumulation / mlp, 8 launches/step)" if t16b else
+                 "gcn_fwd_split_kernel<%d, 1, %d> (fused diffusion GCN forward, bf16 operands, 8 launches/step)"
+                 % ((N + 31) // 32, (N + 31) // 32))
+        traffic, mfma_busy, src = (pmc("pmc_bench_pems.json", "gcn_fwd_t16b_kernel" if t16b else "gcn_fwd_split_kernel")
+                                   if N == 325 else (None,) * 3)
+        return {"kernel": kname,
                 "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
                 "pmc_mfma_busy_frac": mfma_busy,
