@@ -54,6 +54,7 @@ struct FusedFwd {
   const float* res_mean; const float* res_scale; const float* res_shift;  // (residual - mean) * scale + shift
   int ksplit, slices; float* kws; int* kcnt;  // support split (ksplit > 1): see unit_of()
   int bn_slots;  // t16 kernels: BN partial slots to write (those past the grid get count 0)
+  float* xg4; int xg4_k;  // bf16 t16 kernel: X and support xg4_k's hop 1 in the tiled activation layout
 };
 
 struct FusedBwd {
@@ -71,6 +72,7 @@ struct FusedBwd {
   const float* fg; const float* dskip; long ld_dskip; long skip_row0; float* dfg;
   long sup_bstride; int sup_batch;  // per-sample supports, as FusedFwd
   int ksplit, slices; float* kws; int* kcnt;  // support split, as FusedFwd
+  float* tg4;  // bf16 t16 kernel: t1 / t2 in the tiled activation layout instead of dhcat's columns
 };
 
 // support k of this workgroup's slice (per-sample supports: sample = slice % sup_batch)
@@ -1351,6 +1353,14 @@ __device__ __forceinline__ T16Range t16_range(int slices, int nt) {
   return {total * blockIdx.x / gridDim.x, total * (blockIdx.x + 1) / gridDim.x};
 }
 
+// a tile's 32 channels (lane (g, j): node w0 + j, channels 16 hf + 4 g .. + 3, as the t16
+// accumulators) into the tiled activation layout of gwn_gram_g4: block (slice, tile, hf), 16 B per lane
+__device__ __forceinline__ void t16_store_g4(float* base, int slice, int nt, int tile, int lane, const f32x4v* v) {
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf)
+    *(f32x4v*)(base + (((long)slice * nt + tile) * 2 + hf) * 256 + lane * 4) = v[hf];
+}
+
 template <int MAXT>
 __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, const PowSup p, const int maximg) {
   extern __shared__ float lds[];
@@ -1534,10 +1544,12 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
         f32x4v x0[2];
         t16_rows_global(hs_out, ldh, w0, n, lane, x0);
         t16_mlp(ws, LDW16, x0, lane, hacc);
+        if (a.xg4) t16_store_g4(a.xg4, sl, nt, tile, lane, x0);
       }
       for (int k = 0; k < a.nsup; ++k) {
         f32x4v acc[2][2];
         t16b_diffuse(xs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, acc);
+        if (a.xg4 && k == a.xg4_k) t16_store_g4(a.xg4 + (long)a.slices * nt * 512, sl, nt, tile, lane, acc[0]);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           t16_mlp(ws + (1 + 2 * k + q) * CH * LDW16, LDW16, acc[q], lane, hacc);
@@ -1688,11 +1700,13 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
           tt[1] = tt[0];
           t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, d0, lane, tt);
           t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[0], lane, tt);
-          t16_store(a.t1 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
+          if (BF && a.tg4) t16_store_g4(a.tg4, s, nt, tile, lane, tt);
+          else t16_store(a.t1 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
           tt[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
           tt[1] = tt[0];
           t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, d0, lane, tt);
-          t16_store(a.t2 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
+          if (BF && a.tg4) t16_store_g4(a.tg4 + (long)a.slices * nt * 512, s, nt, tile, lane, tt);
+          else t16_store(a.t2 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
         }
       }
       if (!a.dfg) {
@@ -2027,6 +2041,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.sup_bstride = g->sup_bstride; a.sup_batch = g->sup_batch;
   a.res_mean = g->residual_mean; a.res_scale = g->residual_scale; a.res_shift = g->residual_shift;
   a.ksplit = 1; a.slices = g->rows / g->n; a.kws = g->ksplit_ws; a.kcnt = g->ksplit_count; a.bn_slots = 0;
+  a.xg4 = g->xg4; a.xg4_k = g->xg4_support;
   GWN_REQUIRE(g->ksplit == 0 || g->ksplit == 1 || g->ksplit == g->nsup, "gcn_fwd: ksplit must be 0, 1 or nsup");
   GWN_REQUIRE(!a.res_scale == !a.res_shift && !a.res_scale == !a.res_mean,
               "gcn_fwd (fused): residual_mean, residual_scale and residual_shift go together");
@@ -2069,6 +2084,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
       return GWN_OK;
     }
   }
+  GWN_REQUIRE(!g->xg4, "gcn_fwd: xg4 is written by the bf16 16-node tile kernel only (sup_g4b, layout 0)");
   if (g->split_planes) {
     GWN_REQUIRE(gwn_gcn_split_eligible(g->c, g->n, g->split_planes) && g->sup_split && g->w_split && g->nsup > 0,
                 "gcn_fwd (split): needs c == 32, an instantiated node-tile count, split supports and weights");
@@ -2149,6 +2165,7 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   a.fg = g->fg; a.dskip = g->dskip; a.ld_dskip = g->ld_dskip; a.skip_row0 = g->skip_row0; a.dfg = g->dfg;
   a.sup_bstride = g->sup_bstride; a.sup_batch = g->sup_batch;
   a.ksplit = 1; a.slices = g->rows / g->n; a.kws = g->ksplit_ws; a.kcnt = g->ksplit_count;
+  a.tg4 = g->tg4;
   GWN_REQUIRE(g->ksplit == 0 || g->ksplit == 1 || g->ksplit == g->nsup, "gcn_bwd: ksplit must be 0, 1 or nsup");
   if (a.sup_batch > 1)
     GWN_REQUIRE((g->rows / g->n) % a.sup_batch == 0 && g->adp_index < 0,
@@ -2188,6 +2205,7 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
       return GWN_OK;
     }
   }
+  GWN_REQUIRE(!g->tg4, "gcn_bwd: tg4 is written by the bf16 16-node tile kernel only (sup_g4b_t, layout 0)");
   if (g->split_planes == 1) return gwn_gcn_bf16_bwd_launch(g, a, s);
   GWN_REQUIRE(g->split_planes == 0, "gcn_bwd (fused): split_planes must be 0 (f32) or 1 (bf16)");
   static bool attr_set = false;
@@ -2879,6 +2897,10 @@ int gwn_gcn_bf16_bwd_launch(const gwn_gcn_bwd_args* g, const FusedBwd& a, hipStr
 }
 
 extern "C" int gwn_gcn_split_supported(int c, int n, int planes) { return gwn_gcn_split_eligible(c, n, planes) ? 1 : 0; }
+// the bf16 16-node tile kernels run for (n, nsup) (c == 32, sup_g4b / sup_g4b_t given, layout 0)
+extern "C" int gwn_gcn_t16b_supported(int n, int nsup) {
+  return n > 0 && nsup > 0 && t16_enabled() && t16b_lds_bytes(n, nsup, 1) <= (size_t)T16_LDS_MAX ? 1 : 0;
+}
 
 extern "C" long gwn_split_support_elems(int n, int planes) {
   const long np = (n + 31) / 32 * 32;

@@ -94,6 +94,7 @@ class GcnArgs(ctypes.Structure):
         ("c_out", c_int),
         ("sup_g4", ctypes.POINTER(c_void_p)),
         ("sup_g4b", ctypes.POINTER(c_void_p)),
+        ("xg4", c_void_p), ("xg4_support", c_int),
     ]
 
 
@@ -135,6 +136,7 @@ class GcnBwdArgs(ctypes.Structure):
         ("c_out", c_int),
         ("sup_g4_t", ctypes.POINTER(c_void_p)),
         ("sup_g4b_t", ctypes.POINTER(c_void_p)),
+        ("tg4", c_void_p),
     ]
 
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time
@@ -173,6 +175,7 @@ _SIGS = [
     ("gwn_gcn_fwd", c_int, [ctypes.POINTER(GcnArgs), c_void_p]),
     ("gwn_gcn_bn_partial_count", c_long, [c_int, c_int, c_int, c_int, c_int]),
     ("gwn_gcn_split_supported", c_int, [c_int, c_int, c_int]),
+    ("gwn_gcn_t16b_supported", c_int, [c_int, c_int]),
     ("gwn_split_support_elems", c_long, [c_int, c_int]),
     ("gwn_split_supports", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_long, c_int, c_void_p]),
     ("gwn_split_mlp_elems", c_long, [c_int, c_int]),
@@ -198,6 +201,9 @@ _SIGS = [
                                      c_float, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     ("gwn_gather_sum", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_long, c_void_p]),
     ("gwn_gram_workspace_floats", c_long, [c_int, c_int]),
+    ("gwn_gram_g4_bf16", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                            c_void_p]),
+    ("gwn_gram_g4_workspace_floats", c_long, [c_int, c_int]),
     ("gwn_gram_bf16", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_int,
                               c_int, c_void_p, c_void_p]),
     ("gwn_batchnorm_fwd", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,

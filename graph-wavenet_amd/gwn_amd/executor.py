@@ -392,6 +392,8 @@ class Executor:
             "dskipcat": e(tf * P, L * D),
             "dxa": e(ts[0] * P, C),
             "dxb": e(ts[0] * P, C),
+            # bf16 mode: t1 / t2 of the adaptive support in the tiled activation layout (gwn_gram_g4_bf16)
+            "tg4": e(2 * (maxrows // N) * ((N + 15) // 16) * 512),
             "dfg": e(maxrows, 2 * D),
             "dh": e(maxrows, C),
             "dhc": e(maxrows, cfg.W),
@@ -413,6 +415,7 @@ class Executor:
             lib.gwn_masked_loss_workspace_floats(B, cfg.O, N, tf),
             lib.gwn_clip_adam_workspace_floats(self.layout.flat_total),
             cfg.NP * cfg.NP,
+            lib.gwn_gram_g4_workspace_floats(N, maxrows // N),
         ]
         # every layer's TCN backward (the largest workspace need may sit at any dilation)
         need += [lib.gwn_gated_tcn_bwd_workspace_floats_ex(ts[i], P, C, cfg.dilations[i], cfg.K, D) for i in range(L)]
@@ -588,6 +591,15 @@ class Executor:
         # of materialising bn(z) (one HBM pass and one launch fewer per layer)
         fold = training and self._bn_fold_ok(sup_batch)
         acts.bn_fold = fold
+        # bf16 mode: the adaptive-support gram on tiled operands -- the bf16 16-node tile kernels
+        # write X and its hop 1 (forward) and t1 / t2 (backward) in gwn_gram_g4_bf16's layout
+        gram_g4 = (training and cfg.adp_params and cfg.use_gcn and sup_batch <= 1 and self._fused_gcn()
+                   and os.environ.get("GWN_GRAM_G4", "1") != "0"
+                   and acts.g4bf_arr is not None and acts.g4bt_arr is not None
+                   and _lib.load().gwn_gcn_t16b_supported(N, cfg.nsup) == 1)
+        acts.gram_g4 = gram_g4
+        if getattr(acts, "XG4", None) is None:
+            acts.XG4 = {}
         for i in range(L):
             d, sh = cfg.dilations[i], cfg.shift(i)
             rows = ts[i + 1] * P
@@ -609,6 +621,12 @@ class Executor:
                 side_ctx.__enter__()
                 st = _lib.stream()
             drop = float(self.dropout) if (training and cfg.use_gcn) else 0.0
+            xg4 = None
+            if gram_g4 and i < L - 1:
+                need_x = 2 * (rows // N) * ((N + 15) // 16) * 512
+                if acts.XG4.get(i) is None or acts.XG4[i].numel() != need_x:
+                    acts.XG4[i] = torch.empty(need_x, device=self.device, dtype=F32)
+                xg4 = acts.XG4[i]
             ga = _lib.GcnArgs(rows=rows, n=N, c=cfg.D, c_out=C, nsup=cfg.nsup if cfg.use_gcn else 0,
                               sup=ctypes.cast(sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=cfg.NP,
                               h=ptr(acts.H[i]), ld_h=cfg.W,
@@ -624,6 +642,7 @@ class Executor:
                               sup2=self._arr_field(acts.sup2_arr), w_mlp_t=ptr(self.pk("mlp_wT%d" % i)),
                               sup_g4=self._arr_field(acts.g4f_arr),
                               sup_g4b=self._arr_field(acts.g4bf_arr),
+                              xg4=ptr(xg4) if xg4 is not None else None, xg4_support=cfg.nsup - 1,
                               **self.split_fields(sp, i), **self.ksplit_fields(scr))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
@@ -1042,6 +1061,8 @@ class Executor:
                                      sup_g4_t=self._arr_field(getattr(acts, "g4b_arr", None))
                                      if os.environ.get("GWN_GCN_POW_BWD", "1") != "0" else None,
                                      sup_g4b_t=self._arr_field(getattr(acts, "g4bt_arr", None)),
+                                     tg4=ptr(sc["tg4"]) if (defer and getattr(acts, "gram_g4", False)
+                                                            and adp_index >= 0) else None,
                                      **self.ksplit_fields(sc))
                 sb = getattr(acts, "sup_batch", 1)
                 if sb > 1:
@@ -1168,6 +1189,14 @@ class Executor:
         gram launch by 20-30 %, more than the 7 reduce launches it saved)."""
         cfg = self.cfg
         C, W = cfg.C, cfg.W
+        if getattr(acts, "gram_g4", False):
+            # bf16 mode, tiled operands: X / hop 1 from the forward (acts.XG4[i]), t1 / t2 from this backward
+            S = rows // cfg.N
+            half = 4 * S * ((cfg.N + 15) // 16) * 512
+            x, t = acts.XG4[i].data_ptr(), sc["tg4"].data_ptr()
+            _lib.call("gwn_gram_g4_bf16", x, t, x + half, t + half, cfg.N, S, ptr(sc["dadp"]), cfg.NP, 0 if first_adp else 1,
+                      ptr(sc["ws"]), st)
+            return
         h = acts.H[i].data_ptr()
         t = dhc.data_ptr()
         fn = "gwn_gram_bf16" if getattr(acts, "sp_bwd", None) is not None else "gwn_gram"

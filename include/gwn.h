@@ -312,6 +312,11 @@ typedef struct gwn_gcn_args {
    * gwn_support_g4_bf16 copies.  Given, the 16-node tile forward runs with the diffusion on bf16
    * MFMA operands (fp32 accumulation; the mlp, hop pieces, z and BN partials in fp32). */
   const void* const* sup_g4b;
+  /* xg4 (optional, the bf16 16-node tile kernel only: gwn_gcn_t16b_supported): X (the node
+   * features, piece 0) and support
+   * xg4_support's hop-1 piece also written in gwn_gram_g4_bf16's tiled activation layout, X at xg4 and
+   * the hop piece at xg4 + slices*ceil(n/16)*512 (the adaptive-support gram's operands) */
+  float* xg4; int xg4_support;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -335,6 +340,9 @@ long gwn_gcn_bn_partial_count(int rows, int n, int c, int nsup, int ld_sup);
  *   reference's gconv.l.mlp.mlp.weight) writes the pieces in the kernel's input order at
  *   dst + l*layer_stride_elems (>= gwn_split_mlp_elems(nsup, planes)).  Element type: bf16. */
 int gwn_gcn_split_supported(int c, int n, int planes); /* 1 if the split path takes (c, n, planes) */
+/* 1 iff the bf16 16-node tile gcn kernels (sup_g4b / sup_g4b_t) run for n nodes and nsup supports
+ * (their LDS fits): the condition for requesting xg4 / tg4 */
+int gwn_gcn_t16b_supported(int n, int nsup);
 /* the bf16 backward's transposed mlp weights: dst[l][piece][c][c'] = bf16(w[l][c'][piece*32 + c]),
  * at dst + l*layer_stride_elems (>= gwn_bf16_mlpT_elems(nsup)) */
 long gwn_bf16_mlpT_elems(int nsup);
@@ -413,6 +421,10 @@ typedef struct gwn_gcn_bwd_args {
   /* sup_g4b_t [2*nsup] (optional, bf16 operands: split_planes == 1): A_k^T and (A_k^2)^T as
    * gwn_support_g4_bf16 copies: the bf16 16-node tile backward (as sup_g4b of gwn_gcn_args) */
   const void* const* sup_g4b_t;
+  /* tg4 (optional, the bf16 16-node tile kernel only): t1 / t2 of the adaptive support in gwn_gram_g4_bf16's
+   * tiled activation layout (t1 at tg4, t2 at tg4 + slices*ceil(n/16)*512) INSTEAD of dhcat's
+   * columns c .. 3c */
+  float* tg4;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);
@@ -469,6 +481,13 @@ int gwn_gram_bf16(const float* x1, const float* t1, const float* x2, const float
 /* workspace for any gwn_gram launch over AT MOST `slices` slices (non-decreasing in slices, so one
  * query at a schedule's largest layer covers every layer) */
 long gwn_gram_workspace_floats(int n, int slices);
+/* gwn_gram_bf16 (bf16 MFMA operands, fp32 accumulation) on operands in the 16-node tiled
+ * activation layout (written by gwn_gcn_fwd's xg4 and gwn_gcn_bwd's tg4): X[s][16 vt + j][16 oh + 4 g + r] at ((s*nt + vt)*2 + oh)*256 + (16 g + j)*4 + r,
+ * nt = ceil(n/16), rows >= n zero.  dA (+)= sum_s X1_s T1_s^T (+ X2_s T2_s^T); ws holds
+ * gwn_gram_g4_workspace_floats(n, slices) floats (a bound for every smaller launch). */
+int gwn_gram_g4_bf16(const float* x1, const float* t1, const float* x2, const float* t2, int n, int slices,
+                     float* dA, int ld_dA, int accumulate, float* ws, hipStream_t stream);
+long gwn_gram_g4_workspace_floats(int n, int slices);
 
 /* ---------------------------------------------------------------------------------------------
  * BatchNorm2d (model.py:236, bn = nn.BatchNorm2d(c) model.py:152) over the rows of z [rows][c].

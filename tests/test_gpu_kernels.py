@@ -865,6 +865,55 @@ def test_gram_vs_fp64(gpu, n, slices, pairs, ld, accumulate):
     assert torch.equal(dA.cpu()[:, n:], init.float()[:, n:])
 
 
+def _to_g4(a, slices, n):
+    """[slices*n][32] -> gwn_gram_g4's tiled activation layout (include/gwn.h), zero rows past n."""
+    nt = (n + 15) // 16
+    x = torch.zeros(slices, nt * 16, 32, dtype=a.dtype)
+    x[:, :n] = a.reshape(slices, n, 32)
+    # [s][vt][j][oh][g][r] -> [s][vt][oh][g][j][r]
+    x = x.reshape(slices, nt, 16, 2, 4, 4).permute(0, 1, 3, 4, 2, 5)
+    return x.reshape(-1).contiguous()
+
+
+@pytest.mark.parametrize("n,slices,pairs", [(207, 50, 2), (16, 3, 1), (325, 7, 2), (33, 1, 2), (207, 768, 2),
+                                            (883, 13, 2)])
+@pytest.mark.parametrize("accumulate", [0, 1])
+def test_gram_g4_vs_fp64(gpu, n, slices, pairs, accumulate):
+    """gwn_gram_g4_bf16 (the bf16 mode's adaptive-support gram on the 16-node tiled operands the bf16
+    tile kernels write) against an fp64 einsum of the bf16-rounded operands: odd and single tiles,
+    one slice, many splits, accumulation.  The products are exact in fp32, so the bound is the fp32
+    accumulation chain's, as test_gram_vs_fp64."""
+    from gwn_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(n + slices + 1)
+    X = [torch.randn(slices * n, 32, dtype=torch.float64).bfloat16().double() for _ in range(pairs)]
+    T = [torch.randn(slices * n, 32, dtype=torch.float64).bfloat16().double() for _ in range(pairs)]
+    ref = torch.zeros(n, n, dtype=torch.float64)
+    absb = torch.zeros(n, n, dtype=torch.float64)
+    for p in range(pairs):
+        xs, ts = X[p].reshape(slices, n, 32), T[p].reshape(slices, n, 32)
+        ref += torch.einsum("svc,swc->vw", xs, ts)
+        absb += torch.einsum("svc,swc->vw", xs.abs(), ts.abs())
+    ldA = n + 3
+    init = torch.randn(n, ldA, dtype=torch.float64)
+    dA = init.float().to(gpu)
+    if accumulate:
+        ref = ref + init[:, :n].float().double()
+        absb = absb + init[:, :n].abs()
+    Xd = [_to_g4(x.float(), slices, n).to(gpu) for x in X]
+    Td = [_to_g4(t.float(), slices, n).to(gpu) for t in T]
+    ws = torch.empty(lib.gwn_gram_g4_workspace_floats(n, slices) + 16, device=gpu)
+    x2 = Xd[1].data_ptr() if pairs == 2 else None
+    t2 = Td[1].data_ptr() if pairs == 2 else None
+    _lib.call("gwn_gram_g4_bf16", Xd[0].data_ptr(), Td[0].data_ptr(), x2, t2, n, slices, dA.data_ptr(), ldA,
+              accumulate, ws.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    got = dA.double().cpu()[:, :n]
+    bound = 2.0 ** -22 * (slices * 32 * pairs + 8) * absb
+    assert torch.all((got - ref).abs() <= bound + 1e-30), float(((got - ref).abs() / (bound + 1e-30)).max())
+    assert torch.equal(dA.cpu()[:, n:], init.float()[:, n:])
+
+
 def test_nconv2_vs_reference_golden(gpu):
     """nconv2 (model.py:16-22, per-sample supports) on the batched MFMA GEMM against the reference's
     own output and fp64 autograd gradients (tests/golden/make_golden_nconv2.py).  fp32 MFMA chain
