@@ -54,7 +54,7 @@ struct FusedFwd {
   const float* res_mean; const float* res_scale; const float* res_shift;  // (residual - mean) * scale + shift
   int ksplit, slices; float* kws; int* kcnt;  // support split (ksplit > 1): see unit_of()
   int bn_slots;  // t16 kernels: BN partial slots to write (those past the grid get count 0)
-  float* xg4; int xg4_k;  // bf16 t16 kernel: X and support xg4_k's hop 1 in the tiled activation layout
+  void* xg4; int xg4_k;  // bf16 t16 kernel: X and support xg4_k's hop 1 in the tiled activation layout
 };
 
 struct FusedBwd {
@@ -72,7 +72,7 @@ struct FusedBwd {
   const float* fg; const float* dskip; long ld_dskip; long skip_row0; float* dfg;
   long sup_bstride; int sup_batch;  // per-sample supports, as FusedFwd
   int ksplit, slices; float* kws; int* kcnt;  // support split, as FusedFwd
-  float* tg4;  // bf16 t16 kernel: t1 / t2 in the tiled activation layout instead of dhcat's columns
+  void* tg4;  // bf16 t16 kernel: t1 / t2 in the tiled activation layout instead of dhcat's columns
 };
 
 // support k of this workgroup's slice (per-sample supports: sample = slice % sup_batch)
@@ -1354,11 +1354,19 @@ __device__ __forceinline__ T16Range t16_range(int slices, int nt) {
 }
 
 // a tile's 32 channels (lane (g, j): node w0 + j, channels 16 hf + 4 g .. + 3, as the t16
-// accumulators) into the tiled activation layout of gwn_gram_g4: block (slice, tile, hf), 16 B per lane
-__device__ __forceinline__ void t16_store_g4(float* base, int slice, int nt, int tile, int lane, const f32x4v* v) {
+// accumulators) as bf16 into the tiled activation layout of gwn_gram_g4_bf16: one KiB per (slice,
+// tile) of operand `which` (regions of slices * nt KiB), lane (g, j)'s 16 B = channels 4g .. 4g+3
+// then 16+4g .. 16+4g+3 (its MFMA k-group)
+typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void t16_store_g4(void* base, int which, int slices, int slice, int nt, int tile, int lane,
+                                             const f32x4v* v) {
+  bf16x8g r;
 #pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
-    *(f32x4v*)(base + (((long)slice * nt + tile) * 2 + hf) * 256 + lane * 4) = v[hf];
+  for (int i = 0; i < 4; ++i) {
+    r[i] = (__bf16)v[0][i];
+    r[4 + i] = (__bf16)v[1][i];
+  }
+  *(bf16x8g*)((char*)base + (((long)which * slices + slice) * nt + tile) * 1024 + lane * 16) = r;
 }
 
 template <int MAXT>
@@ -1544,12 +1552,12 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
         f32x4v x0[2];
         t16_rows_global(hs_out, ldh, w0, n, lane, x0);
         t16_mlp(ws, LDW16, x0, lane, hacc);
-        if (a.xg4) t16_store_g4(a.xg4, sl, nt, tile, lane, x0);
+        if (a.xg4) t16_store_g4(a.xg4, 0, a.slices, sl, nt, tile, lane, x0);
       }
       for (int k = 0; k < a.nsup; ++k) {
         f32x4v acc[2][2];
         t16b_diffuse(xs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, acc);
-        if (a.xg4 && k == a.xg4_k) t16_store_g4(a.xg4 + (long)a.slices * nt * 512, sl, nt, tile, lane, acc[0]);
+        if (a.xg4 && k == a.xg4_k) t16_store_g4(a.xg4, 1, a.slices, sl, nt, tile, lane, acc[0]);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           t16_mlp(ws + (1 + 2 * k + q) * CH * LDW16, LDW16, acc[q], lane, hacc);
@@ -1700,12 +1708,12 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
           tt[1] = tt[0];
           t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, d0, lane, tt);
           t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[0], lane, tt);
-          if (BF && a.tg4) t16_store_g4(a.tg4, s, nt, tile, lane, tt);
+          if (BF && a.tg4) t16_store_g4(a.tg4, 0, a.slices, s, nt, tile, lane, tt);
           else t16_store(a.t1 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
           tt[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
           tt[1] = tt[0];
           t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, d0, lane, tt);
-          if (BF && a.tg4) t16_store_g4(a.tg4 + (long)a.slices * nt * 512, s, nt, tile, lane, tt);
+          if (BF && a.tg4) t16_store_g4(a.tg4, 1, a.slices, s, nt, tile, lane, tt);
           else t16_store(a.t2 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
         }
       }

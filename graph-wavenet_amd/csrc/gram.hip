@@ -181,113 +181,97 @@ int gram_nsplit(int n, int slices) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// The bf16 mode's gram on operands in the 16-node tiled activation layout (gwn_gcn_args.xg4 /
-// gwn_gcn_bwd_args.tg4, include/gwn.h): a (slice, node tile, channel half) block is one KiB, lane
-// (g, j) holding the 16 B of node 16 vt + j, channels 16 oh + 4 g .. + 3.  One wave owns a 32 x 32
-// output block (2 x 2 tiles of 16 nodes) over a slice range; per (slice, pair) it issues eight
-// 16-B loads (two channel halves of its two row tiles of X and its two column tiles of T, each load
-// a contiguous KiB) for four v_mfma_f32_16x16x32_bf16: lane (g, j)'s eight k values are channels
-// 4g .. 4g+3 and 16+4g .. 16+4g+3 of node j, the same permutation on both operands.  The next
-// step's eight loads are in flight under the current MFMAs.  The row-fragment gram_kernel<., true>
-// issued a load per 32 rows (64 distinct 64-B segments per instruction) instead.
+// The bf16 mode's gram on bf16 operands in the 16-node tiled activation layout (gwn_gcn_args.xg4
+// / gwn_gcn_bwd_args.tg4, include/gwn.h): a (slice, node tile) block is one KiB, lane (g, j)
+// holding the 16 B of node 16 vt + j, channels 4g .. 4g+3 then 16+4g .. 16+4g+3 -- exactly its
+// k-group of v_mfma_f32_16x16x32_bf16 (the same channel permutation on both operands).  One wave
+// owns a TB x TB block of 16-node output tiles over a slice range; per (slice, pair) it issues 2 TB
+// 16-B loads (each a contiguous KiB) for TB^2 MFMAs, the next step's loads in flight.  The operand
+// re-reads (ceil(nt / TB) per side) are the cost: L2-to-CU bandwidth bound, hence bf16 operands
+// written by the producers (half the bytes of fp32).  PEMS bf16 (N = 325, 7 layers): 658 us per
+// step on the row-fragment gram_kernel<., true> (a load per 32 rows), 344 on fp32 tiled operands
+// (TB = 2), 167 on bf16 ones, TB = 2 / 3 / 4 alike (21.51k / 21.54k / 21.53k samples/s).
 typedef float f32x4g __attribute__((ext_vector_type(4)));
 constexpr int G4_WAVES = 2048;  // target waves of a launch
+constexpr int G4_TB = 3;        // 16-node tiles per side of a wave's output block
 
 struct GramG4 {
-  const float* X[2]; const float* T[2];  // [slices][nt][2][256] each
-  int nt, slices, nsplit, npair, nb;     // nb = ceil(nt / 2) output blocks per side
+  const void* X[2]; const void* T[2];    // [slices][nt] KiB each
+  int nt, slices, nsplit, npair, nb;     // nb = ceil(nt / TB) output blocks per side
   long np;                               // partial row stride (32 * ceil(n / 32))
   float* part;                           // [nsplit][np][np]
 };
 
-__device__ __forceinline__ bf16x8 g4_bf16x8(const f32x4g& a, const f32x4g& b) {
-  bf16x8 r;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    r[i] = (__bf16)a[i];
-    r[4 + i] = (__bf16)b[i];
-  }
-  return r;
-}
-
+template <int TB>
 __global__ __launch_bounds__(64) void gram_g4_kernel(const GramG4 g) {
   const int lane = threadIdx.x, gq = lane >> 4, j = lane & 15;
   const int b = blockIdx.x, xcd = b % NXCD, q = b / NXCD;
   const int per_split = g.nb * g.nb;
   const int blk = q % per_split, split = (q / per_split) * NXCD + xcd;  // a split's blocks share an XCD
   if (split >= g.nsplit) return;
-  const int vt0 = 2 * (blk / g.nb), wt0 = 2 * (blk % g.nb);
-  const bool v2 = vt0 + 1 < g.nt, w2 = wt0 + 1 < g.nt;  // wave-uniform: a second tile exists
+  const int vt0 = TB * (blk / g.nb), wt0 = TB * (blk % g.nb);
   const int s0 = (int)((long)g.slices * split / g.nsplit), s1 = (int)((long)g.slices * (split + 1) / g.nsplit);
-  const long bytes = (long)g.slices * g.nt * 2048;
+  const long bytes = (long)g.slices * g.nt * 1024;
   __amdgpu_buffer_rsrc_t rx[2], rt[2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     rx[p] = rsrc(g.X[p], bytes);
     rt[p] = rsrc(g.T[p], bytes);
   }
-  // block (s, tile, oh) at ((s * nt + tile) * 2 + oh) KiB; lane's 16 B at lane * 16
-  auto off = [&](int s_, int tile, bool ok) {
-    return ok && s_ < s1 ? (int)(((long)s_ * g.nt + tile) * 2048 + lane * 16) : OOR;
+  // block (s, tile) at (s * nt + tile) KiB; lane's 16 B at lane * 16; tiles past nt (wave-uniform)
+  // read zeros
+  auto off = [&](int s_, int tile) {
+    return tile < g.nt && s_ < s1 ? (int)(((long)s_ * g.nt + tile) * 1024 + lane * 16) : OOR;
   };
-  f32x4g acc[2][2];
+  f32x4g acc[TB][TB];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < TB; ++x)
 #pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
-  // fragments of (slice, pair): [tile][half]; p unrolled so the buffer resources stay scalar
-  auto load = [&](int s_, int p, f32x4g (*av)[2], f32x4g (*bv)[2]) {
-    const int ox[2] = {off(s_, vt0, true), off(s_, vt0 + 1, v2)};
-    const int ot[2] = {off(s_, wt0, true), off(s_, wt0 + 1, w2)};
+    for (int y = 0; y < TB; ++y) acc[x][y] = f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
+  // fragments of (slice, pair); p unrolled so the buffer resources stay scalar
+  auto load = [&](int s_, int p, bf16x8* av, bf16x8* bv) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        av[t][h] = __builtin_bit_cast(f32x4g, __builtin_amdgcn_raw_buffer_load_b128(rx[p], ox[t], 1024 * h, 0));
-        bv[t][h] = __builtin_bit_cast(f32x4g, __builtin_amdgcn_raw_buffer_load_b128(rt[p], ot[t], 1024 * h, 0));
-      }
+    for (int t = 0; t < TB; ++t) {
+      av[t] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx[p], off(s_, vt0 + t), 0, 0));
+      bv[t] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rt[p], off(s_, wt0 + t), 0, 0));
+    }
   };
-  f32x4g a[2][2], bb[2][2];
+  bf16x8 a[TB], bb[TB];
   load(s0, 0, a, bb);
   for (int s_ = s0; s_ < s1; ++s_) {
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       if (p >= g.npair) break;
-      f32x4g na[2][2], nb[2][2];
+      bf16x8 na[TB], nb[TB];
       if (p + 1 < g.npair) load(s_, 1, na, nb);
       else load(s_ + 1, 0, na, nb);
       __builtin_amdgcn_sched_barrier(0);
-      const bf16x8 ax[2] = {g4_bf16x8(a[0][0], a[0][1]), g4_bf16x8(a[1][0], a[1][1])};
-      const bf16x8 by[2] = {g4_bf16x8(bb[0][0], bb[0][1]), g4_bf16x8(bb[1][0], bb[1][1])};
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+      for (int x = 0; x < TB; ++x)
 #pragma unroll
-        for (int y = 0; y < 2; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[x], by[y], acc[x][y], 0, 0, 0);
+        for (int y = 0; y < TB; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[x], bb[y], acc[x][y], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          a[t][h] = na[t][h];
-          bb[t][h] = nb[t][h];
-        }
+      for (int t = 0; t < TB; ++t) {
+        a[t] = na[t];
+        bb[t] = nb[t];
+      }
     }
   }
   // D[v][w]: lane (g, j) holds rows 4 g + r of the tile, column j
   float* out = g.part + (long)split * g.np * g.np;
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < TB; ++x)
 #pragma unroll
-    for (int y = 0; y < 2; ++y) {
-      if ((x && !v2) || (y && !w2)) continue;
+    for (int y = 0; y < TB; ++y) {
+      if (vt0 + x >= g.nt || wt0 + y >= g.nt) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         out[(long)(16 * (vt0 + x) + 4 * gq + r) * g.np + 16 * (wt0 + y) + j] = acc[x][y][r];
     }
 }
 
-int gram_g4_nsplit(int nt, int slices) {
-  const int nb = (nt + 1) / 2;
+int gram_g4_nsplit(int nb, int slices) {
   int target = G4_WAVES / (nb * nb);
   target = (target / NXCD) * NXCD;
   if (target < NXCD) target = NXCD;
@@ -298,24 +282,24 @@ int gram_g4_nsplit(int nt, int slices) {
 }  // namespace
 
 // dA (+)= sum_s X1_s T1_s^T (+ X2_s T2_s^T) on bf16 operands in the 16-node tiled activation layout
-int gwn_gram_g4_bf16(const float* x1, const float* t1, const float* x2, const float* t2, int n, int slices, float* dA,
+int gwn_gram_g4_bf16(const void* x1, const void* t1, const void* x2, const void* t2, int n, int slices, float* dA,
                 int ld_dA, int accumulate, float* ws, hipStream_t s) {
   GWN_REQUIRE(n > 0 && slices > 0 && x1 && t1 && ws && !x2 == !t2, "gram_g4_bf16: bad arguments");
   GramG4 g = {};
   g.X[0] = x1; g.T[0] = t1; g.X[1] = x2 ? x2 : x1; g.T[1] = t2 ? t2 : t1;
   g.npair = x2 ? 2 : 1;
   g.nt = (n + 15) / 16;
-  g.nb = (g.nt + 1) / 2;
+  g.nb = (g.nt + G4_TB - 1) / G4_TB;
   g.slices = slices;
-  g.nsplit = gram_g4_nsplit(g.nt, slices);
+  g.nsplit = gram_g4_nsplit(g.nb, slices);
   g.np = 32L * ((n + 31) / 32);
   g.part = ws;
-  GWN_REQUIRE((long)slices * g.nt * 2048 < 0x7fff0000L, "gram_g4_bf16: operand beyond a 2 GB buffer window");
+  GWN_REQUIRE((long)slices * g.nt * 1024 < 0x7fff0000L, "gram_g4_bf16: operand beyond a 2 GB buffer window");
   GWN_REQUIRE((long)g.nsplit * g.np * g.np <= gwn_gram_workspace_floats(n, slices) ||
                   (long)g.nsplit * g.np * g.np <= gwn_gram_g4_workspace_floats(n, slices),
               "gram_g4_bf16: workspace");
   const int blocks = ((g.nsplit + NXCD - 1) / NXCD) * NXCD * g.nb * g.nb;
-  gram_g4_kernel<<<blocks, 64, 0, s>>>(g);
+  gram_g4_kernel<G4_TB><<<blocks, 64, 0, s>>>(g);
   GWN_CHECK_LAUNCH();
   const long outs = (long)n * n;
   gram_reduce_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(ws, g.nsplit, n, (int)g.np, dA, ld_dA, accumulate);
@@ -324,13 +308,9 @@ int gwn_gram_g4_bf16(const float* x1, const float* t1, const float* x2, const fl
 }
 
 long gwn_gram_g4_workspace_floats(int n, int slices) {
-  const int nt = (n + 15) / 16, nb = (nt + 1) / 2;
-  int bound = G4_WAVES / (nb * nb);
-  bound = (bound / NXCD) * NXCD;
-  if (bound < NXCD) bound = NXCD;
-  if (bound > slices) bound = slices;
+  const int nt = (n + 15) / 16;
   const long np = 32L * ((n + 31) / 32);
-  return (long)(bound < 1 ? 1 : bound) * np * np;
+  return (long)gram_g4_nsplit((nt + G4_TB - 1) / G4_TB, slices) * np * np;
 }
 
 // Partial-sum floats of a gram launch over AT MOST `slices` slices.  gram_nsplit is not monotone

@@ -393,7 +393,7 @@ class Executor:
             "dxa": e(ts[0] * P, C),
             "dxb": e(ts[0] * P, C),
             # bf16 mode: t1 / t2 of the adaptive support in the tiled activation layout (gwn_gram_g4_bf16)
-            "tg4": e(2 * (maxrows // N) * ((N + 15) // 16) * 512),
+            "tg4": e(2 * (maxrows // N) * ((N + 15) // 16) * 256),
             "dfg": e(maxrows, 2 * D),
             "dh": e(maxrows, C),
             "dhc": e(maxrows, cfg.W),
@@ -623,7 +623,7 @@ class Executor:
             drop = float(self.dropout) if (training and cfg.use_gcn) else 0.0
             xg4 = None
             if gram_g4 and i < L - 1:
-                need_x = 2 * (rows // N) * ((N + 15) // 16) * 512
+                need_x = 2 * (rows // N) * ((N + 15) // 16) * 256  # two bf16 operands, a KiB per tile
                 if acts.XG4.get(i) is None or acts.XG4[i].numel() != need_x:
                     acts.XG4[i] = torch.empty(need_x, device=self.device, dtype=F32)
                 xg4 = acts.XG4[i]
@@ -1192,7 +1192,7 @@ class Executor:
         if getattr(acts, "gram_g4", False):
             # bf16 mode, tiled operands: X / hop 1 from the forward (acts.XG4[i]), t1 / t2 from this backward
             S = rows // cfg.N
-            half = 4 * S * ((cfg.N + 15) // 16) * 512
+            half = S * ((cfg.N + 15) // 16) * 1024  # bytes of one bf16 operand
             x, t = acts.XG4[i].data_ptr(), sc["tg4"].data_ptr()
             _lib.call("gwn_gram_g4_bf16", x, t, x + half, t + half, cfg.N, S, ptr(sc["dadp"]), cfg.NP, 0 if first_adp else 1,
                       ptr(sc["ws"]), st)

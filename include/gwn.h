@@ -313,10 +313,10 @@ typedef struct gwn_gcn_args {
    * MFMA operands (fp32 accumulation; the mlp, hop pieces, z and BN partials in fp32). */
   const void* const* sup_g4b;
   /* xg4 (optional, the bf16 16-node tile kernel only: gwn_gcn_t16b_supported): X (the node
-   * features, piece 0) and support
-   * xg4_support's hop-1 piece also written in gwn_gram_g4_bf16's tiled activation layout, X at xg4 and
-   * the hop piece at xg4 + slices*ceil(n/16)*512 (the adaptive-support gram's operands) */
-  float* xg4; int xg4_support;
+   * features, piece 0) and support xg4_support's hop-1 piece also written as bf16 in
+   * gwn_gram_g4_bf16's tiled activation layout, X in the first slices*ceil(n/16) KiB, the hop piece
+   * in the next (the adaptive-support gram's operands) */
+  void* xg4; int xg4_support;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -421,10 +421,10 @@ typedef struct gwn_gcn_bwd_args {
   /* sup_g4b_t [2*nsup] (optional, bf16 operands: split_planes == 1): A_k^T and (A_k^2)^T as
    * gwn_support_g4_bf16 copies: the bf16 16-node tile backward (as sup_g4b of gwn_gcn_args) */
   const void* const* sup_g4b_t;
-  /* tg4 (optional, the bf16 16-node tile kernel only): t1 / t2 of the adaptive support in gwn_gram_g4_bf16's
-   * tiled activation layout (t1 at tg4, t2 at tg4 + slices*ceil(n/16)*512) INSTEAD of dhcat's
-   * columns c .. 3c */
-  float* tg4;
+  /* tg4 (optional, the bf16 16-node tile kernel only): t1 / t2 of the adaptive support as bf16
+   * in gwn_gram_g4_bf16's tiled activation layout (t1 in the first slices*ceil(n/16) KiB, t2 in the
+   * next) INSTEAD of dhcat's columns c .. 3c */
+  void* tg4;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);
 long gwn_gcn_bwd_workspace_floats(int rows, int n, int c, int nsup);
@@ -481,11 +481,12 @@ int gwn_gram_bf16(const float* x1, const float* t1, const float* x2, const float
 /* workspace for any gwn_gram launch over AT MOST `slices` slices (non-decreasing in slices, so one
  * query at a schedule's largest layer covers every layer) */
 long gwn_gram_workspace_floats(int n, int slices);
-/* gwn_gram_bf16 (bf16 MFMA operands, fp32 accumulation) on operands in the 16-node tiled
- * activation layout (written by gwn_gcn_fwd's xg4 and gwn_gcn_bwd's tg4): X[s][16 vt + j][16 oh + 4 g + r] at ((s*nt + vt)*2 + oh)*256 + (16 g + j)*4 + r,
- * nt = ceil(n/16), rows >= n zero.  dA (+)= sum_s X1_s T1_s^T (+ X2_s T2_s^T); ws holds
+/* gwn_gram_bf16 on bf16 operands in the 16-node tiled activation layout (written by gwn_gcn_fwd's
+ * xg4 and gwn_gcn_bwd's tg4): X[s][16 vt + j][c] at byte ((s*nt + vt)*64 + 16 g + j)*16 + 2 e for
+ * c = 4 g + e (e < 4) and c = 16 + 4 g + e - 4 (e >= 4), nt = ceil(n/16), nodes >= n zero.
+ * dA (+)= sum_s X1_s T1_s^T (+ X2_s T2_s^T) with fp32 accumulation; ws holds
  * gwn_gram_g4_workspace_floats(n, slices) floats (a bound for every smaller launch). */
-int gwn_gram_g4_bf16(const float* x1, const float* t1, const float* x2, const float* t2, int n, int slices,
+int gwn_gram_g4_bf16(const void* x1, const void* t1, const void* x2, const void* t2, int n, int slices,
                      float* dA, int ld_dA, int accumulate, float* ws, hipStream_t stream);
 long gwn_gram_g4_workspace_floats(int n, int slices);
 

@@ -866,13 +866,14 @@ def test_gram_vs_fp64(gpu, n, slices, pairs, ld, accumulate):
 
 
 def _to_g4(a, slices, n):
-    """[slices*n][32] -> gwn_gram_g4's tiled activation layout (include/gwn.h), zero rows past n."""
+    """[slices*n][32] -> gwn_gram_g4_bf16's bf16 tiled activation layout (include/gwn.h): lane (g, j)
+    of a (slice, tile) KiB holds node 16 vt + j, channels 4g .. 4g+3 then 16+4g .. 16+4g+3."""
     nt = (n + 15) // 16
     x = torch.zeros(slices, nt * 16, 32, dtype=a.dtype)
     x[:, :n] = a.reshape(slices, n, 32)
-    # [s][vt][j][oh][g][r] -> [s][vt][oh][g][j][r]
-    x = x.reshape(slices, nt, 16, 2, 4, 4).permute(0, 1, 3, 4, 2, 5)
-    return x.reshape(-1).contiguous()
+    # [s][vt][j][oh][g][r] -> [s][vt][g][j][oh][r]
+    x = x.reshape(slices, nt, 16, 2, 4, 4).permute(0, 1, 4, 2, 3, 5)
+    return x.reshape(-1).contiguous().bfloat16()
 
 
 @pytest.mark.parametrize("n,slices,pairs", [(207, 50, 2), (16, 3, 1), (325, 7, 2), (33, 1, 2), (207, 768, 2),
