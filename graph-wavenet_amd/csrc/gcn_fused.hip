@@ -1854,8 +1854,18 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_bwd_pow_kernel(const FusedBwd a, 
 // 4-wave workgroup per 32 x 32 output tile on v_mfma_f32_32x32x2_f32, each wave a quarter of K
 // (np / 2 k-steps, a multiple of 16) with its operands loaded four k-steps ahead; the four partial
 // tiles are added in wave order through LDS.  Also A^T when at != nullptr.
+// element (r, c) of a padded support into its gwn_support_g4 copy (r, c < 16 * nt)
+__device__ __forceinline__ void g4_put(float* dst, int nt, int r, int c, float v) {
+  if (r < 16 * nt && c < 16 * nt)
+    dst[((long)((r >> 4) * nt + (c >> 4)) * 64 + 16 * (r & 3) + (c & 15)) * 4 + ((r & 15) >> 2)] = v;
+}
+
+// A^2, (A^2)^T and optionally A^T of a padded support; with g4, also the gwn_support_g4 copies of
+// A and A^2 (g4 + 0 / 1 * g4_stride) and, with g4_count == 4, of A^T and (A^2)^T (2 / 3) -- the
+// adaptive support's per-step preparation in one launch
 __global__ __launch_bounds__(256) void support_square_kernel(const float* A, int np, int ld, float* C, float* CT,
-                                                             float* AT) {
+                                                             float* AT, float* g4, long g4_stride, int g4_nt,
+                                                             int g4_count) {
   __shared__ float red[4][32][33];
   const int ti = blockIdx.y * 32, tj = blockIdx.x * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
@@ -1882,12 +1892,24 @@ __global__ __launch_bounds__(256) void support_square_kernel(const float* A, int
     C[(long)(ti + i) * ld + tj + j] = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
     const int jt = e >> 5, it = e & 31;  // C^T rows: C[. ][jt] down the column
     CT[(long)(tj + jt) * ld + ti + it] = ((red[0][it][jt] + red[1][it][jt]) + red[2][it][jt]) + red[3][it][jt];
+    if (g4) {
+      const float v = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
+      g4_put(g4 + g4_stride, g4_nt, ti + i, tj + j, v);
+      if (g4_count == 4) g4_put(g4 + 3 * g4_stride, g4_nt, tj + j, ti + i, v);
+    }
   }
-  if (AT) {
+  if (AT || g4) {
     __syncthreads();
     for (int e = threadIdx.x; e < 1024; e += 256) red[0][e >> 5][e & 31] = A[(long)(ti + (e >> 5)) * ld + tj + (e & 31)];
     __syncthreads();
-    for (int e = threadIdx.x; e < 1024; e += 256) AT[(long)(tj + (e >> 5)) * ld + ti + (e & 31)] = red[0][e & 31][e >> 5];
+    for (int e = threadIdx.x; e < 1024; e += 256) {
+      if (AT) AT[(long)(tj + (e >> 5)) * ld + ti + (e & 31)] = red[0][e & 31][e >> 5];
+      if (g4) {
+        const int i = e >> 5, j = e & 31;
+        g4_put(g4, g4_nt, ti + i, tj + j, red[0][i][j]);
+        if (g4_count == 4) g4_put(g4 + 2 * g4_stride, g4_nt, tj + j, ti + i, red[0][i][j]);
+      }
+    }
   }
 }
 
@@ -2291,9 +2313,18 @@ extern "C" long gwn_gcn_bn_partial_count(int rows, int n, int c, int nsup, int l
 }
 
 extern "C" int gwn_support_square(const float* a, int np, int ld, float* a2, float* a2_t, float* a_t, hipStream_t s) {
+  return gwn_support_square_g4(a, np, ld, a2, a2_t, a_t, 0, nullptr, 0, 0, s);
+}
+
+extern "C" int gwn_support_square_g4(const float* a, int np, int ld, float* a2, float* a2_t, float* a_t, int n,
+                                     float* g4, long g4_stride, int g4_count, hipStream_t s) {
   GWN_REQUIRE(a && a2 && a2_t && np > 0 && np % 32 == 0 && ld >= np, "support_square: np must be a multiple of 32");
+  GWN_REQUIRE(!g4 || (n > 0 && (n + 31) / 32 * 32 <= np && (g4_count == 2 || g4_count == 4) &&
+                      g4_stride >= gwn_support_g4_floats(n)),
+              "support_square_g4: needs n <= np, g4_count 2 or 4 and g4_stride >= gwn_support_g4_floats(n)");
   dim3 grid(np / 32, np / 32);
-  support_square_kernel<<<grid, 256, 0, s>>>(a, np, ld, a2, a2_t, a_t);
+  support_square_kernel<<<grid, 256, 0, s>>>(a, np, ld, a2, a2_t, a_t, g4, g4_stride, g4 ? (n + 15) / 16 : 0,
+                                             g4_count);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

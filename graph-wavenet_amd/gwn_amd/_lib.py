@@ -217,6 +217,8 @@ _SIGS = [
                                        c_void_p, c_void_p, c_void_p]),
     ("gwn_fused_occupancy", c_int, [c_int, c_int, c_int]),
     ("gwn_support_square", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("gwn_support_square_g4", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_long,
+                                      c_int, c_void_p]),
     ("gwn_support_g4_floats", c_long, [c_int]),
     ("gwn_support_g4_bf16_elems", c_long, [c_int]),
     ("gwn_support_g4_bf16", c_int, [ctypes.POINTER(c_void_p), c_int, c_int, c_int, c_void_p, c_long, c_void_p]),

@@ -534,18 +534,20 @@ class Executor:
                     if getattr(acts, "supT", None) is None or len(acts.supT) != len(sups) or acts.supT[0].numel() != sq:
                         acts.supT = [torch.empty(sq, device=self.device, dtype=F32) for _ in sups]
                     adp_t, adp_t_done = acts.supT[-1], True
-                lib.call("gwn_support_square", ptr(acts.adp), cfg.NP, cfg.NP, ptr(acts.adp2), ptr(acts.adp2_t),
-                         ptr(adp_t), st)
                 sq2, sq2t = sq2 + [acts.adp2], sq2t + [acts.adp2_t]
                 if self._t16_ok():
-                    # the adaptive support's 16-node tile copies, rewritten every step (one launch)
-                    mats = [acts.adp, acts.adp2] + ([adp_t, acts.adp2_t] if training else [])
+                    # the square, the transposes and the adaptive support's 16-node tile copies
+                    # (A, A^2 and, training, A^T, (A^2)^T), rewritten every step by one launch
                     fl = int(_lib.load().gwn_support_g4_floats(N))
-                    if getattr(acts, "g4_adp", None) is None or acts.g4_adp.shape[0] < len(mats):
+                    if getattr(acts, "g4_adp", None) is None:
                         acts.g4_adp = torch.empty(4, fl, device=self.device, dtype=F32)
-                    self._g4_into(mats, acts.g4_adp)
+                    lib.call("gwn_support_square_g4", ptr(acts.adp), cfg.NP, cfg.NP, ptr(acts.adp2), ptr(acts.adp2_t),
+                             ptr(adp_t), N, ptr(acts.g4_adp), fl, 4 if training else 2, st)
                     g4f_p += [acts.g4_adp[0].data_ptr(), acts.g4_adp[1].data_ptr()]
                     g4b_p += [acts.g4_adp[2].data_ptr(), acts.g4_adp[3].data_ptr()]
+                else:
+                    lib.call("gwn_support_square", ptr(acts.adp), cfg.NP, cfg.NP, ptr(acts.adp2), ptr(acts.adp2_t),
+                             ptr(adp_t), st)
             acts.sup2_arr = (ctypes.c_void_p * len(sq2))(*[t_.data_ptr() for t_ in sq2])
             acts.sup2t_arr = (ctypes.c_void_p * len(sq2t))(*[t_.data_ptr() for t_ in sq2t])
             if self._t16_ok() and len(g4f_p) == 2 * len(sups):

@@ -532,6 +532,11 @@ int gwn_fused_occupancy(int n, int backward, int pow);
  * a2 = a a, a2_t = (a a)^T, and a_t = a^T when a_t != NULL, all [np][ld] like a (a padded support,
  * zero outside [n][n]; np a multiple of 32).  One launch (f32 MFMA). */
 int gwn_support_square(const float* a, int np, int ld, float* a2, float* a2_t, float* a_t, hipStream_t stream);
+/* gwn_support_square that also writes the gwn_support_g4 copies (g4_stride floats apart) of A and
+ * A^2 (copies 0, 1) and, with g4_count == 4, of A^T and (A^2)^T (copies 2, 3): the adaptive
+ * support's per-step preparation for the 16-node tile kernels in one launch (n <= np) */
+int gwn_support_square_g4(const float* a, int np, int ld, float* a2, float* a2_t, float* a_t, int n, float* g4,
+                          long g4_stride, int g4_count, hipStream_t stream);
 /* 16-node k-interleaved copies of `count` padded [np][ld] supports src[c] (zero outside [n][n]) for
  * the 16-node tile kernels (gwn_gcn_args.sup_g4): with nt = ceil(n/16) column tiles and
  * nkg = ceil(n/16) groups of four 4-row k-steps,

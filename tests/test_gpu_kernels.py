@@ -548,6 +548,39 @@ def test_support_g4_layout(gpu, n):
 
 
 @pytest.mark.parametrize("n", [16, 37, 207, 325])
+@pytest.mark.parametrize("count", [2, 4])
+def test_support_square_g4(gpu, n, count):
+    """gwn_support_square_g4: the square / transposes as gwn_support_square, and the 16-node tile
+    copies of A, A^2 (, A^T, (A^2)^T) bit-identical to gwn_support_g4 of those matrices."""
+    import ctypes
+    from gwn_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(n + count)
+    NP = (n + 31) // 32 * 32
+    a = torch.zeros(NP, NP, device=gpu)
+    a[:n, :n] = torch.rand(n, n, device=gpu)
+    fl = lib.gwn_support_g4_floats(n)
+    outs = [torch.full((NP, NP), float("nan"), device=gpu) for _ in range(3)]
+    g4 = torch.full((4, fl), float("nan"), device=gpu)
+    _lib.call("gwn_support_square_g4", a.data_ptr(), NP, NP, outs[0].data_ptr(), outs[1].data_ptr(),
+              outs[2].data_ptr(), n, g4.data_ptr(), fl, count, _lib.stream())
+    ref_sq = [torch.full((NP, NP), float("nan"), device=gpu) for _ in range(3)]
+    _lib.call("gwn_support_square", a.data_ptr(), NP, NP, ref_sq[0].data_ptr(), ref_sq[1].data_ptr(),
+              ref_sq[2].data_ptr(), _lib.stream())
+    mats = [a, ref_sq[0], ref_sq[2], ref_sq[1]][:count]
+    ref = torch.full((count, fl), float("nan"), device=gpu)
+    src = (ctypes.c_void_p * count)(*[m.data_ptr() for m in mats])
+    _lib.call("gwn_support_g4", ctypes.cast(src, ctypes.POINTER(ctypes.c_void_p)), count, n, NP, ref.data_ptr(), fl,
+              _lib.stream())
+    torch.cuda.synchronize()
+    for o, r in zip(outs, ref_sq):
+        assert torch.equal(o, r)
+    assert torch.equal(g4[:count], ref)
+    if count == 2:
+        assert torch.all(torch.isnan(g4[2:]))
+
+
+@pytest.mark.parametrize("n", [16, 37, 207, 325])
 def test_support_square(gpu, n):
     """gwn_support_square: A^2 and its transpose (and A^T) of a padded support against fp64; the
     padding stays zero.  Bound: fp32 FMA chain over K = np terms."""
