@@ -37,12 +37,11 @@ BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 CONFIGS = {
     # batch per GPU, nodes, steps, graph, workload label, oracle / CPU sample batch
     "metr": dict(B=64, N=207, T=12, dense=False, graph_seed=0, sample_b=64,
-                 workload="METR-LA train step B=64/GPU N=207 T=12 fp32 (configs[1])"),
+                 workload="METR-LA train step B=64/GPU N=207 T=12 {dtype} (configs[1])"),
     "pems": dict(B=64, N=325, T=12, dense=False, graph_seed=6, sample_b=16, dtype="bf16",
-                 workload="PEMS-BAY-shape train step B=64/GPU N=325 T=12, bf16 MFMA operands with fp32 "
-                          "accumulation in the diffusion GCN (configs[2])"),
+                 workload="PEMS-BAY-shape train step B=64/GPU N=325 T=12 {dtype} (configs[2])"),
     "n2048": dict(B=32, N=2048, T=24, dense=True, graph_seed=15, sample_b=1,
-                  workload="synthetic dense-graph train step B=32/GPU N=2048 T=24 fp32 (configs[4])"),
+                  workload="synthetic dense-graph train step B=32/GPU N=2048 T=24 {dtype} (configs[4])"),
 }
 
 
@@ -110,6 +109,7 @@ def main():
     # puts every rank on cuda:0 over gloo (RCCL refuses two ranks on one device)
     if os.environ.get("GWN_SHARE_DEVICE", "0") != "0":
         local = 0
+    backend = None
     if world > 1:
         backend = os.environ.get("GWN_DIST_BACKEND", "nccl")
         if backend == "nccl":
@@ -160,10 +160,11 @@ def main():
         last = eng.train(xs[i % nb], ys[i % nb])
     barrier()
     elapsed = time.perf_counter() - t0
+    dist_info = None
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, dist_info = rank_timing(elapsed, world, rank, dev)
+        dist_info["device_per_rank"] = ("cuda:%d" % local if os.environ.get("GWN_SHARE_DEVICE", "0") == "0"
+                                        else "cuda:0 (shared: rehearsal)")
     samples = world * B * args.steps
     value = samples / elapsed
     ms = 1000.0 * elapsed / args.steps
@@ -190,7 +191,9 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if bf16 else "f32",
             "data": "synthetic (%s, seeded; random-init weights)"
                     % ("METR-LA tensor format" if not cfg["dense"] else "METR-LA tensor format, dense random graph"),
-            "config": {"workload": cfg["workload"], "global_batch": B * world, "nodes": N, "seq_len": T,
+            "config": {"workload": cfg["workload"].format(
+                           dtype="bf16 MFMA operands with fp32 accumulation in the diffusion GCN" if bf16 else "fp32"),
+                       "global_batch": B * world, "nodes": N, "seq_len": T,
                        "parallelism": "dp%d" % world if world > 1 else "single"},
             "mae12": round(mae12, 6), "mae12_oracle_f64": round(mae12_ref, 6),
             "mae12_delta": float("%.3g" % abs(mae12 - mae12_ref)), "mae12_sample_batch": sb,
@@ -198,12 +201,32 @@ def main():
             "step_effective_tflops": round(step_flops(N, T) * B * world / (elapsed / args.steps) / 1e12 / world, 3),
             "roofline": roof,
         }
+        if dist_info is not None:
+            result["distributed"] = dist_info
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfg)
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+
+
+def rank_timing(elapsed, world, rank, dev):
+    """MAX over ranks of the timed region (the contract's whole-job time) and a record of what
+    torch.distributed saw: backend, world size, min / max of the per-rank timed regions.  Without
+    GWN_DIST_BACKEND (the driver's runs) the backend must be nccl (= RCCL)."""
+    t = torch.zeros(world, device=dev, dtype=torch.float64)
+    t[rank] = elapsed
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM)
+    per_rank = [float(v) for v in t.cpu()]
+    seen_backend = str(torch.distributed.get_backend())
+    seen_world = torch.distributed.get_world_size()
+    if "GWN_DIST_BACKEND" not in os.environ and seen_backend != "nccl":
+        raise SystemExit("bench.py: expected the nccl (RCCL) backend, torch.distributed reports %s" % seen_backend)
+    if seen_world != world:
+        raise SystemExit("bench.py: WORLD_SIZE %d but torch.distributed sees %d ranks" % (world, seen_world))
+    return max(per_rank), {"backend": seen_backend, "world_seen": seen_world,
+                           "rank_seconds_min": round(min(per_rank), 6), "rank_seconds_max": round(max(per_rank), 6)}
 
 
 def measure_dominant(eng, dev, rounds=5, bf16=False):
@@ -258,14 +281,16 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
     fused = N <= 512
     def pmc(name, key):
         # HBM bytes per launch and MFMA busy fraction from the committed PMC passes of this kernel
-        # over this bench (tools/gpu_pmc_r3.sh + tools/pmc_summary.py: separate --pmc runs for
+        # over this bench (tools/gpu.sh pmc:<cfg> + tools/pmc_summary.py: separate --pmc runs for
         # FETCH_SIZE, WRITE_SIZE and the SQ counters; FETCH x2 per the gfx950 correction)
-        path = os.path.join(ROOT, "profiles", "r03", name)
-        if not os.path.exists(path):
-            return None, None, None
-        with open(path) as f:
-            rec = json.load(f).get(key, {})
-        return rec.get("hbm_bytes_per_dispatch"), rec.get("mfma_busy_frac"), "profiles/r03/" + name
+        # (the newest round's committed passes)
+        for rnd in ("r04", "r03"):
+            path = os.path.join(ROOT, "profiles", rnd, name)
+            if os.path.exists(path):
+                with open(path) as f:
+                    rec = json.load(f).get(key, {})
+                return rec.get("hbm_bytes_per_dispatch"), rec.get("mfma_busy_frac"), "profiles/%s/%s" % (rnd, name)
+        return None, None, None
 
     if bf16:
         # bf16 operands: arithmetic intensity (~80 FLOP/B algorithmic) sits far below the bf16

@@ -661,16 +661,23 @@ __global__ void loss_terms_kernel(const float* out, const float* real, long rsb,
   s_mae = block_sum<256>(s_mae, sh);
   s_mape = block_sum<256>(s_mape, sh);
   s_mse = block_sum<256>(s_mse, sh);
-  // hand-off to the last block to arrive (MI355X_MICROARCH.md, inter-workgroup visibility, the
-  // one-lane-per-workgroup row: sc1 (write-through) partial stores, drained, one agent-scope add;
-  // the last arriver reads every partial with sc1 loads)
+  // hand-off to the last block to arrive (MI355X_MICROARCH.md, inter-workgroup visibility): sc1
+  // (write-through) partial stores, an agent release before the one agent-scope add, and an agent
+  // acquire in the last arriver before it reads every partial (sc1 loads); one lane per block, so
+  // the fences cost ~2 x 1.7 us once per step
   __shared__ int last;
   if (threadIdx.x == 0) {
     __hip_atomic_store(ws + 1 + blockIdx.x * 3, s_mae, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(ws + 2 + blockIdx.x * 3, s_mape, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(ws + 3 + blockIdx.x * 3, s_mse, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = atomicAdd((int*)(ws + LOSS_ARRIVE), 1) == (int)gridDim.x - 1;
+    const int is_last = atomicAdd((int*)(ws + LOSS_ARRIVE), 1) == (int)gridDim.x - 1;
+    if (is_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    last = is_last;
   }
   __syncthreads();
   if (!last) return;
@@ -1246,6 +1253,10 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
               "(sup_t given, c == 32, n <= 512)");
   const float* dh = a->bn_dy ? a->dh_out : a->dh;
   const bool wgrads = !a->skip_weight_grads;  // else the caller runs gwn_wgrad / gwn_gram itself
+  // with tg4 the bf16 tile backward writes t1 / t2 there instead of dhcat's columns c..3c, so the
+  // in-library adjacency gram (which reads those columns) would see stale memory
+  GWN_REQUIRE(!a->tg4 || !wgrads || a->adp_index < 0 || !a->dadp,
+              "gcn_bwd: tg4 needs skip_weight_grads (the caller runs gwn_gram_g4_bf16 on tg4)");
   int rc = GWN_OK;
   if (fused) {
     // fused: dxg -> dhcat piece 0 (or dfg through the gate epilogue); for the adaptive support

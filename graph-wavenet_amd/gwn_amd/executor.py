@@ -579,7 +579,8 @@ class Executor:
         acts.sp_bwd = (self.split_bwd_operands(acts.supT_arr, len(sups))
                        if planes == 1 and training and acts.supT_arr is not None else None)
         acts.g4bt_arr = None
-        acts.g4bf_arr = self._g4_bf16(fixed_sups, acts, st) if planes == 1 and sups else None
+        # (shared supports only: planes is 0 for per-sample graphs, whose padded stacks are fresh per call)
+        acts.g4bf_arr = self._g4_bf16(fixed_sups, acts, st) if planes == 1 and sups and sup_batch <= 1 else None
         # the last layer's gcn + bn only update bn[L-1]'s running statistics (their output is dead,
         # model.py:225-236): GWN_TAIL_OVERLAP=1 runs them on a second stream beside the head GEMMs
         # (the head needs only the skip sum), joined before the forward returns.  Off by default:

@@ -423,7 +423,9 @@ typedef struct gwn_gcn_bwd_args {
   const void* const* sup_g4b_t;
   /* tg4 (optional, the bf16 16-node tile kernel only): t1 / t2 of the adaptive support as bf16
    * in gwn_gram_g4_bf16's tiled activation layout (t1 in the first slices*ceil(n/16) KiB, t2 in the
-   * next) INSTEAD of dhcat's columns c .. 3c */
+   * next) INSTEAD of dhcat's columns c .. 3c.  Requires skip_weight_grads (or no dadp / adp_index
+   * < 0): the in-library adjacency gram reads dhcat's columns, so the caller runs
+   * gwn_gram_g4_bf16 on tg4 itself; GWN_ERR_ARG otherwise */
   void* tg4;
 } gwn_gcn_bwd_args;
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t stream);

@@ -63,3 +63,42 @@ def test_gloo_world2_broadcast_and_grad_average():
     expect = torch.arange(res[0][1].numel(), dtype=torch.float32) * 1.5  # mean of (1x, 2x)
     assert torch.allclose(res[0][1], expect) and torch.allclose(res[1][1], expect)
     assert res[0][2] == res[1][2]
+
+
+def _timing_worker(rank, world, port, out_q):
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["GWN_DIST_BACKEND"] = "gloo"
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        t, info = bench.rank_timing(1.0 + rank, world, rank, "cpu")
+        out_q.put((rank, t, info))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_bench_rank_timing_gloo_world2():
+    """bench.py's multi-rank record (SCALE lines): the timed region is the MAX over ranks, and the
+    JSON carries the backend and world size torch.distributed saw plus the per-rank min / max."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timing_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, t, info = q.get(timeout=300)
+        res[r] = (t, info)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        t, info = res[r]
+        assert t == 2.0
+        assert info == {"backend": "gloo", "world_seen": 2, "rank_seconds_min": 1.0, "rank_seconds_max": 2.0}

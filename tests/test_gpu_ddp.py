@@ -228,3 +228,7 @@ def test_bench_gpus_2_self_launch(gpu):
     rec = lines[0]
     assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 128 and rec["config"]["parallelism"] == "dp2"
     assert rec["value"] > 0 and rec["mae12_delta"] <= 1e-4
+    dist = rec["distributed"]  # what torch.distributed saw (SCALE lines carry the same record)
+    assert dist["backend"] == "gloo" and dist["world_seen"] == 2
+    assert 0 < dist["rank_seconds_min"] <= dist["rank_seconds_max"]
+    assert abs(rec["ms_per_step"] - 1000.0 * dist["rank_seconds_max"] / 3) < 0.01
