@@ -156,9 +156,6 @@ __device__ __forceinline__ void split_sum_to_lds(const float* part, int parts, i
   }
 }
 
-// bf16 kernels: support batches prefetched ahead of their MFMAs (whole hop up to this many)
-constexpr int GWN_BF16_PD = 11;
-
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
@@ -1987,9 +1984,6 @@ bool gwn_gcn_fused_eligible(int c, int n, int nsup, int ld_sup) {
   return c == CH && n > 0 && n <= 512 && nsup >= 0 && nsup <= 8 && ld_sup >= (n + 31) / 32 * 32;
 }
 
-bool gwn_gcn_split_eligible(int c, int n, int planes);
-int gwn_gcn_split_fwd_launch(const gwn_gcn_args* g, const FusedFwd& a, hipStream_t s);
-int gwn_gcn_bf16_bwd_launch(const gwn_gcn_bwd_args* g, const FusedBwd& a, hipStream_t s);
 
 // the 16-node tile kernels (GWN_GCN_T16=0 selects the 32-node tile power kernels)
 constexpr int T16_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS of a t16 workgroup
@@ -2115,12 +2109,9 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
     }
   }
   GWN_REQUIRE(!g->xg4, "gcn_fwd: xg4 is written by the bf16 16-node tile kernel only (sup_g4b, layout 0)");
-  if (g->split_planes) {
-    GWN_REQUIRE(gwn_gcn_split_eligible(g->c, g->n, g->split_planes) && g->sup_split && g->w_split && g->nsup > 0,
-                "gcn_fwd (split): needs c == 32, an instantiated node-tile count, split supports and weights");
-    const int rc = gwn_gcn_split_fwd_launch(g, a, s);
-    return rc ? rc : bn_part_tail(a.x_out ? nullptr : bn_part, g->rows / g->n, CH, s);
-  }
+  GWN_REQUIRE(!g->split_planes,
+              "gcn_fwd: bf16 operands (split_planes 1) run on the 16-node tile kernel only: sup_g4b, layout 0, shared "
+              "supports, no forced support split, gwn_gcn_t16b_supported(n, nsup)");
   static bool attr_set = false;
   if (!attr_set) {
     ensure_lds_attr(gcn_fwd_fused_kernel<512, false>);
@@ -2236,8 +2227,9 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
     }
   }
   GWN_REQUIRE(!g->tg4, "gcn_bwd: tg4 is written by the bf16 16-node tile kernel only (sup_g4b_t, layout 0)");
-  if (g->split_planes == 1) return gwn_gcn_bf16_bwd_launch(g, a, s);
-  GWN_REQUIRE(g->split_planes == 0, "gcn_bwd (fused): split_planes must be 0 (f32) or 1 (bf16)");
+  GWN_REQUIRE(!g->split_planes,
+              "gcn_bwd: bf16 operands (split_planes 1) run on the 16-node tile kernel only: sup_g4b_t, layout 0, "
+              "shared supports, no forced support split, gwn_gcn_t16b_supported(n, nsup)");
   static bool attr_set = false;
   if (!attr_set) {
     ensure_lds_attr(gcn_bwd_fused_kernel<512, false>);
@@ -2420,575 +2412,7 @@ extern "C" int gwn_pad_square_batched(const float* src, int batch, long src_bstr
   return GWN_OK;
 }
 
-// =============================================================================================
-// Split-bf16 forward (the same schedule as gcn_fwd_fused_kernel on v_mfma_f32_32x32x16_bf16).
-//
-// Every fp32 operand x is carried as P bf16 pieces x = x_0 + x_1 (+ x_2) + r (x_0 = bf16(x),
-// x_1 = bf16(x - x_0), ...; each difference is exact in fp32), and a product a*b is the sum of
-// the piece products a_i*b_j with i + j < P, accumulated in fp32.  P = 3 (6 products) leaves a
-// representation error of 2^-24 relative per operand: the results stay at fp32 accuracy (the
-// tests hold it to the fp32 path's tolerances), at 6 x 32 cycles per 16-deep K step against
-// 8 x 64 cycles for the f32 MFMA: 2.67x the matrix throughput.  P = 2 (3 products, ~1e-5
-// relative) is kept for measurements only.
-//
-// Operand images:
-//   * node features (A operand, LDS): P planes of [channel][node] bf16, row stride SB bytes
-//     (SB = 16 mod 256: the 16 lanes of a ds_read_b128 group hit 16 distinct 16-B bank slots);
-//   * supports (B operand, global / L2): P planes of G^T [w][v] bf16 (gwn_split_supports), read as
-//     two 16-B buffer loads per lane per 32-node K batch;
-//   * mlp weights (A operand of the channel contraction): P planes [piece][c'][32], the 32 inputs of
-//     each piece in "lane order" j = 16 s + 8 h + i (gwn_split_mlp_weights): for pieces >= 1 that
-//     is the MFMA accumulator row order crow(8 s + i, h), so the hop accumulator is the B operand
-//     as it stands (K permuted consistently on both sides); for piece 0 it is the channel order.
-// K permutation of the diffusion: K step j of batch b, lane half h, element i is node
-// 32 b + 16 h + 8 j + i, so each lane reads 32 contiguous bytes of a G^T row / LDS plane row.
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-
-namespace {
-
-constexpr int split_row_bytes(int np) { return ((2 * np - 16 + 255) / 256) * 256 + 16; }
-constexpr int cmax(int a, int b) { return a > b ? a : b; }
-// bytes of the forward kernel's first LDS region: the P node-feature planes, and the fp32
-// [np][LDR] rows the epilogue stages there (the larger of the two for P = 1)
-constexpr int split_xs_bytes(int np, int P) { return cmax(P * 32 * split_row_bytes(np), np * LDR * 4); }
-
-template <int P>
-__device__ __forceinline__ void split8(const float* x, bf16x8* out) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    float r = x[i];
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      const __bf16 h = (__bf16)r;
-      out[p][i] = h;
-      if (p + 1 < P) r -= (float)h;
-    }
-  }
-}
-
-// acc += sum_{i+j<P} a_i b_j, smallest terms first
-template <int P>
-__device__ __forceinline__ f32x16 mfma_split(const bf16x8* a, const bf16x8* b, f32x16 acc) {
-#pragma unroll
-  for (int s = P - 1; s >= 0; --s)
-#pragma unroll
-    for (int i = 0; i <= s; ++i) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[s - i], acc, 0, 0, 0);
-  return acc;
-}
-
-template <int P, int PD>
-struct SplitPre {
-  i32x4 v[PD][P][2];
-};
-
-struct SplitG {
-  __amdgpu_buffer_rsrc_t rs;
-  int voff;    // this lane's byte offset in a plane: row w, K half
-  int planeb;  // bytes per plane
-};
-
-__device__ __forceinline__ SplitG split_g(const void* gs, int np, int ldg, int P, int w, int half) {
-  SplitG g;
-  g.planeb = np * ldg * 2;
-  g.rs = __builtin_amdgcn_make_buffer_rsrc((void*)gs, (short)0, P * g.planeb, 0x00020000);
-  g.voff = (w * ldg + 16 * half) * 2;
-  return g;
-}
-
-__device__ __forceinline__ i32x4 gload16(const SplitG& g, int extra, int soff) {
-  return __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(g.rs, g.voff + extra, soff, 0));
-}
-
-template <int P, int PD>
-__device__ __forceinline__ SplitPre<P, PD> split_pre(const SplitG& g) {
-  SplitPre<P, PD> s;
-#pragma unroll
-  for (int b = 0; b < PD; ++b)
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      s.v[b][p][0] = gload16(g, 0, p * g.planeb + b * 64);
-      s.v[b][p][1] = gload16(g, 16, p * g.planeb + b * 64);
-    }
-  return s;
-}
-
-// acc[c][w] += sum_v img[v][c] * G[v][w]: img = LDS planes, G = split support (first PD batches in g0)
-template <int NKB, int P, int PD>
-__device__ __forceinline__ f32x16 diffuse_split(const char* img, const SplitG& g, int lane, f32x16 acc,
-                                                const SplitPre<P, PD>& g0) {
-  constexpr int SB = split_row_bytes(NKB * 32);
-  constexpr int PLX = 32 * SB;
-  const int col = lane & 31, half = lane >> 5;
-  const char* ab = img + col * SB + half * 32;
-  i32x4 gv[NKB][P][2];
-#pragma unroll
-  for (int b = 0; b < PD && b < NKB; ++b)
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      gv[b][p][0] = g0.v[b][p][0];
-      gv[b][p][1] = g0.v[b][p][1];
-    }
-#pragma unroll
-  for (int b = 0; b < NKB; ++b) {
-    if (b + PD < NKB) {
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        gv[b + PD][p][0] = gload16(g, 0, p * g.planeb + (b + PD) * 64);
-        gv[b + PD][p][1] = gload16(g, 16, p * g.planeb + (b + PD) * 64);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      bf16x8 av[P], bv[P];
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        av[p] = *(const bf16x8*)(ab + p * PLX + b * 64 + j * 16);
-        bv[p] = __builtin_bit_cast(bf16x8, gv[b][p][j]);
-      }
-      acc = mfma_split<P>(av, bv, acc);
-    }
-  }
-  return acc;
-}
-
-template <int P>
-struct SplitW {
-  bf16x8 v[2][P];
-};
-
-// weight fragments of mlp piece `piece` (A operand: row c' = lane & 31, lane-order inputs)
-template <int P>
-__device__ __forceinline__ SplitW<P> split_w(const void* ws, int piece, int lane) {
-  const int col = lane & 31, half = lane >> 5;
-  SplitW<P> f;
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int p = 0; p < P; ++p)
-      f.v[s][p] = *((const bf16x8*)ws + ((piece * P + p) * 32 + col) * 4 + s * 2 + half);
-  return f;
-}
-
-// acc[c'][w] += sum_c W[c'][c] * D[c][w] with D = the hop accumulator (rows in crow order)
-template <int P>
-__device__ __forceinline__ f32x16 mlp_acc_split(const SplitW<P>& wf, const f32x16& d, f32x16 acc) {
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    float x[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = d[8 * s + i];
-    bf16x8 bv[P];
-    split8<P>(x, bv);
-    acc = mfma_split<P>(wf.v[s], bv, acc);
-  }
-  return acc;
-}
-
-// hop accumulator D[c][w] -> the LDS planes [c][w] (the next hop's A operand)
-template <int NKB, int P>
-__device__ __forceinline__ void acc_to_planes(char* img, const f32x16& d, int w0, int lane) {
-  constexpr int SB = split_row_bytes(NKB * 32);
-  constexpr int PLX = 32 * SB;
-  const int col = lane & 31, half = lane >> 5;
-  char* base = img + (w0 + col) * 2;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    float v = d[r];
-    const int c = crow(r, half);
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      const __bf16 h = (__bf16)v;
-      *(__bf16*)(base + p * PLX + c * SB) = h;
-      if (p + 1 < P) v -= (float)h;
-    }
-  }
-}
-
-template <int NKB, int P, int PD>
-__global__ __launch_bounds__(64 * NKB) void gcn_fwd_split_kernel(const FusedFwd a, const void* gsplit,
-                                                                 long gstride, int ldg, const void* wsplit) {
-  constexpr int NP = NKB * 32;
-  constexpr int SB = split_row_bytes(NP);
-  extern __shared__ float lds[];
-  __shared__ float red[2][64 * NKB];
-  char* xs = (char*)lds;
-  char* ys = xs + split_xs_bytes(NP, P);  // the first region also stages the fp32 epilogue rows
-  const int n = a.n;
-  const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
-  const int col = lane & 31, half = lane >> 5;
-  const long row0 = (long)blockIdx.x * n;
-  const float* hs = a.h + row0 * a.ld_h;
-
-  SplitG g = split_g(gsplit, NP, ldg, P, w0 + col, half);
-  SplitPre<P, PD> g0{};
-  if (a.nsup > 0) g0 = split_pre<P, PD>(g);
-  SplitW<P> wf = split_w<P>(wsplit, 0, lane);
-  // stage the node features as P planes [c][v] (rows >= n zero)
-  for (int e = threadIdx.x; e < NP * CH; e += blockDim.x) {
-    const int w = e >> 5, c = e & 31;
-    float v = (w < n) ? hs[(long)w * a.ld_h + c] : 0.0f;
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      const __bf16 h = (__bf16)v;
-      *(__bf16*)(xs + p * 32 * SB + c * SB + w * 2) = h;
-      if (p + 1 < P) v -= (float)h;
-    }
-  }
-  // mlp piece 0 straight from the rows of h (B operand: row w, channels 16 s + 8 h + i)
-  f32x16 hacc = zero16();
-  {
-    const int w = w0 + col;
-    const float* xr = hs + (long)min(w, n - 1) * a.ld_h + 8 * half;
-    const float keep = (w < n) ? 1.0f : 0.0f;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const float4 q0 = *(const float4*)(xr + 16 * s);
-      const float4 q1 = *(const float4*)(xr + 16 * s + 4);
-      float x[8] = {q0.x * keep, q0.y * keep, q0.z * keep, q0.w * keep,
-                    q1.x * keep, q1.y * keep, q1.z * keep, q1.w * keep};
-      bf16x8 bv[P];
-      split8<P>(x, bv);
-      hacc = mfma_split<P>(wf.v[s], bv, hacc);
-    }
-  }
-  __syncthreads();
-  for (int k = 0; k < a.nsup; ++k) {
-    wf = split_w<P>(wsplit, 1 + 2 * k, lane);
-    f32x16 d = diffuse_split<NKB, P, PD>(xs, g, lane, zero16(), g0);
-    g0 = split_pre<P, PD>(g);  // hop 2 re-reads the same support
-    hacc = mlp_acc_split<P>(wf, d, hacc);
-    wf = split_w<P>(wsplit, 2 + 2 * k, lane);
-    __syncthreads();  // ys is free once every wave finished the previous support's hop 2
-    acc_to_planes<NKB, P>(ys, d, w0, lane);
-    if (a.store_pieces) acc_to_global((float*)hs + (1 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
-    __syncthreads();
-    d = diffuse_split<NKB, P, PD>(ys, g, lane, zero16(), g0);
-    if (k + 1 < a.nsup) {
-      g = split_g((const char*)gsplit + (k + 1) * gstride * 2, NP, ldg, P, w0 + col, half);
-      g0 = split_pre<P, PD>(g);
-    }
-    hacc = mlp_acc_split<P>(wf, d, hacc);
-    if (a.store_pieces) acc_to_global((float*)hs + (2 + 2 * k) * CH, a.ld_h, d, w0, lane, n);
-  }
-  __syncthreads();
-  acc_to_lds((float*)xs, hacc, w0, lane);
-  __syncthreads();
-  fwd_epilogue<EPT>(a, (float*)xs, red[0], red[1], row0, n, blockIdx.x);
-}
-
-// dst[s][p][w][v] (bf16, [np][ld_dst] per plane) = piece p of G_s^T, G_s = padded support [np][ld_src]
-struct SplitSupArgs {
-  const float* src[8];
-};
-
-template <int P>
-__global__ void split_supports_kernel(SplitSupArgs sa, int np, int ld_src, __bf16* dst, long sup_stride,
-                                      int ld_dst) {
-  __shared__ float tile[32][33];
-  const float* src = sa.src[blockIdx.z];
-  __bf16* out = dst + blockIdx.z * sup_stride;
-  const long plane = (long)np * ld_dst;
-  const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int r = ty; r < 32; r += 8) tile[r][tx] = src[(long)(by + r) * ld_src + bx + tx];  // G[v = by+r][w = bx+tx]
-  __syncthreads();
-  for (int r = ty; r < 32; r += 8) {
-    float v = tile[tx][r];  // G[by + tx][bx + r] -> G^T[w = bx + r][v = by + tx]
-    __bf16* o = out + (long)(bx + r) * ld_dst + by + tx;
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      const __bf16 h = (__bf16)v;
-      o[p * plane] = h;
-      if (p + 1 < P) v -= (float)h;
-    }
-  }
-}
-
-struct SplitWArgs {
-  const float* w[16];
-};
-
-// dst[l][piece][p][c'][j] = piece p of W_l[c'][piece*32 + ch(j)], j = 16 s + 8 h + i in lane order
-template <int P>
-__global__ void split_mlp_kernel(SplitWArgs wa, int width, __bf16* dst, long layer_stride) {
-  const int l = blockIdx.y;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // over pieces * 32 * 32
-  const int npieces = width / CH;
-  if (e >= npieces * CH * CH) return;
-  const int j = e & 31, cp = (e >> 5) & 31, piece = e >> 10;
-  const int s = j >> 4, h = (j >> 3) & 1, i = j & 7;
-  const int ch = (piece == 0) ? j : crow(8 * s + i, h);
-  float v = wa.w[l][(long)cp * width + piece * CH + ch];
-  __bf16* o = dst + l * layer_stride + ((long)(piece * P) * CH + cp) * CH + j;
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    const __bf16 hh = (__bf16)v;
-    o[(long)p * CH * CH] = hh;
-    if (p + 1 < P) v -= (float)hh;
-  }
-}
-
-// dst[l][piece][c][c'] (bf16) = W_l[c'][piece*32 + c]: the A operand of the backward's channel
-// contraction dP = W^T dh (row c, inputs c' in plain order, matching the dh image rows)
-__global__ void mlpT_bf16_kernel(SplitWArgs wa, int width, __bf16* dst, long layer_stride) {
-  const int l = blockIdx.y;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // over pieces * 32 * 32
-  const int npieces = width / CH;
-  if (e >= npieces * CH * CH) return;
-  const int cp = e & 31, c = (e >> 5) & 31, piece = e >> 10;
-  dst[l * layer_stride + e] = (__bf16)wa.w[l][(long)cp * width + piece * CH + c];
-}
-
-// ---------------------------------------------------------------------------------------------
-// bf16 backward (the schedule of gcn_bwd_fused_kernel with bf16 operands, fp32 accumulation):
-//   dh image: LDS rows [w][32 c'] bf16 (row stride DHB), the B operand of dP = W^T dh;
-//   hop image: one bf16 plane [c][v] (the A operand of the diffusions through G^T);
-//   supports: gwn_split_supports(planes = 1) of the TRANSPOSED supports, i.e. planes of A [w][v].
-constexpr int DHB = 80;  // 64 B of bf16 + 16: the 16 lanes of a ds_read_b128 group hit distinct bank slots
-
-__device__ __forceinline__ f32x16 mlpT_bf16(const void* wt, int piece, const char* dhimg, int w0, int lane,
-                                            f32x16 acc) {
-  const int col = lane & 31, half = lane >> 5;
-  const bf16x8* wp = (const bf16x8*)wt + (piece * CH + col) * 4 + half;  // row c = col, inputs 8h + 16s
-  const char* bp = dhimg + (w0 + col) * DHB + half * 16;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const bf16x8 a = wp[2 * s];
-    const bf16x8 b = *(const bf16x8*)(bp + 32 * s);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
-  }
-  return acc;
-}
-
-template <int NKB, int PD>
-__global__ __launch_bounds__(64 * NKB) void gcn_bwd_bf16_kernel(const FusedBwd a, const void* gsplit, long gstride,
-                                                                int ldg, const void* wtsplit) {
-  constexpr int NP = NKB * 32;
-  constexpr int DHI = NP * DHB;        // bf16 dh image; the fp32 rows [w][LDR] of the prologue dh
-                                       // and the epilogue dx are staged at the base as well
-  extern __shared__ float lds[];
-  char* dhimg = (char*)lds;            // aliases the prologue staging (converted in registers)
-  char* img = dhimg + DHI;
-  float* stg = lds;
-  const int n = a.n;
-  const int lane = threadIdx.x & 63, w0 = (threadIdx.x >> 6) * 32;
-  const int col = lane & 31, half = lane >> 5;
-  const long row0 = (long)blockIdx.x * n;
-
-  SplitG g = split_g(gsplit, NP, ldg, 1, w0 + col, half);
-  SplitPre<1, PD> g0{};
-  if (a.nsup > 0) g0 = split_pre<1, PD>(g);
-  bwd_prologue<EPT>(a, stg, row0, n, NP);  // dh (fp32) for rows < np, zero beyond n
-  __syncthreads();
-  {
-    // fp32 staging -> bf16 dh image (each thread converts the same 16 elements it reads)
-    float v[EPT];
-    const int c = threadIdx.x & 31, wb = threadIdx.x >> 5, ws = blockDim.x >> 5;
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-      const int w = wb + i * ws;
-      v[i] = (w < NP) ? stg[w * LDR + c] : 0.0f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-      const int w = wb + i * ws;
-      if (w < NP) *(__bf16*)(dhimg + w * DHB + c * 2) = (__bf16)v[i];
-    }
-  }
-  __syncthreads();
-  f32x16 dx = mlpT_bf16(wtsplit, 0, dhimg, w0, lane, zero16());
-  for (int k = 0; k < a.nsup; ++k) {
-    const f32x16 u = mlpT_bf16(wtsplit, 2 + 2 * k, dhimg, w0, lane, zero16());
-    __syncthreads();  // img free: every wave finished the previous diffusion
-    acc_to_planes<NKB, 1>(img, u, w0, lane);
-    if (k == a.adp_index) acc_to_global(a.t2 + row0 * a.ld_t, a.ld_t, u, w0, lane, n);
-    __syncthreads();
-    f32x16 t = mlpT_bf16(wtsplit, 1 + 2 * k, dhimg, w0, lane, zero16());
-    t = diffuse_split<NKB, 1, PD>(img, g, lane, t, g0);  // dx1 = dP_x1 + A dP_x2
-    g0 = split_pre<1, PD>(g);
-    __syncthreads();
-    acc_to_planes<NKB, 1>(img, t, w0, lane);
-    if (k == a.adp_index) acc_to_global(a.t1 + row0 * a.ld_t, a.ld_t, t, w0, lane, n);
-    __syncthreads();
-    dx = diffuse_split<NKB, 1, PD>(img, g, lane, dx, g0);  // dxg += A dx1
-    if (k + 1 < a.nsup) {
-      g = split_g((const char*)gsplit + (k + 1) * gstride * 2, NP, ldg, 1, w0 + col, half);
-      g0 = split_pre<1, PD>(g);
-    }
-  }
-  if (!a.dfg) {
-    acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
-    return;
-  }
-  __syncthreads();  // every wave finished reading the images
-  acc_to_lds(stg, dx, w0, lane);
-  __syncthreads();
-  bwd_gate_epilogue<EPT>(a, stg, row0, n);
-}
-
-template <int NKB>
-void launch_bf16_bwd(const FusedBwd& a, const gwn_gcn_bwd_args* g, int slices, hipStream_t s) {
-  constexpr int NP = NKB * 32;
-  // whole-hop prefetch where a workgroup holds a CU on its own anyway (9+ node tiles); below that
-  // its extra registers would cost the second co-resident workgroup (N=207: 144 vs 104 VGPRs)
-  constexpr int PD = NKB >= 9 ? (NKB < GWN_BF16_PD ? NKB : GWN_BF16_PD) : (NKB > 1 ? 2 : 1);
-  const size_t lds = (size_t)cmax(NP * LDR * 4, NP * DHB + 32 * split_row_bytes(NP));
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gcn_bwd_bf16_kernel<NKB, PD>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    attr_set = true;
-  }
-  gcn_bwd_bf16_kernel<NKB, PD><<<slices, 64 * NKB, lds, s>>>(a, g->supT_split, g->sup_split_stride, g->ld_split,
-                                                             g->wT_split);
-}
-
-template <int NKB, int P, int PD>
-void launch_split(const FusedFwd& a, const gwn_gcn_args* g, int slices, hipStream_t s) {
-  constexpr int NP = NKB * 32;
-  const size_t lds = (size_t)split_xs_bytes(NP, P) + P * 32 * split_row_bytes(NP);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gcn_fwd_split_kernel<NKB, P, PD>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
-  gcn_fwd_split_kernel<NKB, P, PD><<<slices, 64 * NKB, lds, s>>>(a, g->sup_split, g->sup_split_stride,
-                                                                  g->ld_split, g->w_split);
-}
-
-}  // namespace
-
-bool gwn_gcn_split_eligible(int c, int n, int planes) {
-  const int nkb = (n + 31) / 32;
-  return c == CH && n > 0 && planes == 1 && nkb <= 16;
-}
-
-// bf16 operands (planes = 1): one instantiation per node-tile count
-// The whole hop's support fragments (NKB batches x 32 B per lane) are issued one phase ahead of
-// the hop: with bf16 operands a batch is 2 MFMAs (64 cycles), far shorter than an L2 round trip,
-// so a short prefetch distance leaves every batch waiting on its loads
-template <int NKB>
-void launch_bf16_fwd(const FusedFwd& a, const gwn_gcn_args* g, int slices, hipStream_t s) {
-  launch_split<NKB, 1, (NKB < GWN_BF16_PD ? NKB : GWN_BF16_PD)>(a, g, slices, s);
-}
-
-int gwn_gcn_split_fwd_launch(const gwn_gcn_args* g, const FusedFwd& a, hipStream_t s) {
-  const int nkb = (g->n + 31) / 32;
-  const int slices = g->rows / g->n;
-  GWN_REQUIRE(g->ld_split >= nkb * 32 && g->sup_split_stride % 8 == 0 && g->ld_split % 8 == 0,
-              "gcn_fwd (split): bad split-support layout");
-  if (g->split_planes == 1) {
-    switch (nkb) {
-      case 1: launch_bf16_fwd<1>(a, g, slices, s); break;
-      case 2: launch_bf16_fwd<2>(a, g, slices, s); break;
-      case 3: launch_bf16_fwd<3>(a, g, slices, s); break;
-      case 4: launch_bf16_fwd<4>(a, g, slices, s); break;
-      case 5: launch_bf16_fwd<5>(a, g, slices, s); break;
-      case 6: launch_bf16_fwd<6>(a, g, slices, s); break;
-      case 7: launch_bf16_fwd<7>(a, g, slices, s); break;
-      case 8: launch_bf16_fwd<8>(a, g, slices, s); break;
-      case 9: launch_bf16_fwd<9>(a, g, slices, s); break;
-      case 10: launch_bf16_fwd<10>(a, g, slices, s); break;
-      case 11: launch_bf16_fwd<11>(a, g, slices, s); break;
-      case 12: launch_bf16_fwd<12>(a, g, slices, s); break;
-      case 13: launch_bf16_fwd<13>(a, g, slices, s); break;
-      case 14: launch_bf16_fwd<14>(a, g, slices, s); break;
-      case 15: launch_bf16_fwd<15>(a, g, slices, s); break;
-      default: launch_bf16_fwd<16>(a, g, slices, s); break;
-    }
-  } else {
-    GWN_REQUIRE(false, "gcn_fwd (split): only bf16 operands (split_planes 1) are built");
-  }
-  GWN_CHECK_LAUNCH();
-  return GWN_OK;
-}
-
-int gwn_gcn_bf16_bwd_launch(const gwn_gcn_bwd_args* g, const FusedBwd& a, hipStream_t s) {
-  const int nkb = (g->n + 31) / 32;
-  const int slices = g->rows / g->n;
-  GWN_REQUIRE(gwn_gcn_split_eligible(g->c, g->n, 1) && g->supT_split && g->wT_split && g->nsup > 0 &&
-                  g->ld_split >= nkb * 32 && g->sup_split_stride % 8 == 0 && g->ld_split % 8 == 0 && a.sup_batch <= 1,
-              "gcn_bwd (bf16): needs c == 32, n <= 512, nsup >= 1, split transposed supports and weights");
-  switch (nkb) {
-    case 1: launch_bf16_bwd<1>(a, g, slices, s); break;
-    case 2: launch_bf16_bwd<2>(a, g, slices, s); break;
-    case 3: launch_bf16_bwd<3>(a, g, slices, s); break;
-    case 4: launch_bf16_bwd<4>(a, g, slices, s); break;
-    case 5: launch_bf16_bwd<5>(a, g, slices, s); break;
-    case 6: launch_bf16_bwd<6>(a, g, slices, s); break;
-    case 7: launch_bf16_bwd<7>(a, g, slices, s); break;
-    case 8: launch_bf16_bwd<8>(a, g, slices, s); break;
-    case 9: launch_bf16_bwd<9>(a, g, slices, s); break;
-    case 10: launch_bf16_bwd<10>(a, g, slices, s); break;
-    case 11: launch_bf16_bwd<11>(a, g, slices, s); break;
-    case 12: launch_bf16_bwd<12>(a, g, slices, s); break;
-    case 13: launch_bf16_bwd<13>(a, g, slices, s); break;
-    case 14: launch_bf16_bwd<14>(a, g, slices, s); break;
-    case 15: launch_bf16_bwd<15>(a, g, slices, s); break;
-    default: launch_bf16_bwd<16>(a, g, slices, s); break;
-  }
-  GWN_CHECK_LAUNCH();
-  return GWN_OK;
-}
-
-extern "C" int gwn_gcn_split_supported(int c, int n, int planes) { return gwn_gcn_split_eligible(c, n, planes) ? 1 : 0; }
 // the bf16 16-node tile kernels run for (n, nsup) (c == 32, sup_g4b / sup_g4b_t given, layout 0)
 extern "C" int gwn_gcn_t16b_supported(int n, int nsup) {
   return n > 0 && nsup > 0 && t16_enabled() && t16b_lds_bytes(n, nsup, 1) <= (size_t)T16_LDS_MAX ? 1 : 0;
-}
-
-extern "C" long gwn_split_support_elems(int n, int planes) {
-  const long np = (n + 31) / 32 * 32;
-  return (long)planes * np * np;
-}
-
-extern "C" int gwn_split_supports(const float* const* sup, int nsup, int n, int ld_sup, int planes, void* dst,
-                                  long sup_stride_elems, int ld_dst, hipStream_t s) {
-  const int np = (n + 31) / 32 * 32;
-  GWN_REQUIRE(nsup >= 1 && nsup <= 8 && planes == 1 && ld_sup >= np && ld_dst >= np &&
-                  sup_stride_elems >= (long)planes * np * ld_dst,
-              "split_supports: bad shape");
-  SplitSupArgs sa;
-  for (int k = 0; k < 8; ++k) sa.src[k] = k < nsup ? sup[k] : nullptr;
-  dim3 grid(np / 32, np / 32, nsup);
-  split_supports_kernel<1><<<grid, 256, 0, s>>>(sa, np, ld_sup, (__bf16*)dst, sup_stride_elems, ld_dst);
-  GWN_CHECK_LAUNCH();
-  return GWN_OK;
-}
-
-extern "C" long gwn_split_mlp_elems(int nsup, int planes) { return (long)(2 * nsup + 1) * planes * CH * CH; }
-
-extern "C" int gwn_split_mlp_weights(const float* const* w, int nlayers, int nsup, int planes, void* dst,
-                                     long layer_stride_elems, hipStream_t s) {
-  const int width = (2 * nsup + 1) * CH;
-  GWN_REQUIRE(nlayers >= 1 && nlayers <= 16 && nsup >= 0 && planes == 1 &&
-                  layer_stride_elems >= gwn_split_mlp_elems(nsup, planes),
-              "split_mlp_weights: bad shape");
-  SplitWArgs wa;
-  for (int l = 0; l < 16; ++l) wa.w[l] = l < nlayers ? w[l] : nullptr;
-  const int total = (2 * nsup + 1) * CH * CH;
-  dim3 grid((total + 255) / 256, nlayers);
-  split_mlp_kernel<1><<<grid, 256, 0, s>>>(wa, width, (__bf16*)dst, layer_stride_elems);
-  GWN_CHECK_LAUNCH();
-  return GWN_OK;
-}
-
-extern "C" long gwn_bf16_mlpT_elems(int nsup) { return (long)(2 * nsup + 1) * CH * CH; }
-
-extern "C" int gwn_bf16_mlpT_weights(const float* const* w, int nlayers, int nsup, void* dst, long layer_stride_elems,
-                                     hipStream_t s) {
-  const int width = (2 * nsup + 1) * CH;
-  GWN_REQUIRE(nlayers >= 1 && nlayers <= 16 && nsup >= 0 && layer_stride_elems >= gwn_bf16_mlpT_elems(nsup),
-              "bf16_mlpT_weights: bad shape");
-  SplitWArgs wa;
-  for (int l = 0; l < 16; ++l) wa.w[l] = l < nlayers ? w[l] : nullptr;
-  const int total = (2 * nsup + 1) * CH * CH;
-  dim3 grid((total + 255) / 256, nlayers);
-  mlpT_bf16_kernel<<<grid, 256, 0, s>>>(wa, width, (__bf16*)dst, layer_stride_elems);
-  GWN_CHECK_LAUNCH();
-  return GWN_OK;
 }

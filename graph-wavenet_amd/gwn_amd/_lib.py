@@ -84,8 +84,6 @@ class GcnArgs(ctypes.Structure):
         ("bn_bias", c_void_p), ("bn_eps", c_float), ("bn_out", c_void_p),
         ("layout", c_int),
         ("split_planes", c_int),
-        ("sup_split", c_void_p), ("sup_split_stride", c_long), ("ld_split", c_int),
-        ("w_split", c_void_p),
         ("sup_bstride", c_long), ("sup_batch", c_int),
         ("residual_mean", c_void_p), ("residual_scale", c_void_p), ("residual_shift", c_void_p),
         ("ksplit", c_int), ("ksplit_ws", c_void_p), ("ksplit_count", c_void_p),
@@ -129,8 +127,6 @@ class GcnBwdArgs(ctypes.Structure):
         ("layout", c_int),
         ("sup_bstride", c_long), ("sup_batch", c_int),
         ("split_planes", c_int),
-        ("supT_split", c_void_p), ("sup_split_stride", c_long), ("ld_split", c_int),
-        ("wT_split", c_void_p),
         ("ksplit", c_int), ("ksplit_ws", c_void_p), ("ksplit_count", c_void_p),
         ("sup2_t", ctypes.POINTER(c_void_p)),
         ("c_out", c_int),
@@ -174,14 +170,7 @@ _SIGS = [
                                     c_long, c_int, c_void_p]),
     ("gwn_gcn_fwd", c_int, [ctypes.POINTER(GcnArgs), c_void_p]),
     ("gwn_gcn_bn_partial_count", c_long, [c_int, c_int, c_int, c_int, c_int]),
-    ("gwn_gcn_split_supported", c_int, [c_int, c_int, c_int]),
     ("gwn_gcn_t16b_supported", c_int, [c_int, c_int]),
-    ("gwn_split_support_elems", c_long, [c_int, c_int]),
-    ("gwn_split_supports", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_long, c_int, c_void_p]),
-    ("gwn_split_mlp_elems", c_long, [c_int, c_int]),
-    ("gwn_split_mlp_weights", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p]),
-    ("gwn_bf16_mlpT_elems", c_long, [c_int]),
-    ("gwn_bf16_mlpT_weights", c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p]),
     ("gwn_gcn_bwd", c_int, [ctypes.POINTER(GcnBwdArgs), c_void_p]),
     ("gwn_gcn_bwd_workspace_floats", c_long, [c_int, c_int, c_int, c_int]),
     ("gwn_gcn_bwd_workspace_floats_ex", c_long, [c_int, c_int, c_int, c_int, c_int]),

@@ -277,6 +277,12 @@ class Acts:
         self.bn_fold = False
 
 
+class _G4Holder:
+    """What Executor._g4_bf16 reads and caches for a forward that has no Acts (the lean eval)."""
+    adp = supT = None
+    training = False
+
+
 class _HeadBufs:
     def __init__(self, skipcat, skr, e1, y):
         self.skipcat, self.skr, self.e1, self.y = skipcat, skr, e1, y
@@ -311,62 +317,15 @@ class Executor:
     def split_planes(self):
         """MFMA operand format of the fused gcn kernels (include/gwn.h gwn_dtype):
         * compute dtype bf16 (gwnet.set_compute_dtype): 1 = bf16 operands, fp32 accumulation,
-          forward AND backward (the mixed-precision path of configs[2]);
+          forward AND backward, on the 16-node tile kernels (the mixed-precision path of configs[2]);
         * else 0: the f32-MFMA kernels (the default: the reference's fp32 arithmetic).
-        0 when the shape has no such instantiation (c != 32, n > 512, no supports)."""
+        0 when the shape has no bf16 tile kernel (c != 32, n > 512, no supports, GWN_GCN_T16=0)."""
         cfg = self.cfg
-        planes = 1 if self.compute_dtype == "bf16" else 0
-        if planes == 0 or not cfg.use_gcn or cfg.nsup < 1 or not cfg.square:
+        if self.compute_dtype != "bf16" or not cfg.use_gcn or cfg.nsup < 1 or not cfg.square:
             return 0
-        return planes if _lib.load().gwn_gcn_split_supported(cfg.C, cfg.N, planes) else 0
-
-    def split_bwd_operands(self, supT_arr, nsup):
-        """bf16 operands of the fused backward: planes of the transposed supports (the backward
-        diffuses through A) and the transposed mlp weights of every layer (dP = W^T dh)."""
-        cfg = self.cfg
-        lib = _lib.load()
-        st = _lib.stream()
-        sup_el = lib.gwn_split_support_elems(cfg.N, 1)
-        w_el = (lib.gwn_bf16_mlpT_elems(nsup) + 7) // 8 * 8
-        key = ("splitT", nsup)
-        b = self._scratch.get(key)
-        if b is None:
-            b = {"sup": torch.empty(nsup * sup_el, device=self.device, dtype=torch.int16),
-                 "w": torch.empty(cfg.L * w_el, device=self.device, dtype=torch.int16)}
-            self._scratch[key] = b
-        _lib.call("gwn_split_supports", ctypes.cast(supT_arr, ctypes.c_void_p), nsup, cfg.N, cfg.NP, 1,
-                  ptr(b["sup"]), sup_el, cfg.NP, st)
-        w_arr = (ctypes.c_void_p * cfg.L)(*[self.pk("mlp_w%d" % i).data_ptr() for i in range(cfg.L)])
-        _lib.call("gwn_bf16_mlpT_weights", ctypes.cast(w_arr, ctypes.c_void_p), cfg.L, nsup, ptr(b["w"]), w_el, st)
-        return {"sup": b["sup"].data_ptr(), "sup_stride": sup_el, "w": b["w"].data_ptr(), "w_stride_bytes": 2 * w_el}
-
-    def split_operands(self, sup_arr, nsup, planes):
-        """bf16 piece planes of the supports (transposed) and of every layer's mlp weights, for
-        the split path of gwn_gcn_fwd; rebuilt each forward (adp and the weights change)."""
-        cfg = self.cfg
-        lib = _lib.load()
-        st = _lib.stream()
-        sup_el = lib.gwn_split_support_elems(cfg.N, planes)
-        w_el = (lib.gwn_split_mlp_elems(nsup, planes) + 7) // 8 * 8
-        key = ("split", planes, nsup)
-        b = self._scratch.get(key)
-        if b is None:
-            b = {"sup": torch.empty(nsup * sup_el, device=self.device, dtype=torch.int16),
-                 "w": torch.empty(cfg.L * w_el, device=self.device, dtype=torch.int16)}
-            self._scratch[key] = b
-        _lib.call("gwn_split_supports", ctypes.cast(sup_arr, ctypes.c_void_p), nsup, cfg.N, cfg.NP, planes,
-                  ptr(b["sup"]), sup_el, cfg.NP, st)
-        w_arr = (ctypes.c_void_p * cfg.L)(*[self.pk("mlp_w%d" % i).data_ptr() for i in range(cfg.L)])
-        _lib.call("gwn_split_mlp_weights", ctypes.cast(w_arr, ctypes.c_void_p), cfg.L, nsup, planes, ptr(b["w"]),
-                  w_el, st)
-        return {"planes": planes, "sup": b["sup"].data_ptr(), "sup_stride": sup_el, "w": b["w"].data_ptr(),
-                "w_stride_bytes": 2 * w_el}
-
-    def split_fields(self, sp, i):
-        if sp is None:
-            return {}
-        return dict(split_planes=sp["planes"], sup_split=sp["sup"], sup_split_stride=sp["sup_stride"],
-                    ld_split=self.cfg.NP, w_split=sp["w"] + i * sp["w_stride_bytes"])
+        if not self._t16_ok() or not self._fused_gcn():
+            return 0
+        return 1 if _lib.load().gwn_gcn_t16b_supported(cfg.N, cfg.nsup) else 0
 
     def pk(self, name, buf=None):
         return self.layout.view(self.packed if buf is None else buf, name)
@@ -575,12 +534,12 @@ class Executor:
         scr = self.scratch(B, ts)
         ws, bnpart = scr["ws"], scr["bnpart"]
         planes = self.split_planes() if sup_batch <= 1 else 0
-        sp = self.split_operands(sup_arr, len(sups), planes) if planes else None
-        acts.sp_bwd = (self.split_bwd_operands(acts.supT_arr, len(sups))
-                       if planes == 1 and training and acts.supT_arr is not None else None)
         acts.g4bt_arr = None
         # (shared supports only: planes is 0 for per-sample graphs, whose padded stacks are fresh per call)
         acts.g4bf_arr = self._g4_bf16(fixed_sups, acts, st) if planes == 1 and sups and sup_batch <= 1 else None
+        planes = 1 if acts.g4bf_arr is not None else 0
+        if not training:
+            acts.g4bt_arr = None
         # the last layer's gcn + bn only update bn[L-1]'s running statistics (their output is dead,
         # model.py:225-236): GWN_TAIL_OVERLAP=1 runs them on a second stream beside the head GEMMs
         # (the head needs only the skip sum), joined before the forward returns.  Off by default:
@@ -646,7 +605,7 @@ class Executor:
                               sup_g4=self._arr_field(acts.g4f_arr),
                               sup_g4b=self._arr_field(acts.g4bf_arr),
                               xg4=ptr(xg4) if xg4 is not None else None, xg4_support=cfg.nsup - 1,
-                              **self.split_fields(sp, i), **self.ksplit_fields(scr))
+                              split_planes=planes, **self.ksplit_fields(scr))
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
             rm, rv, mom, eps, nbt = bn_bufs[i]
@@ -914,7 +873,15 @@ class Executor:
             if self._t16_ok() and len(g4f_p) == 2 * len(sups):
                 bf["g4f_arr"] = (ctypes.c_void_p * len(g4f_p))(*g4f_p)
         planes = self.split_planes()
-        sp = self.split_operands(sup_arr, len(sups), planes) if planes else None
+        g4bf = None
+        if planes and sups:
+            # bf16 mode: the bf16 tile copies of (A_k, A_k^2), the adaptive one's rebuilt per call
+            hold = bf.get("g4b_holder")
+            if hold is None:
+                hold = bf["g4b_holder"] = _G4Holder()
+            hold.adp, hold.training, hold.supT = bf["adp"], False, None
+            g4bf = self._g4_bf16(fixed_sups, hold, st)
+        planes = 1 if g4bf is not None else 0
         sx = x.stride()
         _lib.call("gwn_start_conv_fwd", ptr(x), sx[0], sx[1], sx[2], sx[3], B, cin, N, t_in, ts[0],
                   ptr(self.pk("start_w")), ptr(self.pk("start_b")), C, ptr(bf["x0"]), None, st)
@@ -942,7 +909,7 @@ class Executor:
                               bn_eps=eps, bn_out=ptr(xnext), sup2=self._arr_field(bf["sup2_arr"]),
                               sup_g4=self._arr_field(bf["g4f_arr"]),
                               w_mlp_t=ptr(self.pk("mlp_wT%d" % i)),
-                              **self.split_fields(sp, i))
+                              sup_g4b=self._arr_field(g4bf), split_planes=planes)
             _lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             xcur = xnext
         self._head_fwd(bf["skipcat"], bf["skr"], bf["e1"], bf["y"], tf * P, None)
@@ -1070,10 +1037,8 @@ class Executor:
                 sb = getattr(acts, "sup_batch", 1)
                 if sb > 1:
                     gb.sup_bstride, gb.sup_batch = cfg.NP * cfg.NP, sb
-                spb = getattr(acts, "sp_bwd", None)
-                if spb is not None:  # bf16 operands (fp32 accumulation) in the fused backward
-                    gb.split_planes, gb.supT_split, gb.sup_split_stride = 1, spb["sup"], spb["sup_stride"]
-                    gb.ld_split, gb.wT_split = cfg.NP, spb["w"] + i * spb["w_stride_bytes"]
+                if getattr(acts, "g4bt_arr", None) is not None:  # bf16 operands (fp32 accumulation)
+                    gb.split_planes = 1
                 if fuse:
                     gb.dh = None
                     gb.bn_dy, gb.bn_z = ptr(dnext), ptr(acts.Z[i])
@@ -1202,7 +1167,7 @@ class Executor:
             return
         h = acts.H[i].data_ptr()
         t = dhc.data_ptr()
-        fn = "gwn_gram_bf16" if getattr(acts, "sp_bwd", None) is not None else "gwn_gram"
+        fn = "gwn_gram_bf16" if getattr(acts, "g4bt_arr", None) is not None else "gwn_gram"
         _lib.call(fn, h, t + 4 * C, h + 4 * (1 + 2 * adp_index) * C, t + 4 * 2 * C, W, W, cfg.N, rows // cfg.N,
                   ptr(sc["dadp"]), cfg.NP, 0 if first_adp else 1, ptr(sc["ws"]), st)
 

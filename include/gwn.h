@@ -261,15 +261,12 @@ typedef struct gwn_gcn_args {
   const float* bn_running_mean; const float* bn_running_var; const float* bn_weight; const float* bn_bias;
   float bn_eps; float* bn_out;
   int layout;
-  /* operand precision of the products (gwn_dtype; 0 = GWN_DTYPE_F32, the f32-MFMA kernels):
-   *   GWN_DTYPE_BF16 (1): bf16 operands, fp32 accumulation (v_mfma_f32_32x32x16_bf16), any
-   *     n <= 512 (the mixed-precision path of configs[2]).
-   * Needs c == 32, nsup >= 1, sup_split = gwn_split_supports output with planes = split_planes
-   * (support k at sup_split + k*sup_split_stride elements, rows ld_split), w_split =
-   * gwn_split_mlp_weights output for this layer.  The fp32 supports `sup` are not read. */
+  /* operand precision of the diffusion products (gwn_dtype; 0 = GWN_DTYPE_F32, the f32-MFMA
+   * kernels): GWN_DTYPE_BF16 (1): bf16 operands, fp32 accumulation (v_mfma_f32_16x16x32_bf16) on the
+   * 16-node tile kernel -- the mixed-precision path of configs[2].  Needs c == 32, nsup >= 1,
+   * sup_g4b, layout 0, shared supports and gwn_gcn_t16b_supported(n, nsup); GWN_ERR_ARG otherwise.
+   * The mlp, the hop pieces, z and the BN partials stay fp32. */
   int split_planes;
-  const void* sup_split; long sup_split_stride; int ld_split;
-  const void* w_split;
   /* per-sample supports (the per-sample-graph variant, gcn2 model.py:57-80; sup_batch <= 1 = shared):
    * slice s = t*sup_batch + b diffuses with support k at sup[k] + b*sup_bstride (floats), same
    * padded [np][ld_sup] layout.  Fused path only (c == 32, n <= 512), f32 MFMA (split_planes 0). */
@@ -331,29 +328,10 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t stream);
  * (gwn_batchnorm_fwd_fold / _partials) takes this as nparts. */
 long gwn_gcn_bn_partial_count(int rows, int n, int c, int nsup, int ld_sup);
 
-/* bf16 piece planes for the split path of gwn_gcn_fwd.
- * gwn_split_supports: for each of the nsup padded supports sup[k] ([np][ld_sup], zero outside
- *   [n][n], np = 32*ceil(n/32)) writes `planes` bf16 planes of sup[k]^T, [np][ld_dst] each, at
- *   dst + k*sup_stride_elems (>= planes*np*ld_dst).  gwn_split_support_elems(n, planes) = the
- *   elements of one support at ld_dst = np.
- * gwn_split_mlp_weights: for each of nlayers gcn mlp weights w[l] ([32][(2*nsup+1)*32], the
- *   reference's gconv.l.mlp.mlp.weight) writes the pieces in the kernel's input order at
- *   dst + l*layer_stride_elems (>= gwn_split_mlp_elems(nsup, planes)).  Element type: bf16. */
-int gwn_gcn_split_supported(int c, int n, int planes); /* 1 if the split path takes (c, n, planes) */
 /* 1 iff the bf16 16-node tile gcn kernels (sup_g4b / sup_g4b_t) run for n nodes and nsup supports
- * (their LDS fits): the condition for requesting xg4 / tg4 */
+ * (c == 32, their LDS fits, the t16 kernels not disabled by GWN_GCN_T16=0): the condition for
+ * split_planes = 1 and for requesting xg4 / tg4 */
 int gwn_gcn_t16b_supported(int n, int nsup);
-/* the bf16 backward's transposed mlp weights: dst[l][piece][c][c'] = bf16(w[l][c'][piece*32 + c]),
- * at dst + l*layer_stride_elems (>= gwn_bf16_mlpT_elems(nsup)) */
-long gwn_bf16_mlpT_elems(int nsup);
-int gwn_bf16_mlpT_weights(const float* const* w, int nlayers, int nsup, void* dst, long layer_stride_elems,
-                          hipStream_t stream);
-long gwn_split_support_elems(int n, int planes);
-int gwn_split_supports(const float* const* sup, int nsup, int n, int ld_sup, int planes, void* dst,
-                       long sup_stride_elems, int ld_dst, hipStream_t stream);
-long gwn_split_mlp_elems(int nsup, int planes);
-int gwn_split_mlp_weights(const float* const* w, int nlayers, int nsup, int planes, void* dst,
-                          long layer_stride_elems, hipStream_t stream);
 
 /* Backward of gwn_gcn_fwd given dh (gradient w.r.t. the dropout output, i.e. dz with the
  * dropout mask and scale already applied).  Produces dW_mlp [c][(2K+1)c], db_mlp [c], the
@@ -398,13 +376,10 @@ typedef struct gwn_gcn_bwd_args {
   /* per-sample supports, as gwn_gcn_args (sup and sup_t alike); needs the fused path and
    * adp_index = -1 (the per-sample variant's supports are inputs: no adjacency gradient) */
   long sup_bstride; int sup_batch;
-  /* operand precision of the fused backward's products (gwn_dtype): GWN_DTYPE_F32 (0) or
-   * GWN_DTYPE_BF16 (1: v_mfma_f32_32x32x16_bf16, fp32 accumulation).  bf16 needs
-   * supT_split = gwn_split_supports(sup_t, planes = 1) (support k at + k*sup_split_stride elements,
-   * rows ld_split) and wT_split = gwn_bf16_mlpT_weights output for this layer. */
+  /* operand precision of the fused backward's diffusion products (gwn_dtype): GWN_DTYPE_F32 (0) or
+   * GWN_DTYPE_BF16 (1: v_mfma_f32_16x16x32_bf16, fp32 accumulation) on the 16-node tile kernel, which
+   * needs sup_g4b_t (as gwn_gcn_args.split_planes) */
   int split_planes;
-  const void* supT_split; long sup_split_stride; int ld_split;
-  const void* wT_split;
   /* support split of the fused f32 backward, as gwn_gcn_args (partial input gradients, the last
    * workgroup of a slice adds them in support order and runs the store / gate epilogue) */
   int ksplit; float* ksplit_ws; int* ksplit_count;

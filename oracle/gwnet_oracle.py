@@ -21,6 +21,15 @@ Parity is PINNED: tests/test_oracle.py checks this restatement against the golde
 tests/golden/*.npz, which tests/golden/make_golden.py produced by running the reference itself.
 Default dtype is float64 (the "truth" the fp32 HIP path is compared against).
 
+bf16 emulation (``Cfg(..., gcn_bf16=True)``): the arithmetic of libgwn's bf16 mode
+(gwnet.set_compute_dtype("bf16"), configs[2]) with everything else exact -- the diffusion products
+of every gcn take bf16-rounded operands (node features, A and A^2 forward; the mlp output
+gradient and A, A^2 in the backward) with exact accumulation, the adaptive support's gradient
+takes bf16-rounded operands, and the mlp, its weight gradient and every other layer stay exact
+(``gcn_bf16``, a custom autograd node).  The HIP path accumulates in fp32 instead, so a test can
+hold it to the fp32 rounding floor around this reference rather than to the bf16 distance from
+the exact model.
+
 Branch pinning (gradient tests only): the head's two ReLUs and the masked MAE (|pred - real|) are
 kinked.  An element within fp32 rounding of a kink takes either branch in two equally valid
 evaluations, and its gradient jumps.  ``forward`` / ``masked_metrics`` therefore accept the
@@ -41,7 +50,7 @@ class Cfg:
 
     def __init__(self, num_nodes, nfixed=2, gcn_bool=True, addaptadj=True, in_dim=2, out_dim=12, nhid=32,
                  skip=None, end=None, blocks=4, layers=2, dropout=0.0, kernel_size=2, dilation_channels=None,
-                 first_dilation=1):
+                 first_dilation=1, gcn_bf16=False):
         self.N, self.nfixed = num_nodes, nfixed
         self.gcn_bool, self.addaptadj = gcn_bool, addaptadj
         self.Cin, self.O, self.C = in_dim, out_dim, nhid
@@ -50,6 +59,7 @@ class Cfg:
         self.E = end if end is not None else 16 * nhid
         self.blocks, self.layers, self.dropout = blocks, layers, dropout
         self.kernel_size = kernel_size
+        self.gcn_bf16 = gcn_bf16  # libgwn's bf16 mode (module docstring)
         # gwnet_diff_G starts every block at dilation 4 (model.py:291)
         self.dilations = [first_dilation * 2 ** j for _ in range(blocks) for j in range(layers)]
         # model.py:130-157: every layer adds (kernel_size - 1) * 2^j -- the reference counts from
@@ -116,6 +126,68 @@ def gcn2(x, supports, w, bias, order=2):
     return pointwise(torch.cat(out, dim=1), w, bias)
 
 
+def bf16_round(t):
+    """Round to bf16 (round to nearest even) and back to t's dtype."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _GcnBf16(torch.autograd.Function):
+    """sum_q W_q . piece_q of gcn.forward (model.py:41-55, without the bias) in libgwn's bf16 mode
+    (csrc/gcn_fused.hip gcn_fwd_t16b_kernel / gcn_bwd_t16_kernel<., true>, gram.hip
+    gwn_gram_g4_bf16): the power schedule, pieces [g, A_1 g, A_1^2 g, A_2 g, ...] with
+    A_k^q g = einsum(rnd(g), rnd(A_k^q)) ('ncvl,vw->ncwl'); the backward of the power schedule:
+      dg  = W_0^T dy + sum_k W_{1+2k}^T (rnd(A_k) rnd(dy)) + W_{2+2k}^T (rnd(A_k^2) rnd(dy)),
+      dW  = dy (x) pieces (exact),
+      dA_k = sum rnd(g) (x) rnd(t1) + rnd(A_k g) (x) rnd(t2),
+             t1 = W_{1+2k}^T dy + W_{2+2k}^T (rnd(A_k) rnd(dy)),  t2 = W_{2+2k}^T dy
+    (the chained-hop gradient of x2 = (x A) A, as the HIP path forms it).  rnd = bf16_round, or the
+    identity (then this equals plain autograd through the chained hops up to reassociation)."""
+
+    @staticmethod
+    def forward(ctx, g, w, rnd, *sups):
+        gb = rnd(g)
+        pieces = [g]
+        for a in sups:
+            pieces += [diffuse(gb, rnd(a)), diffuse(gb, rnd(a @ a))]
+        h = torch.cat(pieces, dim=1)
+        ctx.rnd = rnd
+        ctx.save_for_backward(g, w, h, *sups)
+        return pointwise(h, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        g, w, h, *sups = ctx.saved_tensors
+        rnd = ctx.rnd
+        C = g.shape[1]
+        wr = w.reshape(w.shape[0], -1)
+
+        def wt(q, y):  # W_q^T y over the channel axis
+            return torch.einsum("oi,bont->bint", wr[:, q * C:(q + 1) * C], y)
+
+        dw = torch.einsum("bont,bint->oi", dy, h).reshape(w.shape)
+        dyb = rnd(dy)
+        dg = wt(0, dy)
+        dsups = []
+        for k, a in enumerate(sups):
+            # (A y)[v] = sum_w A[v][w] y[w] = diffuse(y, A^T)
+            e1 = diffuse(dyb, rnd(a).t())
+            e2 = diffuse(dyb, rnd(a @ a).t())
+            dg = dg + wt(1 + 2 * k, e1) + wt(2 + 2 * k, e2)
+            da = None
+            if ctx.needs_input_grad[3 + k]:
+                t1 = wt(1 + 2 * k, dy) + wt(2 + 2 * k, e1)
+                t2 = wt(2 + 2 * k, dy)
+                x1 = h[:, (1 + 2 * k) * C:(2 + 2 * k) * C]
+                da = torch.einsum("bcvt,bcwt->vw", rnd(g), rnd(t1)) + torch.einsum("bcvt,bcwt->vw", rnd(x1), rnd(t2))
+            dsups.append(da)
+        return (dg, dw, None, *dsups)
+
+
+def gcn_bf16(g, w, sups, rnd=bf16_round):
+    """libgwn's bf16-mode gcn products (_GcnBf16): sum_q W_q piece_q, no bias."""
+    return _GcnBf16.apply(g, w, rnd, *sups)
+
+
 def pointwise(x, w, bias=None):
     """1x1 convolution over NCHW: y[b,o,n,t] = sum_i w[o,i] x[b,i,n,t] + bias[o]."""
     y = torch.einsum("oi,bint->bont", w.reshape(w.shape[0], -1), x)
@@ -175,7 +247,13 @@ def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, ma
         g = filt * gate
         s = pointwise(g, p["skip_convs.%d.weight" % i], p["skip_convs.%d.bias" % i])
         skip = s if skip is None else s + skip[..., -s.shape[-1]:]
-        if cfg.use_gcn:
+        if cfg.use_gcn and getattr(cfg, "gcn_bf16", False):
+            h = gcn_bf16(g, p["gconv.%d.mlp.mlp.weight" % i], sups) + p["gconv.%d.mlp.mlp.bias" % i].view(1, -1, 1, 1)
+            if training and cfg.dropout > 0:
+                m = dropout_masks[i] if dropout_masks is not None else \
+                    (torch.rand_like(h) >= cfg.dropout).to(h.dtype)
+                h = h * m / (1 - cfg.dropout)
+        elif cfg.use_gcn:
             pieces = [g]
             for a in sups:
                 y1 = diffuse(g, a)

@@ -2,12 +2,16 @@
 runs the fused diffusion-GCN forward and backward on v_mfma_f32_32x32x16_bf16 (bf16 operands,
 fp32 accumulation); parameters, activations, gradients and Adam state stay fp32.
 
-Tolerances, against the reference's own f64 runs:
-* forward max-rel <= 2e-2 (measured 1.9e-3 at N=325, 6.4e-3 at N=207);
-* loss rel <= 1e-3; every gradient norm-rel <= 0.1 and their median <= 5e-2 (measured worst
-  5.1e-2 / 6.4e-2, median 2.6e-2 / 3.8e-2 at N=325 / 207).  For scale: the reference itself under
-  torch.autocast(bfloat16) (the oracle, CPU) is 7.5e-2 / 8.5e-2 median and 0.13 / 0.12 worst off
-  the same f64 truth -- this path keeps the TCN, skip, head and BN in fp32 and is ~2x closer.
+Tolerances:
+* the gate: against the bf16-EMULATING oracle (oracle Cfg(gcn_bf16=True): the same bf16-rounded
+  operands with exact accumulation, every other layer exact) -- forward max-rel <= 1e-4, loss rel
+  <= 1e-5, every gradient norm-rel <= 1e-3.  What is left is fp32 accumulation, so an error in the
+  bf16 arithmetic (a wrong rounding, a missing term, a wrong operand) shows up at its own size;
+* the report: the distance from the reference's own f64 run (the bf16 distance itself) is printed
+  and held to the loose bounds of rounds 2-3 (forward 2e-2, gradients 0.1 each / 5e-2 median).
+  For scale: the reference itself under torch.autocast(bfloat16) (the oracle, CPU) is 7.5e-2 /
+  8.5e-2 median and 0.13 / 0.12 worst off the same f64 truth -- this path keeps the TCN, skip,
+  head and BN in fp32 and is ~2x closer.
 Plus: the bf16 kernels against the fp32 kernels at N=16 (one node tile) and N=37 (two tiles), and
 the per-sample independence of a bf16 eval batch."""
 import numpy as np
@@ -30,17 +34,45 @@ def _trainer(gpu, g, n, dropout=0.0, nhid=32):
     return eng
 
 
-def _check_grads(model, ref, tag):
+def _check_grads(model, ref, tag, emul=None):
+    """emul: the bf16-emulating oracle's gradients (the gate, 1e-3 norm-rel per tensor); ref: the
+    reference's f64 gradients (the report, loose bounds)."""
     got = {k: p.grad.detach().cpu().numpy() for k, p in model.named_parameters() if p.grad is not None}
     assert set(got) == set(ref), (tag, sorted(set(got) ^ set(ref)))
-    errs = []
+    scale = max(float(np.max(np.abs(v))) for v in ref.values())
+    errs, gate = [], {}
     for k, v in ref.items():
         if k.endswith("mlp.bias") or np.linalg.norm(v) == 0:
-            continue  # analytically zero (BN-cancelled)
+            # analytically zero (BN-cancelled): fp32 noise only
+            assert float(np.max(np.abs(got[k]))) <= 1e-5 * scale, (tag, k)
+            continue
         e = norm_rel(got[k], v)
         assert e <= 0.1, (tag, k, e)
         errs.append(e)
+        if emul is not None:
+            gate[k] = norm_rel(got[k], emul[k].numpy())
     assert np.median(errs) <= 5e-2, (tag, np.median(errs))
+    if emul is not None:
+        worst = max(gate, key=gate.get)
+        print("%s: vs bf16 emulation worst %.2e (%s), median %.2e; vs f64 worst %.2e, median %.2e"
+              % (tag, gate[worst], worst, np.median(list(gate.values())), max(errs), np.median(errs)))
+        for k, e in gate.items():
+            assert e <= 1e-3, (tag, k, e)
+
+
+def _emulated(g, n, x, y=None):
+    """The bf16-emulating oracle (oracle Cfg(gcn_bf16=True)) on a fixture: eval output (y None) or
+    (train-mode output, metrics, gradients)."""
+    from oracle import gwnet_oracle as orc
+    sd = state_dict_of(g)
+    cfg = orc.Cfg(n, gcn_bf16=True)
+    if y is None:
+        p = {k: torch.tensor(v, dtype=torch.float64) for k, v in sd.items() if "running" not in k and "num_batches" not in k}
+        bn = {k: torch.tensor(v, dtype=torch.float64) for k, v in sd.items() if "running" in k}
+        return orc.forward(p, [torch.tensor(g["sup0"], dtype=torch.float64), torch.tensor(g["sup1"], dtype=torch.float64)],
+                           torch.tensor(x, dtype=torch.float64), cfg, False, bn)
+    out, met, gr, _ = orc.grads(sd, [g["sup0"], g["sup1"]], x, y, cfg, 54.4, 19.5)
+    return out, met, gr
 
 
 @pytest.mark.parametrize("name,n,xkey,okey", [("g5b_fwd_eval_n325.npz", 325, "x", "out_f64"),
@@ -52,7 +84,11 @@ def test_bf16_eval_forward(gpu, name, n, xkey, okey):
     with torch.no_grad():
         out = m(torch.tensor(g[xkey], device=gpu))
     torch.cuda.synchronize()
-    assert rel_err(out.cpu().numpy(), g[okey]) <= 2e-2
+    emu = _emulated(g, n, g[xkey]).numpy()
+    e_emu, e_f64 = rel_err(out.cpu().numpy(), emu), rel_err(out.cpu().numpy(), g[okey])
+    print("bf16 eval forward N=%d: vs bf16 emulation %.2e, vs f64 %.2e" % (n, e_emu, e_f64))
+    assert e_emu <= 1e-4
+    assert e_f64 <= 2e-2
 
 
 @pytest.mark.parametrize("name,n,pre", [("g13_train_n325.npz", 325, ""), ("g12_metr_n207.npz", 207, "g2_")])
@@ -62,8 +98,10 @@ def test_bf16_train_step_grads(gpu, name, n, pre):
     met = eng.train(torch.tensor(g[pre + "x"], device=gpu), torch.tensor(g[pre + "y"], device=gpu))
     mref = g["metrics_f64" if pre == "" else "g2_metrics_f64"]
     assert abs(met[0] / mref[0] - 1) <= 1e-3
+    _, emet, egr = _emulated(g, n, g[pre + "x"], g[pre + "y"])
+    assert abs(met[0] / emet[0] - 1) <= 1e-5, (met[0], emet[0])
     gkey = "grad_f64/" if pre == "" else "g2_grad_f64/"
-    _check_grads(eng.model, {k[len(gkey):]: v for k, v in g.items() if k.startswith(gkey)}, name)
+    _check_grads(eng.model, {k[len(gkey):]: v for k, v in g.items() if k.startswith(gkey)}, name, emul=egr)
     # the bf16 kernels really ran: the same step in fp32 differs
     eng2 = _trainer(gpu, g, n)
     eng2.model.set_compute_dtype("fp32")

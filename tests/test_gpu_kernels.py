@@ -1130,3 +1130,152 @@ def test_gcn_t16_bf16_forward(gpu, n):
     st = _bn_all(bnp, rows, n, C, K, NP)
     assert torch.all(st[:, 0] == rows)
     assert rel_err(st[:, 1].numpy(), Z.mean(0, keepdim=True).numpy()) <= 1e-2
+
+
+def _from_g4(buf, which, slices, n):
+    """Inverse of _to_g4 for operand `which` of a tiled bf16 buffer: [slices*nt*16][32] fp64
+    (rows >= n are the tiles' padding nodes)."""
+    nt = (n + 15) // 16
+    x = buf.view(torch.bfloat16)[which * slices * nt * 512:(which + 1) * slices * nt * 512].double().cpu()
+    # [s][vt][g][j][oh][r] -> [s][vt][j][oh][g][r]
+    x = x.reshape(slices, nt, 4, 16, 2, 4).permute(0, 1, 3, 4, 2, 5)
+    return x.reshape(slices, nt * 16, 32)
+
+
+@pytest.mark.parametrize("n", [16, 207, 325])
+@pytest.mark.parametrize("mode", ["bn_gate", "bn_gate_tg4", "plain"])
+def test_gcn_t16_bf16_backward(gpu, n, mode):
+    """The bf16 16-node tile backward (gcn_bwd_t16_kernel<1024, true>: gwn_gcn_bwd_args.sup_g4b_t,
+    split_planes 1) against fp64, kernel level (model.py:41-55 backward): the BN-backward prologue
+    (dres, dh_out with the dropout mask rebuilt on the host), the diffusion of bf16(dh) through
+    bf16(A_k^T), bf16((A_k^2)^T), the channel maps W^T in fp32, t1 / t2 of the adaptive support
+    (dhcat columns, or bf16 in gwn_gram_g4_bf16's tiled layout with tg4), and the gate-backward
+    epilogue (dfg from dxg + dskip and the saved (tanh f, sigmoid s)) or the plain dxg store.
+    Bounds: against an fp64 evaluation of the same bf16-rounded operands (the arithmetic the kernel
+    implements, fp32 accumulation the only difference) 2e-5 of each output's max magnitude (tg4: one
+    bf16 rounding, 2^-8); against the exact fp64 gradient 1e-2 (the forward test's bound)."""
+    import ctypes
+    from gwn_amd import _lib
+    from test_gpu_model import _np_uniform
+    torch.manual_seed(n + 11)
+    C, K, S = 32, 3, 21
+    NP = (n + 31) // 32 * 32
+    W = (2 * K + 1) * C
+    rows = S * n
+    nt = (n + 15) // 16
+    sups = []
+    for _ in range(K):
+        s_ = torch.zeros(NP, NP, device=gpu)
+        a = torch.rand(n, n, device=gpu)
+        s_[:n, :n] = a / a.sum(1, keepdim=True)
+        sups.append(s_)
+    supT = [s_.t().contiguous() for s_ in sups]
+    sq = _squares(gpu, sups)
+    P = ctypes.POINTER(ctypes.c_void_p)
+    el = _lib.load().gwn_support_g4_bf16_elems(n)
+    mats = [m for t_, q in zip(supT, sq) for m in (t_, q[1])]  # A_k^T, (A_k^2)^T
+    g4bt = torch.zeros(len(mats), el // 2, device=gpu)
+    src = (ctypes.c_void_p * len(mats))(*[m.data_ptr() for m in mats])
+    _lib.call("gwn_support_g4_bf16", ctypes.cast(src, P), len(mats), n, NP, g4bt.data_ptr(), el, _lib.stream())
+    arrb = (ctypes.c_void_p * len(mats))(*[g4bt[i].data_ptr() for i in range(len(mats))])
+    arr = (ctypes.c_void_p * K)(*[s_.data_ptr() for s_ in sups])
+    arrT = (ctypes.c_void_p * K)(*[s_.data_ptr() for s_ in supT])
+    wm = torch.randn(C, W, device=gpu) * 0.1
+    h = torch.zeros(rows, W, device=gpu)
+    dhc = torch.zeros(rows, W, device=gpu)
+    bn = mode != "plain"
+    kw = {}
+    drop, salt, seedv = 0.3, 4, 77
+    seed = torch.full((1,), seedv, device=gpu, dtype=torch.int64)
+    if bn:
+        bn_dy, bn_z = torch.randn(rows, C, device=gpu), torch.randn(rows, C, device=gpu) * 2 + 0.5
+        gamma, bmean, brstd = torch.randn(C, device=gpu), torch.randn(C, device=gpu), torch.rand(C, device=gpu) + 0.5
+        sums = torch.randn(2 * C, device=gpu) * 50
+        fg = torch.rand(rows, 2 * C, device=gpu)
+        fg[:, 0::2] = fg[:, 0::2] * 2 - 1  # tanh f in (-1, 1), sigmoid s in (0, 1)
+        dskip = torch.randn(rows, C, device=gpu)
+        skip_row0 = (S - 3) * n
+        dres, dh_out = torch.zeros(rows, C, device=gpu), torch.zeros(rows, C, device=gpu)
+        dfg = torch.zeros(rows, 2 * C, device=gpu)
+        dg, db = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
+        kw = dict(dh=None, bn_dy=bn_dy.data_ptr(), bn_z=bn_z.data_ptr(), bn_gamma=gamma.data_ptr(),
+                  bn_mean=bmean.data_ptr(), bn_rstd=brstd.data_ptr(), bn_sums=sums.data_ptr(),
+                  bn_dgamma=dg.data_ptr(), bn_dbeta=db.data_ptr(), dres=dres.data_ptr(), dh_out=dh_out.data_ptr(),
+                  seed_ptr=seed.data_ptr(), salt=salt, drop_p=drop, fg=fg.data_ptr(), dskip=dskip.data_ptr(),
+                  ld_dskip=C, skip_row0=skip_row0, dfg=dfg.data_ptr())
+    else:
+        dh = torch.randn(rows, C, device=gpu)
+        kw = dict(dh=dh.data_ptr())
+    tg4 = None
+    if mode == "bn_gate_tg4":
+        tg4 = torch.full((2 * S * nt * 512,), -1, device=gpu, dtype=torch.int16)
+        kw["tg4"] = tg4.data_ptr()
+    gb = _lib.GcnBwdArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, P), ld_sup=NP, h=h.data_ptr(), ld_h=W,
+                         w_mlp=wm.data_ptr(), dhcat=dhc.data_ptr(), ld_dhcat=W, adp_index=K - 1, accumulate_dadp=0,
+                         sup_t=ctypes.cast(arrT, P), skip_weight_grads=1, split_planes=1, sup_g4b_t=ctypes.cast(arrb, P),
+                         **kw)
+    _lib.call("gwn_gcn_bwd", ctypes.byref(gb), _lib.stream())
+    torch.cuda.synchronize()
+    # fp64: the BN-backward prologue and dropout (gwn_uniform rebuilt on the host)
+    if bn:
+        z, dy = bn_z.double().cpu(), bn_dy.double().cpu()
+        mu, rs, gm = bmean.double().cpu(), brstd.double().cpu(), gamma.double().cpu()
+        k1, k2 = sums[:C].double().cpu() / rows, sums[C:].double().cpu() / rows
+        dz = gm * rs * (dy - k1 - (z - mu) * rs * k2)
+        keep = _np_uniform(seedv, salt, np.arange(rows * C, dtype=np.int64)).reshape(rows, C) >= drop
+        dhr = dz * torch.tensor(keep, dtype=torch.float64) / (1 - drop)
+        assert rel_err(dres.cpu().numpy(), dz.numpy()) <= 2e-6
+        assert rel_err(dh_out.cpu().numpy(), dhr.numpy()) <= 2e-6
+        assert torch.equal(db.cpu(), sums[:C].cpu()) and torch.equal(dg.cpu(), sums[C:].cpu())
+    else:
+        dhr = dh.double().cpu()
+    bf = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
+    Wd = wm.double().cpu()
+    wq = lambda y, q: y @ Wd[:, q * C:(q + 1) * C]  # noqa: E731  (W_q^T applied to rows)
+
+    def grads(rnd):
+        D = dhr.view(S, n, C)
+        Db = rnd(D)
+        dxg = wq(dhr, 0)
+        t1 = t2 = None
+        for k in range(K):
+            a = rnd(sups[k][:n, :n].double().cpu())
+            a2 = rnd(sq[k][0][:n, :n].double().cpu())
+            e1 = torch.einsum("vw,swc->svc", a, Db).reshape(rows, C)
+            e2 = torch.einsum("vw,swc->svc", a2, Db).reshape(rows, C)
+            dxg = dxg + wq(e1, 1 + 2 * k) + wq(e2, 2 + 2 * k)
+            if k == K - 1:
+                t1 = wq(dhr, 1 + 2 * k) + wq(e1, 2 + 2 * k)
+                t2 = wq(dhr, 2 + 2 * k)
+        return dxg, t1, t2
+
+    exact, emul = grads(lambda t: t), grads(bf)
+    if bn:
+        f, s = fg[:, 0::2].double().cpu(), fg[:, 1::2].double().cpu()
+        sk = torch.zeros(rows, C, dtype=torch.float64)
+        sk[skip_row0:] = dskip.double().cpu()[skip_row0:]
+
+        def gate(dxg):
+            gv = dxg + sk
+            out = torch.empty(rows, 2 * C, dtype=torch.float64)
+            out[:, 0::2] = gv * s * (1 - f * f)
+            out[:, 1::2] = gv * f * s * (1 - s)
+            return out
+        got_main, want_main, want_exact = dfg.cpu().numpy(), gate(emul[0]).numpy(), gate(exact[0]).numpy()
+    else:
+        got_main, want_main, want_exact = dhc[:, :C].cpu().numpy(), emul[0].numpy(), exact[0].numpy()
+    assert rel_err(got_main, want_main) <= 2e-5
+    assert rel_err(got_main, want_exact) <= 1e-2
+    if tg4 is not None:
+        for which, (em, ex) in enumerate(((emul[1], exact[1]), (emul[2], exact[2]))):
+            got = _from_g4(tg4, which, S, n)
+            assert torch.all(got[:, n:] == 0)  # the tiles' padding nodes
+            got = got[:, :n].reshape(rows, C).numpy()
+            assert rel_err(got, em.numpy()) <= 2 ** -8 + 2e-5
+            assert rel_err(got, ex.numpy()) <= 1e-2
+        assert torch.all(dhc[:, C:3 * C] == 0)  # t1 / t2 went to tg4 only
+    else:
+        for j, (em, ex) in enumerate(((emul[1], exact[1]), (emul[2], exact[2]))):
+            got = dhc[:, (1 + j) * C:(2 + j) * C].cpu().numpy()
+            assert rel_err(got, em.numpy()) <= 2e-5
+            assert rel_err(got, ex.numpy()) <= 1e-2
