@@ -928,6 +928,7 @@ long gwn_abi_sizeof(const char* name) {
   if (!strcmp(name, "gwn_reduce_seg")) return (long)sizeof(gwn_reduce_seg);
   if (!strcmp(name, "gwn_gcn_args")) return (long)sizeof(gwn_gcn_args);
   if (!strcmp(name, "gwn_gcn_bwd_args")) return (long)sizeof(gwn_gcn_bwd_args);
+  if (!strcmp(name, "gwn_wgrad_problem")) return (long)sizeof(gwn_wgrad_problem);
   return -1;
 }
 

@@ -105,6 +105,16 @@ class ReduceSeg(ctypes.Structure):
     ]
 
 
+class WgradProblem(ctypes.Structure):
+    _fields_ = [
+        ("dY", c_void_p), ("ldy", c_long),
+        ("X", c_void_p), ("ldx", c_long), ("x_rows", c_long), ("shift", c_long),
+        ("x_mean", c_void_p), ("x_scale", c_void_p), ("x_shift", c_void_p),
+        ("part", c_void_p),
+        ("R", c_int),
+    ]
+
+
 class GcnBwdArgs(ctypes.Structure):
     _fields_ = [
         ("rows", c_int), ("n", c_int), ("c", c_int), ("nsup", c_int),
@@ -137,7 +147,8 @@ class GcnBwdArgs(ctypes.Structure):
 
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time
 _STRUCTS = {"gwn_gemm_desc": GemmDesc, "gwn_tcn_args": TcnArgs, "gwn_tcn_bwd_args": TcnBwdArgs,
-            "gwn_gcn_args": GcnArgs, "gwn_gcn_bwd_args": GcnBwdArgs}
+            "gwn_gcn_args": GcnArgs, "gwn_gcn_bwd_args": GcnBwdArgs, "gwn_reduce_seg": ReduceSeg,
+            "gwn_wgrad_problem": WgradProblem}
 
 
 # (name, restype, argtypes) of every exported entry point declared in include/gwn.h
@@ -182,6 +193,9 @@ _SIGS = [
     ("gwn_wgrad_partials", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gwn_reduce_partials", c_int, [ctypes.POINTER(ReduceSeg), c_int, c_void_p]),
+    ("gwn_wgrad_group_supported", c_int, [c_int, c_int, c_int]),
+    ("gwn_wgrad_group_plan", c_int, [ctypes.POINTER(c_int), c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
+    ("gwn_wgrad_group", c_int, [ctypes.POINTER(WgradProblem), c_int, c_int, c_int, c_int, c_void_p]),
     ("gwn_wgrad_bn", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,
                              c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     ("gwn_gram", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_long, c_int, c_int, c_void_p, c_int,

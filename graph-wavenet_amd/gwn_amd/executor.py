@@ -393,10 +393,27 @@ class Executor:
                 pm.append(e(max(1, lib.gwn_wgrad_partial_count(rows, C, cfg.W)) * (C * cfg.W + C)))
                 pt.append(e(max(1, lib.gwn_wgrad_partial_count(rows, 2 * C, 2 * C)) * (4 * C * C + 2 * C)))
             s["part_mlp"], s["part_tcn"] = pm, pt
+            # grouped weight gradients (gwn_wgrad_group): every layer's mlp / TCN dW in one launch
+            # each at the end of the backward, so each layer keeps its own dh / dfg
+            if self._group_ok():
+                rows_l = [ts[i + 1] * P for i in range(L)]
+                gm = self._group_plan(rows_l[:L - 1], C, cfg.W, 1)
+                gt = self._group_plan(rows_l, 2 * C, C, 2)
+                if gm is not None and gt is not None and L >= 2:
+                    s["group_mlp"] = [e(n * (C * cfg.W + C)) for n in gm]
+                    s["group_tcn"] = [e(n * (4 * C * C + 2 * C)) for n in gt]
+                    s["group_np"] = (gm, gt)
+                    s["dh_l"] = [e(r, C) for r in rows_l]
+                    s["dfg_l"] = [e(r, 2 * D) for r in rows_l]
+                    s["aff_id"] = torch.cat([torch.zeros(C, device=self.device), torch.ones(C, device=self.device),
+                                             torch.zeros(C, device=self.device)])
             if cfg.Cin <= 4 and 256 % C == 0:  # the start conv's weight gradient (narrow form)
                 s["part_start"] = e(max(1, lib.gwn_wgrad_partial_count(ts[0] * P, C, cfg.Cin)) * (C * cfg.Cin + C))
             if cfg.E % 32 == 0 and (cfg.OP // 32) * (cfg.E // 32) <= 16:  # end_conv_2's weight gradient
                 s["part_e2"] = e(max(1, lib.gwn_wgrad_partial_count(tf * P, cfg.OP, cfg.E)) * (cfg.OP * cfg.E + cfg.OP))
+            ge = self._group_plan([tf * P], cfg.OP, cfg.E, 1) if self._group_ok() else None
+            if ge is not None:
+                s["part_e2g"] = (e(ge[0] * (cfg.OP * cfg.E + cfg.OP)), ge[0])
 
         side_need = [lib.gwn_wgrad_workspace_floats(maxrows, C, cfg.W),
                      lib.gwn_wgrad_workspace_floats(maxrows, 2 * C, 2 * C),
@@ -964,7 +981,14 @@ class Executor:
         nt = self._head_nt()
         # end_conv_2: its weight gradient from the 32-column padded output gradient on the row
         # reduction kernel (deferred), else the split-K GEMM
-        if defer and "part_e2" in sc:
+        if defer and "part_e2g" in sc:  # one-problem gwn_wgrad_group (4 column groups per workgroup)
+            part, nparts = sc["part_e2g"]
+            pr = _lib.WgradProblem(dY=ptr(sc["dy"]), ldy=OP, X=ptr(acts.e1), ldx=E, x_rows=rows_f, shift=0,
+                                   part=ptr(part), R=rows_f)
+            lib.call("gwn_wgrad_group", (_lib.WgradProblem * 1)(pr), 1, OP, E, 1, st)
+            segs.append(_lib.ReduceSeg(part=ptr(part), nparts=nparts, part_stride=OP * E + OP, J=O, Kc=E,
+                                       out=ptr(self.gk("e2_w")), ld_out=E, out2=ptr(self.gk("e2_b")), db_off=OP * E))
+        elif defer and "part_e2" in sc:
             part = sc["part_e2"]
             lib.call("gwn_wgrad_partials", ptr(sc["dy"]), OP, OP, ptr(acts.e1), E, rows_f, E, 1, 0, rows_f,
                      None, None, None, ptr(part), st)
@@ -1002,6 +1026,9 @@ class Executor:
             dx = bufs[i % 2]
             par = "" if (i % 2 == 0 or not overlap) else "2"
             dh, dhc, dfg = sc["dh" + par], sc["dhc" + par], sc["dfg" + par]
+            grouped = defer and "dh_l" in sc
+            if grouped:  # this layer's own dh / dfg, read by the grouped weight gradients at the end
+                dh, dfg = sc["dh_l"][i], sc["dfg_l"][i]
             if overlap and (i + 2) in side_done:
                 main.wait_event(side_done[i + 2])
             dxg, ld_dxg, acc = None, 0, 0
@@ -1052,7 +1079,8 @@ class Executor:
                 if overlap:
                     self._side_gcn_grads(main, side, acts, i, rows, dh, dhc, adp_index, first_adp, sc)
                 if defer:
-                    self._defer_gcn_grads(acts, i, rows, dh, sc, segs, st)
+                    if not grouped:
+                        self._defer_gcn_grads(acts, i, rows, dh, sc, segs, st)
                     if adp_index >= 0:  # issued after the layer's TCN backward (below)
                         gram_now = (dhc, first_adp)
                 if adp_index >= 0:
@@ -1078,13 +1106,15 @@ class Executor:
             if overlap:
                 side_done[i] = self._side_tcn_grads(main, side, acts, i, rows, dfg, sc)
             if defer:
-                part = sc["part_tcn"][i]
-                lib.call("gwn_wgrad_partials", ptr(dfg), 2 * C, 2 * C, xin, C, ts[i] * P, C, 2, d * P, rows,
-                         raff[0], raff[1], raff[2], ptr(part), st)
-                segs.append(_lib.ReduceSeg(part=ptr(part), nparts=_lib.load().gwn_wgrad_partial_count(rows, 2 * C, 2 * C),
-                                           part_stride=4 * C * C + 2 * C, J=2 * C, Kc=2 * C,
-                                           out=ptr(self.gk("fg_w%d" % i)), ld_out=2 * C,
-                                           out2=ptr(self.gk("fg_b%d" % i))))
+                if not grouped:
+                    part = sc["part_tcn"][i]
+                    lib.call("gwn_wgrad_partials", ptr(dfg), 2 * C, 2 * C, xin, C, ts[i] * P, C, 2, d * P, rows,
+                             raff[0], raff[1], raff[2], ptr(part), st)
+                    segs.append(_lib.ReduceSeg(part=ptr(part),
+                                               nparts=_lib.load().gwn_wgrad_partial_count(rows, 2 * C, 2 * C),
+                                               part_stride=4 * C * C + 2 * C, J=2 * C, Kc=2 * C,
+                                               out=ptr(self.gk("fg_w%d" % i)), ld_out=2 * C,
+                                               out2=ptr(self.gk("fg_b%d" % i))))
                 if gram_now is not None:
                     self._defer_gram(acts, i, rows, gram_now[0], adp_index, gram_now[1], sc, st)
                     gram_now = None
@@ -1102,6 +1132,8 @@ class Executor:
                                        ld_out=cfg.Cin, out2=ptr(self.gk("start_b"))))
         else:
             wgrad(dnext, C, acts.xin, cfg.Cin, rows0, self.gk("start_w"), ws, self.gk("start_b"))
+        if defer and "dh_l" in sc:
+            self._group_wgrads(acts, sc, segs, st)
         if defer:
             for k in range(0, len(segs), 32):  # <= 32 segments per launch (include/gwn.h)
                 chunk = segs[k:k + 32]
@@ -1139,6 +1171,55 @@ class Executor:
         """Deferred weight / adjacency gradients (GWN_DEFER_WGRAD=0: each reduced in its own
         launches right after its layer)."""
         return os.environ.get("GWN_DEFER_WGRAD", "1") != "0" and "part_mlp" in sc
+
+    def _group_ok(self):
+        """Grouped weight gradients (gwn_wgrad_group, one launch per weight family for all layers);
+        GWN_WGRAD_GROUP=0 keeps one gwn_wgrad_partials launch per layer (A/B measurements)."""
+        return os.environ.get("GWN_WGRAD_GROUP", "1") != "0"
+
+    @staticmethod
+    def _group_plan(rows, J, Kt, ntaps):
+        """Partial slots per problem of a gwn_wgrad_group launch (None: shape not built)."""
+        lib = _lib.load()
+        if not rows or len(rows) > 8 or not lib.gwn_wgrad_group_supported(J, Kt, ntaps):
+            return None
+        R = (ctypes.c_int * len(rows))(*rows)
+        nb = (ctypes.c_int * len(rows))()
+        if lib.gwn_wgrad_group_plan(R, len(rows), J, Kt, ntaps, nb) <= 0:
+            return None
+        return list(nb)
+
+    def _group_wgrads(self, acts, sc, segs, st):
+        """Every layer's gcn-mlp dW / db and gated-TCN dW / db: two gwn_wgrad_group launches over the
+        layers' own dh / dfg, their partials reduced with the rest by gwn_reduce_partials."""
+        cfg = self.cfg
+        C, W, L, P = cfg.C, cfg.W, cfg.L, acts.P
+        ts = acts.ts
+        gm, gt = sc["group_np"]
+        probs = []
+        for i in range(L - 1):
+            rows = ts[i + 1] * P
+            part = sc["group_mlp"][i]
+            probs.append(_lib.WgradProblem(dY=ptr(sc["dh_l"][i]), ldy=C, X=ptr(acts.H[i]), ldx=W, x_rows=rows, shift=0,
+                                           part=ptr(part), R=rows))
+            segs.append(_lib.ReduceSeg(part=ptr(part), nparts=gm[i], part_stride=C * W + C, J=C, Kc=W,
+                                       out=ptr(self.gk("mlp_w%d" % i)), ld_out=W, out2=ptr(self.gk("mlp_b%d" % i))))
+        _lib.call("gwn_wgrad_group", (_lib.WgradProblem * len(probs))(*probs), len(probs), C, W, 1, st)
+        probs = []
+        ida = sc["aff_id"].data_ptr()
+        for i in range(L):
+            rows = ts[i + 1] * P
+            xin, _, _, raff = self.layer_input(acts, i)
+            if raff[0] is None:  # identity affine: (x - 0) * 1 + 0, exact
+                raff = (ida, ida + 4 * C, ida + 8 * C)
+            part = sc["group_tcn"][i]
+            probs.append(_lib.WgradProblem(dY=ptr(sc["dfg_l"][i]), ldy=2 * C, X=xin, ldx=C, x_rows=ts[i] * P,
+                                           shift=cfg.dilations[i] * P, x_mean=raff[0], x_scale=raff[1],
+                                           x_shift=raff[2], part=ptr(part), R=rows))
+            segs.append(_lib.ReduceSeg(part=ptr(part), nparts=gt[i], part_stride=4 * C * C + 2 * C, J=2 * C,
+                                       Kc=2 * C, out=ptr(self.gk("fg_w%d" % i)), ld_out=2 * C,
+                                       out2=ptr(self.gk("fg_b%d" % i))))
+        _lib.call("gwn_wgrad_group", (_lib.WgradProblem * len(probs))(*probs), len(probs), 2 * C, C, 2, st)
 
     def _defer_gcn_grads(self, acts, i, rows, dh, sc, segs, st):
         """Layer i's dW_mlp / db_mlp partials for the end-of-backward reduction."""

@@ -43,7 +43,8 @@ typedef enum gwn_dtype {
 void gwn_set_sync_check(int mode);
 const char* gwn_last_error(void);
 /* sizeof of the argument structs below, for bindings that mirror them (ctypes, cgo):
- * "gwn_gemm_desc", "gwn_tcn_args", "gwn_tcn_bwd_args", "gwn_gcn_args", "gwn_gcn_bwd_args";
+ * "gwn_gemm_desc", "gwn_tcn_args", "gwn_tcn_bwd_args", "gwn_gcn_args", "gwn_gcn_bwd_args",
+ * "gwn_reduce_seg", "gwn_wgrad_problem";
  * -1 for an unknown name */
 long gwn_abi_sizeof(const char* struct_name);
 
@@ -446,6 +447,26 @@ int gwn_wgrad_partials(const float* dY, long ldy, int J, const float* X, long ld
                        long shift, int R, const float* x_mean, const float* x_scale, const float* x_shift, float* part,
                        hipStream_t stream);
 int gwn_reduce_partials(const gwn_reduce_seg* segs, int nseg, hipStream_t stream);
+
+/* Grouped weight gradients: the gwn_wgrad_bn problem for the same weight shape of up to 8 layers
+ * in ONE launch (the deferred gcn-mlp or gated-TCN weight gradients of a whole backward).  Problem
+ * p writes nparts[p] partials [nparts][J*Kc + J] (bias last) at its `part`, where nparts comes from
+ * gwn_wgrad_group_plan (the device's CUs dealt to the problems in proportion to R; the return value
+ * is their sum, 0 for an unsupported shape); gwn_reduce_partials then sums them (a segment per
+ * problem).  Built shapes (gwn_wgrad_group_supported): (J, Kt, ntaps) = (32, 224, 1) the gcn mlp
+ * with 3 supports, (64, 32, 2) the gated TCN, (32, 512, 1) end_conv_2 on its 32-row padded
+ * gradient.  x_mean / x_scale / x_shift: all three for every problem, or for none.  dY, X 16-B
+ * aligned, ldy / ldx multiples of 4.  Deterministic (fixed-order sums, no float atomics). */
+typedef struct gwn_wgrad_problem {
+  const float* dY; long ldy;
+  const float* X; long ldx; long x_rows; long shift;
+  const float* x_mean; const float* x_scale; const float* x_shift;
+  float* part;
+  int R;
+} gwn_wgrad_problem;
+int gwn_wgrad_group_supported(int J, int Kt, int ntaps);
+int gwn_wgrad_group_plan(const int* R, int nprob, int J, int Kt, int ntaps, int* nparts);
+int gwn_wgrad_group(const gwn_wgrad_problem* problems, int nprob, int J, int Kt, int ntaps, hipStream_t stream);
 
 /* Adjacency gradient of order-2 diffusion over all slices (c = 32 channels per row):
  *   dA[v][w] (+)= sum_s sum_c X1[s*n + v][c] T1[s*n + w][c]  (+ same for X2, T2 when non-NULL)

@@ -1253,7 +1253,7 @@ def test_gcn_t16_bf16_backward(gpu, n, mode):
     if bn:
         f, s = fg[:, 0::2].double().cpu(), fg[:, 1::2].double().cpu()
         sk = torch.zeros(rows, C, dtype=torch.float64)
-        sk[skip_row0:] = dskip.double().cpu()[skip_row0:]
+        sk[skip_row0:] = dskip.double().cpu()[:rows - skip_row0]  # dskip row m - skip_row0 (include/gwn.h)
 
         def gate(dxg):
             gv = dxg + sk
@@ -1279,3 +1279,81 @@ def test_gcn_t16_bf16_backward(gpu, n, mode):
             got = dhc[:, (1 + j) * C:(2 + j) * C].cpu().numpy()
             assert rel_err(got, em.numpy()) <= 2e-5
             assert rel_err(got, ex.numpy()) <= 1e-2
+
+
+@pytest.mark.parametrize("shape", ["mlp", "tcn", "e2"])
+def test_wgrad_group_vs_fp64(gpu, shape):
+    """gwn_wgrad_group (the deferred weight gradients of several layers in one launch, then
+    gwn_reduce_partials) against fp64, per problem: the gcn mlp of 7 layers (J = 32, Kc = 224,
+    the METR-LA row counts scaled down, ragged), the gated TCN of 8 layers (J = 64, two taps
+    d*P apart, BatchNorm affine on load, identity affine for the first), end_conv_2 on its 32-row
+    padded gradient (J = 32, Kc = 512, one problem).  Bound per element: an fp32 FMA chain over the
+    rows, |err| <= 2^-22 R sum|dY||X|.  A second launch is bitwise identical (fixed-order sums)."""
+    import ctypes
+    from gwn_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed({"mlp": 1, "tcn": 2, "e2": 3}[shape])
+    P = 207 * 3
+    if shape == "mlp":
+        J, Kt, ntaps, Ts = 32, 224, 1, [12, 10, 9, 7, 6, 4, 3]
+    elif shape == "tcn":
+        J, Kt, ntaps, Ts = 64, 32, 2, [12, 10, 9, 7, 6, 4, 3, 1]
+    else:
+        J, Kt, ntaps, Ts = 32, 512, 1, [1]
+    dil = [1, 2, 1, 2, 1, 2, 1, 2]
+    probs, host = [], []
+    for p, t in enumerate(Ts):
+        R = t * P + (p % 3)  # ragged
+        shift = dil[p] * P if ntaps == 2 else 0
+        x_rows = R + (ntaps - 1) * shift
+        dY = torch.randn(R, J, dtype=torch.float64)
+        if shape == "e2":
+            dY[:, 12:] = 0.0  # the padded output gradient
+        X = torch.randn(x_rows, Kt, dtype=torch.float64) * 2 + 1
+        aff = None
+        if shape == "tcn":
+            aff = (torch.zeros(Kt), torch.ones(Kt), torch.zeros(Kt)) if p == 0 else \
+                (torch.randn(Kt) + 1, torch.rand(Kt) + 0.5, torch.randn(Kt))
+        host.append((dY, X, aff, R, shift))
+    nb = (ctypes.c_int * len(Ts))()
+    total = lib.gwn_wgrad_group_plan((ctypes.c_int * len(Ts))(*[h[3] for h in host]), len(Ts), J, Kt, ntaps, nb)
+    assert total > 0 and sum(nb) == total
+    keep = []
+    for p, (dY, X, aff, R, shift) in enumerate(host):
+        dYd, Xd = dY.float().to(gpu), X.float().to(gpu)
+        affd = [a.float().to(gpu) for a in aff] if aff is not None else [None] * 3
+        part = torch.full((nb[p] * (J * Kt * ntaps + J),), float("nan"), device=gpu)
+        keep.append((dYd, Xd, affd, part))
+        probs.append(_lib.WgradProblem(dY=dYd.data_ptr(), ldy=J, X=Xd.data_ptr(), ldx=Kt, x_rows=X.shape[0], shift=shift,
+                                       x_mean=affd[0].data_ptr() if aff is not None else None,
+                                       x_scale=affd[1].data_ptr() if aff is not None else None,
+                                       x_shift=affd[2].data_ptr() if aff is not None else None,
+                                       part=part.data_ptr(), R=R))
+    arr = (_lib.WgradProblem * len(probs))(*probs)
+    Kc = Kt * ntaps
+    outs = []
+    for rep in range(2):
+        _lib.call("gwn_wgrad_group", arr, len(probs), J, Kt, ntaps, _lib.stream())
+        res = []
+        segs = []
+        for p in range(len(probs)):
+            dw, db = torch.empty(J, Kc, device=gpu), torch.empty(J, device=gpu)
+            res.append((dw, db))
+            segs.append(_lib.ReduceSeg(part=keep[p][3].data_ptr(), nparts=nb[p], part_stride=J * Kc + J, J=J, Kc=Kc,
+                                       out=dw.data_ptr(), ld_out=Kc, out2=db.data_ptr()))
+        _lib.call("gwn_reduce_partials", (_lib.ReduceSeg * len(segs))(*segs), len(segs), _lib.stream())
+        torch.cuda.synchronize()
+        outs.append(res)
+    for p, (dY, X, aff, R, shift) in enumerate(host):
+        Xf = X.float().double()
+        if aff is not None:
+            Xf = ((X.float() - aff[0].float()) * aff[1].float() + aff[2].float()).double()
+        Xk = torch.cat([Xf[tap * shift:tap * shift + R] for tap in range(ntaps)], dim=1)
+        dYf = dY.float().double()
+        ref_w, ref_b = dYf.t() @ Xk, dYf.sum(0)
+        bw = 2.0 ** -22 * R * (dYf.abs().t() @ Xk.abs()) + 1e-30
+        bb = 2.0 ** -22 * R * dYf.abs().sum(0) + 1e-30
+        dw, db = outs[0][p]
+        assert torch.all((dw.double().cpu() - ref_w).abs() <= bw), (p, float(((dw.double().cpu() - ref_w).abs() / bw).max()))
+        assert torch.all((db.double().cpu() - ref_b).abs() <= bb), p
+        assert torch.equal(outs[1][p][0], dw) and torch.equal(outs[1][p][1], db)
