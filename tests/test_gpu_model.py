@@ -375,3 +375,46 @@ def test_power_schedule_matches_chained_hops(gpu, monkeypatch):
             assert float((a - b).norm() / b.norm()) <= 2e-5, k
         else:
             assert float((a - b).abs().max()) <= 1e-5 * scale, k
+
+
+def test_num_batches_tracked_counts_train_forwards(gpu):
+    """BatchNorm2d.num_batches_tracked is advanced on the device by the BatchNorm finalise (inside
+    the next layer's gated-TCN launch, or gwn_batchnorm_fwd_fold / _partials), once per train-mode
+    forward as torch does: three trainer.train steps (the first eager, then HIP-graph replays), one
+    autograd train-mode forward, eval forwards (no change), and gwnet_diff_G called without
+    supports (the residual-only schedule, model.py:391-398)."""
+    from gwn_amd import synthetic, util
+    from gwn_amd.engine import trainer
+    from gwn_amd.model import gwnet_diff_G
+    n = 37
+    adj = synthetic.random_sensor_graph(n, density=0.2, seed=5)
+    sups = [torch.tensor(a, device=gpu) for a in synthetic.double_transition(adj)]
+    x, y = synthetic.synthetic_batch(4, n, 12, seed=9)
+    torch.manual_seed(3)
+    eng = trainer(util.StandardScaler(54.4, 19.5), 2, 12, n, 32, 0.3, 1e-3, 1e-4, gpu, sups, True, True, None, 4, 2)
+    bns = [eng.model.bn[i] for i in range(len(eng.model.bn))]
+    assert all(int(b.num_batches_tracked) == 0 for b in bns)
+    for step in range(3):
+        eng.train(torch.tensor(x, device=gpu), torch.tensor(y, device=gpu))
+        torch.cuda.synchronize()
+        assert [int(b.num_batches_tracked) for b in bns] == [step + 1] * len(bns), step
+    m = eng.model
+    m.train()
+    out = m(torch.nn.functional.pad(torch.tensor(x, device=gpu), (1, 0, 0, 0)))
+    out.sum().backward()
+    torch.cuda.synchronize()
+    assert [int(b.num_batches_tracked) for b in bns] == [4] * len(bns)
+    m.eval()
+    with torch.no_grad():
+        m(torch.tensor(x, device=gpu))
+        eng.eval(torch.tensor(x, device=gpu), torch.tensor(y, device=gpu))
+    torch.cuda.synchronize()
+    assert [int(b.num_batches_tracked) for b in bns] == [4] * len(bns)
+    dg = gwnet_diff_G(gpu, 16, 0.0, supports_len=2, gcn_bool=True, addaptadj=False, residual_channels=16,
+                      dilation_channels=16, skip_channels=64, end_channels=128, blocks=2, layers=2)
+    dg.train()
+    xd = torch.randn(2, 2, 16, 13, device=gpu)
+    for k in range(2):
+        dg(xd, None, None).sum().backward()
+    torch.cuda.synchronize()
+    assert [int(b.num_batches_tracked) for b in dg.bn] == [2] * len(dg.bn)

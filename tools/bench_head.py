@@ -65,6 +65,12 @@ def main():
             ks = max(1, min(1024 // tiles, K // 256))
         ws = torch.empty(max(1, _lib.load().gwn_gemm_workspace_floats(M, N, ks)), device=dev)
         t_gwn = timeit(lambda: gwn_mm(A, B, C, ks, ws))
+        if K > 4 * max(M, N) and M >= 256:  # split-K sweep of the head weight gradients
+            sweep = []
+            for k2 in (4, 8, 12, 16, 24, 32, 48, 64, 96):
+                ws2 = torch.empty(max(1, _lib.load().gwn_gemm_workspace_floats(M, N, k2)), device=dev)
+                sweep.append("ks%d %.1f" % (k2, timeit(lambda: gwn_mm(A, B, C, k2, ws2))))
+            print("   ", name, "split-K sweep (us):", ", ".join(sweep), flush=True)
         print("%-9s M=%6d N=%4d K=%6d  rocBLAS %7.1f us (%5.1f TF)  hipBLASLt %7.1f us (%5.1f TF)  "
               "gwn_gemm %7.1f us (%5.1f TF)"
               % (name, M, N, K, t_torch, flop / t_torch / 1e6, t_lt, flop / t_lt / 1e6, t_gwn, flop / t_gwn / 1e6),
