@@ -28,11 +28,13 @@ constexpr int NXCD = 8;
 #define GRAM_WAVES 1792  // target wave count of a gram launch
 #endif
 
+constexpr int GL = 8;  // layers of a grouped launch (gwn_gram_group)
 struct Gram {
-  const float* X[2]; const float* T[2]; int npairs;  // pair 1 used iff npairs == 2
+  const float* X[GL][2]; const float* T[GL][2]; int npairs;  // pair 1 used iff npairs == 2
+  int lslices[GL], lsplit0[GL + 1], nlayers;  // layer l: its slices, splits [lsplit0[l], lsplit0[l+1])
   long ldx, ldt;
-  int n, nt, slices, nsplit;  // nt = ceil(n / 32)
-  float* part;                // [nsplit][32 nt][32 nt]
+  int n, nt, nsplit;  // nt = ceil(n / 32); nsplit = all layers' splits
+  float* part;        // [nsplit][32 nt][32 nt]
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long bytes) {
@@ -64,14 +66,18 @@ __global__ __launch_bounds__(64) void gram_kernel(const Gram g) {
   if (split >= g.nsplit) return;
   const int vt = blk / ntp, wt0 = 2 * (blk % ntp);
   const bool two = wt0 + 1 < g.nt;  // wave-uniform: the last pair of an odd tile count has one tile
-  const int s0 = (int)((long)g.slices * split / g.nsplit), s1 = (int)((long)g.slices * (split + 1) / g.nsplit);
+  // the layer of this split (grouped launch) and its slice range within that layer
+  int L = 0;
+  while (L + 1 < g.nlayers && split >= g.lsplit0[L + 1]) ++L;
+  const int lsl = g.lslices[L], ls = split - g.lsplit0[L], lns = g.lsplit0[L + 1] - g.lsplit0[L];
+  const int s0 = (int)((long)lsl * ls / lns), s1 = (int)((long)lsl * (ls + 1) / lns);
 
   __amdgpu_buffer_rsrc_t rx[NP], rt[NP];
-  const long rows = (long)g.slices * g.n;
+  const long rows = (long)lsl * g.n;
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    rx[p] = rsrc(g.X[p], rows * g.ldx * 4);
-    rt[p] = rsrc(g.T[p], rows * g.ldt * 4);
+    rx[p] = rsrc(g.X[L][p], rows * g.ldx * 4);
+    rt[p] = rsrc(g.T[L][p], rows * g.ldt * 4);
   }
   const int v = 32 * vt + col, w0 = 32 * wt0 + col, w1 = w0 + 32;
   // fragments of (slice s, pair p); p must be a compile-time constant after unrolling so the buffer
@@ -345,11 +351,12 @@ int gwn_gram_dtype(const float* x1, const float* t1, const float* x2, const floa
               "gram: operands must be 16-B aligned with ld % 4 == 0");
   GWN_REQUIRE((long)slices * n * (ldx > ldt ? ldx : ldt) * 4 < 0x7fff0000L, "gram: operand beyond a 2 GB buffer window");
   Gram g = {};
-  g.X[0] = x1; g.T[0] = t1; g.X[1] = x2; g.T[1] = t2;
+  g.X[0][0] = x1; g.T[0][0] = t1; g.X[0][1] = x2; g.T[0][1] = t2;
   g.npairs = x2 ? 2 : 1;
   g.ldx = ldx; g.ldt = ldt;
-  g.n = n; g.nt = (n + 31) / 32; g.slices = slices;
+  g.n = n; g.nt = (n + 31) / 32;
   g.nsplit = gram_nsplit(n, slices);
+  g.nlayers = 1; g.lslices[0] = slices; g.lsplit0[0] = 0; g.lsplit0[1] = g.nsplit;
   g.part = ws;
   {
     const long rows = (long)slices * n;  // the loads stay inside rows * ld of each operand
@@ -374,6 +381,81 @@ int gwn_gram_dtype(const float* x1, const float* t1, const float* x2, const floa
   const long outs = (long)n * n;
   gram_reduce_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(ws, g.nsplit, n, 32 * g.nt, dA, ld_dA,
                                                                      accumulate);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Grouped gram: the adaptive-support gradient of every layer of a backward in ONE launch (and one
+// reduction), all layers accumulating into the same dA.  The gram_kernel waves of a layer-size
+// launch are latency-bound at the small T (METR B=64, round-4 trace: ~7.7 us fixed per launch + a
+// 5.5 us reduce each, on 22-63 us kernels); here the wave target is dealt to the layers in
+// proportion to their slices, every split inside one layer.
+namespace {
+int gram_group_plan(int n, const int* slices, int nlayers, int* nsp) {
+  const int nt = (n + 31) / 32;
+  int target = GRAM_WAVES / (nt * ((nt + 1) / 2));
+  target = (target / NXCD) * NXCD;
+  if (target < NXCD) target = NXCD;
+  long tot = 0;
+  for (int l = 0; l < nlayers; ++l) tot += slices[l];
+  int used = 0;
+  for (int l = 0; l < nlayers; ++l) {
+    int k = (int)((double)target * slices[l] / (double)tot + 0.5);
+    if (k < 1) k = 1;
+    if (k > slices[l]) k = slices[l];
+    nsp[l] = k;
+    used += k;
+  }
+  return used;
+}
+}  // namespace
+
+long gwn_gram_group_workspace_floats(int n, const int* slices, int nlayers) {
+  if (n <= 0 || nlayers < 1 || nlayers > GL || !slices) return 0;
+  int nsp[GL];
+  for (int l = 0; l < nlayers; ++l)
+    if (slices[l] <= 0) return 0;
+  const long np = 32L * ((n + 31) / 32);
+  return (long)gram_group_plan(n, slices, nlayers, nsp) * np * np;
+}
+
+int gwn_gram_group(const gwn_gram_layer* layers, int nlayers, long ldx, long ldt, int n, float* dA, int ld_dA,
+                   int accumulate, float* ws, hipStream_t s) {
+  GWN_REQUIRE(layers && nlayers >= 1 && nlayers <= GL && n > 0 && dA && ws, "gram_group: 1..8 layers, n, dA, ws");
+  GWN_REQUIRE((ldx & 3) == 0 && (ldt & 3) == 0, "gram_group: ld % 4 == 0");
+  Gram g = {};
+  int sl[GL], nsp[GL];
+  for (int l = 0; l < nlayers; ++l) {
+    const gwn_gram_layer& q = layers[l];
+    GWN_REQUIRE(q.slices > 0 && q.x1 && q.t1 && q.x2 && q.t2 && ((uintptr_t)q.x1 & 15) == 0 &&
+                    ((uintptr_t)q.t1 & 15) == 0 && ((uintptr_t)q.x2 & 15) == 0 && ((uintptr_t)q.t2 & 15) == 0,
+                "gram_group: every layer needs slices > 0 and both 16-B aligned pairs");
+    GWN_REQUIRE((long)q.slices * n * (ldx > ldt ? ldx : ldt) * 4 < 0x7fff0000L,
+                "gram_group: operand beyond a 2 GB buffer window");
+    g.X[l][0] = q.x1; g.T[l][0] = q.t1; g.X[l][1] = q.x2; g.T[l][1] = q.t2;
+    sl[l] = q.slices;
+  }
+  g.nsplit = gram_group_plan(n, sl, nlayers, nsp);
+  g.nlayers = nlayers;
+  g.lsplit0[0] = 0;
+  for (int l = 0; l < nlayers; ++l) {
+    g.lslices[l] = sl[l];
+    g.lsplit0[l + 1] = g.lsplit0[l] + nsp[l];
+  }
+  g.npairs = 2;
+  g.ldx = ldx; g.ldt = ldt;
+  g.n = n; g.nt = (n + 31) / 32;
+  g.part = ws;
+  const long np = 32L * g.nt;
+  GWN_DEBUG_RANGE(ws, g.nsplit * np * np * 4, "gram_group partials");
+  GWN_DEBUG_RANGE(dA, ((long)(n - 1) * ld_dA + n) * 4, "gram_group dA");
+  const int per_split = g.nt * ((g.nt + 1) / 2);
+  const int blocks = ((g.nsplit + NXCD - 1) / NXCD) * NXCD * per_split;
+  gram_kernel<2><<<blocks, 64, 0, s>>>(g);
+  GWN_CHECK_LAUNCH();
+  const long outs = (long)n * n;
+  gram_reduce_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(ws, g.nsplit, n, (int)np, dA, ld_dA, accumulate);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

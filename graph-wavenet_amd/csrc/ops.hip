@@ -929,6 +929,7 @@ long gwn_abi_sizeof(const char* name) {
   if (!strcmp(name, "gwn_gcn_args")) return (long)sizeof(gwn_gcn_args);
   if (!strcmp(name, "gwn_gcn_bwd_args")) return (long)sizeof(gwn_gcn_bwd_args);
   if (!strcmp(name, "gwn_wgrad_problem")) return (long)sizeof(gwn_wgrad_problem);
+  if (!strcmp(name, "gwn_gram_layer")) return (long)sizeof(gwn_gram_layer);
   return -1;
 }
 

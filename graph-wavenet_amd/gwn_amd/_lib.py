@@ -120,6 +120,10 @@ class WgradProblem(ctypes.Structure):
     ]
 
 
+class GramLayer(ctypes.Structure):
+    _fields_ = [("x1", c_void_p), ("t1", c_void_p), ("x2", c_void_p), ("t2", c_void_p), ("slices", c_int)]
+
+
 class GcnBwdArgs(ctypes.Structure):
     _fields_ = [
         ("rows", c_int), ("n", c_int), ("c", c_int), ("nsup", c_int),
@@ -153,7 +157,7 @@ class GcnBwdArgs(ctypes.Structure):
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time
 _STRUCTS = {"gwn_gemm_desc": GemmDesc, "gwn_tcn_args": TcnArgs, "gwn_tcn_bwd_args": TcnBwdArgs,
             "gwn_gcn_args": GcnArgs, "gwn_gcn_bwd_args": GcnBwdArgs, "gwn_reduce_seg": ReduceSeg,
-            "gwn_wgrad_problem": WgradProblem}
+            "gwn_wgrad_problem": WgradProblem, "gwn_gram_layer": GramLayer}
 
 
 # (name, restype, argtypes) of every exported entry point declared in include/gwn.h
@@ -199,6 +203,9 @@ _SIGS = [
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gwn_reduce_partials", c_int, [ctypes.POINTER(ReduceSeg), c_int, c_void_p]),
     ("gwn_wgrad_group_supported", c_int, [c_int, c_int, c_int]),
+    ("gwn_gram_group_workspace_floats", c_long, [c_int, ctypes.POINTER(c_int), c_int]),
+    ("gwn_gram_group", c_int, [ctypes.POINTER(GramLayer), c_int, c_long, c_long, c_int, c_void_p, c_int, c_int,
+                               c_void_p, c_void_p]),
     ("gwn_wgrad_group_plan", c_int, [ctypes.POINTER(c_int), c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     ("gwn_wgrad_group", c_int, [ctypes.POINTER(WgradProblem), c_int, c_int, c_int, c_int, c_void_p]),
     ("gwn_wgrad_bn", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,

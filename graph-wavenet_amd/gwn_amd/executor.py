@@ -407,6 +407,12 @@ class Executor:
                     s["dfg_l"] = [e(r, 2 * D) for r in rows_l]
                     s["aff_id"] = torch.cat([torch.zeros(C, device=self.device), torch.ones(C, device=self.device),
                                              torch.zeros(C, device=self.device)])
+                # grouped adaptive-support gradient (gwn_gram_group, fp32 mode): each layer keeps its
+                # t1 / t2 ([rows][96]: the gcn backward's dhcat with only columns 32..96 written)
+                if cfg.adp_live and cfg.use_gcn and os.environ.get("GWN_GRAM_GROUP", "1") != "0":
+                    sl = (ctypes.c_int * (L - 1))(*[rows_l[i] // N for i in range(L - 1)])
+                    s["tt_l"] = [e(rows_l[i], 3 * C) for i in range(L - 1)]
+                    s["ws_gram_group"] = e(int(lib.gwn_gram_group_workspace_floats(N, sl, L - 1)) + 16)
             if cfg.Cin <= 4 and 256 % C == 0:  # the start conv's weight gradient (narrow form)
                 s["part_start"] = e(max(1, lib.gwn_wgrad_partial_count(ts[0] * P, C, cfg.Cin)) * (C * cfg.Cin + C))
             if cfg.E % 32 == 0 and (cfg.OP // 32) * (cfg.E // 32) <= 16:  # end_conv_2's weight gradient
@@ -980,6 +986,10 @@ class Executor:
         defer = not overlap and fuse and self._defer_ok(sc)
         segs = []
         gram_now = None
+        # the adaptive support's gradient of every layer in one gwn_gram_group launch at the end
+        # (fp32 mode; the bf16 mode's tiled-operand gram stays per layer)
+        gram_group = (defer and "tt_l" in sc and cfg.adp_live and not getattr(acts, "gram_g4", False)
+                      and getattr(acts, "g4bt_arr", None) is None and L >= 2)
         main = torch.cuda.current_stream()
         side = self._side_stream() if overlap else None
 
@@ -1044,6 +1054,9 @@ class Executor:
             grouped = defer and "dh_l" in sc
             if grouped:  # this layer's own dh / dfg, read by the grouped weight gradients at the end
                 dh, dfg = sc["dh_l"][i], sc["dfg_l"][i]
+            ld_dhc = cfg.W
+            if gram_group and i < L - 1:  # this layer's own t1 / t2 (grouped gram at the end)
+                dhc, ld_dhc = sc["tt_l"][i], 3 * C
             if overlap and (i + 2) in side_done:
                 main.wait_event(side_done[i + 2])
             dxg, ld_dxg, acc = None, 0, 0
@@ -1058,7 +1071,7 @@ class Executor:
                                      sup=ctypes.cast(acts.sup_arr, ctypes.POINTER(ctypes.c_void_p)),
                                      ld_sup=cfg.NP,
                                      h=ptr(acts.H[i]), ld_h=cfg.W, w_mlp=ptr(self.pk("mlp_w%d" % i)),
-                                     dh=ptr(dh), dhcat=ptr(dhc), ld_dhcat=cfg.W,
+                                     dh=ptr(dh), dhcat=ptr(dhc), ld_dhcat=ld_dhc,
                                      dw_mlp=ptr(self.gk("mlp_w%d" % i)), db_mlp=ptr(self.gk("mlp_b%d" % i)),
                                      adp_index=adp_index, dadp=ptr(sc["dadp"]),
                                      accumulate_dadp=0 if first_adp else 1, workspace=ptr(ws),
@@ -1096,11 +1109,11 @@ class Executor:
                 if defer:
                     if not grouped:
                         self._defer_gcn_grads(acts, i, rows, dh, sc, segs, st)
-                    if adp_index >= 0:  # issued after the layer's TCN backward (below)
+                    if adp_index >= 0 and not gram_group:  # issued after the layer's TCN backward (below)
                         gram_now = (dhc, first_adp)
                 if adp_index >= 0:
                     first_adp = False
-                dxg, ld_dxg, acc = dhc, cfg.W, 1
+                dxg, ld_dxg, acc = dhc, ld_dhc, 1
             xin, _, _, raff = self.layer_input(acts, i)
             tb = _lib.TcnBwdArgs(x=xin, x_mean=raff[0], x_scale=raff[1], x_shift=raff[2], t_in=ts[i], P=P, c=C,
                                  dilation=d, ntaps=cfg.K, c_out=D,
@@ -1149,6 +1162,14 @@ class Executor:
             wgrad(dnext, C, acts.xin, cfg.Cin, rows0, self.gk("start_w"), ws, self.gk("start_b"))
         if defer and "dh_l" in sc:
             self._group_wgrads(acts, sc, segs, st)
+        if gram_group:
+            lay = []
+            for i in range(L - 1):
+                h, t = acts.H[i].data_ptr(), sc["tt_l"][i].data_ptr()
+                lay.append(_lib.GramLayer(x1=h, t1=t + 4 * C, x2=h + 4 * (1 + 2 * adp_index) * C, t2=t + 8 * C,
+                                          slices=ts[i + 1] * P // N))
+            lib.call("gwn_gram_group", (_lib.GramLayer * len(lay))(*lay), len(lay), cfg.W, 3 * C, N, ptr(sc["dadp"]),
+                     cfg.NP, 0, ptr(sc["ws_gram_group"]), st)
         if defer:
             for k in range(0, len(segs), 32):  # <= 32 segments per launch (include/gwn.h)
                 chunk = segs[k:k + 32]

@@ -44,7 +44,7 @@ void gwn_set_sync_check(int mode);
 const char* gwn_last_error(void);
 /* sizeof of the argument structs below, for bindings that mirror them (ctypes, cgo):
  * "gwn_gemm_desc", "gwn_tcn_args", "gwn_tcn_bwd_args", "gwn_gcn_args", "gwn_gcn_bwd_args",
- * "gwn_reduce_seg", "gwn_wgrad_problem";
+ * "gwn_reduce_seg", "gwn_wgrad_problem", "gwn_gram_layer";
  * -1 for an unknown name */
 long gwn_abi_sizeof(const char* struct_name);
 
@@ -486,6 +486,17 @@ int gwn_wgrad_group(const gwn_wgrad_problem* problems, int nprob, int J, int Kt,
  * i.e. both pairs (xg, dx1) and (x1, dx2) of gcn.forward's adaptive support in one launch. */
 int gwn_gram(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
              int slices, float* dA, int ld_dA, int accumulate, float* workspace, hipStream_t stream);
+/* The same for the adaptive support of up to 8 layers in ONE launch (+ one reduction), every layer's
+ * both pairs summed into dA: layer l contributes sum over its slices of x1^T t1 + x2^T t2 (its own
+ * operand pointers, common ldx / ldt, c = 32).  Workspace: gwn_gram_group_workspace_floats(n,
+ * slices[], nlayers) floats.  fp32 operands (the f32 mode's training step). */
+typedef struct gwn_gram_layer {
+  const float* x1; const float* t1; const float* x2; const float* t2;
+  int slices;
+} gwn_gram_layer;
+long gwn_gram_group_workspace_floats(int n, const int* slices, int nlayers);
+int gwn_gram_group(const gwn_gram_layer* layers, int nlayers, long ldx, long ldt, int n, float* dA, int ld_dA,
+                   int accumulate, float* workspace, hipStream_t stream);
 /* gwn_gram on bf16 MFMA operands with fp32 accumulation (the bf16 mode, gwn_dtype BF16) */
 int gwn_gram_bf16(const float* x1, const float* t1, const float* x2, const float* t2, long ldx, long ldt, int n,
                   int slices, float* dA, int ld_dA, int accumulate, float* workspace, hipStream_t stream);

@@ -1357,3 +1357,47 @@ def test_wgrad_group_vs_fp64(gpu, shape):
         assert torch.all((dw.double().cpu() - ref_w).abs() <= bw), (p, float(((dw.double().cpu() - ref_w).abs() / bw).max()))
         assert torch.all((db.double().cpu() - ref_b).abs() <= bb), p
         assert torch.equal(outs[1][p][0], dw) and torch.equal(outs[1][p][1], db)
+
+
+@pytest.mark.parametrize("n", [207, 16, 325])
+def test_gram_group_vs_fp64(gpu, n):
+    """gwn_gram_group (the adaptive-support gradient of several layers in one launch: splits dealt to
+    the layers by slice count, one reduction) against fp64: layers of 36 / 30 / 9 / 3 slices with the
+    training step's operand layout (x in h [rows][224] columns 0 and 160, t1 / t2 in [rows][96]
+    columns 32 and 64), accumulating into dA.  Bound: the fp32 FMA chain over all terms."""
+    import ctypes
+    from gwn_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(n + 5)
+    slices = [36, 30, 9, 3] if n != 325 else [12, 5]
+    ldx, ldt = 224, 96
+    ref = torch.zeros(n, n, dtype=torch.float64)
+    absb = torch.zeros(n, n, dtype=torch.float64)
+    keep, lay = [], []
+    for S in slices:
+        H = torch.randn(S * n, ldx, dtype=torch.float64)
+        Tt = torch.randn(S * n, ldt, dtype=torch.float64)
+        X1, X2 = H[:, :32].reshape(S, n, 32), H[:, 160:192].reshape(S, n, 32)
+        T1, T2 = Tt[:, 32:64].reshape(S, n, 32), Tt[:, 64:96].reshape(S, n, 32)
+        for x, t in ((X1, T1), (X2, T2)):
+            xf, tf_ = x.float().double(), t.float().double()
+            ref += torch.einsum("svc,swc->vw", xf, tf_)
+            absb += torch.einsum("svc,swc->vw", xf.abs(), tf_.abs())
+        Hd, Td = H.float().to(gpu), Tt.float().to(gpu)
+        keep += [Hd, Td]
+        lay.append(_lib.GramLayer(x1=Hd.data_ptr(), t1=Td.data_ptr() + 4 * 32, x2=Hd.data_ptr() + 4 * 160,
+                                  t2=Td.data_ptr() + 4 * 64, slices=S))
+    ldA = n + 3
+    init = torch.randn(n, ldA, dtype=torch.float64)
+    dA = init.float().to(gpu)
+    ref = ref + init[:, :n].float().double()
+    absb = absb + init[:, :n].abs()
+    sl = (ctypes.c_int * len(slices))(*slices)
+    ws = torch.empty(lib.gwn_gram_group_workspace_floats(n, sl, len(slices)) + 16, device=gpu)
+    _lib.call("gwn_gram_group", (_lib.GramLayer * len(lay))(*lay), len(lay), ldx, ldt, n, dA.data_ptr(), ldA, 1,
+              ws.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    got = dA.double().cpu()[:, :n]
+    bound = 2.0 ** -22 * (sum(slices) * 64 + 8) * absb
+    assert torch.all((got - ref).abs() <= bound + 1e-30), float(((got - ref).abs() / (bound + 1e-30)).max())
+    assert torch.equal(dA.cpu()[:, n:], init.float()[:, n:])
