@@ -272,9 +272,12 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
         for ga in launches:
             slices = ga.rows // N
             total_flop += slices * (K * 2 * 2.0 * C * N * N + 2.0 * (2 * K + 1) * C * C * N)
-            # compulsory bytes: xg + residual in, 2K hop outputs + z out; the
-            # last layer (output dead but for BN running stats) stores no hop pieces
-            total_bytes += slices * N * C * 4.0 * (2 + (0 if ga.no_pieces else 2 * K) + 1)
+            # compulsory bytes: xg + residual in, 2K hop outputs + z out (the
+            # hop pieces as bf16 where the bf16 mode stores them so, and its bf16 gram operand
+            # copies xg4: X and one hop piece); the last layer (output dead but for BN running
+            # stats) stores no hop pieces
+            piece_b = 0 if ga.no_pieces else 2 * K * (2.0 if ga.pieces_bf16 else 4.0)
+            total_bytes += slices * N * C * (4.0 * 3 + piece_b + (4.0 if ga.xg4 else 0.0))
             count += 1
     avg_us = 1000.0 * total_ms / count
     achieved = total_flop / (total_ms / 1000.0) / 1e12

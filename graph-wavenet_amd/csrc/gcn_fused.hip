@@ -55,6 +55,7 @@ struct FusedFwd {
   int ksplit, slices; float* kws; int* kcnt;  // support split (ksplit > 1): see unit_of()
   int bn_slots;  // t16 kernels: BN partial slots to write (those past the grid get count 0)
   void* xg4; int xg4_k;  // bf16 t16 kernel: X and support xg4_k's hop 1 in the tiled activation layout
+  void* pb; long ld_pb;  // bf16 t16 kernel: the hop pieces as bf16 [rows][ld_pb] instead of h's columns
 };
 
 struct FusedBwd {
@@ -1558,7 +1559,18 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           t16_mlp(ws + (1 + 2 * k + q) * CH * LDW16, LDW16, acc[q], lane, hacc);
-          if (a.store_pieces && w0 + j < n) {
+          if (a.store_pieces && a.pb && w0 + j < n) {
+            // bf16 pieces: node w0 + j, channels 16 hf + 4 g .. +3 as 8-B stores (non-temporal)
+            __bf16* bp = (__bf16*)a.pb + (row0 + w0 + j) * a.ld_pb + (2 * k + q) * CH + 4 * g;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+              typedef __bf16 bf16x4p __attribute__((ext_vector_type(4)));
+              bf16x4p v;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = (__bf16)acc[q][hf][e];
+              __builtin_nontemporal_store(v, (bf16x4p*)(bp + 16 * hf));
+            }
+          } else if (a.store_pieces && w0 + j < n) {
             float* dp = hs_out + (long)(w0 + j) * ldh + (1 + 2 * k + q) * CH + 4 * g;
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
@@ -2066,6 +2078,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.res_mean = g->residual_mean; a.res_scale = g->residual_scale; a.res_shift = g->residual_shift;
   a.ksplit = 1; a.slices = g->rows / g->n; a.kws = g->ksplit_ws; a.kcnt = g->ksplit_count; a.bn_slots = 0;
   a.xg4 = g->xg4; a.xg4_k = g->xg4_support;
+  a.pb = g->pieces_bf16; a.ld_pb = g->ld_pb;
   GWN_REQUIRE(g->ksplit == 0 || g->ksplit == 1 || g->ksplit == g->nsup, "gcn_fwd: ksplit must be 0, 1 or nsup");
   GWN_REQUIRE(!a.res_scale == !a.res_shift && !a.res_scale == !a.res_mean,
               "gcn_fwd (fused): residual_mean, residual_scale and residual_shift go together");
@@ -2083,6 +2096,9 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
     const size_t fixed = t16b_lds_bytes(g->n, g->nsup, 0), img = t16b_lds_bytes(g->n, g->nsup, 1) - fixed;
     if (fixed + img <= (size_t)T16_LDS_MAX) {
       GWN_REQUIRE(g->w_mlp_t, "gcn_fwd (16-node tiles, bf16): w_mlp_t is required with sup_g4b");
+      GWN_REQUIRE(!g->pieces_bf16 || (g->ld_pb >= 2L * g->nsup * CH && g->ld_pb % 4 == 0 &&
+                                      ((uintptr_t)g->pieces_bf16 & 7) == 0),
+                  "gcn_fwd (bf16 pieces): ld_pb >= 2*nsup*c, a multiple of 4, 8-B aligned pieces_bf16");
       static bool attr_b = false;
       if (!attr_b) {
         (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2108,7 +2124,8 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
       return GWN_OK;
     }
   }
-  GWN_REQUIRE(!g->xg4, "gcn_fwd: xg4 is written by the bf16 16-node tile kernel only (sup_g4b, layout 0)");
+  GWN_REQUIRE(!g->xg4 && !g->pieces_bf16,
+              "gcn_fwd: xg4 / pieces_bf16 are written by the bf16 16-node tile kernel only (sup_g4b, layout 0)");
   GWN_REQUIRE(!g->split_planes,
               "gcn_fwd: bf16 operands (split_planes 1) run on the 16-node tile kernel only: sup_g4b, layout 0, shared "
               "supports, no forced support split, gwn_gcn_t16b_supported(n, nsup)");

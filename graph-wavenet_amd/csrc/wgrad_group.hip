@@ -33,6 +33,7 @@ constexpr int GMAX = 8;  // problems per launch
 struct WProb {
   const float* dY; long ldy;
   const float* X; long ldx; long x_rows; long shift;
+  const __bf16* Xb; long ldxb;  // XB: columns 32 .. 224 (the bf16 mode's hop pieces)
   const float* mean; const float* scale; const float* shiftb;
   float* part;
   int R, nb, b0;  // rows, workgroups, first workgroup of this problem
@@ -48,7 +49,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long by
 
 // JW: dY floats per lane (2: J = 32, 4: J = 64); NX16 / NX8: 64- / 32-column X chunks of a column
 // group; WK column groups x WR = 4 / WK row groups per 4-wave workgroup; PD quads in flight.
-template <int JW, int NX16, int NX8, int WK, int PD, bool AFF>
+// XB (the gcn mlp in bf16 mode, Kc = 224): column chunk 0 (32 fp32 columns, 8-B loads) from X, the
+// hop pieces from Xb as bf16 -- a 16-B load (8 columns per lane: 128) and an 8-B load (4: 64);
+// converted to fp32 in registers (exact), the same 14 output tiles as the fp32 form
+template <int JW, int NX16, int NX8, int WK, int PD, bool AFF, bool XB = false>
 __global__ __launch_bounds__(256) void wgrad_group_kernel(const WGroup G) {
   constexpr int J = 16 * JW;
   constexpr int KCG = 64 * NX16 + 32 * NX8;  // columns of a column group
@@ -56,6 +60,7 @@ __global__ __launch_bounds__(256) void wgrad_group_kernel(const WGroup G) {
   constexpr int WR = 4 / WK;
   constexpr int NT = 4 * NX16 + 2 * NX8;     // 16-column output tiles per J-tile row
   constexpr int XR = 4 * NX16 + 2 * NX8;     // X floats per lane per quad
+  static_assert(!XB || (NX16 == 3 && NX8 == 1 && WK == 1 && !AFF), "XB: the gcn mlp shape only");
   extern __shared__ float red[];             // [WR][J*KC + J]
 
   // the problem of this workgroup (a short scalar search)
@@ -69,6 +74,7 @@ __global__ __launch_bounds__(256) void wgrad_group_kernel(const WGroup G) {
   const int r0 = (int)((long)P.R * b / P.nb), r1 = (int)((long)P.R * (b + 1) / P.nb);
   const __amdgpu_buffer_rsrc_t ry = rsrc(P.dY, (long)r1 * P.ldy * 4);
   const __amdgpu_buffer_rsrc_t rx = rsrc(P.X, P.x_rows * P.ldx * 4);
+  const __amdgpu_buffer_rsrc_t rxb = rsrc(XB ? (const void*)P.Xb : (const void*)P.X, XB ? P.x_rows * P.ldxb * 2 : 0);
 
   // per-chunk X column / tap offsets (floats) and the lane's affine constants
   int xoff[NX16 + NX8];
@@ -112,6 +118,29 @@ __global__ __launch_bounds__(256) void wgrad_group_kernel(const WGroup G) {
       const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy, 0, 0));
 #pragma unroll
       for (int e = 0; e < JW; ++e) yv[e] = v[e];
+    }
+    if constexpr (XB) {
+      const int ox = (u < nq) ? (int)(((long)row * P.ldx + 2 * i) * 4) : 0x7ffffff0;
+      const f32x2 v0 = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rx, ox, 0, 0));
+      xv[0] = v0[0]; xv[1] = v0[1];
+      const int ob = (u < nq) ? (int)(((long)row * P.ldxb + 8 * i) * 2) : 0x7ffffff0;
+      const int ob2 = (u < nq) ? (int)(((long)row * P.ldxb + 128 + 4 * i) * 2) : 0x7ffffff0;
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      const u32x4 b1 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rxb, ob, 0, 0));
+      const u32x2 b2 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rxb, ob2, 0, 0));
+      // bf16 -> fp32: the high half of a float (exact)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xv[2 + 2 * e] = __builtin_bit_cast(float, b1[e] << 16);
+        xv[3 + 2 * e] = __builtin_bit_cast(float, b1[e] & 0xffff0000u);
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        xv[10 + 2 * e] = __builtin_bit_cast(float, b2[e] << 16);
+        xv[11 + 2 * e] = __builtin_bit_cast(float, b2[e] & 0xffff0000u);
+      }
+      return;
     }
     const long xrow = (long)row * P.ldx;
 #pragma unroll
@@ -169,7 +198,9 @@ __global__ __launch_bounds__(256) void wgrad_group_kernel(const WGroup G) {
       const int c = t < 4 * NX16 ? t / 4 : NX16 + (t - 4 * NX16) / 2;
       const int ep = t < 4 * NX16 ? t % 4 : (t - 4 * NX16) % 2;
       const int col0 = kg * KCG + (c < NX16 ? 64 * c : 64 * NX16 + 32 * (c - NX16));
-      const int k = col0 + (c < NX16 ? 4 * i : 2 * i) + ep;
+      // XB: X floats 0-1 = fp32 columns 2i + e, 2-9 = bf16 columns 32 + 8i + e, 10-13 = 160 + 4i + e
+      const int k = XB ? (t < 2 ? 2 * i + t : (t < 10 ? 32 + 8 * i + (t - 2) : 160 + 4 * i + (t - 10)))
+                       : col0 + (c < NX16 ? 4 * i : 2 * i) + ep;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = JW * (4 * q + r) + e;
@@ -194,9 +225,9 @@ struct Shape {
   int J, Kt, ntaps;
 };
 
-template <int JW, int NX16, int NX8, int WK, int PD>
+template <int JW, int NX16, int NX8, int WK, int PD, bool XB = false>
 int launch(const WGroup& g, bool aff, int blocks, size_t lds, hipStream_t s) {
-  auto k = aff ? wgrad_group_kernel<JW, NX16, NX8, WK, PD, true> : wgrad_group_kernel<JW, NX16, NX8, WK, PD, false>;
+  auto k = aff ? wgrad_group_kernel<JW, NX16, NX8, WK, PD, true> : wgrad_group_kernel<JW, NX16, NX8, WK, PD, false, XB>;
   static bool attr[2] = {false, false};
   if (!attr[aff]) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -276,6 +307,8 @@ extern "C" int gwn_wgrad_group(const gwn_wgrad_problem* probs, int nprob, int J,
   g.nprob = nprob;
   g.Kt = Kt;
   const bool aff = probs[0].x_mean != nullptr;
+  const bool xb = probs[0].Xb != nullptr;
+  GWN_REQUIRE(!xb || (kind == 1 && !aff), "wgrad_group: Xb (bf16 hop pieces) is for the gcn-mlp shape, no affine");
   int b0 = 0;
   for (int p = 0; p < nprob; ++p) {
     const gwn_wgrad_problem& q = probs[p];
@@ -284,6 +317,9 @@ extern "C" int gwn_wgrad_group(const gwn_wgrad_problem* probs, int nprob, int J,
                 "wgrad_group: dY, X, part required; ldy >= J, ldx >= Kt, multiples of 4; 16-B aligned operands");
     GWN_REQUIRE((q.x_mean != nullptr) == aff && !q.x_mean == !q.x_scale && !q.x_mean == !q.x_shift,
                 "wgrad_group: x_mean / x_scale / x_shift go together, for every problem or none");
+    GWN_REQUIRE((q.Xb != nullptr) == xb && (!xb || (q.ldxb >= 192 && q.ldxb % 8 == 0 && ((uintptr_t)q.Xb & 15) == 0 &&
+                                                    (long)q.R * q.ldxb * 2 < 0x7fff0000L)),
+                "wgrad_group: Xb for every problem or none; ldxb >= 192, a multiple of 8, 16-B aligned");
     GWN_REQUIRE(q.x_rows >= (long)q.R + (ntaps - 1) * q.shift && q.shift >= 0, "wgrad_group: X rows do not cover the taps");
     GWN_REQUIRE((long)q.R * q.ldy * 4 < 0x7fff0000L && q.x_rows * q.ldx * 4 < 0x7fff0000L,
                 "wgrad_group: operand beyond a 2 GB buffer window");
@@ -291,11 +327,12 @@ extern "C" int gwn_wgrad_group(const gwn_wgrad_problem* probs, int nprob, int J,
     w.dY = q.dY; w.ldy = q.ldy; w.X = q.X; w.ldx = q.ldx; w.x_rows = q.x_rows; w.shift = q.shift;
     w.mean = q.x_mean; w.scale = q.x_scale; w.shiftb = q.x_shift;
     w.part = q.part; w.R = q.R; w.nb = nb[p]; w.b0 = b0;
+    w.Xb = (const __bf16*)q.Xb; w.ldxb = q.ldxb;
     b0 += nb[p];
   }
   const size_t lds = shape_lds(kind);
   switch (kind) {
-    case 1: return launch<2, 3, 1, 1, 4>(g, aff, blocks, lds, s);
+    case 1: return xb ? launch<2, 3, 1, 1, 4, true>(g, false, blocks, lds, s) : launch<2, 3, 1, 1, 4>(g, aff, blocks, lds, s);
     case 2: return launch<4, 0, 2, 1, 6>(g, aff, blocks, lds, s);
     default: return launch<2, 2, 0, 4, 6>(g, aff, blocks, lds, s);
   }

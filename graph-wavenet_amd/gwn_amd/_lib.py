@@ -98,6 +98,7 @@ class GcnArgs(ctypes.Structure):
         ("sup_g4", ctypes.POINTER(c_void_p)),
         ("sup_g4b", ctypes.POINTER(c_void_p)),
         ("xg4", c_void_p), ("xg4_support", c_int),
+        ("pieces_bf16", c_void_p), ("ld_pb", c_long),
     ]
 
 
@@ -117,6 +118,7 @@ class WgradProblem(ctypes.Structure):
         ("x_mean", c_void_p), ("x_scale", c_void_p), ("x_shift", c_void_p),
         ("part", c_void_p),
         ("R", c_int),
+        ("Xb", c_void_p), ("ldxb", c_long),
     ]
 
 

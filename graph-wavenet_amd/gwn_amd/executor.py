@@ -588,6 +588,15 @@ class Executor:
         acts.gram_g4 = gram_g4
         if getattr(acts, "XG4", None) is None:
             acts.XG4 = {}
+        # bf16 mode: the hop pieces' only reader is then the grouped mlp weight gradient -- stored
+        # as bf16 (half the bytes written here and read there); GWN_BF16_PIECES=0 keeps them fp32
+        pieces_b = (gram_g4 and "group_mlp" in scr and self._group_ok() and self._defer_ok(scr)
+                    and not self._overlap_ok(acts) and self._fuse_ok(acts)
+                    and os.environ.get("GWN_BF16_PIECES", "1") != "0")
+        acts.pieces_b = pieces_b
+        if pieces_b and (getattr(acts, "HB", None) is None or len(acts.HB) != L - 1):
+            acts.HB = [torch.empty(ts[i + 1] * P, 2 * cfg.nsup * cfg.D, device=self.device, dtype=torch.int16)
+                       for i in range(L - 1)]
         for i in range(L):
             d, sh = cfg.dilations[i], cfg.shift(i)
             rows = ts[i + 1] * P
@@ -642,6 +651,8 @@ class Executor:
                               sup_g4b=self._arr_field(acts.g4bf_arr),
                               xg4=ptr(xg4) if xg4 is not None else None, xg4_support=cfg.nsup - 1,
                               split_planes=planes, **self.ksplit_fields(scr))
+            if pieces_b and i < L - 1:
+                ga.pieces_bf16, ga.ld_pb = acts.HB[i].data_ptr(), 2 * cfg.nsup * cfg.D
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
             rm, rv, mom, eps, nbt = bn_bufs[i]
@@ -984,6 +995,9 @@ class Executor:
         fuse = self._fuse_ok(acts)
         # weight / adjacency gradients as partials, one reduction launch for the whole backward
         defer = not overlap and fuse and self._defer_ok(sc)
+        if getattr(acts, "pieces_b", False) and not (defer and "dh_l" in sc):
+            raise RuntimeError("gwn_amd: the forward stored bf16 hop pieces for the grouped weight gradient, "
+                               "which this backward does not run")
         segs = []
         gram_now = None
         # the adaptive support's gradient of every layer in one gwn_gram_group launch at the end
@@ -1236,8 +1250,11 @@ class Executor:
         for i in range(L - 1):
             rows = ts[i + 1] * P
             part = sc["group_mlp"][i]
-            probs.append(_lib.WgradProblem(dY=ptr(sc["dh_l"][i]), ldy=C, X=ptr(acts.H[i]), ldx=W, x_rows=rows, shift=0,
-                                           part=ptr(part), R=rows))
+            pr = _lib.WgradProblem(dY=ptr(sc["dh_l"][i]), ldy=C, X=ptr(acts.H[i]), ldx=W, x_rows=rows, shift=0,
+                                   part=ptr(part), R=rows)
+            if getattr(acts, "pieces_b", False):  # the hop pieces as bf16 (columns 32 .. W)
+                pr.Xb, pr.ldxb = acts.HB[i].data_ptr(), W - C
+            probs.append(pr)
             segs.append(_lib.ReduceSeg(part=ptr(part), nparts=gm[i], part_stride=C * W + C, J=C, Kc=W,
                                        out=ptr(self.gk("mlp_w%d" % i)), ld_out=W, out2=ptr(self.gk("mlp_b%d" % i))))
         _lib.call("gwn_wgrad_group", (_lib.WgradProblem * len(probs))(*probs), len(probs), C, W, 1, st)

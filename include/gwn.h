@@ -328,6 +328,10 @@ typedef struct gwn_gcn_args {
    * gwn_gram_g4_bf16's tiled activation layout, X in the first slices*ceil(n/16) KiB, the hop piece
    * in the next (the adaptive-support gram's operands) */
   void* xg4; int xg4_support;
+  /* pieces_bf16 (optional, the bf16 16-node tile kernel only): the hop pieces 1 .. 2*nsup written
+   * as bf16 to pieces_bf16[row * ld_pb + (piece - 1) * c + ch] INSTEAD of h's fp32 columns c .. (their
+   * only reader in the bf16 training step is the mlp weight gradient, gwn_wgrad_problem.Xb) */
+  void* pieces_bf16; long ld_pb;
 } gwn_gcn_args;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
@@ -476,6 +480,10 @@ typedef struct gwn_wgrad_problem {
   const float* x_mean; const float* x_scale; const float* x_shift;
   float* part;
   int R;
+  /* Xb (optional, the gcn-mlp shape only): columns 32 .. Kc of X come from this bf16 matrix
+   * (Xb[r * ldxb + k - 32], gwn_gcn_args.pieces_bf16) and only columns 0 .. 32 from X: the bf16
+   * mode's hop pieces.  For every problem of the launch or for none. */
+  const void* Xb; long ldxb;
 } gwn_wgrad_problem;
 int gwn_wgrad_group_supported(int J, int Kt, int ntaps);
 int gwn_wgrad_group_plan(const int* R, int nprob, int J, int Kt, int ntaps, int* nparts);

@@ -137,7 +137,7 @@ class _GcnBf16(torch.autograd.Function):
     gwn_gram_g4_bf16): the power schedule, pieces [g, A_1 g, A_1^2 g, A_2 g, ...] with
     A_k^q g = einsum(rnd(g), rnd(A_k^q)) ('ncvl,vw->ncwl'); the backward of the power schedule:
       dg  = W_0^T dy + sum_k W_{1+2k}^T (rnd(A_k) rnd(dy)) + W_{2+2k}^T (rnd(A_k^2) rnd(dy)),
-      dW  = dy (x) pieces (exact),
+      dW  = dy (x) [g, rnd(pieces)] (exact products; the pieces are stored as bf16 for it),
       dA_k = sum rnd(g) (x) rnd(t1) + rnd(A_k g) (x) rnd(t2),
              t1 = W_{1+2k}^T dy + W_{2+2k}^T (rnd(A_k) rnd(dy)),  t2 = W_{2+2k}^T dy
     (the chained-hop gradient of x2 = (x A) A, as the HIP path forms it).  rnd = bf16_round, or the
@@ -164,7 +164,8 @@ class _GcnBf16(torch.autograd.Function):
         def wt(q, y):  # W_q^T y over the channel axis
             return torch.einsum("oi,bont->bint", wr[:, q * C:(q + 1) * C], y)
 
-        dw = torch.einsum("bont,bint->oi", dy, h).reshape(w.shape)
+        hb = torch.cat([h[:, :C], rnd(h[:, C:])], dim=1)  # the bf16-stored hop pieces
+        dw = torch.einsum("bont,bint->oi", dy, hb).reshape(w.shape)
         dyb = rnd(dy)
         dg = wt(0, dy)
         dsups = []
