@@ -157,12 +157,15 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
         }
       }
       __syncthreads();  // (also: the unscaled weights are staged)
-      // folded bias of output column nn: b[nn] + sum_k w[nn][k] beta[k % KH], k in order
+      // output column nn (thread nn owns its LDS row): the folded bias b[nn] + sum_k w[nn][k]
+      // beta[k % KH] (k in order), then the row scaled in place, w_fold[nn][k] = w[nn][k] *
+      // scale[k % KH]
       if (threadIdx.x < N) {
         const int nn = threadIdx.x;
         float acc = p.bias[nn];
         for (int k = 0; k < K; ++k) acc = fmaf(bt[nn * LDT + k], p.fbn_beta[k % KH], acc);
         s_bias[nn] = acc;
+        for (int k = 0; k < K; ++k) bt[nn * LDT + k] *= s_scale[k % KH];
       }
     }
     __syncthreads();
@@ -174,10 +177,6 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
       for (int q = 0; q < KH / 4; ++q) {
         const float4 v = src[q];
         w[t][4 * q] = v.x; w[t][4 * q + 1] = v.y; w[t][4 * q + 2] = v.z; w[t][4 * q + 3] = v.w;
-      }
-      if (FOLD) {  // w_fold[nn][k] = w[nn][k] * scale[k % KH] (the lane's k = half*KH + j)
-#pragma unroll
-        for (int jj = 0; jj < KH; ++jj) w[t][jj] *= s_scale[jj];
       }
       bn[t] = FOLD ? s_bias[nb] : p.bias[nb];
     }
@@ -191,7 +190,9 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
   // CENTER (BatchNorm on load, gwn_batchnorm_fwd_fold): the column means are wave-uniform
   float cmu[KH];
 #pragma unroll
-  for (int j = 0; j < KH; ++j) cmu[j] = FOLD ? s_mean[j] : (CENTER ? p.center[j] : 0.0f);
+  for (int j = 0; j < KH; ++j)  // wave-uniform: scalar registers, as the CENTER path's scalar loads
+    cmu[j] = FOLD ? __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, s_mean[j])))
+                  : (CENTER ? p.center[j] : 0.0f);
   // BNSTAT (N = 32: channel n = col): running sums of the final C and C*xhat over this wave's rows
   const __amdgpu_buffer_rsrc_t rz = rsrc(BNSTAT ? p.bn_z : p.C, BNSTAT ? (long)p.M * 32 * 4 : 0);
   const float bmu = BNSTAT ? p.bn_mean[col] : 0.0f, brs = BNSTAT ? p.bn_rstd[col] : 0.0f;
