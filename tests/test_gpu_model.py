@@ -413,7 +413,7 @@ def test_num_batches_tracked_counts_train_forwards(gpu):
     dg = gwnet_diff_G(gpu, 16, 0.0, supports_len=2, gcn_bool=True, addaptadj=False, residual_channels=16,
                       dilation_channels=16, skip_channels=64, end_channels=128, blocks=2, layers=2)
     dg.train()
-    xd = torch.randn(2, 2, 16, 13, device=gpu)
+    xd = torch.randn(2, 2, 16, 31, device=gpu)  # (dilations 4, 8 per block: T >= 25)
     for k in range(2):
         dg(xd, None, None).sum().backward()
     torch.cuda.synchronize()
