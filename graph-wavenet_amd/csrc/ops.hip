@@ -1076,8 +1076,7 @@ int gwn_gated_tcn_fwd(const gwn_tcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a->c % 16 == 0 && co % 16 == 0, "gated_tcn_fwd: channels must be multiples of 16");
   const int c = a->c, P = a->P, t_out = a->t_in - a->dilation * (taps - 1);
   if (c == 32 && taps == 2 && co == c && aligned16(a->x) && aligned16(a->fg)) return gwn_rowgemm_tcn_fwd(a, s);
-  GWN_REQUIRE(a->fg != nullptr && !a->x_mean && !a->bn_partials,
-              "gated_tcn_fwd: fg may only be NULL (and x_mean / bn_partials set) on the c == 32 path");
+  GWN_REQUIRE(a->fg != nullptr && !a->x_mean, "gated_tcn_fwd: fg may only be NULL (and x_mean set) on the c == 32 path");
   gwn_gemm_desc d = gemm_zero();
   d.A = a->x; d.lda_m = c; d.lda_k = 1; d.a_kin = c; d.a_row_shift = a->dilation * P;
   d.a_rows = a->t_in * P;

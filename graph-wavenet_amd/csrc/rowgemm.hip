@@ -29,15 +29,6 @@ struct RowGemm {
   const float* bn_z; const float* bn_mean; const float* bn_rstd; // BNSTAT: per-wave partials of sum C and
   float* bn_part;                                                //   sum C*xhat(bn_z), [wave][2][32]
   const float* center;                                           // CENTER: A[.][h*a_tap + j] - center[j]
-  // FOLD (GATE + CENTER): the BatchNorm of A (the pre-BN z of the layer below) finalised here from
-  // gwn_gcn_fwd's partial slots instead of by gwn_batchnorm_fwd_fold -- every block merges them
-  // (the same fixed order, so every block derives the same mean / scale), centres A on load with the
-  // mean, scales the weight columns and folds beta into the bias; block 0 writes the statistics
-  const float* fbn_part; int fbn_nparts;
-  const float* fbn_gamma; const float* fbn_beta;
-  float* fbn_rm; float* fbn_rv; float fbn_mom, fbn_eps;
-  float* fbn_mean_out; float* fbn_rstd_out; float* fbn_scale_out;
-  long long* fbn_nbt;
 };
 
 // Branch-free gate nonlinearities on v_exp_f32 / v_rcp_f32: absolute error ~1e-7 (a few ulp of
@@ -69,17 +60,7 @@ __device__ __forceinline__ float ld32(__amdgpu_buffer_rsrc_t r, int off) {
 #ifndef GWN_ROWGEMM_WPE
 #define GWN_ROWGEMM_WPE  // measurement hook: -DGWN_ROWGEMM_WPE='__attribute__((amdgpu_waves_per_eu(2)))'
 #endif
-// (Chan merge, the arithmetic of bn_merge_channel / bn_finalize_fold_kernel in ops.hip)
-__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double nb, double mb, double m2b) {
-  if (nb <= 0.0) return;
-  const double nn = n + nb;
-  const double d = mb - mean;
-  mean += d * nb / nn;
-  m2 += m2b + d * d * n * nb / nn;
-  n = nn;
-}
-
-template <int KH, bool GATE, bool BNSTAT, bool CENTER = false, bool FOLD = false>
+template <int KH, bool GATE, bool BNSTAT, bool CENTER = false>
 __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowGemm p) {
   constexpr int NQ = KH / 4;  // float4 per lane per chunk
   constexpr int NT = GATE ? 2 : 1;
@@ -115,7 +96,6 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
   constexpr int K = 2 * KH, LDT = K + 4;
   float w[NT][KH];
   float bn[NT];
-  __shared__ float s_mean[FOLD ? KH : 1], s_scale[FOLD ? KH : 1], s_bias[FOLD ? 64 : 1];
   if (GATE) {
     const int N = 64;
     extern __shared__ float4 bt4[];
@@ -123,50 +103,6 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
     for (int e = threadIdx.x; e < K * N; e += blockDim.x) {
       const int k = e % K, nn = e / K;
       bt[nn * LDT + k] = p.B[(k % KH) * p.ldb_k + (k / KH) * p.ldb_tap + (long)nn * p.ldb_n];
-    }
-    if (FOLD) {
-      // the statistics of channel j = tid % 32 over partial slots tid / 32, + 8, ... (fixed order),
-      // then the 8 groups merged in group order by the channel's thread
-      __shared__ double sn[8][32], sm[8][32], sq[8][32];
-      const int j = threadIdx.x & 31, gq = threadIdx.x >> 5;
-      double n = 0.0, mean = 0.0, m2 = 0.0;
-      for (int q0 = gq; q0 < p.fbn_nparts; q0 += 8) {
-        const float* pp = p.fbn_part + (long)q0 * 3 * KH;
-        chan_merge(n, mean, m2, pp[j], pp[KH + j], pp[2 * KH + j]);
-      }
-      sn[gq][j] = n; sm[gq][j] = mean; sq[gq][j] = m2;
-      __syncthreads();
-      if (threadIdx.x < KH) {
-        double tn = 0.0, tmean = 0.0, tm2 = 0.0;
-        for (int g2 = 0; g2 < 8; ++g2) chan_merge(tn, tmean, tm2, sn[g2][j], sm[g2][j], sq[g2][j]);
-        const double var = (tn > 0.0) ? tm2 / tn : 0.0;
-        const float rs = (float)(1.0 / sqrt(var + (double)p.fbn_eps));
-        const float sc = rs * p.fbn_gamma[j];  // bn(z) = (z - mean) * sc + beta
-        s_mean[j] = (float)tmean;
-        s_scale[j] = sc;
-        if (blockIdx.x == 0) {
-          p.fbn_mean_out[j] = (float)tmean;
-          p.fbn_rstd_out[j] = rs;
-          p.fbn_scale_out[j] = sc;
-          if (p.fbn_rm) {
-            const double unbiased = (tn > 1.0) ? tm2 / (tn - 1.0) : var;
-            p.fbn_rm[j] = (float)((1.0 - p.fbn_mom) * p.fbn_rm[j] + p.fbn_mom * tmean);
-            p.fbn_rv[j] = (float)((1.0 - p.fbn_mom) * p.fbn_rv[j] + p.fbn_mom * unbiased);
-          }
-          if (p.fbn_nbt && j == 0) *p.fbn_nbt += 1;  // BatchNorm2d.num_batches_tracked
-        }
-      }
-      __syncthreads();  // (also: the unscaled weights are staged)
-      // output column nn (thread nn owns its LDS row): the folded bias b[nn] + sum_k w[nn][k]
-      // beta[k % KH] (k in order), then the row scaled in place, w_fold[nn][k] = w[nn][k] *
-      // scale[k % KH]
-      if (threadIdx.x < N) {
-        const int nn = threadIdx.x;
-        float acc = p.bias[nn];
-        for (int k = 0; k < K; ++k) acc = fmaf(bt[nn * LDT + k], p.fbn_beta[k % KH], acc);
-        s_bias[nn] = acc;
-        for (int k = 0; k < K; ++k) bt[nn * LDT + k] *= s_scale[k % KH];
-      }
     }
     __syncthreads();
 #pragma unroll
@@ -178,7 +114,7 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
         const float4 v = src[q];
         w[t][4 * q] = v.x; w[t][4 * q + 1] = v.y; w[t][4 * q + 2] = v.z; w[t][4 * q + 3] = v.w;
       }
-      bn[t] = FOLD ? s_bias[nb] : p.bias[nb];
+      bn[t] = p.bias[nb];
     }
   } else {
     const long nb = 32 * tile + col;
@@ -190,9 +126,7 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
   // CENTER (BatchNorm on load, gwn_batchnorm_fwd_fold): the column means are wave-uniform
   float cmu[KH];
 #pragma unroll
-  for (int j = 0; j < KH; ++j)  // wave-uniform: scalar registers, as the CENTER path's scalar loads
-    cmu[j] = FOLD ? __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, s_mean[j])))
-                  : (CENTER ? p.center[j] : 0.0f);
+  for (int j = 0; j < KH; ++j) cmu[j] = CENTER ? p.center[j] : 0.0f;
   // BNSTAT (N = 32: channel n = col): running sums of the final C and C*xhat over this wave's rows
   const __amdgpu_buffer_rsrc_t rz = rsrc(BNSTAT ? p.bn_z : p.C, BNSTAT ? (long)p.M * 32 * 4 : 0);
   const float bmu = BNSTAT ? p.bn_mean[col] : 0.0f, brs = BNSTAT ? p.bn_rstd[col] : 0.0f;
@@ -281,7 +215,7 @@ inline int rowgemm_grid(int M, int ntiles, bool gate) {
   return (waves + 3) / 4;  // 4 | 4*grid, so every tile gets grid*4/ntiles waves
 }
 
-template <int KH, bool GATE, bool BNSTAT = false, bool CENTER = false, bool FOLD = false>
+template <int KH, bool GATE, bool BNSTAT = false, bool CENTER = false>
 int launch(const RowGemm& p, hipStream_t s) {
   GWN_REQUIRE((long)p.a_rows * p.lda * 4 < 0x7fff0000L && (long)p.M * p.ldc * 4 < 0x7fff0000L &&
                   (long)p.M * p.ld_aux * 4 < 0x7fff0000L && (long)p.M * p.ld_aux2 * 4 < 0x7fff0000L,
@@ -294,7 +228,7 @@ int launch(const RowGemm& p, hipStream_t s) {
   (void)nchunks;
   const int grid = rowgemm_grid(p.M, p.ntiles, GATE);
   const size_t lds = GATE ? (size_t)64 * (2 * KH + 4) * sizeof(float) : 0;
-  rowgemm_kernel<KH, GATE, BNSTAT, CENTER, FOLD><<<grid, 256, lds, s>>>(p);
+  rowgemm_kernel<KH, GATE, BNSTAT, CENTER><<<grid, 256, lds, s>>>(p);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -317,15 +251,6 @@ int gwn_rowgemm_tcn_fwd(const gwn_tcn_args* a, hipStream_t s) {
   p.aux2 = a->skipcat; p.ld_aux2 = a->ld_skip; p.aux2_row0 = a->skip_row0;
   p.M = t_out * P; p.ntiles = 2;
   p.center = a->x_mean;
-  if (a->bn_partials) {
-    GWN_REQUIRE(a->bn_nparts > 0 && a->bn_gamma && a->bn_beta && a->bn_save_mean && a->bn_save_rstd && a->bn_scale,
-                "rowgemm tcn_fwd: the BatchNorm fold needs nparts, gamma, beta and the mean / rstd / scale outputs");
-    p.fbn_part = a->bn_partials; p.fbn_nparts = a->bn_nparts; p.fbn_gamma = a->bn_gamma; p.fbn_beta = a->bn_beta;
-    p.fbn_rm = a->bn_running_mean; p.fbn_rv = a->bn_running_var; p.fbn_mom = a->bn_momentum; p.fbn_eps = a->bn_eps;
-    p.fbn_mean_out = a->bn_save_mean; p.fbn_rstd_out = a->bn_save_rstd; p.fbn_scale_out = a->bn_scale;
-    p.fbn_nbt = a->bn_num_batches_tracked;
-    return launch<32, true, false, true, true>(p, s);
-  }
   if (p.center) return launch<32, true, false, true>(p, s);
   return launch<32, true>(p, s);
 }

@@ -48,11 +48,6 @@ class TcnArgs(ctypes.Structure):
         ("skipcat", c_void_p), ("ld_skip", c_long), ("skip_row0", c_int),
         ("x_mean", c_void_p),
         ("ntaps", c_int), ("c_out", c_int),
-        ("bn_partials", c_void_p), ("bn_nparts", c_int),
-        ("bn_gamma", c_void_p), ("bn_beta", c_void_p),
-        ("bn_running_mean", c_void_p), ("bn_running_var", c_void_p), ("bn_momentum", c_float), ("bn_eps", c_float),
-        ("bn_save_mean", c_void_p), ("bn_save_rstd", c_void_p), ("bn_scale", c_void_p),
-        ("bn_num_batches_tracked", c_void_p),
     ]
 
 

@@ -576,9 +576,6 @@ class Executor:
         # of materialising bn(z) (one HBM pass and one launch fewer per layer)
         fold = training and self._bn_fold_ok(sup_batch)
         acts.bn_fold = fold
-        # ... and finalised inside the next layer's gated-TCN launch (one launch per layer fewer);
-        # GWN_BN_FUSE=0 keeps gwn_batchnorm_fwd_fold (A/B measurements)
-        fuse_bn = fold and cfg.square and cfg.C == 32 and os.environ.get("GWN_BN_FUSE", "1") != "0"
         # bf16 mode: the adaptive-support gram on tiled operands -- the bf16 16-node tile kernels
         # write X and its hop 1 (forward) and t1 / t2 (backward) in gwn_gram_g4_bf16's layout
         gram_g4 = (training and cfg.adp_params and cfg.use_gcn and sup_batch <= 1 and self._fused_gcn()
@@ -605,16 +602,6 @@ class Executor:
                               xg=ptr(acts.H[i]), ld_xg=cfg.W, fg=ptr(acts.FG[i]),
                               skipcat=acts.skipcat.data_ptr() + 4 * i * cfg.D, ld_skip=L * cfg.D,
                               skip_row0=(ts[i + 1] - tf) * P, ntaps=cfg.K, c_out=cfg.D)
-            if fuse_bn and i >= 1:
-                # BatchNorm i-1 finalised and folded by this TCN launch (its own weights, the
-                # statistics from gcn i-1's partial slots; include/gwn.h gwn_tcn_args.bn_partials)
-                rm_, rv_, mom_, eps_, nbt_ = bn_bufs[i - 1]
-                ta.w_fg, ta.b_fg = ptr(self.pk("fg_w%d" % i)), ptr(self.pk("fg_b%d" % i))
-                ta.bn_partials, ta.bn_nparts = ptr(bnpart), self._bn_parts(ts[i] * P)
-                ta.bn_gamma, ta.bn_beta = ptr(self.pk("bn_g%d" % (i - 1))), ptr(self.pk("bn_b%d" % (i - 1)))
-                ta.bn_running_mean, ta.bn_running_var, ta.bn_momentum, ta.bn_eps = ptr(rm_), ptr(rv_), mom_, eps_
-                ta.bn_save_mean, ta.bn_save_rstd = ptr(acts.mean[i - 1]), ptr(acts.rstd[i - 1])
-                ta.bn_scale, ta.bn_num_batches_tracked = acts.bn_scale[i - 1].data_ptr(), ptr(nbt_)
             lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), st)
             if i == L - 1 and not training:
                 continue  # the last gcn / bn output is dead in eval (only skip reaches the output)
@@ -656,9 +643,7 @@ class Executor:
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
             rm, rv, mom, eps, nbt = bn_bufs[i]
-            if fold and fuse_bn and i + 1 < L:
-                pass  # finalised by the next layer's TCN launch
-            elif fold:
+            if fold:
                 nxt = i + 1 < L
                 lib.call("gwn_batchnorm_fwd_fold", ptr(bnpart), self._bn_parts(rows), C, ptr(self.pk("bn_g%d" % i)),
                          ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps, ptr(acts.mean[i]), ptr(acts.rstd[i]),

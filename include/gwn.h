@@ -182,19 +182,6 @@ typedef struct gwn_tcn_args {
    * c_out (resp. 2*c_out) channels.  0 = the defaults ntaps 2, c_out c.  Non-default values run
    * the generic GEMM path (no x_mean fold). */
   int ntaps, c_out;
-  /* bn_partials (optional, c == 32 row-GEMM path): x is the pre-BatchNorm z of the layer below and
-   * its BatchNorm (model.py:236) is finalised by this launch instead of gwn_batchnorm_fwd_fold --
-   * the statistics merged from gwn_gcn_fwd's bn_nparts partial slots (every workgroup derives the
-   * same values in the same fixed order), x centred on load with the mean, w_fg / b_fg the layer's
-   * OWN weights, folded here (column k scaled by gamma[k % c] * rstd[k % c], beta folded into the
-   * bias).  bn_save_mean / bn_save_rstd / bn_scale [c] receive mean, 1/sqrt(var + eps) and
-   * gamma * rstd; the running statistics (momentum, unbiased variance) and num_batches_tracked are
-   * updated as gwn_batchnorm_fwd_fold does (NULL = not kept).  x_mean is ignored. */
-  const float* bn_partials; int bn_nparts;
-  const float* bn_gamma; const float* bn_beta;
-  float* bn_running_mean; float* bn_running_var; float bn_momentum, bn_eps;
-  float* bn_save_mean; float* bn_save_rstd; float* bn_scale;
-  long long* bn_num_batches_tracked;
 } gwn_tcn_args;
 /* fg may be NULL when no backward follows (inference; c == 32 row-GEMM path): the (tanh, sigmoid)
  * pairs are then not stored. */

@@ -378,8 +378,8 @@ def test_power_schedule_matches_chained_hops(gpu, monkeypatch):
 
 
 def test_num_batches_tracked_counts_train_forwards(gpu):
-    """BatchNorm2d.num_batches_tracked is advanced on the device by the BatchNorm finalise (inside
-    the next layer's gated-TCN launch, or gwn_batchnorm_fwd_fold / _partials), once per train-mode
+    """BatchNorm2d.num_batches_tracked is advanced on the device by the BatchNorm finalise
+    (gwn_batchnorm_fwd_fold / _partials / the eval-free paths), once per train-mode
     forward as torch does: three trainer.train steps (the first eager, then HIP-graph replays), one
     autograd train-mode forward, eval forwards (no change), and gwnet_diff_G called without
     supports (the residual-only schedule, model.py:391-398)."""
