@@ -1345,9 +1345,12 @@ def _ksplit_thin(M, N, K):
 
 
 def _ksplit(M, N, K):
-    """Same policy as pick_ksplit() in csrc/ops.hip."""
+    """Split-K of the head weight gradients (K = positions): up to 1024 tiles x splits, chunks of
+    >= 192 rows.  Measured (tools/bench_head.py, METR B=64, profiles/r04/head_gemm_sweep.txt):
+    end_conv_1 dW 49 splits 63.9 us, 64 splits 53.0 us (128 x 128 tiles fill the chip); skip dW
+    35.4 / 33.7 us."""
     tiles = ((M + 127) // 128) * ((N + 63) // 64)
-    ks = max(1, min(1024 // max(tiles, 1), K // 256))
+    ks = max(1, min(1024 // max(tiles, 1), K // 192))
     return ks
 
 
