@@ -55,7 +55,11 @@ __device__ __forceinline__ bf16x8 to_bf16x8(const float4& a, const float4& b) {
 // v_mfma_f32_32x32x16_bf16 (K permuted alike on both operands: group s of half h = channels
 // 16h + 8s .. +7), 2 MFMAs per tile and slice instead of 16 (the bf16 mode's adaptive-support
 // gradient; fp32 accumulation)
-template <int NP, bool BF16 = false>
+// LINES: each (slice, pair) step's 96 rows x 128 B (32 rows of X, 64 of T) arrive by full-line
+// loads (64 lanes x 16 B = 8 whole rows per instruction) into the wave's LDS image [96][36]
+// (padded rows: conflict-free ds_read_b128), from which the lanes read their fragments -- instead
+// of fragment-shaped loads that touch 32 rows (16 B of each) per instruction
+template <int NP, bool BF16 = false, bool LINES = false>
 __global__ __launch_bounds__(64) void gram_kernel(const Gram g) {
   const int lane = threadIdx.x, half = lane >> 5, col = lane & 31;
   const int ntp = (g.nt + 1) / 2;  // column tile pairs
@@ -86,6 +90,25 @@ __global__ __launch_bounds__(64) void gram_kernel(const Gram g) {
   auto load = [&](int s, int p, float4* fa, float4* fb) {
     const bool ok = s < s1;
     const long base = (long)s * g.n;
+    if (LINES) {  // float4 f = q*64 + lane of the step's [96 rows][8 float4] image
+#pragma unroll
+      for (int q = 0; q < 12; ++q) {
+        const int f = q * 64 + lane, rr = f >> 3, c4 = f & 7;
+        float4 v;
+        if (rr < 32) {
+          const int vv = 32 * vt + rr;
+          const int o = (ok && vv < g.n) ? (int)(((base + vv) * g.ldx + 4 * c4) * 4) : OOR;
+          v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx[p], o, 0, 0));
+        } else {
+          const int ww = 32 * wt0 + (rr - 32);
+          const int o = (ok && ww < g.n && (rr < 64 || two)) ? (int)(((base + ww) * g.ldt + 4 * c4) * 4) : OOR;
+          v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt[p], o, 0, 0));
+        }
+        if (q < 4) fa[q] = v;
+        else fb[q - 4] = v;
+      }
+      return;
+    }
     const int ox = (ok && v < g.n) ? (int)(((base + v) * g.ldx + 16 * half) * 4) : OOR;
     const int o0 = (ok && w0 < g.n) ? (int)(((base + w0) * g.ldt + 16 * half) * 4) : OOR;
     const int o1 = (ok && two && w1 < g.n) ? (int)(((base + w1) * g.ldt + 16 * half) * 4) : OOR;
@@ -104,7 +127,25 @@ __global__ __launch_bounds__(64) void gram_kernel(const Gram g) {
     acc1[r] = 0.0f;
   }
   float4 fa[4], fb[8];
+  extern __shared__ float4 gimg4[];
+  float* gimg = (float*)gimg4;
+  // LINES: the staged lines -> the wave's image -> this lane's fragments (rows col, 32 + col, 64 + col)
+  auto restage = [&](float4* fa_, float4* fb_) {
+    if (!LINES) return;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      const int f = q * 64 + lane, rr = f >> 3, c4 = f & 7;
+      *(float4*)(gimg + rr * 36 + 4 * c4) = q < 4 ? fa_[q] : fb_[q - 4];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      fa_[q] = *(const float4*)(gimg + col * 36 + 16 * half + 4 * q);
+      fb_[q] = *(const float4*)(gimg + (32 + col) * 36 + 16 * half + 4 * q);
+      fb_[4 + q] = *(const float4*)(gimg + (64 + col) * 36 + 16 * half + 4 * q);
+    }
+  };
   load(s0, 0, fa, fb);
+  restage(fa, fb);
   for (int s = s0; s < s1; ++s) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
@@ -138,6 +179,7 @@ __global__ __launch_bounds__(64) void gram_kernel(const Gram g) {
         fb[q] = nb[q];
         fb[4 + q] = nb[4 + q];
       }
+      restage(fa, fb);
     }
   }
   // D[v][w]: col = lane&31 -> w, rows -> v
@@ -169,6 +211,12 @@ __global__ void gram_reduce_kernel(const float* part, int nsplit, int n, int np,
   const float s = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   float* o = dA + (long)v * ld + w;
   *o = accumulate ? *o + s : s;
+}
+
+constexpr size_t GRAM_IMG = 96 * 36 * sizeof(float);  // LINES: a wave's [96][36] image
+bool gram_lines() {
+  const char* e = getenv("GWN_GRAM_LINES");  // 0: the fragment-shaped direct loads (A/B)
+  return !(e && e[0] == '0');
 }
 
 int gram_nsplit(int n, int slices) {
@@ -373,6 +421,9 @@ int gwn_gram_dtype(const float* x1, const float* t1, const float* x2, const floa
   if (bf16) {
     if (g.npairs == 2) gram_kernel<2, true><<<blocks, 64, 0, s>>>(g);
     else gram_kernel<1, true><<<blocks, 64, 0, s>>>(g);
+  } else if (gram_lines()) {
+    if (g.npairs == 2) gram_kernel<2, false, true><<<blocks, 64, GRAM_IMG, s>>>(g);
+    else gram_kernel<1, false, true><<<blocks, 64, GRAM_IMG, s>>>(g);
   } else {
     if (g.npairs == 2) gram_kernel<2><<<blocks, 64, 0, s>>>(g);
     else gram_kernel<1><<<blocks, 64, 0, s>>>(g);
@@ -452,7 +503,8 @@ int gwn_gram_group(const gwn_gram_layer* layers, int nlayers, long ldx, long ldt
   GWN_DEBUG_RANGE(dA, ((long)(n - 1) * ld_dA + n) * 4, "gram_group dA");
   const int per_split = g.nt * ((g.nt + 1) / 2);
   const int blocks = ((g.nsplit + NXCD - 1) / NXCD) * NXCD * per_split;
-  gram_kernel<2><<<blocks, 64, 0, s>>>(g);
+  if (gram_lines()) gram_kernel<2, false, true><<<blocks, 64, GRAM_IMG, s>>>(g);
+  else gram_kernel<2><<<blocks, 64, 0, s>>>(g);
   GWN_CHECK_LAUNCH();
   const long outs = (long)n * n;
   gram_reduce_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(ws, g.nsplit, n, (int)np, dA, ld_dA, accumulate);
