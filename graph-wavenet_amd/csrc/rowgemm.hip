@@ -60,14 +60,7 @@ __device__ __forceinline__ float ld32(__amdgpu_buffer_rsrc_t r, int off) {
 #ifndef GWN_ROWGEMM_WPE
 #define GWN_ROWGEMM_WPE  // measurement hook: -DGWN_ROWGEMM_WPE='__attribute__((amdgpu_waves_per_eu(2)))'
 #endif
-// LINES: the A rows of a chunk (both taps: 64 rows x KH floats) arrive by full-line loads -- one
-// wave instruction = 64 lanes x 16 B of consecutive rows (8 rows of 128 B at KH = 32) -- into a
-// per-wave LDS image [64][KH + 4] (padded: the ds_read_b128 of 16 lanes at stride KH + 4 floats
-// hit distinct bank quads), from which each lane reads its row segment.  The direct form's
-// fragment-shaped loads touch 64 rows per instruction (16 B of each): the per-instruction line
-// count, not the bytes, bounds it (cdna_hip_programming.md: fragment-shaped operand loads
-// +18...45 %, TA_BUSY 2x at identical traffic).  Wave-private image: no barrier.
-template <int KH, bool GATE, bool BNSTAT, bool CENTER = false, bool LINES = false>
+template <int KH, bool GATE, bool BNSTAT, bool CENTER = false>
 __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowGemm p) {
   constexpr int NQ = KH / 4;  // float4 per lane per chunk
   constexpr int NT = GATE ? 2 : 1;
@@ -87,34 +80,10 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
   const __amdgpu_buffer_rsrc_t rk = rsrc(GATE && p.aux2 ? p.aux2 : p.C, skip_rows > 0 ? skip_rows * p.ld_aux2 * 4 : 0);
 
   auto load = [&](int chunk, float4* a) {
-    if (LINES) {  // full lines: float4 f = q*64 + lane of the chunk's 64 x KH image
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int f = q * 64 + lane, rr = f / NQ, c4 = f % NQ, h = rr >> 5;
-        const long row = (long)chunk * 32 + (rr & 31) + h * p.shift;
-        const int voff = (row >= 0 && row < p.a_rows) ? (int)((row * p.lda + h * p.a_tap + 4 * c4) * 4) : OOR;
-        a[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, voff, 0, 0));
-      }
-      return;
-    }
     const long row = (long)chunk * 32 + col + half * p.shift;
     const int voff = (row >= 0 && row < p.a_rows) ? (int)((row * p.lda + half * p.a_tap) * 4) : OOR;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) a[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, voff, 16 * q, 0));
-  };
-  // LINES: the staged lines -> the wave's LDS image -> this lane's row segment (half*32 + col)
-  constexpr int LDR = KH + 4;
-  extern __shared__ float4 dyn4[];
-  float* wimg = (float*)dyn4 + (GATE ? 64 * (2 * KH + 4) : 0) + (threadIdx.x >> 6) * 64 * LDR;
-  auto restage = [&](float4* a) {
-    if (!LINES) return;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int f = q * 64 + lane, rr = f / NQ, c4 = f % NQ;
-      *(float4*)(wimg + rr * LDR + 4 * c4) = a[q];
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) a[q] = *(const float4*)(wimg + (half * 32 + col) * LDR + 4 * q);
   };
 
   // the first chunk's loads go out before the weight staging (they do not depend on it)
@@ -129,7 +98,8 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
   float bn[NT];
   if (GATE) {
     const int N = 64;
-    float* bt = (float*)dyn4;
+    extern __shared__ float4 bt4[];
+    float* bt = (float*)bt4;
     for (int e = threadIdx.x; e < K * N; e += blockDim.x) {
       const int k = e % K, nn = e / K;
       bt[nn * LDT + k] = p.B[(k % KH) * p.ldb_k + (k / KH) * p.ldb_tap + (long)nn * p.ldb_n];
@@ -153,7 +123,6 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
     bn[0] = 0.0f;
   }
   if (wave >= nwaves) return;  // after the block-wide staging barrier
-  restage(a);
   // CENTER (BatchNorm on load, gwn_batchnorm_fwd_fold): the column means are wave-uniform
   float cmu[KH];
 #pragma unroll
@@ -226,7 +195,6 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) a[q] = an[q];
-    restage(a);
   }
   if (BNSTAT) {
     // lane halves hold disjoint rows of the same channel: fold half 1 onto half 0 (fixed order)
@@ -247,11 +215,6 @@ inline int rowgemm_grid(int M, int ntiles, bool gate) {
   return (waves + 3) / 4;  // 4 | 4*grid, so every tile gets grid*4/ntiles waves
 }
 
-static bool rowgemm_lines() {
-  const char* e = getenv("GWN_ROWGEMM_LINES");  // 0: the direct fragment-shaped loads (A/B)
-  return !(e && e[0] == '0');
-}
-
 template <int KH, bool GATE, bool BNSTAT = false, bool CENTER = false>
 int launch(const RowGemm& p, hipStream_t s) {
   GWN_REQUIRE((long)p.a_rows * p.lda * 4 < 0x7fff0000L && (long)p.M * p.ldc * 4 < 0x7fff0000L &&
@@ -264,20 +227,8 @@ int launch(const RowGemm& p, hipStream_t s) {
   GWN_REQUIRE(!BNSTAT || (p.ntiles == 1 && p.ldc == 32), "rowgemm: BN statistics need N = ldc = 32");
   (void)nchunks;
   const int grid = rowgemm_grid(p.M, p.ntiles, GATE);
-  const bool lines = rowgemm_lines();
-  const size_t lds = (GATE ? (size_t)64 * (2 * KH + 4) * sizeof(float) : 0) +
-                     (lines ? (size_t)4 * 64 * (KH + 4) * sizeof(float) : 0);
-  if (lines) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)rowgemm_kernel<KH, GATE, BNSTAT, CENTER, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr = true;
-    }
-    rowgemm_kernel<KH, GATE, BNSTAT, CENTER, true><<<grid, 256, lds, s>>>(p);
-  } else {
-    rowgemm_kernel<KH, GATE, BNSTAT, CENTER><<<grid, 256, lds, s>>>(p);
-  }
+  const size_t lds = GATE ? (size_t)64 * (2 * KH + 4) * sizeof(float) : 0;
+  rowgemm_kernel<KH, GATE, BNSTAT, CENTER><<<grid, 256, lds, s>>>(p);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
