@@ -331,9 +331,21 @@ extern "C" int gwn_wgrad_group(const gwn_wgrad_problem* probs, int nprob, int J,
     b0 += nb[p];
   }
   const size_t lds = shape_lds(kind);
+  // quads in flight per wave (A/B: GWN_WGRAD_DEEP=0 -> 4 / 6 / 6): the mlp launch holds one
+  // workgroup (one wave per SIMD) per CU, so its loads in flight are all the latency hiding it has
+  static const bool deep = [] {
+    const char* e = getenv("GWN_WGRAD_DEEP");
+    return !(e && e[0] == '0');
+  }();
   switch (kind) {
-    case 1: return xb ? launch<2, 3, 1, 1, 4, true>(g, false, blocks, lds, s) : launch<2, 3, 1, 1, 4>(g, aff, blocks, lds, s);
-    case 2: return launch<4, 0, 2, 1, 6>(g, aff, blocks, lds, s);
-    default: return launch<2, 2, 0, 4, 6>(g, aff, blocks, lds, s);
+    case 1:
+      if (deep) return xb ? launch<2, 3, 1, 1, 8, true>(g, false, blocks, lds, s) : launch<2, 3, 1, 1, 8>(g, aff, blocks, lds, s);
+      return xb ? launch<2, 3, 1, 1, 4, true>(g, false, blocks, lds, s) : launch<2, 3, 1, 1, 4>(g, aff, blocks, lds, s);
+    case 2:
+      if (deep) return launch<4, 0, 2, 1, 10>(g, aff, blocks, lds, s);
+      return launch<4, 0, 2, 1, 6>(g, aff, blocks, lds, s);
+    default:
+      if (deep) return launch<2, 2, 0, 4, 10>(g, aff, blocks, lds, s);
+      return launch<2, 2, 0, 4, 6>(g, aff, blocks, lds, s);
   }
 }
