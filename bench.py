@@ -232,7 +232,8 @@ def rank_timing(elapsed, world, rank, dev):
 def measure_dominant(eng, dev, rounds=5, bf16=False):
     """The dominant kernel is the diffusion graph convolution forward (gwn_gcn_fwd: 3 supports x 2
     hops of 'ncvl,vw->ncwl' + the 224->32 mlp + residual + dropout + BN partials, one call per
-    layer, 8 per step; for N <= 512 ONE fused launch, gcn_fwd_t16_kernel).  Replay
+    layer, 8 per step; for N <= 512 ONE fused launch, gcn_fwd_t16_kernel, followed by the BN
+    finalize + fold its bn_fold argument issues).  Replay
     exactly the last training step's 8 calls (same arguments and buffers; the replay is
     idempotent) as one captured HIP graph between HIP events on the launch stream; achieved =
     algorithmic FLOP / time,

@@ -56,6 +56,7 @@ struct FusedFwd {
   int bn_slots;  // t16 kernels: BN partial slots to write (those past the grid get count 0)
   void* xg4; int xg4_k;  // bf16 t16 kernel: X and support xg4_k's hop 1 in the tiled activation layout
   void* pb; long ld_pb;  // bf16 t16 kernel: the hop pieces as bf16 [rows][ld_pb] instead of h's columns
+  gwn_bn_fold fold;      // t16 kernels: BN finalize + fold by the last workgroup (fold.arrive != NULL)
 };
 
 struct FusedBwd {
@@ -1213,8 +1214,36 @@ __device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* ha
 }
 
 // the waves' running partials (wave order) -> the workgroup's BN partial, slot blockIdx.x
+__device__ void t16_bn_fold_last(const FusedFwd& a, float* lds, const float* wv, const float* bv);
+#ifndef GWN_FOLD_EXP
+#define GWN_FOLD_EXP 0
+#endif
+// GWN_FOLD_EXP == 3 (timing probe builds only): phase timestamps of the last workgroup written past
+// the grid's partial slots
+#if GWN_FOLD_EXP == 3
+#define FOLD_TS(a, k)                                                                                  \
+  do {                                                                                                 \
+    if (threadIdx.x == 0)                                                                              \
+      ((unsigned long long*)((a).bn_part + (long)gridDim.x * 3 * CH))[k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define FOLD_TS(a, k) do {} while (0)
+#endif
+
 __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn, float* wpart) {
   if (a.bn_part == nullptr || a.x_out) return;
+  const bool fold = a.fold.arrive != nullptr;
+  // fold: the next TCN's weights (w_next[2c][2c], four per thread) and the products of the bias
+  // fold do not depend on the statistics: loaded before the hand-off
+  float wv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, bv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (fold && a.fold.w_next) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = (4 * threadIdx.x + e) & (2 * CH - 1);  // column tap*c + ci of row threadIdx.x / 16
+      wv[e] = a.fold.w_next[4 * threadIdx.x + e];
+      bv[e] = wv[e] * a.fold.beta[k & (CH - 1)];
+    }
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   if (j == 0) {
     float* wp = wpart + wave * 3 * CH;
@@ -1241,13 +1270,114 @@ __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn,
       nn = tot;
     }
     float* sp = a.bn_part + (long)blockIdx.x * 3 * CH;
-    sp[c] = nn;
-    sp[CH + c] = mean;
-    sp[2 * CH + c] = m2;
+    if (fold) {
+      // write-through (read by another XCD's workgroup in the same launch), channel-major
+      // [3][c][gridDim.x] so that the last workgroup's loads of 32 consecutive slots are one line
+      const int parts = gridDim.x;
+      const __amdgpu_buffer_rsrc_t r =
+          __builtin_amdgcn_make_buffer_rsrc((void*)a.bn_part, (short)0, 3 * CH * parts * 4, 0x00020000);
+      const int o = (c * parts + blockIdx.x) * 4;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, nn), r, o, 0, SC1);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mean), r, o + CH * parts * 4, 0, SC1);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m2), r, o + 2 * CH * parts * 4, 0, SC1);
+    } else {
+      sp[c] = nn;
+      sp[CH + c] = mean;
+      sp[2 * CH + c] = m2;
+    }
+  }
+  if (fold) {
+    if (split_arrive(a.fold.arrive, gridDim.x, (int*)wpart)) {
+      FOLD_TS(a, 0);
+      t16_bn_fold_last(a, wpart + 4, wv, bv);
+    }
+    return;
   }
   // the slots past the grid (gwn_bn_part_slots: at least one per slice) hold no rows
   for (long slot = blockIdx.x + gridDim.x; slot < a.bn_slots; slot += gridDim.x)
     if (threadIdx.x < 3 * CH) a.bn_part[slot * 3 * CH + threadIdx.x] = 0.0f;
+}
+
+// gwn_batchnorm_fwd_fold (bn_finalize_fold_kernel's arithmetic) by the launch's last workgroup on
+// its gridDim.x channel-major partials (1024 threads): channel j's partials are merged by the 32 lanes of one
+// half-wave (slots sub, sub + 32, ... sequentially, in double), then down a fixed shuffle tree;
+// wv / bv: this thread's four elements of w_next (row tid / 16) and their products with beta
+__device__ void t16_bn_fold_last(const FusedFwd& a, float* lds, const float* wv, const float* bv) {
+  static_assert(T16_WAVES * 64 == 32 * CH && T16_WAVES * 64 * 4 == 4 * CH * CH, "fold: 1024 threads, c = 32");
+  const gwn_bn_fold& f = a.fold;
+  const int j = threadIdx.x >> 5, sub = threadIdx.x & 31;
+  const int parts = gridDim.x;
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.bn_part, (short)0, parts * 3 * CH * 4, 0x00020000);
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  constexpr int U = 8;
+  for (int i0 = sub; i0 < parts; i0 += 32 * U) {
+    float nbv[U], mbv[U], qbv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + 32 * u;
+      const bool ok = i < parts;  // else an out-of-range offset: zero
+      const int off = (j * parts + i) * 4;  // channel-major [3][c][parts] (t16_bn_flush)
+      nbv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, ok ? off : 0x7ffffff0, 0, SC1));
+      mbv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, ok ? off + CH * parts * 4 : 0x7ffffff0, 0, SC1));
+      qbv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, ok ? off + 2 * CH * parts * 4 : 0x7ffffff0, 0, SC1));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const double nb = nbv[u];
+      if (nb <= 0.0) continue;
+      const double nn = n + nb, delta = (double)mbv[u] - mean, w = nb / nn;
+      mean += delta * w;
+      m2 += (double)qbv[u] + delta * delta * n * w;
+      n = nn;
+    }
+  }
+#pragma unroll
+  FOLD_TS(a, 1);
+  for (int off = 16; off > 0; off >>= 1) {
+    const double nb = __shfl_down(n, off, 32), mb = __shfl_down(mean, off, 32), qb = __shfl_down(m2, off, 32);
+    if (sub < off && nb > 0.0) {
+      const double nn = n + nb, delta = mb - mean, w = nb / nn;
+      mean += delta * w;
+      m2 += qb + delta * delta * n * w;
+      n = nn;
+    }
+  }
+  if (sub == 0) {
+    const double var = (n > 0.0) ? m2 / n : 0.0;
+    const float rs = (float)(1.0 / sqrt(var + (double)f.eps));
+    f.save_mean[j] = (float)mean;
+    f.save_rstd[j] = rs;
+    if (f.running_mean) {
+      const double unbiased = (n > 1.0) ? m2 / (n - 1.0) : var;
+      f.running_mean[j] = (float)((1.0 - f.momentum) * f.running_mean[j] + f.momentum * mean);
+      f.running_var[j] = (float)((1.0 - f.momentum) * f.running_var[j] + f.momentum * unbiased);
+    }
+    const float sc = rs * f.gamma[j];  // bn(z) = (z - mean) * sc + beta
+    f.scale[j] = sc;
+    lds[j] = sc;
+  }
+  if (threadIdx.x == 0 && f.num_batches_tracked) *f.num_batches_tracked += 1;
+  FOLD_TS(a, 2);
+  if (!f.w_next) return;
+  __syncthreads();
+  // w_fold[row][k] = w_next[row][k] * scale[k % c]; b_fold[row] = b_next[row] + sum_k w_next[row][k] *
+  // beta[k % c] (the 16 threads of a row: four products each, then a fixed shuffle tree)
+  float s = 0.0f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = (4 * threadIdx.x + e) & (2 * CH - 1);
+    f.w_fold[4 * threadIdx.x + e] = wv[e] * lds[k & (CH - 1)];
+    s += bv[e];
+  }
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) s += __shfl_down(s, off, 16);
+  const int row = threadIdx.x >> 4;
+  if ((threadIdx.x & 15) == 0) f.b_fold[row] = f.b_next[row] + s;
+  if (GWN_FOLD_EXP == 3) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FOLD_TS(a, 3);
+  }
 }
 
 // the channel map of one piece held in accumulators acc[hf] (register s = input channel
@@ -2059,7 +2189,15 @@ int bn_part_tail(float* bn_part, int slices, int c, hipStream_t s) {
 
 }  // namespace
 
-int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
+// GWN_BN_FOLD_LAST=1: the 16-node tile kernels run gwn_gcn_args.bn_fold in their last workgroup
+// (off by default: measured break-even); else it is a separate launch
+static bool fold_last_enabled() {
+  const char* e = getenv("GWN_BN_FOLD_LAST");
+  return e && e[0] == '1';
+}
+
+int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded, hipStream_t s) {
+  *folded = false;
   const int nwt = (g->n + 31) / 32;
   GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_fwd (fused): supports must be padded to 32*ceil(n/32)");
   GWN_REQUIRE(g->layout == 0 || g->layout == 1, "gcn_fwd (fused): layout must be 0 or 1 (one wave per node tile)");
@@ -2079,6 +2217,10 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.ksplit = 1; a.slices = g->rows / g->n; a.kws = g->ksplit_ws; a.kcnt = g->ksplit_count; a.bn_slots = 0;
   a.xg4 = g->xg4; a.xg4_k = g->xg4_support;
   a.pb = g->pieces_bf16; a.ld_pb = g->ld_pb;
+  a.fold = gwn_bn_fold{};
+  // the t16 kernels' last-workgroup finalize (their 1024-thread workgroups map 32 channels x 32
+  // partial lanes, and the 64 x 64 folded weights four per thread)
+  const bool fold_here = g->bn_fold && bn_part && !a.x_out && fold_last_enabled();
   GWN_REQUIRE(g->ksplit == 0 || g->ksplit == 1 || g->ksplit == g->nsup, "gcn_fwd: ksplit must be 0, 1 or nsup");
   GWN_REQUIRE(!a.res_scale == !a.res_shift && !a.res_scale == !a.res_mean,
               "gcn_fwd (fused): residual_mean, residual_scale and residual_shift go together");
@@ -2119,8 +2261,10 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
       for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = (const float*)g->sup_g4b[k];
       a.ksplit = 1;
       a.bn_slots = (int)gwn_bn_part_slots(slices);
+      if (fold_here) a.fold = *g->bn_fold;
       gcn_fwd_t16b_kernel<1024><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       GWN_CHECK_LAUNCH();
+      *folded = fold_here;
       return GWN_OK;
     }
   }
@@ -2155,8 +2299,10 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
     // 16-node tile waves, one workgroup per CU over an equal tile range; it writes every BN
     // partial slot (gwn_bn_part_slots)
     a.bn_slots = (int)gwn_bn_part_slots(slices);
+    if (fold_here) a.fold = *g->bn_fold;
     gcn_fwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
     GWN_CHECK_LAUNCH();
+    *folded = fold_here;
     return GWN_OK;
   }
   if (g->sup2 && a.sup_batch <= 1 && g->nsup > 0) {

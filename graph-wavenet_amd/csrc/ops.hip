@@ -930,6 +930,7 @@ long gwn_abi_sizeof(const char* name) {
   if (!strcmp(name, "gwn_gcn_bwd_args")) return (long)sizeof(gwn_gcn_bwd_args);
   if (!strcmp(name, "gwn_wgrad_problem")) return (long)sizeof(gwn_wgrad_problem);
   if (!strcmp(name, "gwn_gram_layer")) return (long)sizeof(gwn_gram_layer);
+  if (!strcmp(name, "gwn_bn_fold")) return (long)sizeof(gwn_bn_fold);
   return -1;
 }
 
@@ -1182,12 +1183,35 @@ int gwn_gated_tcn_bwd(const gwn_tcn_bwd_args* a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------
+static int gcn_fwd_unfolded(const gwn_gcn_args* a, hipStream_t s);
+
 int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_fwd: rows must be slices*n");
+  const gwn_bn_fold* f = a->bn_fold;
+  if (f) {
+    const int co = a->c_out > 0 ? a->c_out : a->c;
+    GWN_REQUIRE(co == 32 && a->bn_partials && !a->bn_out && f->arrive && f->gamma && f->beta && f->save_mean &&
+                    f->save_rstd && f->scale,
+                "gcn_fwd: bn_fold needs c_out == 32, bn_partials, no bn_out, arrive, gamma / beta and the outputs");
+    GWN_REQUIRE(!f->w_next || (f->b_next && f->w_fold && f->b_fold && f->w_fold != f->w_next),
+                "gcn_fwd: bn_fold.w_next needs b_next, w_fold, b_fold (w_fold not aliasing w_next)");
+  }
+  const int c = a->c, n = a->n;
+  const int co = a->c_out > 0 ? a->c_out : c;
+  bool folded = false;
+  int rc = (co == c && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup))
+               ? gwn_gcn_fused_fwd_launch(a, a->bn_partials, &folded, s)
+               : gcn_fwd_unfolded(a, s);
+  if (rc || !f || folded) return rc;
+  return gwn_batchnorm_fwd_fold(a->bn_partials, (int)gwn_bn_part_slots(a->rows / n), co, f->gamma, f->beta,
+                                f->running_mean, f->running_var, f->momentum, f->eps, f->save_mean, f->save_rstd,
+                                f->scale, f->w_next, f->b_next, f->w_fold, f->b_fold, f->num_batches_tracked, s);
+}
+
+static int gcn_fwd_unfolded(const gwn_gcn_args* a, hipStream_t s) {
   const int c = a->c, n = a->n, slices = a->rows / n;
   GWN_REQUIRE(a->c_out >= 0, "gcn_fwd: bad c_out");
   const int co = a->c_out > 0 ? a->c_out : c;
-  if (co == c && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup)) return gwn_gcn_fused_fwd_launch(a, a->bn_partials, s);
   GWN_REQUIRE(a->sup_batch <= 1, "gcn_fwd: per-sample supports need the fused path (c == 32, n <= 512)");
   GWN_REQUIRE(!a->no_pieces && !a->bn_out && !a->residual_scale && !a->residual_mean,
               "gcn_fwd: no_pieces / bn_out / residual_scale need the fused path (c == 32, n <= 512)");

@@ -69,6 +69,17 @@ class TcnBwdArgs(ctypes.Structure):
     ]
 
 
+class BnFold(ctypes.Structure):
+    _fields_ = [
+        ("gamma", c_void_p), ("beta", c_void_p), ("running_mean", c_void_p), ("running_var", c_void_p),
+        ("momentum", c_float), ("eps", c_float),
+        ("save_mean", c_void_p), ("save_rstd", c_void_p), ("scale", c_void_p),
+        ("w_next", c_void_p), ("b_next", c_void_p), ("w_fold", c_void_p), ("b_fold", c_void_p),
+        ("num_batches_tracked", c_void_p),
+        ("arrive", c_void_p),
+    ]
+
+
 class GcnArgs(ctypes.Structure):
     _fields_ = [
         ("rows", c_int), ("n", c_int), ("c", c_int), ("nsup", c_int),
@@ -94,6 +105,7 @@ class GcnArgs(ctypes.Structure):
         ("sup_g4b", ctypes.POINTER(c_void_p)),
         ("xg4", c_void_p), ("xg4_support", c_int),
         ("pieces_bf16", c_void_p), ("ld_pb", c_long),
+        ("bn_fold", ctypes.POINTER(BnFold)),
     ]
 
 
@@ -154,7 +166,8 @@ class GcnBwdArgs(ctypes.Structure):
 # ctypes mirrors checked against the library's own sizeof (gwn_abi_sizeof) at load time
 _STRUCTS = {"gwn_gemm_desc": GemmDesc, "gwn_tcn_args": TcnArgs, "gwn_tcn_bwd_args": TcnBwdArgs,
             "gwn_gcn_args": GcnArgs, "gwn_gcn_bwd_args": GcnBwdArgs, "gwn_reduce_seg": ReduceSeg,
-            "gwn_wgrad_problem": WgradProblem, "gwn_gram_layer": GramLayer}
+            "gwn_wgrad_problem": WgradProblem, "gwn_gram_layer": GramLayer,
+            "gwn_bn_fold": BnFold}
 
 
 # (name, restype, argtypes) of every exported entry point declared in include/gwn.h

@@ -365,6 +365,8 @@ class Executor:
             "bnsums": e(2 * C),  # BN-backward statistics handed from a layer's TCN backward to the next
             # BN partials of one layer: gwn_gcn_bn_partial_count slots (>= one per slice)
             "bnpart": e(self._bn_parts(ts[0] * B * N) * 3 * C),
+            # per-layer arrival counters of the gcn forward's in-launch BN finalize (gwn_bn_fold.arrive)
+            "bnarrive": torch.zeros(L, device=self.device, dtype=torch.int32),
         }
         lib = _lib.load()
         need = [
@@ -640,18 +642,25 @@ class Executor:
                               split_planes=planes, **self.ksplit_fields(scr))
             if pieces_b and i < L - 1:
                 ga.pieces_bf16, ga.ld_pb = acts.HB[i].data_ptr(), 2 * cfg.nsup * cfg.D
-            lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
-            acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
             rm, rv, mom, eps, nbt = bn_bufs[i]
             if fold:
+                # the BN finalize + fold into the next TCN rides on the gcn launch (gwn_gcn_args.bn_fold:
+                # its last workgroup merges the partials on the 16-node tile kernels)
                 nxt = i + 1 < L
-                lib.call("gwn_batchnorm_fwd_fold", ptr(bnpart), self._bn_parts(rows), C, ptr(self.pk("bn_g%d" % i)),
-                         ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps, ptr(acts.mean[i]), ptr(acts.rstd[i]),
-                         acts.bn_scale[i].data_ptr(),
-                         ptr(self.pk("fg_w%d" % (i + 1))) if nxt else None,
-                         ptr(self.pk("fg_b%d" % (i + 1))) if nxt else None,
-                         acts.w_fold[i + 1].data_ptr() if nxt else None,
-                         acts.b_fold[i + 1].data_ptr() if nxt else None, ptr(nbt), st)
+                bf = _lib.BnFold(gamma=ptr(self.pk("bn_g%d" % i)), beta=ptr(self.pk("bn_b%d" % i)),
+                                 running_mean=ptr(rm), running_var=ptr(rv), momentum=mom, eps=eps,
+                                 save_mean=ptr(acts.mean[i]), save_rstd=ptr(acts.rstd[i]),
+                                 scale=acts.bn_scale[i].data_ptr(),
+                                 w_next=ptr(self.pk("fg_w%d" % (i + 1))) if nxt else None,
+                                 b_next=ptr(self.pk("fg_b%d" % (i + 1))) if nxt else None,
+                                 w_fold=acts.w_fold[i + 1].data_ptr() if nxt else None,
+                                 b_fold=acts.b_fold[i + 1].data_ptr() if nxt else None,
+                                 num_batches_tracked=ptr(nbt), arrive=scr["bnarrive"].data_ptr() + 4 * i)
+                ga.bn_fold = ctypes.pointer(bf)
+            lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
+            acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
+            if fold:
+                pass  # done by the gcn launch
             elif training:
                 lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnpart), self._bn_parts(rows),
                          ptr(self.pk("bn_g%d" % i)), ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps,

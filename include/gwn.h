@@ -44,7 +44,7 @@ void gwn_set_sync_check(int mode);
 const char* gwn_last_error(void);
 /* sizeof of the argument structs below, for bindings that mirror them (ctypes, cgo):
  * "gwn_gemm_desc", "gwn_tcn_args", "gwn_tcn_bwd_args", "gwn_gcn_args", "gwn_gcn_bwd_args",
- * "gwn_reduce_seg", "gwn_wgrad_problem", "gwn_gram_layer";
+ * "gwn_reduce_seg", "gwn_wgrad_problem", "gwn_gram_layer", "gwn_bn_fold";
  * -1 for an unknown name */
 long gwn_abi_sizeof(const char* struct_name);
 
@@ -319,7 +319,23 @@ typedef struct gwn_gcn_args {
    * as bf16 to pieces_bf16[row * ld_pb + (piece - 1) * c + ch] INSTEAD of h's fp32 columns c .. (their
    * only reader in the bf16 training step is the mlp weight gradient, gwn_wgrad_problem.Xb) */
   void* pieces_bf16; long ld_pb;
+  /* bn_fold (optional, train mode, c == 32, bn_partials given): gwn_batchnorm_fwd_fold on this
+   * launch's partials, issued by gwn_gcn_fwd itself (a second launch on the same stream); the
+   * caller then does not call gwn_batchnorm_fwd_fold.  With GWN_BN_FOLD_LAST=1 in the environment
+   * the persistent 16-node tile kernels run it in their last workgroup to finish instead (partials
+   * written through in a private channel-major order: bn_partials' content is then unspecified). */
+  const struct gwn_bn_fold* bn_fold;
 } gwn_gcn_args;
+/* gwn_batchnorm_fwd_fold's arguments (same meaning) for gwn_gcn_args.bn_fold, plus arrive: one
+ * device int, zero before the first launch and left zero by every launch (the workgroup count). */
+typedef struct gwn_bn_fold {
+  const float* gamma; const float* beta; float* running_mean; float* running_var;
+  float momentum; float eps;
+  float* save_mean; float* save_rstd; float* scale;
+  const float* w_next; const float* b_next; float* w_fold; float* b_fold;
+  long long* num_batches_tracked;
+  int* arrive;
+} gwn_bn_fold;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
  * accumulators, residual + dropout + BN partials in the epilogue).  In that case the supports

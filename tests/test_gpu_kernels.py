@@ -1132,6 +1132,94 @@ def test_gcn_t16_bf16_forward(gpu, n):
     assert rel_err(st[:, 1].numpy(), Z.mean(0, keepdim=True).numpy()) <= 1e-2
 
 
+@pytest.mark.parametrize("n", [16, 207, 325])
+@pytest.mark.parametrize("path", ["t16", "t16_last", "t16b", "t16b_last", "t32"])
+def test_gcn_fwd_bn_fold(gpu, n, path, monkeypatch):
+    """gwn_gcn_args.bn_fold: the BatchNorm finalize + fold into the next gated TCN issued by
+    gwn_gcn_fwd (a second launch; *_last = GWN_BN_FOLD_LAST=1, run by the 16-node tile kernel's last
+    workgroup on channel-major write-through partials; t32 = GWN_GCN_T16=0, the 32-node kernels).
+    Against fp64 statistics of the z the launch wrote (model.py:236, train mode): mean / rstd /
+    running stats within 1e-5, scale = gamma * rstd, w_fold = w_next * scale (same fp32 product),
+    b_fold within 1e-5, num_batches_tracked advanced once per launch, the arrival counter left 0
+    (two launches back to back)."""
+    from gwn_amd import _lib
+    monkeypatch.setenv("GWN_GCN_T16", "0" if path == "t32" else "1")
+    monkeypatch.setenv("GWN_BN_FOLD_LAST", "1" if path.endswith("_last") else "0")
+    path = path.replace("_last", "")
+    torch.manual_seed(n + 11)
+    C, K, S = 32, 3, 23
+    NP = (n + 31) // 32 * 32
+    W = (2 * K + 1) * C
+    rows = S * n
+    sups = []
+    for _ in range(K):
+        s_ = torch.zeros(NP, NP, device=gpu)
+        a = torch.rand(n, n, device=gpu)
+        s_[:n, :n] = a / a.sum(1, keepdim=True)
+        sups.append(s_)
+    supT = [s_.t().contiguous() for s_ in sups]
+    sq = _squares(gpu, sups)
+    P = ctypes.POINTER(ctypes.c_void_p)
+    arr = (ctypes.c_void_p * K)(*[s_.data_ptr() for s_ in sups])
+    arr2 = (ctypes.c_void_p * K)(*[q[0].data_ptr() for q in sq])
+    g4f, _ = _g4s(gpu, n, sups, sq, supT)
+    extra = {}
+    if path == "t16b":
+        el = _lib.load().gwn_support_g4_bf16_elems(n)
+        mats = [m for s_, q in zip(sups, sq) for m in (s_, q[0])]
+        g4bf = torch.zeros(len(mats), el // 2, device=gpu)
+        src = (ctypes.c_void_p * len(mats))(*[m.data_ptr() for m in mats])
+        _lib.call("gwn_support_g4_bf16", ctypes.cast(src, P), len(mats), n, NP, g4bf.data_ptr(), el, _lib.stream())
+        arrb = (ctypes.c_void_p * len(mats))(*[g4bf[i].data_ptr() for i in range(len(mats))])
+        extra = dict(split_planes=1, sup_g4b=ctypes.cast(arrb, P))
+    elif path == "t16":
+        extra = dict(sup_g4=g4f[1])
+    wm = torch.randn(C, W, device=gpu) * 0.1
+    wmt = wm.t().contiguous()
+    bm = torch.randn(C, device=gpu)
+    res = torch.randn(rows, C, device=gpu) + 5.0 * torch.randn(C, device=gpu)  # channel offsets
+    h = torch.zeros(rows, W, device=gpu)
+    h[:, :C] = torch.randn(rows, C, device=gpu)
+    z = torch.empty(rows, C, device=gpu)
+    seed = torch.zeros(1, device=gpu, dtype=torch.int64)
+    bnp = torch.full((_lib.load().gwn_gcn_bn_partial_count(rows, n, C, K, NP) * 3 * C,), float("nan"), device=gpu)
+    gamma, beta = torch.randn(C, device=gpu), torch.randn(C, device=gpu)
+    rm, rv = torch.randn(C, device=gpu), torch.rand(C, device=gpu) + 0.5
+    rm0, rv0 = rm.clone(), rv.clone()
+    mean, rstd, scale = (torch.full((C,), float("nan"), device=gpu) for _ in range(3))
+    wfg = torch.randn(2 * C, 2 * C, device=gpu) * 0.2
+    bfg = torch.randn(2 * C, device=gpu)
+    wfold, bfold = torch.full_like(wfg, float("nan")), torch.full_like(bfg, float("nan"))
+    nbt = torch.full((1,), 7, device=gpu, dtype=torch.int64)
+    arrive = torch.zeros(1, device=gpu, dtype=torch.int32)
+    bf = _lib.BnFold(gamma=gamma.data_ptr(), beta=beta.data_ptr(), running_mean=rm.data_ptr(),
+                     running_var=rv.data_ptr(), momentum=0.1, eps=1e-5, save_mean=mean.data_ptr(),
+                     save_rstd=rstd.data_ptr(), scale=scale.data_ptr(), w_next=wfg.data_ptr(), b_next=bfg.data_ptr(),
+                     w_fold=wfold.data_ptr(), b_fold=bfold.data_ptr(), num_batches_tracked=nbt.data_ptr(),
+                     arrive=arrive.data_ptr())
+    ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, P), ld_sup=NP, h=h.data_ptr(), ld_h=W,
+                      w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(), residual=res.data_ptr(), z=z.data_ptr(),
+                      seed_ptr=seed.data_ptr(), salt=0, drop_p=0.0, bn_partials=bnp.data_ptr(), w_mlp_t=wmt.data_ptr(),
+                      sup2=ctypes.cast(arr2, P), bn_fold=ctypes.pointer(bf), **extra)
+    for launch in range(2):
+        rm.copy_(rm0)
+        rv.copy_(rv0)
+        _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
+        torch.cuda.synchronize()
+        assert int(arrive.item()) == 0
+        assert int(nbt.item()) == 8 + launch
+        zd = z.double().cpu()
+        mu, var = zd.mean(0), zd.var(0, unbiased=False)
+        assert rel_err(mean.cpu().numpy(), mu.numpy()) < 1e-5
+        assert rel_err(rstd.cpu().numpy(), (1 / torch.sqrt(var + 1e-5)).numpy()) < 1e-5
+        assert rel_err(rm.cpu().numpy(), (0.9 * rm0.double().cpu() + 0.1 * mu).numpy()) < 1e-5
+        assert rel_err(rv.cpu().numpy(), (0.9 * rv0.double().cpu() + 0.1 * zd.var(0, unbiased=True)).numpy()) < 1e-5
+        assert torch.equal(scale, rstd * gamma)
+        assert torch.equal(wfold, wfg * scale.repeat(2)[None, :])
+        ref_b = bfg.double().cpu() + wfg.double().cpu() @ beta.double().cpu().repeat(2)
+        assert rel_err(bfold.cpu().numpy(), ref_b.numpy()) < 1e-5
+
+
 def _from_g4(buf, which, slices, n):
     """Inverse of _to_g4 for operand `which` of a tiled bf16 buffer: [slices*nt*16][32] fp64
     (rows >= n are the tiles' padding nodes)."""
