@@ -1130,6 +1130,43 @@ __device__ __forceinline__ void global_to_lds16(const float* src, long ld, int n
   }
 }
 
+// A phase's staging: rows [0, rows) of nsl consecutive slices (src: slice 0's row 0, slice stride
+// n * ld floats, 16-B aligned, ld % 4 == 0; rows >= n load as zeros) as float4 elements e ->
+// put(slice, row, quad, value).  Each thread's U elements of a round are all loaded before the
+// first put, and the rounds run over the whole phase (not slice by slice): one memory round trip
+// per U * blockDim elements.  mid() runs once with round 0's loads in flight (the channel-map
+// staging shares their round trip).
+template <int U, typename Put, typename Mid>
+__device__ __forceinline__ void stage_rows4(const float* src, long ld, int n, int rows, int nsl, Put put, Mid mid) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((long)nsl * n * ld * 4), 0x00020000);
+  const int per = rows * 8, total = nsl * per;
+  bool first = true;
+  for (int e0 = threadIdx.x; e0 < total || first; e0 += U * (int)blockDim.x) {
+    float4 v[U];
+    int key[U];  // (slice * rows + row) * 8 + quad, -1 past the phase
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      const int e = e0 + i * (int)blockDim.x;
+      const int sl = e / per, rem = e - sl * per, w = rem >> 3, q = rem & 7;
+      const bool ok = e < total && w < n;
+      v[i] = __builtin_bit_cast(
+          float4, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (int)(((long)(sl * n + w) * ld + 4 * q) * 4) : 0x7ffffff0, 0, 0));
+      key[i] = e < total ? e : -1;
+    }
+    if (first) {
+      mid();
+      first = false;
+    }
+#pragma unroll
+    for (int i = 0; i < U; ++i)
+      if (key[i] >= 0) {
+        const int sl = key[i] / per, rem = key[i] - sl * per;
+        put(sl, rem >> 3, rem & 7, v[i]);
+      }
+  }
+}
+
 // x += (x rotated by 8, 4, 2, 1 lanes within its 16-lane row): the row sum in every lane (each lane
 // in its own order; callers take lane 0 of the row: deterministic)
 __device__ __forceinline__ float row16_sum(float x) {
@@ -1497,6 +1534,19 @@ __device__ __forceinline__ void t16_store_g4(void* base, int which, int slices, 
   *(bf16x8g*)((char*)base + (((long)which * slices + slice) * nt + tile) * 1024 + lane * 16) = r;
 }
 
+// GWN_T16_PROBE builds (tools/exp/t16_probe.py only): per-workgroup s_memrealtime stamps into
+// kws (unused by the 16-node tile path): [block][20] = start, first phase staged, wave 0..15
+// loop end, after the BN flush
+#ifdef GWN_T16_PROBE
+#define T16_TS(a, k)                                                                            \
+  do {                                                                                          \
+    if ((threadIdx.x & 63) == 0 && (a).kws)                                                     \
+      ((unsigned long long*)(a).kws)[blockIdx.x * 20 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define T16_TS(a, k) do {} while (0)
+#endif
+
 template <int MAXT>
 __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, const PowSup p, const int maximg) {
   extern __shared__ float lds[];
@@ -1510,18 +1560,33 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   const int nwaves = blockDim.x >> 6;
   const long ldh = a.ld_h;
   const T16Range rg = t16_range(a.slices, nt);
+  if (threadIdx.x == 0) T16_TS(a, 0);
   BnRun bn;
   bn.n = 0.0f;
 #pragma unroll
   for (int q = 0; q < 8; ++q) bn.mean[q] = bn.m2[q] = 0.0f;
-  t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
+  // the phase's slices staged in one pass (stage_rows4; the channel maps inside its first round
+  // trip), else slice by slice
+  const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
+  if (!h16) t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
   for (long p0 = rg.tb; p0 < rg.te;) {
     const int s0 = (int)(p0 / nt);
     const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
     const int s1 = (int)((p1 - 1) / nt);
     if (p0 != rg.tb) __syncthreads();  // the previous phase's images are released
-    for (int s = s0; s <= s1; ++s) global_to_lds16(a.h + (long)s * n * ldh, ldh, n, rows_img, imgs + (s - s0) * imgf);
+    if (h16) {
+      const bool maps = p0 == rg.tb;
+      stage_rows4<8>(
+          a.h + (long)s0 * n * ldh, ldh, n, rows_img, s1 - s0 + 1,
+          [&](int sl, int w, int q, float4 x) { *(float4*)(imgs + sl * imgf + (q >> 2) * hs + w * 16 + 4 * (q & 3)) = x; },
+          [&] {
+            if (maps) t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
+          });
+    } else {
+      for (int s = s0; s <= s1; ++s) global_to_lds16(a.h + (long)s * n * ldh, ldh, n, rows_img, imgs + (s - s0) * imgf);
+    }
     __syncthreads();
+    if (threadIdx.x == 0 && p0 == rg.tb) T16_TS(a, 1);
     for (long t = p0 + ((wave - p0 % nwaves) + nwaves) % nwaves; t < p1; t += nwaves) {
       const int s = (int)(t / nt), tile = (int)(t - (long)s * nt);
       const float* xs = imgs + (s - s0) * imgf;
@@ -1560,7 +1625,9 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
     }
     p0 = p1;
   }
+  T16_TS(a, 2 + wave);
   t16_bn_flush(a, bn, wpart);
+  if (threadIdx.x == 0) T16_TS(a, 18);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1580,6 +1647,14 @@ __host__ __device__ inline int t16b_s16(int n) { return 32 * ((n + 31) / 32) + 8
 size_t t16b_lds_bytes(int n, int nsup, int maximg) {
   return (size_t)((2 * nsup + 1) * CH * LDW16 + T16_WAVES * 3 * CH) * sizeof(float) +
          (size_t)maximg * CH * t16b_s16(n) * 2;
+}
+
+// channels 4q .. 4q+3 of node w into the channel-major bf16 image [32][s16]
+__device__ __forceinline__ void put_bf16_cm(__bf16* img, int s16, int w, int q, float4 x) {
+  img[(4 * q) * s16 + w] = (__bf16)x.x;
+  img[(4 * q + 1) * s16 + w] = (__bf16)x.y;
+  img[(4 * q + 2) * s16 + w] = (__bf16)x.z;
+  img[(4 * q + 3) * s16 + w] = (__bf16)x.w;
 }
 
 // a slice's node features (rows >= n zero) -> the channel-major bf16 image [32][s16]
@@ -1658,13 +1733,24 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
   bn.n = 0.0f;
 #pragma unroll
   for (int q = 0; q < 8; ++q) bn.mean[q] = bn.m2[q] = 0.0f;
-  t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
+  const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
+  if (!h16) t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
   for (long p0 = rg.tb; p0 < rg.te;) {
     const int s0 = (int)(p0 / nt);
     const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
     const int s1 = (int)((p1 - 1) / nt);
     if (p0 != rg.tb) __syncthreads();  // the previous phase's images are released
-    for (int sl = s0; sl <= s1; ++sl) global_to_lds16_bf16(a.h + (long)sl * n * ldh, ldh, n, imgs + (sl - s0) * imgb);
+    if (h16) {  // as the f32 kernel: the phase in one pass, the maps inside its first round trip
+      const bool maps = p0 == rg.tb;
+      stage_rows4<8>(
+          a.h + (long)s0 * n * ldh, ldh, n, s16 - 8, s1 - s0 + 1,
+          [&](int sl, int w, int q, float4 x) { put_bf16_cm(imgs + sl * imgb, s16, w, q, x); },
+          [&] {
+            if (maps) t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
+          });
+    } else {
+      for (int sl = s0; sl <= s1; ++sl) global_to_lds16_bf16(a.h + (long)sl * n * ldh, ldh, n, imgs + (sl - s0) * imgb);
+    }
     __syncthreads();
     for (long t = p0 + ((wave - p0 % nwaves) + nwaves) % nwaves; t < p1; t += nwaves) {
       const int sl = (int)(t / nt), tile = (int)(t - (long)sl * nt);
@@ -1728,51 +1814,85 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
 // written for the workgroup's own tiles only [r0, r1).
 // BF: the image is the bf16 channel-major one of the bf16 forward ([32][s16], rows = s16 - 8)
 template <bool BF>
-__device__ __forceinline__ void t16_bwd_prologue(const FusedBwd& a, float* img, long row0, int n, int rows, int r0,
-                                                 int r1) {
-  const int hs = rows * 16;
+__device__ __forceinline__ void t16_bwd_put(float* img, int rows, int w, int q, float4 x) {
+  if (BF) put_bf16_cm((__bf16*)img, rows + 8, w, q, x);
+  else *(float4*)(img + (q >> 2) * rows * 16 + w * 16 + 4 * (q & 3)) = x;
+}
+
+// A phase's dh images (slices s0 .. s0 + nsl - 1, imgf floats apart): dh itself, or with the
+// BatchNorm-backward prologue dz = gamma*rstd*(dy - k1 - xhat*k2), dh = dropout'(dz), dres / dh_out
+// written for the workgroup's own rows (its tiles [rg.tb, rg.te)).  Whole phase in rounds of U
+// float4 per thread (stage_rows4's pattern: every load of a round before its first store); mid()
+// with round 0's loads in flight.
+// BF: the images are the bf16 channel-major ones of the bf16 forward ([32][s16], rows = s16 - 8)
+template <bool BF, typename Mid>
+__device__ __forceinline__ void t16_bwd_stage(const FusedBwd& a, float* imgs, int imgf, int s0, int nsl,
+                                              const T16Range& rg, int nt, int n, int rows, Mid mid) {
   if (!a.bn_dy) {
-    if (BF) global_to_lds16_bf16(a.dh + row0 * CH, CH, n, (__bf16*)img);
-    else global_to_lds16(a.dh + row0 * CH, CH, n, rows, img);
+    stage_rows4<8>(a.dh + (long)s0 * n * CH, CH, n, rows, nsl,
+                   [&](int sl, int w, int q, float4 x) { t16_bwd_put<BF>(imgs + sl * imgf, rows, w, q, x); }, mid);
     return;
   }
+  constexpr int U = 4;
   const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
   const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
-  const int c = threadIdx.x & 31;  // blockDim is a multiple of 64: every element of a thread has channel c
-  const float mu = a.bn_mean[c], rs = a.bn_rstd[c], gm = a.bn_gamma[c];
-  const float k1 = a.bn_sums[c] * a.inv_rows, k2 = a.bn_sums[CH + c] * a.inv_rows;
-  const int total = rows * CH;
-  float* ip = img + (c >> 4) * hs + (c & 15);
-  for (int e0 = threadIdx.x; e0 < total; e0 += 4 * (int)blockDim.x) {
-    float dy[4], zv[4];  // all loads before the first store
+  const int q = threadIdx.x & 7;  // blockDim % 8 == 0: every element of a thread has channel quad q
+  float mu[4], rs[4], gm[4], k1[4], k2[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int w = min((e0 + i * (int)blockDim.x) >> 5, n - 1);
-      dy[i] = a.bn_dy[(row0 + w) * CH + c];
-      zv[i] = a.bn_z[(row0 + w) * CH + c];
+  for (int e = 0; e < 4; ++e) {
+    const int c = 4 * q + e;
+    mu[e] = a.bn_mean[c]; rs[e] = a.bn_rstd[c]; gm[e] = a.bn_gamma[c];
+    k1[e] = a.bn_sums[c] * a.inv_rows; k2[e] = a.bn_sums[CH + c] * a.inv_rows;
+  }
+  const long base = (long)s0 * n * CH;  // first element of the phase
+  const int bytes = (int)((long)nsl * n * CH * 4);
+  const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc((void*)(a.bn_dy + base), (short)0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)(a.bn_z + base), (short)0, bytes, 0x00020000);
+  const int per = rows * 8, total = nsl * per;
+  bool first = true;
+  for (int e0 = threadIdx.x; e0 < total || first; e0 += U * (int)blockDim.x) {
+    float4 dy[U], zv[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      const int e = e0 + i * (int)blockDim.x;
+      const int sl = e / per, w = (e - sl * per) >> 3;
+      const int off = (e < total && w < n) ? ((sl * n + w) * CH + 4 * q) * 4 : 0x7ffffff0;
+      dy[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rdy, off, 0, 0));
+      zv[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rz, off, 0, 0));
+    }
+    if (first) {
+      mid();
+      first = false;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < U; ++i) {
       const int e = e0 + i * (int)blockDim.x;
       if (e >= total) break;
-      const int w = e >> 5;
-      float v = 0.0f;
+      const int sl = e / per, w = (e - sl * per) >> 3;
+      float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
       if (w < n) {
-        const long idx = (row0 + w) * CH + c;
-        const float xhat = (zv[i] - mu) * rs;
-        const float dz = gm * rs * (dy[i] - k1 - xhat * k2);
-        v = dz;
-        if (a.drop_p > 0.0f) {
-          const float u = gwn_uniform(seed, a.salt, (unsigned long long)idx);
-          v = (u >= a.drop_p) ? v * keep_scale : 0.0f;
+        const long row = (long)(s0 + sl) * n + w;
+        const float dyv[4] = {dy[i].x, dy[i].y, dy[i].z, dy[i].w}, zz[4] = {zv[i].x, zv[i].y, zv[i].z, zv[i].w};
+        float dz[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float xhat = (zz[c] - mu[c]) * rs[c];
+          dz[c] = gm[c] * rs[c] * (dyv[c] - k1[c] - xhat * k2[c]);
+          v[c] = dz[c];
+          if (a.drop_p > 0.0f) {
+            const float u = gwn_uniform(seed, a.salt, (unsigned long long)(row * CH + 4 * q + c));
+            v[c] = (u >= a.drop_p) ? v[c] * keep_scale : 0.0f;
+          }
         }
-        if (w >= r0 && w < r1) {
-          a.dres[idx] = dz;
-          a.dh_out[idx] = v;
+        // this workgroup's rows of the slice: its tiles of it
+        const long sb = (long)(s0 + sl) * nt;
+        const long t0 = max(rg.tb - sb, 0l), t1 = min(rg.te - sb, (long)nt);
+        if (w >= 16 * t0 && w < 16 * t1) {
+          *(float4*)(a.dres + row * CH + 4 * q) = make_float4(dz[0], dz[1], dz[2], dz[3]);
+          *(float4*)(a.dh_out + row * CH + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
         }
       }
-      if (BF) ((__bf16*)img)[c * (rows + 8) + w] = (__bf16)v;
-      else ip[w * 16] = v;
+      t16_bwd_put<BF>(imgs + sl * imgf, rows, w, q, make_float4(v[0], v[1], v[2], v[3]));
     }
   }
 }
@@ -1806,17 +1926,16 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
     if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
     if (a.bn_dgamma) a.bn_dgamma[threadIdx.x] = a.bn_sums[CH + threadIdx.x];
   }
-  t16_stage_maps(a.w_mlp, a.ld_w, true, 2 * a.nsup + 1, ws);
   for (long p0 = rg.tb; p0 < rg.te;) {
     const int s0 = (int)(p0 / nt);
     const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
     const int s1 = (int)((p1 - 1) / nt);
     if (p0 != rg.tb) __syncthreads();
-    for (int s = s0; s <= s1; ++s) {
-      // this workgroup's rows of slice s
-      const long t0 = max(rg.tb - (long)s * nt, 0l), t1 = min(rg.te - (long)s * nt, (long)nt);
-      t16_bwd_prologue<BF>(a, imgs + (s - s0) * imgf, (long)s * n, n, rows_img, 16 * (int)t0, 16 * (int)t1);
-    }
+    // the phase's dh images in one pass, the channel maps inside its first round trip
+    const bool maps = p0 == rg.tb;
+    t16_bwd_stage<BF>(a, imgs, imgf, s0, s1 - s0 + 1, rg, nt, n, rows_img, [&] {
+      if (maps) t16_stage_maps(a.w_mlp, a.ld_w, true, 2 * a.nsup + 1, ws);
+    });
     __syncthreads();
     for (long t = p0 + ((wave - p0 % nwaves) + nwaves) % nwaves; t < p1; t += nwaves) {
       const int s = (int)(t / nt), tile = (int)(t - (long)s * nt);
@@ -2360,8 +2479,12 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   else
     GWN_REQUIRE(a.dh != nullptr, "gcn_bwd (fused): dh is required without the BN prologue");
   if (a.dfg) GWN_REQUIRE(a.fg != nullptr, "gcn_bwd (fused): the gate epilogue needs fg");
+  // the t16 backward stages dh (or dy / z, writing dres / dh_out) as 16-B rows
+  const auto a16 = [](const void* ptr) { return ((uintptr_t)ptr & 15) == 0; };
+  const bool t16_rows16 = a.bn_dy ? a16(a.bn_dy) && a16(a.bn_z) && a16(a.dres) && a16(a.dh_out) : a16(a.dh);
   if (g->split_planes == 1 && g->sup_g4b_t && a.sup_batch <= 1 && g->nsup > 0 && g->layout == 0 && t16_enabled() &&
       g->ksplit != g->nsup) {
+    GWN_REQUIRE(t16_rows16, "gcn_bwd (16-node tiles, bf16): dh, or bn_dy / bn_z / dres / dh_out, must be 16-B aligned");
     const int slices = g->rows / g->n;
     const size_t fixed = t16b_lds_bytes(g->n, g->nsup, 0), img = t16b_lds_bytes(g->n, g->nsup, 1) - fixed;
     if (fixed + img <= (size_t)T16_LDS_MAX) {
@@ -2412,7 +2535,7 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   const int grid = a.ksplit > 1 ? (slices + 7) / 8 * 8 * a.ksplit : slices;
   const T16Plan pl = t16_plan(g->n, g->nsup, slices);
   if (g->sup_g4_t && a.sup_batch <= 1 && g->nsup > 0 && (a.ksplit <= 1 || g->ksplit != g->nsup) && g->layout == 0 &&
-      t16_enabled() && pl.ok) {
+      t16_enabled() && pl.ok && t16_rows16) {
     PowSup p = {};
     for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = g->sup_g4_t[k];
     a.ksplit = 1;

@@ -25,7 +25,7 @@ namespace {
 constexpr int OOR = 0x7ffffff0;
 constexpr int NXCD = 8;
 #ifndef GRAM_WAVES
-#define GRAM_WAVES 1792  // target wave count of a gram launch
+#define GRAM_WAVES 2048  // target wave count of a gram launch (1792: 263.8 us per METR step, 2048: 242.4, 3072: 273.2, 4096: 245.2)
 #endif
 
 constexpr int GL = 8;  // layers of a grouped launch (gwn_gram_group)
@@ -460,6 +460,126 @@ int gram_group_plan(int n, const int* slices, int nlayers, int* nsp) {
   }
   return used;
 }
+
+// ---------------------------------------------------------------------------------------------
+// CU-resident gram (fp32, n <= 256): the whole contraction as one split-K GEMM per CU.  A 16-wave
+// workgroup per CU keeps the entire [np16][np16] output (np16 = 16 ceil(n / 16); 16-node tiles of
+// v_mfma_f32_16x16x4_f32, a contiguous row-major run of <= MAXT tiles per wave, 4 accumulator
+// registers each) over an equal range of the launch's (layer, slice, pair) steps.  Each step's X
+// and T rows (np16 x 32 floats each) are staged ONCE per CU into LDS -- double-buffered, the next
+// step's loads in flight during the current step's products, one barrier per step -- and read by
+// all 16 waves, so an operand row crosses L2 -> CU once per CU instead of once per 32 x 64 output
+// block (gram_kernel: ~2.2 GB of fragment traffic per METR step).  The K permutation of
+// gram_kernel: lane group q takes channels 8q .. 8q+7 (two ds_read_b128 per operand and tile), the
+// same on both operands.  Partials [CU][np16][np16], summed in a fixed order by gram_reduce_kernel.
+constexpr int GCU_LDR = 36;  // LDS row stride (floats): the 16 rows of a ds_read_b128 pass on distinct banks
+
+struct GramCu {
+  const float* X[GL][2]; const float* T[GL][2];
+  int lsteps0[GL + 1];  // layer l's steps [lsteps0[l], lsteps0[l+1]) = (slice, pair), pair fastest
+  int nlayers;
+  long ldx, ldt;
+  int n, nt16;
+  float* part;  // [gridDim.x][16 nt16][16 nt16]
+};
+
+template <int MAXT>
+__global__ __launch_bounds__(1024) void gram_cu_kernel(const GramCu g) {
+  extern __shared__ float4 gcu_lds4[];
+  float* lds = (float*)gcu_lds4;
+  const int rows = 16 * g.nt16, opf = rows * GCU_LDR;  // staged rows per operand (>= n: zeros)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, i = lane & 15;
+  const int total = g.lsteps0[g.nlayers];
+  const int st0 = (int)((long)total * blockIdx.x / gridDim.x), st1 = (int)((long)total * (blockIdx.x + 1) / gridDim.x);
+  const int ntiles = g.nt16 * g.nt16;
+  const int tb = ntiles * wave / 16, cnt = ntiles * (wave + 1) / 16 - tb;
+  f32x4g acc[MAXT];
+#pragma unroll
+  for (int u = 0; u < MAXT; ++u) acc[u] = f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
+  // staging: operand rows as float4 e = row * 8 + quad, e < rows * 8 <= 2048: two per thread
+  const int per = rows * 8;
+  float4 sx[2], stt[2];
+  auto stage_load = [&](int st) {
+    int L = 0;
+    while (L + 1 < g.nlayers && st >= g.lsteps0[L + 1]) ++L;
+    const int ls = st - g.lsteps0[L], sl = ls >> 1, p = ls & 1;
+    const long base = (long)sl * g.n;
+    const __amdgpu_buffer_rsrc_t rx = rsrc(g.X[L][p] + base * g.ldx, (long)g.n * g.ldx * 4);
+    const __amdgpu_buffer_rsrc_t rt = rsrc(g.T[L][p] + base * g.ldt, (long)g.n * g.ldt * 4);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = (int)threadIdx.x + 1024 * u, r = e >> 3, c4 = e & 7;
+      const bool ok = e < per && r < g.n;
+      sx[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? (int)((r * g.ldx + 4 * c4) * 4) : OOR, 0, 0));
+      stt[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, ok ? (int)((r * g.ldt + 4 * c4) * 4) : OOR, 0, 0));
+    }
+  };
+  auto stage_store = [&](int buf) {
+    float* xi = lds + buf * 2 * opf;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = (int)threadIdx.x + 1024 * u, r = e >> 3, c4 = e & 7;
+      if (e < per) {
+        *(float4*)(xi + r * GCU_LDR + 4 * c4) = sx[u];
+        *(float4*)(xi + opf + r * GCU_LDR + 4 * c4) = stt[u];
+      }
+    }
+  };
+  auto frag = [&](const float* img, int t16, float4* f) {
+    const float* r = img + (16 * t16 + i) * GCU_LDR + 8 * q;
+    f[0] = *(const float4*)r;
+    f[1] = *(const float4*)(r + 4);
+  };
+  if (st0 < st1) {
+    stage_load(st0);
+    stage_store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int st = st0; st < st1; ++st) {
+    const bool more = st + 1 < st1;
+    if (more) stage_load(st + 1);
+    const float* xi = lds + buf * 2 * opf;
+    const float* ti_ = xi + opf;
+    // (the 16 waves of the CU hide the LDS latency: no in-wave prefetch, which would cost 8 of the
+    // registers the accumulators need)
+#pragma unroll
+    for (int u = 0; u < MAXT; ++u) {
+      if (u < cnt) {
+        const int t = tb + u, ti = t / g.nt16;
+        float4 a[2], b[2];
+        frag(xi, ti, a);
+        frag(ti_, t - ti * g.nt16, b);
+        const float av[8] = {a[0].x, a[0].y, a[0].z, a[0].w, a[1].x, a[1].y, a[1].z, a[1].w};
+        const float bv[8] = {b[0].x, b[0].y, b[0].z, b[0].w, b[1].x, b[1].y, b[1].z, b[1].w};
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc[u], 0, 0, 0);
+      }
+    }
+    if (more) stage_store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // D[v][w]: lane (q, i) holds rows 16 ti + 4 q + r, column 16 tj + i
+  const long np = rows;
+  float* out = g.part + (long)blockIdx.x * np * np;
+#pragma unroll
+  for (int u = 0; u < MAXT; ++u) {
+    if (u < cnt) {
+      const int t = tb + u, ti = t / g.nt16, tj = t - ti * g.nt16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(long)(16 * ti + 4 * q + r) * np + 16 * tj + i] = acc[u][r];
+    }
+  }
+}
+
+// the CU-resident gram applies (GWN_GRAM_CU=0: gram_kernel)
+bool gram_cu_ok(int n) {
+  const char* e = getenv("GWN_GRAM_CU");
+  if (e && e[0] == '0') return false;
+  return n <= 256;
+}
+size_t gram_cu_lds(int n) { return (size_t)2 * 2 * 16 * ((n + 15) / 16) * GCU_LDR * sizeof(float); }
 }  // namespace
 
 long gwn_gram_group_workspace_floats(int n, const int* slices, int nlayers) {
@@ -468,7 +588,10 @@ long gwn_gram_group_workspace_floats(int n, const int* slices, int nlayers) {
   for (int l = 0; l < nlayers; ++l)
     if (slices[l] <= 0) return 0;
   const long np = 32L * ((n + 31) / 32);
-  return (long)gram_group_plan(n, slices, nlayers, nsp) * np * np;
+  const long classic = (long)gram_group_plan(n, slices, nlayers, nsp) * np * np;
+  const long np16 = 16L * ((n + 15) / 16);
+  const long cu = n <= 256 ? (long)gwn_device_cus() * np16 * np16 : 0;  // gram_cu_kernel's partials
+  return classic > cu ? classic : cu;
 }
 
 int gwn_gram_group(const gwn_gram_layer* layers, int nlayers, long ldx, long ldt, int n, float* dA, int ld_dA,
@@ -493,6 +616,46 @@ int gwn_gram_group(const gwn_gram_layer* layers, int nlayers, long ldx, long ldt
   for (int l = 0; l < nlayers; ++l) {
     g.lslices[l] = sl[l];
     g.lsplit0[l + 1] = g.lsplit0[l] + nsp[l];
+  }
+  if (gram_cu_ok(n)) {
+    GramCu c = {};
+    c.nlayers = nlayers;
+    c.lsteps0[0] = 0;
+    for (int l = 0; l < nlayers; ++l) {
+      for (int p = 0; p < 2; ++p) {
+        c.X[l][p] = g.X[l][p];
+        c.T[l][p] = g.T[l][p];
+      }
+      c.lsteps0[l + 1] = c.lsteps0[l] + 2 * sl[l];
+    }
+    c.ldx = ldx; c.ldt = ldt;
+    c.n = n; c.nt16 = (n + 15) / 16;
+    c.part = ws;
+    const int grid = gwn_device_cus();
+    const long np16 = 16L * c.nt16;
+    GWN_DEBUG_RANGE(ws, grid * np16 * np16 * 4, "gram_group (CU) partials");
+    GWN_DEBUG_RANGE(dA, ((long)(n - 1) * ld_dA + n) * 4, "gram_group dA");
+    const size_t lds = gram_cu_lds(n);
+    const int need = (c.nt16 * c.nt16 + 15) / 16;  // tiles per wave
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)gram_cu_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)gram_cu_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)gram_cu_kernel<11>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)gram_cu_kernel<12>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)gram_cu_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    if (need <= 4) gram_cu_kernel<4><<<grid, 1024, lds, s>>>(c);
+    else if (need <= 8) gram_cu_kernel<8><<<grid, 1024, lds, s>>>(c);
+    else if (need <= 11) gram_cu_kernel<11><<<grid, 1024, lds, s>>>(c);  // n = 161 .. 208
+    else if (need <= 12) gram_cu_kernel<12><<<grid, 1024, lds, s>>>(c);
+    else gram_cu_kernel<16><<<grid, 1024, lds, s>>>(c);
+    GWN_CHECK_LAUNCH();
+    const long outs = (long)n * n;
+    gram_reduce_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(ws, grid, n, (int)np16, dA, ld_dA, accumulate);
+    GWN_CHECK_LAUNCH();
+    return GWN_OK;
   }
   g.npairs = 2;
   g.ldx = ldx; g.ldt = ldt;

@@ -1448,13 +1448,17 @@ def test_wgrad_group_vs_fp64(gpu, shape):
 
 
 @pytest.mark.parametrize("n", [207, 16, 325])
-def test_gram_group_vs_fp64(gpu, n):
-    """gwn_gram_group (the adaptive-support gradient of several layers in one launch: splits dealt to
-    the layers by slice count, one reduction) against fp64: layers of 36 / 30 / 9 / 3 slices with the
-    training step's operand layout (x in h [rows][224] columns 0 and 160, t1 / t2 in [rows][96]
-    columns 32 and 64), accumulating into dA.  Bound: the fp32 FMA chain over all terms."""
+@pytest.mark.parametrize("cu", ["1", "0"])
+def test_gram_group_vs_fp64(gpu, n, cu, monkeypatch):
+    """gwn_gram_group (the adaptive-support gradient of several layers in one launch) against fp64:
+    layers of 36 / 30 / 9 / 3 slices with the training step's operand layout (x in h [rows][224]
+    columns 0 and 160, t1 / t2 in [rows][96] columns 32 and 64), accumulating into dA, on both
+    kernels: the CU-resident one (n <= 256: one workgroup per CU over an equal range of (layer,
+    slice, pair) steps, the whole output in its accumulators) and, GWN_GRAM_CU=0 or n > 256,
+    gram_kernel (splits dealt to the layers by slice count).  Bound: the fp32 FMA chain."""
     import ctypes
     from gwn_amd import _lib
+    monkeypatch.setenv("GWN_GRAM_CU", cu)
     lib = _lib.load()
     torch.manual_seed(n + 5)
     slices = [36, 30, 9, 3] if n != 325 else [12, 5]
