@@ -1089,15 +1089,29 @@ size_t t16_lds_bytes(int n, int nsup, int maximg) {
   return (size_t)((2 * nsup + 1) * CH * LDW16 + T16_WAVES * 3 * CH + maximg * t16_img_rows(n) * CH) * sizeof(float);
 }
 
-// the channel maps M_p[out][in] of pieces p < npieces into LDS as m[(p*32 + in)*LDW16 + out]:
-// forward M_p = W[:, p-block] read from W^T rows (w_t + (p*32 + in)*32); backward M_p = W[:, p-block]^T
-// read from W rows (w + in*ld_w + p*32: in = output channel of the mlp)
-__device__ __forceinline__ void t16_stage_maps(const float* src, int ld_w, bool backward, int npieces, float* dst) {
-  const int total = npieces * CH * 8;  // float4s
-  for (int e = threadIdx.x; e < total; e += blockDim.x) {
-    const int r = e >> 3, q = e & 7;
-    const float* row = backward ? src + (long)(r & 31) * ld_w + (r >> 5) * CH : src + (long)r * CH;
-    *(float4*)(dst + r * LDW16 + 4 * q) = *(const float4*)(row + 4 * q);
+// the channel maps M_p[out][in] of pieces p < npieces into LDS as m[(p*32 + out)*LDW16 + in] (a
+// lane's four consecutive input channels one ds_read_b128 in t16_mlp), from the mlp weights W
+// [32][ld_w] (row = mlp output channel): forward M_p = W[:, p-block] (rows of W, 16-B loads);
+// backward M_p = W[:, p-block]^T (M_p[c][o] = W[o][p*32 + c]: strided 4-B loads)
+#ifndef GWN_T16_MLP128
+#define GWN_T16_MLP128 0  // 0: the round-3 layout m[(p*32 + in)*LDW16 + out], 16 ds_read_b32 per piece
+#endif
+__device__ __forceinline__ void t16_stage_maps(const float* w, int ld_w, bool backward, int npieces, float* dst) {
+  if (!GWN_T16_MLP128) {
+    backward = !backward;  // the transposed layout: the other gather
+  }
+  if (!backward) {
+    const int total = npieces * CH * 8;  // float4s
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+      const int r = e >> 3, q = e & 7;  // r = p*32 + out
+      *(float4*)(dst + r * LDW16 + 4 * q) = *(const float4*)(w + (long)(r & 31) * ld_w + (r >> 5) * CH + 4 * q);
+    }
+  } else {
+    const int total = npieces * CH * CH;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+      const int r = e >> 5, o = e & 31;  // r = p*32 + c
+      dst[r * LDW16 + o] = w[(long)o * ld_w + (r >> 5) * CH + (r & 31)];
+    }
   }
 }
 
@@ -1419,26 +1433,44 @@ __device__ void t16_bn_fold_last(const FusedFwd& a, float* lds, const float* wv,
 
 // the channel map of one piece held in accumulators acc[hf] (register s = input channel
 // 16 hf + 4 g + s): hacc[oh] (output channel 16 oh + 4 g + r) += M x piece with the A operand
-// M[out][in] read as m[in * ld_m + out] -- forward: the piece's block of W^T (ld_m = 32);
-// backward: the piece's column block of W itself (ld_m = ld_w), i.e. W^T applied to dh
+// M[out][in] read as m[out * ld_m + in] (t16_stage_maps: forward the piece's block of W, backward
+// its transpose, i.e. W^T applied to dh)
 __device__ __forceinline__ void t16_mlp(const float* m, int ld_m, const f32x4v* acc, int lane, f32x4v* hacc) {
   const int g = lane >> 4, j = lane & 15;
-  float wf[2][2][4];
+  if (!GWN_T16_MLP128) {
+    float wf[2][2][4];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int oh = 0; oh < 2; ++oh) wf[hf][oh][s] = m[(16 * hf + 4 * g + s) * ld_m + 16 * oh + j];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int oh = 0; oh < 2; ++oh)
+          hacc[oh] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[hf][oh][s], acc[hf][s], hacc[oh], 0, 0, 0);
+    return;
+  }
+  float4 wq[2][2];  // [hf][oh]: M[16 oh + j][16 hf + 4 g .. + 3]
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int oh = 0; oh < 2; ++oh) wf[hf][oh][s] = m[(16 * hf + 4 * g + s) * ld_m + 16 * oh + j];
-  // all 16 fragment reads in flight before the first product (one LDS latency, not sixteen)
+    for (int oh = 0; oh < 2; ++oh) wq[hf][oh] = *(const float4*)(m + (16 * oh + j) * ld_m + 16 * hf + 4 * g);
+  // all four fragment reads in flight before the first product (one LDS latency)
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int oh = 0; oh < 2; ++oh)
-        hacc[oh] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[hf][oh][s], acc[hf][s], hacc[oh], 0, 0, 0);
+      for (int oh = 0; oh < 2; ++oh) {
+        const float wv = s == 0 ? wq[hf][oh].x : s == 1 ? wq[hf][oh].y : s == 2 ? wq[hf][oh].z : wq[hf][oh].w;
+        hacc[oh] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv, acc[hf][s], hacc[oh], 0, 0, 0);
+      }
 }
 
 // both powers of one support for the wave's 16-node tile: acc[q][hf] (q = 0: G1, 1: G2) holds
@@ -1568,7 +1600,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   // the phase's slices staged in one pass (stage_rows4; the channel maps inside its first round
   // trip), else slice by slice
   const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
-  if (!h16) t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
+  if (!h16) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
   for (long p0 = rg.tb; p0 < rg.te;) {
     const int s0 = (int)(p0 / nt);
     const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
@@ -1580,7 +1612,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
           a.h + (long)s0 * n * ldh, ldh, n, rows_img, s1 - s0 + 1,
           [&](int sl, int w, int q, float4 x) { *(float4*)(imgs + sl * imgf + (q >> 2) * hs + w * 16 + 4 * (q & 3)) = x; },
           [&] {
-            if (maps) t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
+            if (maps) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
           });
     } else {
       for (int s = s0; s <= s1; ++s) global_to_lds16(a.h + (long)s * n * ldh, ldh, n, rows_img, imgs + (s - s0) * imgf);
@@ -1734,7 +1766,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
 #pragma unroll
   for (int q = 0; q < 8; ++q) bn.mean[q] = bn.m2[q] = 0.0f;
   const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
-  if (!h16) t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
+  if (!h16) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
   for (long p0 = rg.tb; p0 < rg.te;) {
     const int s0 = (int)(p0 / nt);
     const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
@@ -1746,7 +1778,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
           a.h + (long)s0 * n * ldh, ldh, n, s16 - 8, s1 - s0 + 1,
           [&](int sl, int w, int q, float4 x) { put_bf16_cm(imgs + sl * imgb, s16, w, q, x); },
           [&] {
-            if (maps) t16_stage_maps(a.w_t, 0, false, 2 * a.nsup + 1, ws);
+            if (maps) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
           });
     } else {
       for (int sl = s0; sl <= s1; ++sl) global_to_lds16_bf16(a.h + (long)sl * n * ldh, ldh, n, imgs + (sl - s0) * imgb);

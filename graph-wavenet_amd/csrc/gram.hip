@@ -193,25 +193,37 @@ __global__ __launch_bounds__(64) void gram_kernel(const Gram g) {
   }
 }
 
-// dA[v][w] (+)= sum_split part[split][v][w], fixed order
-__global__ void gram_reduce_kernel(const float* part, int nsplit, int n, int np, float* dA, int ld,
-                                   int accumulate) {
-  const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (idx >= (long)n * n) return;
-  const int v = (int)(idx / n), w = (int)(idx - (long)v * n);
+// dA[v][w] (+)= sum_split part[split][v][w], fixed order.  A 256-thread block takes 64 outputs x 4
+// contiguous quarters of the splits (8 independent chains per thread: loads in flight together),
+// the quarters merged in LDS as (q0 + q1) + (q2 + q3): four times the blocks of a thread per
+// output (a 224 x 224 output is 49k threads -- under a fifth of the chip's wave slots)
+__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* part, int nsplit, int n, int np, float* dA,
+                                                          int ld, int accumulate) {
+  __shared__ float sh[4][64];
+  const int o = threadIdx.x & 63, qq = threadIdx.x >> 6;
+  const long idx = blockIdx.x * 64L + o;
+  const bool ok = idx < (long)n * n;
+  const int v = ok ? (int)(idx / n) : 0, w = ok ? (int)(idx - (long)v * n) : 0;
   const float* p = part + (long)v * np + w;
   const long st = (long)np * np;
-  // eight independent chains (loads in flight together), merged in a fixed order
+  const int k0 = nsplit * qq / 4, k1 = nsplit * (qq + 1) / 4;
   float a[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  int k = 0;
-  for (; k + 8 <= nsplit; k += 8)
+  int k = k0;
+  if (ok) {
+    for (; k + 8 <= k1; k += 8)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) a[u] += p[(k + u) * st];
-  for (; k < nsplit; ++k) a[k & 7] += p[k * st];
-  const float s = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-  float* o = dA + (long)v * ld + w;
-  *o = accumulate ? *o + s : s;
+      for (int u = 0; u < 8; ++u) a[u] += p[(k + u) * st];
+    for (; k < k1; ++k) a[(k - k0) & 7] += p[k * st];
+  }
+  sh[qq][o] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (qq != 0 || !ok) return;
+  const float s = (sh[0][o] + sh[1][o]) + (sh[2][o] + sh[3][o]);
+  float* d = dA + (long)v * ld + w;
+  *d = accumulate ? *d + s : s;
 }
+
+inline unsigned gram_reduce_blocks(int n) { return (unsigned)(((long)n * n + 63) / 64); }
 
 constexpr size_t GRAM_IMG = 96 * 36 * sizeof(float);  // LINES: a wave's [96][36] image
 bool gram_lines() {
@@ -355,8 +367,7 @@ int gwn_gram_g4_bf16(const void* x1, const void* t1, const void* x2, const void*
   const int blocks = ((g.nsplit + NXCD - 1) / NXCD) * NXCD * g.nb * g.nb;
   gram_g4_kernel<G4_TB><<<blocks, 64, 0, s>>>(g);
   GWN_CHECK_LAUNCH();
-  const long outs = (long)n * n;
-  gram_reduce_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(ws, g.nsplit, n, (int)g.np, dA, ld_dA, accumulate);
+  gram_reduce_kernel<<<gram_reduce_blocks(n), 256, 0, s>>>(ws, g.nsplit, n, (int)g.np, dA, ld_dA, accumulate);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
@@ -429,8 +440,7 @@ int gwn_gram_dtype(const float* x1, const float* t1, const float* x2, const floa
     else gram_kernel<1><<<blocks, 64, 0, s>>>(g);
   }
   GWN_CHECK_LAUNCH();
-  const long outs = (long)n * n;
-  gram_reduce_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(ws, g.nsplit, n, 32 * g.nt, dA, ld_dA,
+  gram_reduce_kernel<<<gram_reduce_blocks(n), 256, 0, s>>>(ws, g.nsplit, n, 32 * g.nt, dA, ld_dA,
                                                                      accumulate);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
@@ -473,6 +483,10 @@ int gram_group_plan(int n, const int* slices, int nlayers, int* nsp) {
 // gram_kernel: lane group q takes channels 8q .. 8q+7 (two ds_read_b128 per operand and tile), the
 // same on both operands.  Partials [CU][np16][np16], summed in a fixed order by gram_reduce_kernel.
 constexpr int GCU_LDR = 36;  // LDS row stride (floats): the 16 rows of a ds_read_b128 pass on distinct banks
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+constexpr int GCG_NB = 4;  // LDS step buffers: three steps' operands in flight
+// s_waitcnt vmcnt(n) (n <= 15), expcnt / lgkmcnt not waited on
+#define GCG_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(0x0F70 | (n))
 
 struct GramCu {
   const float* X[GL][2]; const float* T[GL][2];
@@ -573,6 +587,104 @@ __global__ __launch_bounds__(1024) void gram_cu_kernel(const GramCu g) {
   }
 }
 
+// The bf16 mode's CU-resident gram on the tiled bf16 operands (gwn_gram_g4_bf16's layout: a KiB per
+// (slice, 16-node tile), lane (g, j)'s 16 B its k-group of v_mfma_f32_16x16x32_bf16).  Like
+// gram_cu_kernel, but the 16x16 output tiles of one CU would need ~28 per wave at n = 325, so the
+// workgroups come in two halves (blockIdx & 1): half h keeps output tile rows [vt0, vt0 + R) of
+// every column (<= MAXT tiles per wave) and walks its own equal share of ALL the (layer, slice,
+// pair) steps; per step it stages R KiB of X and nt KiB of T (double-buffered, the next step's
+// 16-B loads in flight) and each wave runs one MFMA per tile, the X fragment reloaded only when
+// its row changes.  Partial slot kb = blockIdx >> 1 holds half 0's rows of share kb and half 1's
+// rows of share kb: [grid / 2][np][np], reduced in a fixed order.
+struct GramCuG4 {
+  const char* X[GL]; const char* T[GL];  // layer l: pair p's operand at + p * slices * nt KiB
+  int lslices[GL], lsteps0[GL + 1], nlayers;
+  int nt, vmid;                          // tile rows [0, vmid) in half 0, [vmid, nt) in half 1
+  long np;
+  float* part;
+};
+
+
+template <int MAXT>
+__global__ __launch_bounds__(1024) void gram_cu_g4_kernel(const GramCuG4 g) {
+  extern __shared__ float4 gcg_lds4[];
+  const int h = blockIdx.x & 1, kb = blockIdx.x >> 1, nh = gridDim.x >> 1;
+  const int vt0 = h ? g.vmid : 0, R = h ? g.nt - g.vmid : g.vmid;
+  const int nblk = R + g.nt;  // KiB staged per step
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int gq = lane >> 4, j = lane & 15;
+  const int total = g.lsteps0[g.nlayers];
+  const int st0 = (int)((long)total * kb / nh), st1 = (int)((long)total * (kb + 1) / nh);
+  const int nst = st1 - st0;
+  const int ntiles = R * g.nt;
+  const int tb = ntiles * wave / 16, cnt = ntiles * (wave + 1) / 16 - tb;
+  f32x4g acc[MAXT];
+#pragma unroll
+  for (int u = 0; u < MAXT; ++u) acc[u] = f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
+  const int bufk = nblk * 64;                    // float4 per step buffer
+  float4* sink = gcg_lds4 + GCG_NB * bufk;       // the target of the padding waves' loads
+  // step st's operands into buffer b by 16-B LDS-DMA loads (buffer_load ... lds): wave w moves
+  // KiB blocks w, w + 16 (a block = one wave instruction, lane-linear); every wave issues
+  // exactly two per step (past nblk: a zero load into the sink) so the vmcnt waits are uniform
+  auto issue = [&](int st, int b) {
+    int L = 0;
+    while (L + 1 < g.nlayers && st >= g.lsteps0[L + 1]) ++L;
+    const int ls = st - g.lsteps0[L], sl = ls >> 1, p = ls & 1;
+    const long blk0 = ((long)p * g.lslices[L] + sl) * g.nt;  // KiB index of the step's slice
+    const __amdgpu_buffer_rsrc_t rx =
+        rsrc(g.X[L] + (blk0 + vt0) * 1024, (long)R * 1024);
+    const __amdgpu_buffer_rsrc_t rt = rsrc(g.T[L] + blk0 * 1024, (long)g.nt * 1024);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int blk = wave + 16 * i;
+      float4* dst = blk < nblk ? gcg_lds4 + b * bufk + blk * 64 : sink;
+      if (blk < R)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)dst, 16, blk * 1024 + lane * 16, 0, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_ptr_t)dst, 16,
+                                                 blk < nblk ? (blk - R) * 1024 + lane * 16 : 0x7ffffff0, 0, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int c = 0; c < GCG_NB - 1; ++c)
+    if (c < nst) issue(st0 + c, c);
+  for (int c = 0; c < nst; ++c) {
+    // this wave's loads of step c have landed (steps c+1, c+2 may still be in flight), then the
+    // barrier: every wave's part of step c landed and every wave is done with step c-1, whose
+    // buffer the next issue reuses
+    if (c + 2 < nst) GCG_WAIT_VM(4);
+    else if (c + 1 < nst) GCG_WAIT_VM(2);
+    else GCG_WAIT_VM(0);
+    __builtin_amdgcn_s_barrier();
+    if (c + GCG_NB - 1 < nst) issue(st0 + c + GCG_NB - 1, (c + GCG_NB - 1) % GCG_NB);
+    const float4* img = gcg_lds4 + (c % GCG_NB) * bufk;
+    bf16x8 a = {};
+    int rprev = -1;
+#pragma unroll
+    for (int u = 0; u < MAXT; ++u) {
+      if (u < cnt) {
+        const int t = tb + u, r = t / g.nt, cc = t - r * g.nt;
+        if (r != rprev) {
+          a = __builtin_bit_cast(bf16x8, img[r * 64 + lane]);
+          rprev = r;
+        }
+        const bf16x8 b = __builtin_bit_cast(bf16x8, img[(R + cc) * 64 + lane]);
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[u], 0, 0, 0);
+      }
+    }
+  }
+  // D[v][w]: lane (gq, j) holds rows 4 gq + r of the tile, column j
+  float* out = g.part + (long)kb * g.np * g.np;
+#pragma unroll
+  for (int u = 0; u < MAXT; ++u) {
+    if (u < cnt) {
+      const int t = tb + u, r = t / g.nt, cc = t - r * g.nt;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) out[(long)(16 * (vt0 + r) + 4 * gq + rr) * g.np + 16 * cc + j] = acc[u][rr];
+    }
+  }
+}
+
 // the CU-resident gram applies (GWN_GRAM_CU=0: gram_kernel)
 bool gram_cu_ok(int n) {
   const char* e = getenv("GWN_GRAM_CU");
@@ -652,8 +764,7 @@ int gwn_gram_group(const gwn_gram_layer* layers, int nlayers, long ldx, long ldt
     else if (need <= 12) gram_cu_kernel<12><<<grid, 1024, lds, s>>>(c);
     else gram_cu_kernel<16><<<grid, 1024, lds, s>>>(c);
     GWN_CHECK_LAUNCH();
-    const long outs = (long)n * n;
-    gram_reduce_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(ws, grid, n, (int)np16, dA, ld_dA, accumulate);
+    gram_reduce_kernel<<<gram_reduce_blocks(n), 256, 0, s>>>(ws, grid, n, (int)np16, dA, ld_dA, accumulate);
     GWN_CHECK_LAUNCH();
     return GWN_OK;
   }
@@ -669,8 +780,63 @@ int gwn_gram_group(const gwn_gram_layer* layers, int nlayers, long ldx, long ldt
   if (gram_lines()) gram_kernel<2, false, true><<<blocks, 64, GRAM_IMG, s>>>(g);
   else gram_kernel<2><<<blocks, 64, 0, s>>>(g);
   GWN_CHECK_LAUNCH();
-  const long outs = (long)n * n;
-  gram_reduce_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(ws, g.nsplit, n, (int)np, dA, ld_dA, accumulate);
+  gram_reduce_kernel<<<gram_reduce_blocks(n), 256, 0, s>>>(ws, g.nsplit, n, (int)np, dA, ld_dA, accumulate);
+  GWN_CHECK_LAUNCH();
+  return GWN_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+namespace {
+// tiles per wave of gram_cu_g4_kernel's larger half
+inline int gcg_need(int nt) { return (((nt + 1) / 2) * nt + 15) / 16; }
+}  // namespace
+
+// 0 where gwn_gram_g4_group does not apply (n > 368: more than 16 output tiles per wave)
+long gwn_gram_g4_group_workspace_floats(int n, const int* slices, int nlayers) {
+  if (n <= 0 || nlayers < 1 || nlayers > GL || !slices || gcg_need((n + 15) / 16) > 16) return 0;
+  const long np = 32L * ((n + 31) / 32);
+  return (long)(gwn_device_cus() / 2) * np * np;
+}
+
+int gwn_gram_g4_group(const gwn_gram_layer* layers, int nlayers, int n, float* dA, int ld_dA, int accumulate,
+                      float* ws, hipStream_t s) {
+  GWN_REQUIRE(layers && nlayers >= 1 && nlayers <= GL && n > 0 && dA && ws, "gram_g4_group: 1..8 layers, n, dA, ws");
+  const int nt = (n + 15) / 16;
+  GWN_REQUIRE(gcg_need(nt) <= 16, "gram_g4_group: n up to 368 (16 output tiles per wave)");
+  GramCuG4 g = {};
+  g.nlayers = nlayers;
+  g.lsteps0[0] = 0;
+  for (int l = 0; l < nlayers; ++l) {
+    const gwn_gram_layer& q = layers[l];
+    GWN_REQUIRE(q.slices > 0 && q.x1 && q.t1 && ((uintptr_t)q.x1 & 15) == 0 && ((uintptr_t)q.t1 & 15) == 0 &&
+                    q.x2 == (const float*)((const char*)q.x1 + (long)q.slices * nt * 1024) &&
+                    q.t2 == (const float*)((const char*)q.t1 + (long)q.slices * nt * 1024),
+                "gram_g4_group: every layer's x2 / t2 must follow x1 / t1 (the xg4 / tg4 layout), 16-B aligned");
+    g.X[l] = (const char*)q.x1;
+    g.T[l] = (const char*)q.t1;
+    g.lslices[l] = q.slices;
+    g.lsteps0[l + 1] = g.lsteps0[l] + 2 * q.slices;
+  }
+  g.nt = nt;
+  g.vmid = (nt + 1) / 2;
+  g.np = 32L * ((n + 31) / 32);
+  g.part = ws;
+  const int grid = (gwn_device_cus() / 2) * 2;
+  GWN_DEBUG_RANGE(ws, (long)(grid / 2) * g.np * g.np * 4, "gram_g4_group partials");
+  GWN_DEBUG_RANGE(dA, ((long)(n - 1) * ld_dA + n) * 4, "gram_g4_group dA");
+  const size_t lds = (size_t)(GCG_NB * (g.vmid + nt) + 1) * 1024;  // + the sink
+  GWN_REQUIRE(lds <= 160 * 1024 && g.vmid + nt <= 32, "gram_g4_group: a step's operands exceed LDS");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gram_cu_g4_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)gram_cu_g4_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int need = gcg_need(nt);
+  if (need <= 8) gram_cu_g4_kernel<8><<<grid, 1024, lds, s>>>(g);
+  else gram_cu_g4_kernel<16><<<grid, 1024, lds, s>>>(g);
+  GWN_CHECK_LAUNCH();
+  gram_reduce_kernel<<<gram_reduce_blocks(n), 256, 0, s>>>(ws, grid / 2, n, (int)g.np, dA, ld_dA, accumulate);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }

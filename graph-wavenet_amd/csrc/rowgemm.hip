@@ -60,6 +60,14 @@ __device__ __forceinline__ float ld32(__amdgpu_buffer_rsrc_t r, int off) {
 #ifndef GWN_ROWGEMM_WPE
 #define GWN_ROWGEMM_WPE  // measurement hook: -DGWN_ROWGEMM_WPE='__attribute__((amdgpu_waves_per_eu(2)))'
 #endif
+// WLDS (default): the stationary weights stay in LDS ([row][2 KH + 4]: 2 KH + 4 = 4 mod 64, so the
+// 16 lanes of a ds_read_b128 pass hit distinct banks) and are read four k-steps at a time next to
+// the MFMAs, instead of 2 KH registers per lane: 228-288 registers (one wave per SIMD, every load
+// stall exposed) -> two waves per SIMD.  -DGWN_ROWGEMM_WLDS=0: weights in registers.
+#ifndef GWN_ROWGEMM_WLDS
+#define GWN_ROWGEMM_WLDS 1
+#endif
+constexpr bool WLDS = GWN_ROWGEMM_WLDS != 0;
 template <int KH, bool GATE, bool BNSTAT, bool CENTER = false>
 __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowGemm p) {
   constexpr int NQ = KH / 4;  // float4 per lane per chunk
@@ -90,15 +98,32 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
   float4 a[NQ];
   int chunk = wave;
   load(chunk, a);
-  // stationary weights w[t][j] = B(half*KH + j, column of (t, col)).  GATE (B = w_fg[n][k], the
-  // fragment is a strided column): staged once per block through LDS as Bt[n][k] (k contiguous),
-  // then read with 16-B LDS loads.  STORE (B(k, n) rows contiguous in n): direct coalesced loads.
+  // stationary weights w[t][j] = B(half*KH + j, column of (t, col)): WLDS, staged once per block
+  // in LDS and read next to the MFMAs; else in registers -- GATE (B = w_fg[n][k], the fragment is a
+  // strided column) through LDS as Bt[n][k] (k contiguous) read with 16-B LDS loads, STORE (B(k, n)
+  // rows contiguous in n) by direct coalesced loads.
   constexpr int K = 2 * KH, LDT = K + 4;
-  float w[NT][KH];
+  float w[NT][WLDS ? 1 : KH];
   float bn[NT];
-  if (GATE) {
+  extern __shared__ float4 bt4[];
+  const float* wrow[NT];  // WLDS: this lane's weight rows in LDS
+  if (WLDS) {
+    // rows: GATE (t, col) -> t*32 + col holds output column 2 col + t; STORE: row n
+    float* bt = (float*)bt4;
+    const int N = GATE ? 64 : 32 * p.ntiles;
+    for (int e = threadIdx.x; e < K * N; e += blockDim.x) {
+      const int k = e % K, nn = e / K;
+      const int row = GATE ? (nn & 1) * 32 + (nn >> 1) : nn;
+      bt[row * LDT + k] = p.B[(k % KH) * p.ldb_k + (k / KH) * p.ldb_tap + (long)nn * p.ldb_n];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      wrow[t] = bt + (GATE ? t * 32 + col : 32 * tile + col) * LDT + half * KH;
+      bn[t] = GATE ? p.bias[2 * col + t] : 0.0f;
+    }
+  } else if (GATE) {
     const int N = 64;
-    extern __shared__ float4 bt4[];
     float* bt = (float*)bt4;
     for (int e = threadIdx.x; e < K * N; e += blockDim.x) {
       const int k = e % K, nn = e / K;
@@ -112,14 +137,17 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
 #pragma unroll
       for (int q = 0; q < KH / 4; ++q) {
         const float4 v = src[q];
-        w[t][4 * q] = v.x; w[t][4 * q + 1] = v.y; w[t][4 * q + 2] = v.z; w[t][4 * q + 3] = v.w;
+        if (!WLDS) {
+          w[t][(4 * q) % (WLDS ? 1 : KH)] = v.x; w[t][(4 * q + 1) % (WLDS ? 1 : KH)] = v.y;
+          w[t][(4 * q + 2) % (WLDS ? 1 : KH)] = v.z; w[t][(4 * q + 3) % (WLDS ? 1 : KH)] = v.w;
+        }
       }
       bn[t] = p.bias[nb];
     }
   } else {
     const long nb = 32 * tile + col;
 #pragma unroll
-    for (int j = 0; j < KH; ++j) w[0][j] = p.B[j * p.ldb_k + half * p.ldb_tap + nb * p.ldb_n];
+    for (int j = 0; j < KH; ++j) w[0][j % (WLDS ? 1 : KH)] = p.B[j * p.ldb_k + half * p.ldb_tap + nb * p.ldb_n];
     bn[0] = 0.0f;
   }
   if (wave >= nwaves) return;  // after the block-wide staging barrier
@@ -164,11 +192,22 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
 #pragma unroll
         for (int e = 0; e < 4; ++e) av[e] -= cmu[4 * q + e];
       }
+      float wq[NT][4];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (WLDS) {
+          const float4 v = *(const float4*)(wrow[t] + 4 * q);
+          wq[t][0] = v.x; wq[t][1] = v.y; wq[t][2] = v.z; wq[t][3] = v.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) wq[t][e] = w[t][(4 * q + e) % (WLDS ? 1 : KH)];
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int t = 0; t < NT; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], w[t][4 * q + e], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], wq[t][e], acc[t], 0, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -227,7 +266,7 @@ int launch(const RowGemm& p, hipStream_t s) {
   GWN_REQUIRE(!BNSTAT || (p.ntiles == 1 && p.ldc == 32), "rowgemm: BN statistics need N = ldc = 32");
   (void)nchunks;
   const int grid = rowgemm_grid(p.M, p.ntiles, GATE);
-  const size_t lds = GATE ? (size_t)64 * (2 * KH + 4) * sizeof(float) : 0;
+  const size_t lds = (GATE || WLDS) ? (size_t)(GATE ? 64 : 32 * p.ntiles) * (2 * KH + 4) * sizeof(float) : 0;
   rowgemm_kernel<KH, GATE, BNSTAT, CENTER><<<grid, 256, lds, s>>>(p);
   GWN_CHECK_LAUNCH();
   return GWN_OK;

@@ -216,6 +216,8 @@ _SIGS = [
     ("gwn_gram_group_workspace_floats", c_long, [c_int, ctypes.POINTER(c_int), c_int]),
     ("gwn_gram_group", c_int, [ctypes.POINTER(GramLayer), c_int, c_long, c_long, c_int, c_void_p, c_int, c_int,
                                c_void_p, c_void_p]),
+    ("gwn_gram_g4_group_workspace_floats", c_long, [c_int, ctypes.POINTER(c_int), c_int]),
+    ("gwn_gram_g4_group", c_int, [ctypes.POINTER(GramLayer), c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("gwn_wgrad_group_plan", c_int, [ctypes.POINTER(c_int), c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     ("gwn_wgrad_group", c_int, [ctypes.POINTER(WgradProblem), c_int, c_int, c_int, c_int, c_void_p]),
     ("gwn_wgrad_bn", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,

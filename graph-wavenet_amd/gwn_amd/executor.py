@@ -586,7 +586,13 @@ class Executor:
                    and _lib.load().gwn_gcn_t16b_supported(N, cfg.nsup) == 1)
         acts.gram_g4 = gram_g4
         if getattr(acts, "XG4", None) is None:
-            acts.XG4 = {}
+            acts.XG4, acts.TG4 = {}, {}
+        # bf16 mode: every layer's adaptive-support gram in one gwn_gram_g4_group launch at the end
+        # of the backward (GWN_GRAM_GROUP=0: one gwn_gram_g4_bf16 per layer)
+        if gram_g4 and L >= 2 and getattr(acts, "ws_g4g", None) is None and os.environ.get("GWN_GRAM_GROUP", "1") != "0":
+            sl = (ctypes.c_int * (L - 1))(*[ts[i + 1] * P // N for i in range(L - 1)])
+            need = int(_lib.load().gwn_gram_g4_group_workspace_floats(N, sl, L - 1))
+            acts.ws_g4g = torch.empty(need + 16, device=self.device, dtype=F32) if need > 0 else False
         # bf16 mode: the hop pieces' only reader is then the grouped mlp weight gradient -- stored
         # as bf16 (half the bytes written here and read there); GWN_BF16_PIECES=0 keeps them fp32
         pieces_b = (gram_g4 and "group_mlp" in scr and self._group_ok() and self._defer_ok(scr)
@@ -622,6 +628,8 @@ class Executor:
                 need_x = 2 * (rows // N) * ((N + 15) // 16) * 256  # two bf16 operands, a KiB per tile
                 if acts.XG4.get(i) is None or acts.XG4[i].numel() != need_x:
                     acts.XG4[i] = torch.empty(need_x, device=self.device, dtype=F32)
+                    # the backward's t1 / t2 of this layer, kept for the grouped gram at its end
+                    acts.TG4[i] = torch.empty(need_x, device=self.device, dtype=F32)
                 xg4 = acts.XG4[i]
             ga = _lib.GcnArgs(rows=rows, n=N, c=cfg.D, c_out=C, nsup=cfg.nsup if cfg.use_gcn else 0,
                               sup=ctypes.cast(sup_arr, ctypes.POINTER(ctypes.c_void_p)), ld_sup=cfg.NP,
@@ -998,6 +1006,10 @@ class Executor:
         # (fp32 mode; the bf16 mode's tiled-operand gram stays per layer)
         gram_group = (defer and "tt_l" in sc and cfg.adp_live and not getattr(acts, "gram_g4", False)
                       and getattr(acts, "g4bt_arr", None) is None and L >= 2)
+        # the bf16 mode's counterpart on the tiled operands (each layer's t1 / t2 in acts.TG4[i])
+        gram_g4_group = (defer and getattr(acts, "gram_g4", False) and cfg.adp_live and L >= 2
+                         and getattr(acts, "ws_g4g", None) is not None and acts.ws_g4g is not False
+                         and len(acts.TG4) == L - 1)
         main = torch.cuda.current_stream()
         side = self._side_stream() if overlap else None
 
@@ -1094,8 +1106,8 @@ class Executor:
                                      sup_g4_t=self._arr_field(getattr(acts, "g4b_arr", None))
                                      if os.environ.get("GWN_GCN_POW_BWD", "1") != "0" else None,
                                      sup_g4b_t=self._arr_field(getattr(acts, "g4bt_arr", None)),
-                                     tg4=ptr(sc["tg4"]) if (defer and getattr(acts, "gram_g4", False)
-                                                            and adp_index >= 0) else None,
+                                     tg4=(ptr(acts.TG4[i]) if gram_g4_group else ptr(sc["tg4"]))
+                                     if (defer and getattr(acts, "gram_g4", False) and adp_index >= 0) else None,
                                      **self.ksplit_fields(sc))
                 sb = getattr(acts, "sup_batch", 1)
                 if sb > 1:
@@ -1117,7 +1129,7 @@ class Executor:
                 if defer:
                     if not grouped:
                         self._defer_gcn_grads(acts, i, rows, dh, sc, segs, st)
-                    if adp_index >= 0 and not gram_group:  # issued after the layer's TCN backward (below)
+                    if adp_index >= 0 and not (gram_group or gram_g4_group):  # after the layer's TCN backward
                         gram_now = (dhc, first_adp)
                 if adp_index >= 0:
                     first_adp = False
@@ -1178,6 +1190,15 @@ class Executor:
                                           slices=ts[i + 1] * P // N))
             lib.call("gwn_gram_group", (_lib.GramLayer * len(lay))(*lay), len(lay), cfg.W, 3 * C, N, ptr(sc["dadp"]),
                      cfg.NP, 0, ptr(sc["ws_gram_group"]), st)
+        if gram_g4_group:
+            lay = []
+            for i in range(L - 1):
+                S = ts[i + 1] * P // N
+                half = S * ((N + 15) // 16) * 1024  # bytes of one bf16 operand
+                x, t = acts.XG4[i].data_ptr(), acts.TG4[i].data_ptr()
+                lay.append(_lib.GramLayer(x1=x, t1=t, x2=x + half, t2=t + half, slices=S))
+            lib.call("gwn_gram_g4_group", (_lib.GramLayer * len(lay))(*lay), len(lay), N, ptr(sc["dadp"]), cfg.NP, 0,
+                     ptr(acts.ws_g4g), st)
         if defer:
             for k in range(0, len(segs), 32):  # <= 32 segments per launch (include/gwn.h)
                 chunk = segs[k:k + 32]

@@ -522,6 +522,15 @@ long gwn_gram_workspace_floats(int n, int slices);
 int gwn_gram_g4_bf16(const void* x1, const void* t1, const void* x2, const void* t2, int n, int slices,
                      float* dA, int ld_dA, int accumulate, float* ws, hipStream_t stream);
 long gwn_gram_g4_workspace_floats(int n, int slices);
+/* gwn_gram_g4_bf16 of up to 8 layers in ONE launch (+ one reduction): each gwn_gram_layer's x1 / t1
+ * point to that layer's bf16 tiled buffers (the pointer type is nominal here), x2 / t2 must be
+ * x1 / t1 + slices*ceil(n/16) KiB (the xg4 / tg4 layout).  One workgroup pair per two CUs splits
+ * the output rows, each walking an equal share of every layer's (slice, pair) steps with the
+ * operands staged once per step in LDS.  Workspace: gwn_gram_g4_group_workspace_floats floats
+ * (0: n > 368, not supported -- use gwn_gram_g4_bf16 per layer). */
+long gwn_gram_g4_group_workspace_floats(int n, const int* slices, int nlayers);
+int gwn_gram_g4_group(const gwn_gram_layer* layers, int nlayers, int n, float* dA, int ld_dA, int accumulate,
+                      float* workspace, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * BatchNorm2d (model.py:236, bn = nn.BatchNorm2d(c) model.py:152) over the rows of z [rows][c].

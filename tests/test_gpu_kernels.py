@@ -948,6 +948,50 @@ def test_gram_g4_vs_fp64(gpu, n, slices, pairs, accumulate):
     assert torch.equal(dA.cpu()[:, n:], init.float()[:, n:])
 
 
+@pytest.mark.parametrize("n,slices", [(325, [36, 30, 9, 3]), (207, [48, 7]), (16, [5, 1, 2]), (33, [1])])
+@pytest.mark.parametrize("accumulate", [0, 1])
+def test_gram_g4_group_vs_fp64(gpu, n, slices, accumulate):
+    """gwn_gram_g4_group (the bf16 mode's adaptive-support gram of several layers in one launch: two
+    half-output workgroups per CU pair, each over an equal share of every layer's (slice, pair)
+    steps) against an fp64 einsum of the bf16-rounded operands, both pairs per layer in the xg4 /
+    tg4 layout (x2 / t2 right after x1 / t1); odd tile counts, a single slice.  Bound: the fp32
+    accumulation chain, as test_gram_g4_vs_fp64."""
+    from gwn_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(n + sum(slices))
+    ref = torch.zeros(n, n, dtype=torch.float64)
+    absb = torch.zeros(n, n, dtype=torch.float64)
+    bufs, lays = [], []
+    for S in slices:
+        X = [torch.randn(S * n, 32, dtype=torch.float64).bfloat16().double() for _ in range(2)]
+        T = [torch.randn(S * n, 32, dtype=torch.float64).bfloat16().double() for _ in range(2)]
+        for p in range(2):
+            xs, ts = X[p].reshape(S, n, 32), T[p].reshape(S, n, 32)
+            ref += torch.einsum("svc,swc->vw", xs, ts)
+            absb += torch.einsum("svc,swc->vw", xs.abs(), ts.abs())
+        xb = torch.cat([_to_g4(x.float(), S, n) for x in X]).to(gpu)
+        tb = torch.cat([_to_g4(t.float(), S, n) for t in T]).to(gpu)
+        half = S * ((n + 15) // 16) * 1024
+        bufs += [xb, tb]
+        lays.append(_lib.GramLayer(x1=xb.data_ptr(), t1=tb.data_ptr(), x2=xb.data_ptr() + half,
+                                   t2=tb.data_ptr() + half, slices=S))
+    ldA = n + 3
+    init = torch.randn(n, ldA, dtype=torch.float64)
+    dA = init.float().to(gpu)
+    if accumulate:
+        ref = ref + init[:, :n].float().double()
+        absb = absb + init[:, :n].abs()
+    sl = (ctypes.c_int * len(slices))(*slices)
+    ws = torch.empty(lib.gwn_gram_g4_group_workspace_floats(n, sl, len(slices)) + 16, device=gpu)
+    _lib.call("gwn_gram_g4_group", (_lib.GramLayer * len(lays))(*lays), len(lays), n, dA.data_ptr(), ldA,
+              accumulate, ws.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    got = dA.double().cpu()[:, :n]
+    bound = 2.0 ** -22 * (sum(slices) * 32 * 2 + 8) * absb
+    assert torch.all((got - ref).abs() <= bound + 1e-30), float(((got - ref).abs() / (bound + 1e-30)).max())
+    assert torch.equal(dA.cpu()[:, n:], init.float()[:, n:])
+
+
 def test_nconv2_vs_reference_golden(gpu):
     """nconv2 (model.py:16-22, per-sample supports) on the batched MFMA GEMM against the reference's
     own output and fp64 autograd gradients (tests/golden/make_golden_nconv2.py).  fp32 MFMA chain
