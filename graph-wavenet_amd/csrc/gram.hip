@@ -482,6 +482,10 @@ int gram_group_plan(int n, const int* slices, int nlayers, int* nsp) {
 // block (gram_kernel: ~2.2 GB of fragment traffic per METR step).  The K permutation of
 // gram_kernel: lane group q takes channels 8q .. 8q+7 (two ds_read_b128 per operand and tile), the
 // same on both operands.  Partials [CU][np16][np16], summed in a fixed order by gram_reduce_kernel.
+#ifndef GWN_GRAM_CU_DMA
+#define GWN_GRAM_CU_DMA 0  // 1: gram_cu_kernel stages by LDS-DMA (measured 211 vs 170 us with paired tiles)
+#endif
+constexpr bool GRAM_CU_DMA = GWN_GRAM_CU_DMA != 0;
 constexpr int GCU_LDR = 36;  // LDS row stride (floats): the 16 rows of a ds_read_b128 pass on distinct banks
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 constexpr int GCG_NB = 4;  // LDS step buffers: three steps' operands in flight
@@ -539,22 +543,62 @@ __global__ __launch_bounds__(1024) void gram_cu_kernel(const GramCu g) {
       }
     }
   };
+  // GWN_GRAM_CU_DMA: the step's rows by 16-B LDS-DMA loads instead (no staging registers),
+  // unpadded 128-B rows with 16-B chunk c of row r at position c ^ ((r >> 1) & 7) (conflict-free
+  // fragment reads); every wave issues the same count per step (padding loads into a sink)
+  const int opb = rows * 32, ninst = rows / 4, G = (ninst + 15) / 16;
+  auto issue = [&](int st, int b) {
+    int L = 0;
+    while (L + 1 < g.nlayers && st >= g.lsteps0[L + 1]) ++L;
+    const int ls = st - g.lsteps0[L], sl = ls >> 1, p = ls & 1;
+    const long base = (long)sl * g.n;
+    const __amdgpu_buffer_rsrc_t rx = rsrc(g.X[L][p] + base * g.ldx, (long)g.n * g.ldx * 4);
+    const __amdgpu_buffer_rsrc_t rt = rsrc(g.T[L][p] + base * g.ldt, (long)g.n * g.ldt * 4);
+    const int wv = __builtin_amdgcn_readfirstlane(wave), lr = lane >> 3, pos = lane & 7;
+    for (int k = 0; k < G; ++k) {
+      const int m = wv + 16 * k;
+      const bool isx = m < rows / 8;
+      const int r = (isx ? m : m - rows / 8) * 8 + lr, c = pos ^ ((r >> 1) & 7);
+      float* dst = m < ninst ? lds + b * 2 * opb + m * 256 : lds + 2 * 2 * opb;
+      const bool ok = m < ninst && r < g.n;
+      if (isx)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)dst, 16, ok ? (int)((r * g.ldx + 4 * c) * 4) : OOR, 0, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_ptr_t)dst, 16, ok ? (int)((r * g.ldt + 4 * c) * 4) : OOR, 0, 0, 0);
+    }
+  };
   auto frag = [&](const float* img, int t16, float4* f) {
+    if (GRAM_CU_DMA) {
+      const int r = 16 * t16 + i, sw = (r >> 1) & 7;
+      f[0] = *(const float4*)(img + r * 32 + 4 * ((2 * q) ^ sw));
+      f[1] = *(const float4*)(img + r * 32 + 4 * ((2 * q + 1) ^ sw));
+      return;
+    }
     const float* r = img + (16 * t16 + i) * GCU_LDR + 8 * q;
     f[0] = *(const float4*)r;
     f[1] = *(const float4*)(r + 4);
   };
-  if (st0 < st1) {
-    stage_load(st0);
-    stage_store(0);
+  if (GRAM_CU_DMA) {
+    if (st0 < st1) issue(st0, 0);
+  } else {
+    if (st0 < st1) {
+      stage_load(st0);
+      stage_store(0);
+    }
+    __syncthreads();
   }
-  __syncthreads();
   int buf = 0;
   for (int st = st0; st < st1; ++st) {
     const bool more = st + 1 < st1;
-    if (more) stage_load(st + 1);
-    const float* xi = lds + buf * 2 * opf;
-    const float* ti_ = xi + opf;
+    if (GRAM_CU_DMA) {
+      GCG_WAIT_VM(0);
+      __builtin_amdgcn_s_barrier();
+      if (more) issue(st + 1, buf ^ 1);
+    } else if (more) {
+      stage_load(st + 1);
+    }
+    const float* xi = lds + buf * 2 * (GRAM_CU_DMA ? opb : opf);
+    const float* ti_ = xi + (GRAM_CU_DMA ? opb : opf);
     // (the 16 waves of the CU hide the LDS latency: no in-wave prefetch, which would cost 8 of the
     // registers the accumulators need)
 #pragma unroll
@@ -570,8 +614,10 @@ __global__ __launch_bounds__(1024) void gram_cu_kernel(const GramCu g) {
         for (int kk = 0; kk < 8; ++kk) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc[u], 0, 0, 0);
       }
     }
-    if (more) stage_store(buf ^ 1);
-    __syncthreads();
+    if (!GRAM_CU_DMA) {
+      if (more) stage_store(buf ^ 1);
+      __syncthreads();
+    }
     buf ^= 1;
   }
   // D[v][w]: lane (q, i) holds rows 16 ti + 4 q + r, column 16 tj + i
@@ -691,7 +737,10 @@ bool gram_cu_ok(int n) {
   if (e && e[0] == '0') return false;
   return n <= 256;
 }
-size_t gram_cu_lds(int n) { return (size_t)2 * 2 * 16 * ((n + 15) / 16) * GCU_LDR * sizeof(float); }
+size_t gram_cu_lds(int n) {
+  return GRAM_CU_DMA ? (size_t)(2 * 2 * 16 * ((n + 15) / 16) * 32 + 256) * sizeof(float)  // + the sink
+                     : (size_t)2 * 2 * 16 * ((n + 15) / 16) * GCU_LDR * sizeof(float);
+}
 }  // namespace
 
 long gwn_gram_group_workspace_floats(int n, const int* slices, int nlayers) {

@@ -246,10 +246,17 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
   }
 }
 
+// waves per CU of the gated TCN forward (GWN_ROWGEMM_GATE_WPC, default 8; its 168 registers allow 12)
+inline int gate_wpc() {
+  const char* e = getenv("GWN_ROWGEMM_GATE_WPC");
+  const int v = e ? atoi(e) : 8;
+  return v >= 4 && v <= 12 ? v : 8;
+}
+
 inline int rowgemm_grid(int M, int ntiles, bool gate) {
   const int nchunks = (M + 31) / 32;
   int waves = nchunks * (gate ? 1 : ntiles);
-  const int cap = 256 * 8;
+  const int cap = 256 * (gate ? gate_wpc() : 8);
   if (waves > cap) waves = cap;
   return (waves + 3) / 4;  // 4 | 4*grid, so every tile gets grid*4/ntiles waves
 }
