@@ -1081,6 +1081,15 @@ __host__ __device__ inline int t16_img_rows(int n) {
 // Slice image in LDS: two channel halves, each [rows][16] (no padding): lane (g, j) of the
 // diffusion's A-operand read (row 4 ks + g, channel 16 hf + j) hits bank 16 g + j of 64.  The
 // half stride hs = rows * 16 floats is a multiple of 64 (ds_read2st64 pairs the two halves).
+// the t16 kernels' 16-B output stores (z, dres / dh_out, dxg / t1 / t2, dfg): non-temporal by
+// plain by default (-DGWN_T16_NT=1: non-temporal)
+#ifndef GWN_T16_NT
+#define GWN_T16_NT 0  // measured: non-temporal 24.64k / 23.54k vs plain 24.79k / 23.67k samples/s (METR / PEMS)
+#endif
+__device__ __forceinline__ void t16_st4(float* p, float4 v) {
+  if (GWN_T16_NT) __builtin_nontemporal_store(f32x4v{v.x, v.y, v.z, v.w}, (f32x4v*)p);
+  else *(float4*)p = v;
+}
 constexpr int LDW16 = 36;  // LDS row stride of the staged channel maps: lane groups g hit banks 16 g + j
 
 // LDS of a t16 workgroup: the channel maps of all 2K+1 pieces (32 x LDW16 floats each), the waves'
@@ -1246,7 +1255,7 @@ __device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* ha
                             (1.0f / sqrtf(((const float*)&rvv)[e] + a.bn_eps)) * ((const float*)&gq)[e] +
                         ((const float*)&bb)[e];
     }
-    if (valid) *(float4*)(dst + m * CH + c0) = make_float4(v[4 * oh], v[4 * oh + 1], v[4 * oh + 2], v[4 * oh + 3]);
+    if (valid) t16_st4(dst + m * CH + c0, make_float4(v[4 * oh], v[4 * oh + 1], v[4 * oh + 2], v[4 * oh + 3]));
   }
   if (a.bn_part == nullptr || a.x_out) return;
   const float cnt = (float)min(16, n - w0);
@@ -1920,8 +1929,8 @@ __device__ __forceinline__ void t16_bwd_stage(const FusedBwd& a, float* imgs, in
         const long sb = (long)(s0 + sl) * nt;
         const long t0 = max(rg.tb - sb, 0l), t1 = min(rg.te - sb, (long)nt);
         if (w >= 16 * t0 && w < 16 * t1) {
-          *(float4*)(a.dres + row * CH + 4 * q) = make_float4(dz[0], dz[1], dz[2], dz[3]);
-          *(float4*)(a.dh_out + row * CH + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
+          t16_st4(a.dres + row * CH + 4 * q, make_float4(dz[0], dz[1], dz[2], dz[3]));
+          t16_st4(a.dh_out + row * CH + 4 * q, make_float4(v[0], v[1], v[2], v[3]));
         }
       }
       t16_bwd_put<BF>(imgs + sl * imgf, rows, w, q, make_float4(v[0], v[1], v[2], v[3]));
@@ -1936,7 +1945,7 @@ __device__ __forceinline__ void t16_store(float* out, long ld, const f32x4v* acc
   if (w0 + j >= n) return;
   float* p = out + (long)(w0 + j) * ld + 4 * g;
 #pragma unroll
-  for (int oh = 0; oh < 2; ++oh) *(float4*)(p + 16 * oh) = make_float4(acc[oh][0], acc[oh][1], acc[oh][2], acc[oh][3]);
+  for (int oh = 0; oh < 2; ++oh) t16_st4(p + 16 * oh, make_float4(acc[oh][0], acc[oh][1], acc[oh][2], acc[oh][3]));
 }
 
 // BF: bf16 operands in the diffusion (the bf16 forward's image / support layouts: sup_g4b_t), the
@@ -2032,8 +2041,8 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
           o[2 * e2] = gv * sg * (1.0f - f * f);
           o[2 * e2 + 1] = gv * f * sg * (1.0f - sg);
         }
-        *(float4*)(a.dfg + m * 2 * CH + 2 * c0) = make_float4(o[0], o[1], o[2], o[3]);
-        *(float4*)(a.dfg + m * 2 * CH + 2 * c0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+        t16_st4(a.dfg + m * 2 * CH + 2 * c0, make_float4(o[0], o[1], o[2], o[3]));
+        t16_st4(a.dfg + m * 2 * CH + 2 * c0 + 4, make_float4(o[4], o[5], o[6], o[7]));
       }
     }
     p0 = p1;
