@@ -1081,8 +1081,8 @@ __host__ __device__ inline int t16_img_rows(int n) {
 // Slice image in LDS: two channel halves, each [rows][16] (no padding): lane (g, j) of the
 // diffusion's A-operand read (row 4 ks + g, channel 16 hf + j) hits bank 16 g + j of 64.  The
 // half stride hs = rows * 16 floats is a multiple of 64 (ds_read2st64 pairs the two halves).
-// the t16 kernels' 16-B output stores (z, dres / dh_out, dxg / t1 / t2, dfg): non-temporal by
-// plain by default (-DGWN_T16_NT=1: non-temporal)
+// the t16 kernels' 16-B output stores (z, dres / dh_out, dxg / t1 / t2, dfg): plain by default
+// (-DGWN_T16_NT=1: non-temporal)
 #ifndef GWN_T16_NT
 #define GWN_T16_NT 0  // measured: non-temporal 24.64k / 23.54k vs plain 24.79k / 23.67k samples/s (METR / PEMS)
 #endif
