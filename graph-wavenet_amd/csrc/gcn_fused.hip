@@ -1698,6 +1698,47 @@ __device__ __forceinline__ void put_bf16_cm(__bf16* img, int s16, int w, int q, 
   img[(4 * q + 3) * s16 + w] = (__bf16)x.w;
 }
 
+typedef __bf16 bf16x8s __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4s __attribute__((ext_vector_type(4)));
+
+// A phase's channel-major bf16 images (nsl slices, imgb bf16 apart, rows = s16 - 8 >= n, rows >= n
+// zero) from fp32 rows (src: slice 0's row 0, slice stride n * ld floats, 16-B aligned, ld % 4 ==
+// 0): work unit = (slice, 8 consecutive nodes, channel quad q), 8 row loads of 16 B (the 8 lanes of
+// a node octet cover a whole 128-B row) then one 16-B LDS write per channel (8 nodes' bf16) --
+// instead of one 2-B write per element (put_bf16_cm).  mid() runs with round 0's loads in flight.
+template <typename Mid>
+__device__ __forceinline__ void stage_bf16_octets(const float* src, long ld, int n, int s16, int nsl, __bf16* imgs,
+                                                  int imgb, Mid mid) {
+  const int rows = s16 - 8, per = rows, total = nsl * per;  // units per slice = (rows / 8) * 8
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((long)nsl * n * ld * 4), 0x00020000);
+  bool first = true;
+  for (int u = threadIdx.x; u < total || first; u += blockDim.x) {
+    const bool ok = u < total;
+    const int sl = ok ? u / per : 0, rem = u - sl * per, k = rem >> 3, q = rem & 7;
+    float4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int w = 8 * k + i;
+      const int off = (ok && w < n) ? (int)((((long)sl * n + w) * ld + 4 * q) * 4) : 0x7ffffff0;
+      v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    }
+    if (first) {
+      mid();
+      first = false;
+    }
+    if (!ok) continue;
+    __bf16* img = imgs + (long)sl * imgb + 8 * k;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bf16x8s o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (__bf16)((const float*)&v[i])[e];
+      *(bf16x8s*)(img + (4 * q + e) * s16) = o;
+    }
+  }
+}
+
 // a slice's node features (rows >= n zero) -> the channel-major bf16 image [32][s16]
 __device__ __forceinline__ void global_to_lds16_bf16(const float* src, long ld, int n, __bf16* img) {
   const int s16 = t16b_s16(n), rows = s16 - 8;
@@ -1783,12 +1824,9 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
     if (p0 != rg.tb) __syncthreads();  // the previous phase's images are released
     if (h16) {  // as the f32 kernel: the phase in one pass, the maps inside its first round trip
       const bool maps = p0 == rg.tb;
-      stage_rows4<8>(
-          a.h + (long)s0 * n * ldh, ldh, n, s16 - 8, s1 - s0 + 1,
-          [&](int sl, int w, int q, float4 x) { put_bf16_cm(imgs + sl * imgb, s16, w, q, x); },
-          [&] {
-            if (maps) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
-          });
+      stage_bf16_octets(a.h + (long)s0 * n * ldh, ldh, n, s16, s1 - s0 + 1, imgs, imgb, [&] {
+        if (maps) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
+      });
     } else {
       for (int sl = s0; sl <= s1; ++sl) global_to_lds16_bf16(a.h + (long)sl * n * ldh, ldh, n, imgs + (sl - s0) * imgb);
     }
@@ -1860,6 +1898,87 @@ __device__ __forceinline__ void t16_bwd_put(float* img, int rows, int w, int q, 
   else *(float4*)(img + (q >> 2) * rows * 16 + w * 16 + 4 * (q & 3)) = x;
 }
 
+// t16_bwd_stage's BatchNorm prologue into the bf16 channel-major images: work unit = (slice, 4
+// consecutive nodes, channel quad), 4 dy / z row loads of 16 B, then dres / dh_out (the
+// workgroup's own rows) as 16-B stores and one 8-B LDS write per channel (4 nodes' bf16)
+template <typename Mid>
+__device__ __forceinline__ void t16_bwd_stage_bn_bf16(const FusedBwd& a, __bf16* imgs, int imgb, int s0, int nsl,
+                                                      const T16Range& rg, int nt, int n, int s16, Mid mid) {
+  const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
+  const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  const int q = threadIdx.x & 7;  // blockDim % 8 == 0: every unit of a thread has channel quad q
+  float mu[4], rs[4], gm[4], k1[4], k2[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = 4 * q + e;
+    mu[e] = a.bn_mean[c]; rs[e] = a.bn_rstd[c]; gm[e] = a.bn_gamma[c];
+    k1[e] = a.bn_sums[c] * a.inv_rows; k2[e] = a.bn_sums[CH + c] * a.inv_rows;
+  }
+  const long base = (long)s0 * n * CH;
+  const int bytes = (int)((long)nsl * n * CH * 4);
+  const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc((void*)(a.bn_dy + base), (short)0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)(a.bn_z + base), (short)0, bytes, 0x00020000);
+  const int rows = s16 - 8, per = 2 * rows, total = nsl * per;  // units per slice = (rows / 4) * 8
+  bool first = true;
+  for (int u = threadIdx.x; u < total || first; u += blockDim.x) {
+    const bool ok = u < total;
+    const int sl = ok ? u / per : 0, rem = u - sl * per, k = rem >> 3;  // nodes 4k .. 4k + 3
+    float4 dy[4], zv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int w = 4 * k + i;
+      const int off = (ok && w < n) ? ((sl * n + w) * CH + 4 * q) * 4 : 0x7ffffff0;
+      dy[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rdy, off, 0, 0));
+      zv[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rz, off, 0, 0));
+    }
+    if (first) {
+      mid();
+      first = false;
+    }
+    if (!ok) continue;
+    const long sb = (long)(s0 + sl) * nt;
+    const long t0 = max(rg.tb - sb, 0l), t1 = min(rg.te - sb, (long)nt);
+    float v[4][4];  // [node][channel]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int w = 4 * k + i;
+      const float dyv[4] = {dy[i].x, dy[i].y, dy[i].z, dy[i].w}, zz[4] = {zv[i].x, zv[i].y, zv[i].z, zv[i].w};
+      float dz[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float xhat = (zz[c] - mu[c]) * rs[c];
+        dz[c] = gm[c] * rs[c] * (dyv[c] - k1[c] - xhat * k2[c]);
+        v[i][c] = dz[c];
+      }
+      if (w < n) {
+        const long row = (long)(s0 + sl) * n + w;
+        if (a.drop_p > 0.0f) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float uu = gwn_uniform(seed, a.salt, (unsigned long long)(row * CH + 4 * q + c));
+            v[i][c] = (uu >= a.drop_p) ? v[i][c] * keep_scale : 0.0f;
+          }
+        }
+        if (w >= 16 * t0 && w < 16 * t1) {
+          t16_st4(a.dres + row * CH + 4 * q, make_float4(dz[0], dz[1], dz[2], dz[3]));
+          t16_st4(a.dh_out + row * CH + 4 * q, make_float4(v[i][0], v[i][1], v[i][2], v[i][3]));
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[i][c] = 0.0f;
+      }
+    }
+    __bf16* img = imgs + (long)sl * imgb + 4 * k;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      bf16x4s o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = (__bf16)v[i][c];
+      *(bf16x4s*)(img + (4 * q + c) * s16) = o;
+    }
+  }
+}
+
 // A phase's dh images (slices s0 .. s0 + nsl - 1, imgf floats apart): dh itself, or with the
 // BatchNorm-backward prologue dz = gamma*rstd*(dy - k1 - xhat*k2), dh = dropout'(dz), dres / dh_out
 // written for the workgroup's own rows (its tiles [rg.tb, rg.te)).  Whole phase in rounds of U
@@ -1870,8 +1989,14 @@ template <bool BF, typename Mid>
 __device__ __forceinline__ void t16_bwd_stage(const FusedBwd& a, float* imgs, int imgf, int s0, int nsl,
                                               const T16Range& rg, int nt, int n, int rows, Mid mid) {
   if (!a.bn_dy) {
-    stage_rows4<8>(a.dh + (long)s0 * n * CH, CH, n, rows, nsl,
-                   [&](int sl, int w, int q, float4 x) { t16_bwd_put<BF>(imgs + sl * imgf, rows, w, q, x); }, mid);
+    if (BF) stage_bf16_octets(a.dh + (long)s0 * n * CH, CH, n, rows + 8, nsl, (__bf16*)imgs, 2 * imgf, mid);
+    else
+      stage_rows4<8>(a.dh + (long)s0 * n * CH, CH, n, rows, nsl,
+                     [&](int sl, int w, int q, float4 x) { t16_bwd_put<BF>(imgs + sl * imgf, rows, w, q, x); }, mid);
+    return;
+  }
+  if (BF) {
+    t16_bwd_stage_bn_bf16(a, (__bf16*)imgs, 2 * imgf, s0, nsl, rg, nt, n, rows + 8, mid);
     return;
   }
   constexpr int U = 4;
