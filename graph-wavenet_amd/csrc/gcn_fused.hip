@@ -1069,6 +1069,14 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int T16_RING = 4;   // k-steps (4 support rows each) of support fragments in flight
 constexpr int T16_WAVES = 16; // waves of a t16 workgroup (one workgroup per CU, persistent over a tile range)
 constexpr int T16_MAXIMG = 4; // slice images a workgroup holds at once (LDS permitting)
+// Tile order within a phase: slice-major (wave w takes every 16th tile).  GWN_T16_COLMAJOR=1:
+// column-major (a node-tile column of every staged slice, slice fastest), so that the waves of
+// consecutive indices -- one per SIMD -- diffuse the same support column at once and share its
+// fragment loads in L1: measured slower (the fragment traffic from L2 is not what bounds it).
+#ifndef GWN_T16_COLMAJOR
+#define GWN_T16_COLMAJOR 0  // measured slower: METR 23.98k vs 24.99k, PEMS 22.95k vs 23.89k samples/s
+#endif
+constexpr bool T16_COLMAJOR = GWN_T16_COLMAJOR != 0;
 
 // rows of a slice image: the tiles' rows, and the diffusion loop's reads (4 rows per k-step, one
 // k-step ahead, whole rings of T16_RING k-steps); rows >= n are zero
@@ -1628,7 +1636,17 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
     }
     __syncthreads();
     if (threadIdx.x == 0 && p0 == rg.tb) T16_TS(a, 1);
-    for (long t = p0 + ((wave - p0 % nwaves) + nwaves) % nwaves; t < p1; t += nwaves) {
+    const int nsl = s1 - s0 + 1;
+    const int span = T16_COLMAJOR ? nt * nsl : (int)(p1 - p0);
+    for (int tp = wave; tp < span; tp += nwaves) {
+      long t;
+      if (T16_COLMAJOR) {  // column tp / nsl of slice s0 + tp % nsl
+        const int c = tp / nsl;
+        t = (long)(s0 + tp - c * nsl) * nt + c;
+        if (t < p0 || t >= p1) continue;
+      } else {
+        t = p0 + tp;
+      }
       const int s = (int)(t / nt), tile = (int)(t - (long)s * nt);
       const float* xs = imgs + (s - s0) * imgf;
       const long row0 = (long)s * n;
@@ -1831,7 +1849,17 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
       for (int sl = s0; sl <= s1; ++sl) global_to_lds16_bf16(a.h + (long)sl * n * ldh, ldh, n, imgs + (sl - s0) * imgb);
     }
     __syncthreads();
-    for (long t = p0 + ((wave - p0 % nwaves) + nwaves) % nwaves; t < p1; t += nwaves) {
+    const int nsl = s1 - s0 + 1;
+    const int span = T16_COLMAJOR ? nt * nsl : (int)(p1 - p0);
+    for (int tp = wave; tp < span; tp += nwaves) {
+      long t;
+      if (T16_COLMAJOR) {  // column tp / nsl of slice s0 + tp % nsl
+        const int c = tp / nsl;
+        t = (long)(s0 + tp - c * nsl) * nt + c;
+        if (t < p0 || t >= p1) continue;
+      } else {
+        t = p0 + tp;
+      }
       const int sl = (int)(t / nt), tile = (int)(t - (long)sl * nt);
       const __bf16* xs = imgs + (sl - s0) * imgb;
       const long row0 = (long)sl * n;
@@ -2103,7 +2131,17 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
       if (maps) t16_stage_maps(a.w_mlp, a.ld_w, true, 2 * a.nsup + 1, ws);
     });
     __syncthreads();
-    for (long t = p0 + ((wave - p0 % nwaves) + nwaves) % nwaves; t < p1; t += nwaves) {
+    const int nsl = s1 - s0 + 1;
+    const int span = T16_COLMAJOR ? nt * nsl : (int)(p1 - p0);
+    for (int tp = wave; tp < span; tp += nwaves) {
+      long t;
+      if (T16_COLMAJOR) {  // column tp / nsl of slice s0 + tp % nsl
+        const int c = tp / nsl;
+        t = (long)(s0 + tp - c * nsl) * nt + c;
+        if (t < p0 || t >= p1) continue;
+      } else {
+        t = p0 + tp;
+      }
       const int s = (int)(t / nt), tile = (int)(t - (long)s * nt);
       const float* dhs = imgs + (s - s0) * imgf;
       const long row0 = (long)s * n;
