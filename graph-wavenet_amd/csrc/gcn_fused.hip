@@ -1214,9 +1214,30 @@ __device__ __forceinline__ float row16_sum(float x) {
 
 // A wave's running BatchNorm partial over its tiles (Chan merge in tile order): lane (g, j) keeps
 // the 8 channels 16 (q >> 2) + 4 g + (q & 3) of its row group (lane j = 0 of a group is the one read)
+// GWN_T16_BN_LDS=1: the running partials live in the wave's BN slot of LDS (the flush's wpart
+// layout, updated by lane j == 0 of each row group) instead of 16 registers per lane (off: no gain)
+#ifndef GWN_T16_BN_LDS
+#define GWN_T16_BN_LDS 0  // 1: PEMS 23.79k vs 23.89k, METR equal (the freed registers buy nothing)
+#endif
+constexpr bool T16_BN_LDS = GWN_T16_BN_LDS != 0;
 struct BnRun {
-  float n, mean[8], m2[8];
+  float n, mean[T16_BN_LDS ? 1 : 8], m2[T16_BN_LDS ? 1 : 8];
+  float* wp;  // T16_BN_LDS: this wave's [3][32] slot of wpart (n, mean, M2 per channel)
 };
+// zero state; T16_BN_LDS: the wave clears its own slot (read back only by its own lanes before the
+// flush's barrier)
+__device__ __forceinline__ void bn_init(BnRun& bn, float* wpart) {
+  bn.n = 0.0f;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  bn.wp = wpart + wave * 3 * 32;
+  if (T16_BN_LDS) {
+    bn.wp[lane] = 0.0f;
+    if (lane < 32) bn.wp[64 + lane] = 0.0f;
+  } else {
+#pragma unroll
+    for (int q = 0; q < (T16_BN_LDS ? 1 : 8); ++q) bn.mean[q] = bn.m2[q] = 0.0f;
+  }
+}
 
 // z tile epilogue (fwd_tile_epilogue's arithmetic on the 16-node tile layout): bias, dropout,
 // residual (BN of the layer below applied on load), z or eval-BN output store; the tile's BN
@@ -1269,8 +1290,30 @@ __device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* ha
   const float cnt = (float)min(16, n - w0);
   const float inv = 1.0f / cnt;
   const float tot = bn.n + cnt;
+  if (T16_BN_LDS) {
+    float mq[8], qq[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < 8; ++q) {
+      mq[q] = row16_sum(valid ? v[q] : 0.0f) * inv;
+      const float d = valid ? v[q] - mq[q] : 0.0f;
+      qq[q] = row16_sum(d * d);
+    }
+    if (j == 0) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int c = 16 * (q >> 2) + 4 * g + (q & 3);
+        const float om = bn.wp[CH + c], o2 = bn.wp[2 * CH + c];
+        const float dm = mq[q] - om;
+        bn.wp[CH + c] = om + dm * (cnt / tot);
+        bn.wp[2 * CH + c] = o2 + qq[q] + dm * dm * (bn.n * cnt / tot);
+        bn.wp[c] = tot;
+      }
+    }
+    bn.n = tot;
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < (T16_BN_LDS ? 1 : 8); ++q) {
     const float mean = row16_sum(valid ? v[q] : 0.0f) * inv;
     const float d = valid ? v[q] - mean : 0.0f;
     const float m2 = row16_sum(d * d);
@@ -1313,10 +1356,10 @@ __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn,
     }
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
-  if (j == 0) {
+  if (!T16_BN_LDS && j == 0) {  // (T16_BN_LDS: the slots already hold the running partials)
     float* wp = wpart + wave * 3 * CH;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < (T16_BN_LDS ? 1 : 8); ++q) {
       const int c = 16 * (q >> 2) + 4 * g + (q & 3);
       wp[c] = bn.n;
       wp[CH + c] = bn.mean[q];
@@ -1611,9 +1654,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   const T16Range rg = t16_range(a.slices, nt);
   if (threadIdx.x == 0) T16_TS(a, 0);
   BnRun bn;
-  bn.n = 0.0f;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) bn.mean[q] = bn.m2[q] = 0.0f;
+  bn_init(bn, wpart);
   // the phase's slices staged in one pass (stage_rows4; the channel maps inside its first round
   // trip), else slice by slice
   const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
@@ -1771,6 +1812,10 @@ __device__ __forceinline__ void global_to_lds16_bf16(const float* src, long ld, 
   }
 }
 
+#ifndef GWN_T16B_AHEAD
+#define GWN_T16B_AHEAD 1  // 2: PEMS 23.65k vs 23.79k samples/s (not latency-bound on the fragments)
+#endif
+constexpr int T16B_AHEAD = GWN_T16B_AHEAD;  // support-fragment groups in flight ahead (1 or 2)
 // both powers of one support on bf16 operands (acc as t16_diffuse); G1 / G2: gwn_support_g4_bf16
 // copies (block (kg, tile) = 64 lanes x 8 bf16)
 __device__ __forceinline__ void t16b_diffuse(const __bf16* img, const __bf16* G1, const __bf16* G2, int n, int tile,
@@ -1785,21 +1830,28 @@ __device__ __forceinline__ void t16b_diffuse(const __bf16* img, const __bf16* G1
   const __bf16* x1 = img + (16 + j) * s16 + 8 * g;  // channel 16 + j (half 1)
 #pragma unroll
   for (int q = 0; q < 2; ++q) acc[q][0] = acc[q][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-  bf16x8b b1 = __builtin_bit_cast(bf16x8b, __builtin_amdgcn_raw_buffer_load_b128(r1, off(0), 0, 0));
-  bf16x8b b2 = __builtin_bit_cast(bf16x8b, __builtin_amdgcn_raw_buffer_load_b128(r2, off(0), 0, 0));
+  // support fragments T16B_AHEAD groups ahead (a group is only 4 MFMAs: one group ahead left the
+  // L2 latency exposed); past the last group the offsets leave the range: zeros, no traffic
+  auto ld = [&](const __amdgpu_buffer_rsrc_t& r, int kg) {
+    return __builtin_bit_cast(bf16x8b, __builtin_amdgcn_raw_buffer_load_b128(r, off(kg), 0, 0));
+  };
+  bf16x8b b1 = ld(r1, 0), b2 = ld(r2, 0);
+  bf16x8b c1 = T16B_AHEAD > 1 ? ld(r1, 1) : b1, c2 = T16B_AHEAD > 1 ? ld(r2, 1) : b2;
   bf16x8b a0 = *(const bf16x8b*)x0, a1 = *(const bf16x8b*)x1;
   for (int kg = 0; kg < nkg; ++kg) {
-    // the next group's operands first (past the last group: out of range, zeros / the pad)
-    const bf16x8b nb1 = __builtin_bit_cast(bf16x8b, __builtin_amdgcn_raw_buffer_load_b128(r1, off(kg + 1), 0, 0));
-    const bf16x8b nb2 = __builtin_bit_cast(bf16x8b, __builtin_amdgcn_raw_buffer_load_b128(r2, off(kg + 1), 0, 0));
+    const bf16x8b nb1 = ld(r1, kg + T16B_AHEAD), nb2 = ld(r2, kg + T16B_AHEAD);
     const int nx = kg + 1 < nkg ? 32 * (kg + 1) : 32 * kg;
     const bf16x8b na0 = *(const bf16x8b*)(x0 + nx), na1 = *(const bf16x8b*)(x1 + nx);
     acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, acc[0][0], 0, 0, 0);
     acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc[0][1], 0, 0, 0);
     acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b2, acc[1][0], 0, 0, 0);
     acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b2, acc[1][1], 0, 0, 0);
-    b1 = nb1;
-    b2 = nb2;
+    if (T16B_AHEAD > 1) {
+      b1 = c1; b2 = c2;
+      c1 = nb1; c2 = nb2;
+    } else {
+      b1 = nb1; b2 = nb2;
+    }
     a0 = na0;
     a1 = na1;
   }
@@ -1830,9 +1882,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
   const long ldh = a.ld_h;
   const T16Range rg = t16_range(a.slices, nt);
   BnRun bn;
-  bn.n = 0.0f;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) bn.mean[q] = bn.m2[q] = 0.0f;
+  bn_init(bn, wpart);
   const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
   if (!h16) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
   for (long p0 = rg.tb; p0 < rg.te;) {
