@@ -1533,6 +1533,54 @@ __device__ __forceinline__ void t16_mlp(const float* m, int ld_m, const f32x4v* 
       }
 }
 
+// bf16 mlp (gwn_dtype GWN_DTYPE_BF16_MLP, the bf16 tile kernels): a piece's channel map as
+// v_mfma_f32_16x16x32_bf16 A operands in LDS, [piece][out half oh][lane][8 bf16] with lane (g, j)
+// holding M[16 oh + j][k] for the permuted K group k = 4g .. 4g+3, 16+4g .. 16+4g+3 -- the
+// channels a lane's accumulators hold (acc[hf][e]: channel 16 hf + 4 g + e), so the piece itself
+// is the B operand as it stands: 2 MFMAs per piece instead of 16 f32 ones.  Forward M_p = W[:,
+// p-block]; backward M_p = its transpose (W^T applied to dh).
+typedef __bf16 bf16x8m __attribute__((ext_vector_type(8)));
+#ifndef GWN_T16_MLPB_SB
+#define GWN_T16_MLPB_SB 1
+#endif
+__device__ __forceinline__ int mlp_perm(int g, int e) { return e < 4 ? 4 * g + e : 16 + 4 * g + (e - 4); }
+__device__ __forceinline__ void t16_stage_maps_bf16(const float* w, int ld_w, bool backward, int npieces, __bf16* dst) {
+  for (int t = threadIdx.x; t < npieces * 2 * 64; t += blockDim.x) {
+    const int p = t >> 7, oh = (t >> 6) & 1, lane = t & 63, g = lane >> 4, j = lane & 15;
+    const int row = 16 * oh + j;
+    bf16x8m v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = mlp_perm(g, e);
+      v[e] = (__bf16)(backward ? w[(long)k * ld_w + p * CH + row] : w[(long)row * ld_w + p * CH + k]);
+    }
+    *(bf16x8m*)(dst + (long)t * 8) = v;
+  }
+}
+// the piece in the t16 accumulator layout (acc[hf][e]: channel 16 hf + 4 g + e) as the B operand
+// of t16_mlp_b; its halves are also the bf16 piece store's 4-channel groups
+__device__ __forceinline__ bf16x8m t16_pack_b(const f32x4v* acc) {
+  bf16x8m b;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    b[e] = (__bf16)acc[0][e];
+    b[4 + e] = (__bf16)acc[1][e];
+  }
+  return b;
+}
+// hacc[oh] += M_p x piece, bf16 operands: both A fragments are read before the first product
+// (one LDS latency per piece, not two)
+__device__ __forceinline__ void t16_mlp_bp(const __bf16* maps, int p, const bf16x8m b, int lane, f32x4v* hacc) {
+  const bf16x8m a0 = *(const bf16x8m*)(maps + ((p * 2 + 0) * 64 + lane) * 8);
+  const bf16x8m a1 = *(const bf16x8m*)(maps + ((p * 2 + 1) * 64 + lane) * 8);
+  if (GWN_T16_MLPB_SB) __builtin_amdgcn_sched_barrier(0);
+  hacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b, hacc[0], 0, 0, 0);
+  hacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b, hacc[1], 0, 0, 0);
+}
+__device__ __forceinline__ void t16_mlp_b(const __bf16* maps, int p, const f32x4v* acc, int lane, f32x4v* hacc) {
+  t16_mlp_bp(maps, p, t16_pack_b(acc), lane, hacc);
+}
+
 // both powers of one support for the wave's 16-node tile: acc[q][hf] (q = 0: G1, 1: G2) holds
 // D[16 hf + 4 g + r][w0 + j] = sum_v img[v][16 hf + 4 g + r] G_q[v][w0 + j]
 // The supports come in gwn_support_g4's k-interleaved layout: one 16-B load per lane fetches the
@@ -1868,7 +1916,7 @@ __device__ __forceinline__ void t16_rows_global(const float* src, long ld, int w
   }
 }
 
-template <int MAXT>
+template <int MAXT, bool MLPB = false>
 __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, const PowSup p, const int maximg) {
   extern __shared__ float lds[];
   const int n = a.n;
@@ -1884,7 +1932,16 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
   BnRun bn;
   bn_init(bn, wpart);
   const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
-  if (!h16) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
+  // the channel maps: f32 for t16_mlp, or bf16 MFMA operands for t16_mlp_b (MLPB)
+  auto stage_maps = [&] {
+    if (MLPB) t16_stage_maps_bf16(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, (__bf16*)ws);
+    else t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
+  };
+  auto mlp = [&](int piece, const f32x4v* x, f32x4v* out) {
+    if (MLPB) t16_mlp_b((const __bf16*)ws, piece, x, lane, out);
+    else t16_mlp(ws + piece * CH * LDW16, LDW16, x, lane, out);
+  };
+  if (!h16) stage_maps();
   for (long p0 = rg.tb; p0 < rg.te;) {
     const int s0 = (int)(p0 / nt);
     const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
@@ -1893,7 +1950,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
     if (h16) {  // as the f32 kernel: the phase in one pass, the maps inside its first round trip
       const bool maps = p0 == rg.tb;
       stage_bf16_octets(a.h + (long)s0 * n * ldh, ldh, n, s16, s1 - s0 + 1, imgs, imgb, [&] {
-        if (maps) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
+        if (maps) stage_maps();
       });
     } else {
       for (int sl = s0; sl <= s1; ++sl) global_to_lds16_bf16(a.h + (long)sl * n * ldh, ldh, n, imgs + (sl - s0) * imgb);
@@ -1922,7 +1979,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
       {  // piece 0: the node features themselves (fp32)
         f32x4v x0[2];
         t16_rows_global(hs_out, ldh, w0, n, lane, x0);
-        t16_mlp(ws, LDW16, x0, lane, hacc);
+        mlp(0, x0, hacc);
         if (a.xg4) t16_store_g4(a.xg4, 0, a.slices, sl, nt, tile, lane, x0);
       }
       for (int k = 0; k < a.nsup; ++k) {
@@ -1931,7 +1988,19 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
         if (a.xg4 && k == a.xg4_k) t16_store_g4(a.xg4, 1, a.slices, sl, nt, tile, lane, acc[0]);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          t16_mlp(ws + (1 + 2 * k + q) * CH * LDW16, LDW16, acc[q], lane, hacc);
+          if (MLPB) {  // one bf16 conversion for the mlp operand and the piece store
+            const bf16x8m b = t16_pack_b(acc[q]);
+            t16_mlp_bp((const __bf16*)ws, 1 + 2 * k + q, b, lane, hacc);
+            if (a.store_pieces && a.pb && w0 + j < n) {
+              __bf16* bp = (__bf16*)a.pb + (row0 + w0 + j) * a.ld_pb + (2 * k + q) * CH + 4 * g;
+              typedef __bf16 bf16x4p __attribute__((ext_vector_type(4)));
+              __builtin_nontemporal_store(bf16x4p{b[0], b[1], b[2], b[3]}, (bf16x4p*)bp);
+              __builtin_nontemporal_store(bf16x4p{b[4], b[5], b[6], b[7]}, (bf16x4p*)(bp + 16));
+              continue;
+            }
+          } else {
+            mlp(1 + 2 * k + q, acc[q], hacc);
+          }
           if (a.store_pieces && a.pb && w0 + j < n) {
             // bf16 pieces: node w0 + j, channels 16 hf + 4 g .. +3 as 8-B stores (non-temporal)
             __bf16* bp = (__bf16*)a.pb + (row0 + w0 + j) * a.ld_pb + (2 * k + q) * CH + 4 * g;
@@ -2154,7 +2223,7 @@ __device__ __forceinline__ void t16_store(float* out, long ld, const f32x4v* acc
 // BF: bf16 operands in the diffusion (the bf16 forward's image / support layouts: sup_g4b_t), the
 // tile's fp32 dh rows for the channel maps of piece 0 and t1 / t2 read back from dh_out (written by
 // this workgroup's prologue for its own rows) or dh
-template <int MAXT, bool BF>
+template <int MAXT, bool BF, bool MLPB = false>
 __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, const PowSup p, const int maximg) {
   extern __shared__ float lds[];
   const int n = a.n;
@@ -2165,6 +2234,10 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
   float* imgs = ws + (2 * a.nsup + 1) * CH * LDW16 + T16_WAVES * 3 * CH;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int nwaves = blockDim.x >> 6;
+  auto mlp = [&](int piece, const f32x4v* x, f32x4v* out) {
+    if (MLPB) t16_mlp_b((const __bf16*)ws, piece, x, lane, out);
+    else t16_mlp(ws + piece * CH * LDW16, LDW16, x, lane, out);
+  };
   const T16Range rg = t16_range(a.slices, nt);
   if (a.bn_dy && blockIdx.x == 0 && threadIdx.x < CH) {
     if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
@@ -2178,7 +2251,10 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
     // the phase's dh images in one pass, the channel maps inside its first round trip
     const bool maps = p0 == rg.tb;
     t16_bwd_stage<BF>(a, imgs, imgf, s0, s1 - s0 + 1, rg, nt, n, rows_img, [&] {
-      if (maps) t16_stage_maps(a.w_mlp, a.ld_w, true, 2 * a.nsup + 1, ws);
+      if (maps) {
+        if (MLPB) t16_stage_maps_bf16(a.w_mlp, a.ld_w, true, 2 * a.nsup + 1, (__bf16*)ws);
+        else t16_stage_maps(a.w_mlp, a.ld_w, true, 2 * a.nsup + 1, ws);
+      }
     });
     __syncthreads();
     const int nsl = s1 - s0 + 1;
@@ -2204,27 +2280,27 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
         f32x4v d0[2];
         if (BF) t16_rows_global(dh_rows, CH, w0, n, lane, d0);
         else t16_rows(dhs, hs, w0, lane, d0);
-        t16_mlp(ws, LDW16, d0, lane, dx);
+        mlp(0, d0, dx);
       }
       for (int k = 0; k < a.nsup; ++k) {
         f32x4v e[2][2];
         if (BF) t16b_diffuse((const __bf16*)dhs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, e);
         else t16_diffuse(dhs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, e);
-        t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, e[0], lane, dx);
-        t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[1], lane, dx);
+        mlp(1 + 2 * k, e[0], dx);
+        mlp(2 + 2 * k, e[1], dx);
         if (k == a.adp_index) {  // t1 = W1^T dh + W2^T (A dh), t2 = W2^T dh
           f32x4v d0[2], tt[2];
           if (BF) t16_rows_global(dh_rows, CH, w0, n, lane, d0);
           else t16_rows(dhs, hs, w0, lane, d0);
           tt[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
           tt[1] = tt[0];
-          t16_mlp(ws + (1 + 2 * k) * CH * LDW16, LDW16, d0, lane, tt);
-          t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, e[0], lane, tt);
+          mlp(1 + 2 * k, d0, tt);
+          mlp(2 + 2 * k, e[0], tt);
           if (BF && a.tg4) t16_store_g4(a.tg4, 0, a.slices, s, nt, tile, lane, tt);
           else t16_store(a.t1 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
           tt[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
           tt[1] = tt[0];
-          t16_mlp(ws + (2 + 2 * k) * CH * LDW16, LDW16, d0, lane, tt);
+          mlp(2 + 2 * k, d0, tt);
           if (BF && a.tg4) t16_store_g4(a.tg4, 1, a.slices, s, nt, tile, lane, tt);
           else t16_store(a.t2 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
         }
@@ -2605,7 +2681,8 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
                 "gcn_fwd (fused): eval BatchNorm needs running mean / var, weight, bias (and no BN partials)");
   else
     GWN_REQUIRE(a.z != nullptr, "gcn_fwd (fused): z is required");
-  if (g->split_planes == 1 && g->sup_g4b && a.sup_batch <= 1 && g->nsup > 0 && g->layout == 0 && t16_enabled() &&
+  GWN_REQUIRE(g->split_planes >= 0 && g->split_planes <= 2, "gcn_fwd: split_planes must be a gwn_dtype (0, 1, 2)");
+  if (g->split_planes >= 1 && g->sup_g4b && a.sup_batch <= 1 && g->nsup > 0 && g->layout == 0 && t16_enabled() &&
       g->ksplit != g->nsup) {
     const int slices = g->rows / g->n;
     const size_t fixed = t16b_lds_bytes(g->n, g->nsup, 0), img = t16b_lds_bytes(g->n, g->nsup, 1) - fixed;
@@ -2618,6 +2695,8 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
       if (!attr_b) {
         (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   T16_LDS_MAX);
+        (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b_kernel<1024, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
         attr_b = true;
       }
       const int nt = (g->n + 15) / 16;
@@ -2635,7 +2714,8 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
       a.ksplit = 1;
       a.bn_slots = (int)gwn_bn_part_slots(slices);
       if (fold_here) a.fold = *g->bn_fold;
-      gcn_fwd_t16b_kernel<1024><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      if (g->split_planes == 2) gcn_fwd_t16b_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      else gcn_fwd_t16b_kernel<1024><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       GWN_CHECK_LAUNCH();
       *folded = fold_here;
       return GWN_OK;
@@ -2736,7 +2816,8 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
   // the t16 backward stages dh (or dy / z, writing dres / dh_out) as 16-B rows
   const auto a16 = [](const void* ptr) { return ((uintptr_t)ptr & 15) == 0; };
   const bool t16_rows16 = a.bn_dy ? a16(a.bn_dy) && a16(a.bn_z) && a16(a.dres) && a16(a.dh_out) : a16(a.dh);
-  if (g->split_planes == 1 && g->sup_g4b_t && a.sup_batch <= 1 && g->nsup > 0 && g->layout == 0 && t16_enabled() &&
+  GWN_REQUIRE(g->split_planes >= 0 && g->split_planes <= 2, "gcn_bwd: split_planes must be a gwn_dtype (0, 1, 2)");
+  if (g->split_planes >= 1 && g->sup_g4b_t && a.sup_batch <= 1 && g->nsup > 0 && g->layout == 0 && t16_enabled() &&
       g->ksplit != g->nsup) {
     GWN_REQUIRE(t16_rows16, "gcn_bwd (16-node tiles, bf16): dh, or bn_dy / bn_z / dres / dh_out, must be 16-B aligned");
     const int slices = g->rows / g->n;
@@ -2745,6 +2826,8 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
       static bool attr_b = false;
       if (!attr_b) {
         (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<1024, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
+        (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<1024, true, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
         attr_b = true;
       }
@@ -2761,7 +2844,8 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
       PowSup p = {};
       for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = (const float*)g->sup_g4b_t[k];
       a.ksplit = 1;
-      gcn_bwd_t16_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      if (g->split_planes == 2) gcn_bwd_t16_kernel<1024, true, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      else gcn_bwd_t16_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       GWN_CHECK_LAUNCH();
       return GWN_OK;
     }

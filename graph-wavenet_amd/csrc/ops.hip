@@ -1318,7 +1318,7 @@ int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
       const float* x1 = a->h + (1 + 2 * k) * c;
       if (gram_eligible(a->h, a->ld_h, t1, a->ld_dhcat, c) && gram_eligible(x1, a->ld_h, t2, a->ld_dhcat, c))
         return gwn_gram_dtype(a->h, t1, x1, t2, a->ld_h, a->ld_dhcat, n, slices, a->dadp, a->ld_sup,
-                              a->accumulate_dadp, a->workspace, a->split_planes == 1 ? 1 : 0, s);
+                              a->accumulate_dadp, a->workspace, a->split_planes >= 1 ? 1 : 0, s);
       rc = gwn_nconv_adj_grad(a->h, a->ld_h, t1, a->ld_dhcat, n, c, slices, a->dadp, a->ld_sup,
                               a->accumulate_dadp, a->workspace, s);
       if (rc) return rc;

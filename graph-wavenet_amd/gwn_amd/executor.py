@@ -316,8 +316,9 @@ class Executor:
     # ---------------------------------------------------------------------------------------
     def split_planes(self):
         """MFMA operand format of the fused gcn kernels (include/gwn.h gwn_dtype):
-        * compute dtype bf16 (gwnet.set_compute_dtype): 1 = bf16 operands, fp32 accumulation,
-          forward AND backward, on the 16-node tile kernels (the mixed-precision path of configs[2]);
+        * compute dtype bf16 (gwnet.set_compute_dtype): 2 = bf16 operands, fp32 accumulation,
+          forward AND backward, on the 16-node tile kernels, the per-hop 1x1 mlp on bf16 MFMA too
+          (the mixed-precision path of configs[2]); GWN_BF16_MLP=0 keeps that mlp in f32 (1);
         * else 0: the f32-MFMA kernels (the default: the reference's fp32 arithmetic).
         0 when the shape has no bf16 tile kernel (c != 32, n > 512, no supports, GWN_GCN_T16=0)."""
         cfg = self.cfg
@@ -325,7 +326,9 @@ class Executor:
             return 0
         if not self._t16_ok() or not self._fused_gcn():
             return 0
-        return 1 if _lib.load().gwn_gcn_t16b_supported(cfg.N, cfg.nsup) else 0
+        if not _lib.load().gwn_gcn_t16b_supported(cfg.N, cfg.nsup):
+            return 0
+        return 2 if os.environ.get("GWN_BF16_MLP", "1") != "0" else 1
 
     def pk(self, name, buf=None):
         return self.layout.view(self.packed if buf is None else buf, name)
@@ -561,8 +564,9 @@ class Executor:
         planes = self.split_planes() if sup_batch <= 1 else 0
         acts.g4bt_arr = None
         # (shared supports only: planes is 0 for per-sample graphs, whose padded stacks are fresh per call)
-        acts.g4bf_arr = self._g4_bf16(fixed_sups, acts, st) if planes == 1 and sups and sup_batch <= 1 else None
-        planes = 1 if acts.g4bf_arr is not None else 0
+        acts.g4bf_arr = self._g4_bf16(fixed_sups, acts, st) if planes >= 1 and sups and sup_batch <= 1 else None
+        planes = planes if acts.g4bf_arr is not None else 0
+        acts.planes = planes
         if not training:
             acts.g4bt_arr = None
         # the last layer's gcn + bn only update bn[L-1]'s running statistics (their output is dead,
@@ -932,7 +936,7 @@ class Executor:
                 hold = bf["g4b_holder"] = _G4Holder()
             hold.adp, hold.training, hold.supT = bf["adp"], False, None
             g4bf = self._g4_bf16(fixed_sups, hold, st)
-        planes = 1 if g4bf is not None else 0
+        planes = planes if g4bf is not None else 0
         sx = x.stride()
         _lib.call("gwn_start_conv_fwd", ptr(x), sx[0], sx[1], sx[2], sx[3], B, cin, N, t_in, ts[0],
                   ptr(self.pk("start_w")), ptr(self.pk("start_b")), C, ptr(bf["x0"]), None, st)
@@ -1113,7 +1117,7 @@ class Executor:
                 if sb > 1:
                     gb.sup_bstride, gb.sup_batch = cfg.NP * cfg.NP, sb
                 if getattr(acts, "g4bt_arr", None) is not None:  # bf16 operands (fp32 accumulation)
-                    gb.split_planes = 1
+                    gb.split_planes = getattr(acts, "planes", 1)
                 if fuse:
                     gb.dh = None
                     gb.bn_dy, gb.bn_z = ptr(dnext), ptr(acts.Z[i])

@@ -35,7 +35,9 @@ int gwn_version(void);
  * every mode (activations, weights, gradients, optimizer state); accumulation is always fp32. */
 typedef enum gwn_dtype {
   GWN_DTYPE_F32 = 0,     /* v_mfma_f32_32x32x2_f32: exact fp32 products (the reference's arithmetic) */
-  GWN_DTYPE_BF16 = 1     /* bf16 operands, fp32 accumulation (mixed precision, configs[2]) */
+  GWN_DTYPE_BF16 = 1,    /* bf16 operands, fp32 accumulation (mixed precision, configs[2]) */
+  GWN_DTYPE_BF16_MLP = 2 /* GWN_DTYPE_BF16 plus the gcn's 1x1 mlp (and its transpose in the
+                            backward) on bf16 operands, fp32 accumulation: the bf16 mode's default */
 } gwn_dtype;
 /* debugging aid: 1 = synchronise the device after every kernel launch and report a fault at the
  * kernel's source line (also enabled by GWN_SYNC_CHECK=1 in the environment), 2 = suspended (while
@@ -266,7 +268,8 @@ typedef struct gwn_gcn_args {
    * kernels): GWN_DTYPE_BF16 (1): bf16 operands, fp32 accumulation (v_mfma_f32_16x16x32_bf16) on the
    * 16-node tile kernel -- the mixed-precision path of configs[2].  Needs c == 32, nsup >= 1,
    * sup_g4b, layout 0, shared supports and gwn_gcn_t16b_supported(n, nsup); GWN_ERR_ARG otherwise.
-   * The mlp, the hop pieces, z and the BN partials stay fp32. */
+   * The mlp, the hop pieces, z and the BN partials stay fp32.  GWN_DTYPE_BF16_MLP (2): the same,
+   * and the mlp takes bf16 operands too (the pieces and W rounded to bf16, fp32 accumulation). */
   int split_planes;
   /* per-sample supports (the per-sample-graph variant, gcn2 model.py:57-80; sup_batch <= 1 = shared):
    * slice s = t*sup_batch + b diffuses with support k at sup[k] + b*sup_bstride (floats), same
@@ -399,7 +402,7 @@ typedef struct gwn_gcn_bwd_args {
   long sup_bstride; int sup_batch;
   /* operand precision of the fused backward's diffusion products (gwn_dtype): GWN_DTYPE_F32 (0) or
    * GWN_DTYPE_BF16 (1: v_mfma_f32_16x16x32_bf16, fp32 accumulation) on the 16-node tile kernel, which
-   * needs sup_g4b_t (as gwn_gcn_args.split_planes) */
+   * needs sup_g4b_t (as gwn_gcn_args.split_planes); GWN_DTYPE_BF16_MLP (2): the W^T products too */
   int split_planes;
   /* support split of the fused f32 backward, as gwn_gcn_args (partial input gradients, the last
    * workgroup of a slice adds them in support order and runs the store / gate epilogue) */

@@ -26,7 +26,8 @@ bf16 emulation (``Cfg(..., gcn_bf16=True)``): the arithmetic of libgwn's bf16 mo
 of every gcn take bf16-rounded operands (node features, A and A^2 forward; the mlp output
 gradient and A, A^2 in the backward) with exact accumulation, the adaptive support's gradient
 takes bf16-rounded operands, and the mlp, its weight gradient and every other layer stay exact
-(``gcn_bf16``, a custom autograd node).  The HIP path accumulates in fp32 instead, so a test can
+(``gcn_bf16``, a custom autograd node); ``gcn_bf16_mlp=True`` also rounds the per-piece mlp's
+operands (weights, pieces, backward inputs) as the default bf16 mode does.  The HIP path accumulates in fp32 instead, so a test can
 hold it to the fp32 rounding floor around this reference rather than to the bf16 distance from
 the exact model.
 
@@ -50,7 +51,7 @@ class Cfg:
 
     def __init__(self, num_nodes, nfixed=2, gcn_bool=True, addaptadj=True, in_dim=2, out_dim=12, nhid=32,
                  skip=None, end=None, blocks=4, layers=2, dropout=0.0, kernel_size=2, dilation_channels=None,
-                 first_dilation=1, gcn_bf16=False):
+                 first_dilation=1, gcn_bf16=False, gcn_bf16_mlp=False):
         self.N, self.nfixed = num_nodes, nfixed
         self.gcn_bool, self.addaptadj = gcn_bool, addaptadj
         self.Cin, self.O, self.C = in_dim, out_dim, nhid
@@ -60,6 +61,7 @@ class Cfg:
         self.blocks, self.layers, self.dropout = blocks, layers, dropout
         self.kernel_size = kernel_size
         self.gcn_bf16 = gcn_bf16  # libgwn's bf16 mode (module docstring)
+        self.gcn_bf16_mlp = gcn_bf16_mlp  # ... with the per-piece mlp on bf16 operands too (_GcnBf16)
         # gwnet_diff_G starts every block at dilation 4 (model.py:291)
         self.dilations = [first_dilation * 2 ** j for _ in range(blocks) for j in range(layers)]
         # model.py:130-157: every layer adds (kernel_size - 1) * 2^j -- the reference counts from
@@ -141,28 +143,32 @@ class _GcnBf16(torch.autograd.Function):
       dA_k = sum rnd(g) (x) rnd(t1) + rnd(A_k g) (x) rnd(t2),
              t1 = W_{1+2k}^T dy + W_{2+2k}^T (rnd(A_k) rnd(dy)),  t2 = W_{2+2k}^T dy
     (the chained-hop gradient of x2 = (x A) A, as the HIP path forms it).  rnd = bf16_round, or the
-    identity (then this equals plain autograd through the chained hops up to reassociation)."""
+    identity (then this equals plain autograd through the chained hops up to reassociation).
+    mrnd: the rounding of the per-piece 1x1 mlp's operands (gwn.h GWN_DTYPE_BF16_MLP, the default
+    bf16 mode; t16_mlp_b): forward W_q . piece_q -> mrnd(W_q) . mrnd(piece_q), every W_q^T y of the
+    backward (dg, t1, t2) -> mrnd(W_q)^T mrnd(y); dW stays exact.  None = exact mlp (GWN_BF16_MLP=0)."""
 
     @staticmethod
-    def forward(ctx, g, w, rnd, *sups):
+    def forward(ctx, g, w, rnd, mrnd, *sups):
         gb = rnd(g)
         pieces = [g]
         for a in sups:
             pieces += [diffuse(gb, rnd(a)), diffuse(gb, rnd(a @ a))]
         h = torch.cat(pieces, dim=1)
-        ctx.rnd = rnd
+        ctx.rnd, ctx.mrnd = rnd, mrnd
         ctx.save_for_backward(g, w, h, *sups)
-        return pointwise(h, w)
+        return pointwise(h, w) if mrnd is None else pointwise(mrnd(h), mrnd(w))
 
     @staticmethod
     def backward(ctx, dy):
         g, w, h, *sups = ctx.saved_tensors
-        rnd = ctx.rnd
+        rnd, mrnd = ctx.rnd, ctx.mrnd
         C = g.shape[1]
         wr = w.reshape(w.shape[0], -1)
+        wm, mr = (wr, lambda t: t) if mrnd is None else (mrnd(wr), mrnd)
 
-        def wt(q, y):  # W_q^T y over the channel axis
-            return torch.einsum("oi,bont->bint", wr[:, q * C:(q + 1) * C], y)
+        def wt(q, y):  # W_q^T y over the channel axis (the mlp's operand rounding)
+            return torch.einsum("oi,bont->bint", wm[:, q * C:(q + 1) * C], mr(y))
 
         hb = torch.cat([h[:, :C], rnd(h[:, C:])], dim=1)  # the bf16-stored hop pieces
         dw = torch.einsum("bont,bint->oi", dy, hb).reshape(w.shape)
@@ -175,18 +181,19 @@ class _GcnBf16(torch.autograd.Function):
             e2 = diffuse(dyb, rnd(a @ a).t())
             dg = dg + wt(1 + 2 * k, e1) + wt(2 + 2 * k, e2)
             da = None
-            if ctx.needs_input_grad[3 + k]:
+            if ctx.needs_input_grad[4 + k]:
                 t1 = wt(1 + 2 * k, dy) + wt(2 + 2 * k, e1)
                 t2 = wt(2 + 2 * k, dy)
                 x1 = h[:, (1 + 2 * k) * C:(2 + 2 * k) * C]
                 da = torch.einsum("bcvt,bcwt->vw", rnd(g), rnd(t1)) + torch.einsum("bcvt,bcwt->vw", rnd(x1), rnd(t2))
             dsups.append(da)
-        return (dg, dw, None, *dsups)
+        return (dg, dw, None, None, *dsups)
 
 
-def gcn_bf16(g, w, sups, rnd=bf16_round):
-    """libgwn's bf16-mode gcn products (_GcnBf16): sum_q W_q piece_q, no bias."""
-    return _GcnBf16.apply(g, w, rnd, *sups)
+def gcn_bf16(g, w, sups, rnd=bf16_round, mrnd=None):
+    """libgwn's bf16-mode gcn products (_GcnBf16): sum_q W_q piece_q, no bias; mrnd = the mlp's
+    operand rounding (None: exact mlp)."""
+    return _GcnBf16.apply(g, w, rnd, mrnd, *sups)
 
 
 def pointwise(x, w, bias=None):
@@ -249,7 +256,9 @@ def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, ma
         s = pointwise(g, p["skip_convs.%d.weight" % i], p["skip_convs.%d.bias" % i])
         skip = s if skip is None else s + skip[..., -s.shape[-1]:]
         if cfg.use_gcn and getattr(cfg, "gcn_bf16", False):
-            h = gcn_bf16(g, p["gconv.%d.mlp.mlp.weight" % i], sups) + p["gconv.%d.mlp.mlp.bias" % i].view(1, -1, 1, 1)
+            h = gcn_bf16(g, p["gconv.%d.mlp.mlp.weight" % i], sups,
+                         mrnd=bf16_round if getattr(cfg, "gcn_bf16_mlp", False) else None) \
+                + p["gconv.%d.mlp.mlp.bias" % i].view(1, -1, 1, 1)
             if training and cfg.dropout > 0:
                 m = dropout_masks[i] if dropout_masks is not None else \
                     (torch.rand_like(h) >= cfg.dropout).to(h.dtype)

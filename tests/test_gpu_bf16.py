@@ -3,10 +3,13 @@ runs the fused diffusion-GCN forward and backward on v_mfma_f32_32x32x16_bf16 (b
 fp32 accumulation); parameters, activations, gradients and Adam state stay fp32.
 
 Tolerances:
-* the gate: against the bf16-EMULATING oracle (oracle Cfg(gcn_bf16=True): the same bf16-rounded
-  operands with exact accumulation, every other layer exact) -- forward max-rel <= 1e-4, loss rel
-  <= 1e-5, every gradient norm-rel <= 1e-3.  What is left is fp32 accumulation, so an error in the
-  bf16 arithmetic (a wrong rounding, a missing term, a wrong operand) shows up at its own size;
+* the gate: against the bf16-EMULATING oracle (oracle Cfg(gcn_bf16=True, gcn_bf16_mlp=True): the
+  same bf16-rounded operands -- diffusion products and the per-piece 1x1 mlp -- with exact
+  accumulation, every other layer exact), on the branches the HIP step took (_branches) --
+  forward max-rel <= 4e-4, loss rel <= 1e-5, every gradient norm-rel <= 2e-3, median <= 3e-4
+  (GWN_BF16_MLP=0, the mlp in f32: 1e-4 / 1e-3 / 2e-4).  What is left is fp32 accumulation and the
+  bf16 rounding flips it causes (_fwd_gate), so an error in the bf16 arithmetic (a wrong
+  rounding, a missing term, a wrong operand) shows up at its own size;
 * the report: the distance from the reference's own f64 run (the bf16 distance itself) is printed
   and held to the loose bounds of rounds 2-3 (forward 2e-2, gradients 0.1 each / 5e-2 median).
   For scale: the reference itself under torch.autocast(bfloat16) (the oracle, CPU) is 7.5e-2 /
@@ -56,22 +59,64 @@ def _check_grads(model, ref, tag, emul=None):
         worst = max(gate, key=gate.get)
         print("%s: vs bf16 emulation worst %.2e (%s), median %.2e; vs f64 worst %.2e, median %.2e"
               % (tag, gate[worst], worst, np.median(list(gate.values())), max(errs), np.median(errs)))
+        worst_gate, median_gate = _grad_gates()
         for k, e in gate.items():
-            assert e <= 1e-3, (tag, k, e)
+            assert e <= worst_gate, (tag, k, e)
+        assert np.median(list(gate.values())) <= median_gate
 
 
-def _emulated(g, n, x, y=None):
+def _mlp_bf16():
+    import os
+    return os.environ.get("GWN_BF16_MLP", "1") != "0"
+
+
+def _fwd_gate():
+    """Forward max-rel gate against the emulation: 1e-4 (fp32 accumulation); 4e-4 with the mlp on
+    bf16 operands -- there every hop piece is rounded to bf16 before the mlp, and a piece whose
+    fp32 sum lies within its accumulation error of a rounding boundary rounds the other way than
+    in fp64 (one bf16 ulp, 2^-8, of one of 224 mlp inputs; ~1e-4 of the output max after 8
+    layers).  The mlp's own arithmetic is pinned at kernel level (test_gcn_t16_bf16_forward /
+    _backward, planes 2: 1e-5 / 3e-4 of an fp64 evaluation of the same bf16 operands)."""
+    return 4e-4 if _mlp_bf16() else 1e-4
+
+
+def _branches(eng, n, y):
+    """The branches the HIP step took (oracle module docstring: branch pinning): the head ReLUs
+    (test_gpu_headline._gpu_branch) and the sign of pred - real of the masked MAE.  With the mlp on
+    bf16 operands the forward sits ~1e-4 off the emulation (_fwd_gate), enough to flip elements
+    that lie that close to a kink; each flipped MAE sign moves every gradient by ~1e-3."""
+    from test_gpu_headline import _gpu_branch
+    B = y.shape[0]
+    m = _gpu_branch(eng, B, n)
+    (acts,) = list(eng._acts.values())
+    pred = acts.y.detach().cpu().double().view(1, B, n, -1).permute(1, 0, 2, 3) * 19.5 + 54.4  # [B,1,N,T]
+    m["sign"] = torch.sign(pred - torch.tensor(y, dtype=torch.float64).unsqueeze(1))
+    return m
+
+
+def _grad_gates():
+    """(per-gradient, median) norm-rel gates against the emulation: 1e-3 / 2e-4 with the mlp in
+    f32; 2e-3 / 3e-4 with it on bf16 operands, where the forward's ~1e-4 bf16 rounding flips
+    (_fwd_gate) reach the bottom layers' gradients (measured worst 1.3e-3, gate_convs.0.bias at
+    N=207; median 1.2e-4).  Missing the forward mlp rounding costs 2-3e-2 (tools/exp/
+    bf16_mlp_probe.py); the backward mlp rounding sits below the flip noise here and is pinned at
+    kernel level (test_gcn_t16_bf16_backward *_mlp)."""
+    return (2e-3, 3e-4) if _mlp_bf16() else (1e-3, 2e-4)
+
+
+def _emulated(g, n, x, y=None, masks=None):
     """The bf16-emulating oracle (oracle Cfg(gcn_bf16=True)) on a fixture: eval output (y None) or
-    (train-mode output, metrics, gradients)."""
+    (train-mode output, metrics, gradients).  The per-piece mlp on bf16 operands too unless
+    GWN_BF16_MLP=0 (executor.split_planes: the library's mode 2 / mode 1)."""
     from oracle import gwnet_oracle as orc
     sd = state_dict_of(g)
-    cfg = orc.Cfg(n, gcn_bf16=True)
+    cfg = orc.Cfg(n, gcn_bf16=True, gcn_bf16_mlp=_mlp_bf16())
     if y is None:
         p = {k: torch.tensor(v, dtype=torch.float64) for k, v in sd.items() if "running" not in k and "num_batches" not in k}
         bn = {k: torch.tensor(v, dtype=torch.float64) for k, v in sd.items() if "running" in k}
         return orc.forward(p, [torch.tensor(g["sup0"], dtype=torch.float64), torch.tensor(g["sup1"], dtype=torch.float64)],
                            torch.tensor(x, dtype=torch.float64), cfg, False, bn)
-    out, met, gr, _ = orc.grads(sd, [g["sup0"], g["sup1"]], x, y, cfg, 54.4, 19.5)
+    out, met, gr, _ = orc.grads(sd, [g["sup0"], g["sup1"]], x, y, cfg, 54.4, 19.5, masks=masks)
     return out, met, gr
 
 
@@ -87,7 +132,7 @@ def test_bf16_eval_forward(gpu, name, n, xkey, okey):
     emu = _emulated(g, n, g[xkey]).numpy()
     e_emu, e_f64 = rel_err(out.cpu().numpy(), emu), rel_err(out.cpu().numpy(), g[okey])
     print("bf16 eval forward N=%d: vs bf16 emulation %.2e, vs f64 %.2e" % (n, e_emu, e_f64))
-    assert e_emu <= 1e-4
+    assert e_emu <= _fwd_gate()
     assert e_f64 <= 2e-2
 
 
@@ -98,7 +143,7 @@ def test_bf16_train_step_grads(gpu, name, n, pre):
     met = eng.train(torch.tensor(g[pre + "x"], device=gpu), torch.tensor(g[pre + "y"], device=gpu))
     mref = g["metrics_f64" if pre == "" else "g2_metrics_f64"]
     assert abs(met[0] / mref[0] - 1) <= 1e-3
-    _, emet, egr = _emulated(g, n, g[pre + "x"], g[pre + "y"])
+    _, emet, egr = _emulated(g, n, g[pre + "x"], g[pre + "y"], masks=_branches(eng, n, g[pre + "y"]))
     assert abs(met[0] / emet[0] - 1) <= 1e-5, (met[0], emet[0])
     gkey = "grad_f64/" if pre == "" else "g2_grad_f64/"
     _check_grads(eng.model, {k[len(gkey):]: v for k, v in g.items() if k.startswith(gkey)}, name, emul=egr)

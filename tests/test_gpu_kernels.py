@@ -1113,13 +1113,16 @@ def test_nconv2_errors_and_strided_input(gpu):
     assert rel_err(y.cpu().numpy(), ref.numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("planes", [1, 2])
 @pytest.mark.parametrize("n", [16, 207, 325])
-def test_gcn_t16_bf16_forward(gpu, n):
-    """The bf16 16-node tile forward (gwn_gcn_args.sup_g4b, split_planes 1): the diffusion on bf16
-    MFMA operands with fp32 accumulation, the mlp / z / BN partials in fp32, against fp64
-    (model.py:41-55 + residual).  Bound: bf16 rounding of the node features and supports (2^-9
-    relative each) over K = n terms of positive weights -- hop pieces and z within 1e-2 of their
-    max magnitude; the BN statistics of z within 1e-2."""
+def test_gcn_t16_bf16_forward(gpu, n, planes):
+    """The bf16 16-node tile forward (gwn_gcn_args.sup_g4b, split_planes 1 / 2): the diffusion on
+    bf16 MFMA operands with fp32 accumulation, the mlp in fp32 (1) or on bf16 MFMA operands (2,
+    GWN_DTYPE_BF16_MLP), z / BN partials in fp32, against fp64 (model.py:41-55 + residual).  Bound:
+    bf16 rounding of the node features and supports (2^-9 relative each) over K = n terms of
+    positive weights -- hop pieces and z within 1e-2 of their max magnitude; the BN statistics of z
+    within 1e-2.  planes 2 also against an fp64 evaluation of z from the bf16-rounded pieces and
+    weights (the arithmetic of t16_mlp_b, fp32 accumulation the only difference): 1e-5."""
     import ctypes
     from gwn_amd import _lib
     torch.manual_seed(n + 3)
@@ -1155,9 +1158,14 @@ def test_gcn_t16_bf16_forward(gpu, n):
     ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, P), ld_sup=NP, h=h.data_ptr(), ld_h=W,
                       w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(), residual=res.data_ptr(), z=z.data_ptr(),
                       seed_ptr=seed.data_ptr(), salt=0, drop_p=0.0, bn_partials=bnp.data_ptr(), w_mlp_t=wmt.data_ptr(),
-                      split_planes=1, sup_g4b=ctypes.cast(arrb, P))
+                      split_planes=planes, sup_g4b=ctypes.cast(arrb, P))
     _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
     torch.cuda.synchronize()
+    if planes == 2:
+        bf = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
+        hb = torch.cat([bf(xg.double().cpu()), bf(h[:, C:].double().cpu())], dim=1)  # the stored pieces
+        zm = hb @ bf(wm.double().cpu()).t() + bm.double().cpu() + res.double().cpu()
+        assert rel_err(z.cpu().numpy(), zm.numpy()) <= 1e-5
     X = xg.double().cpu().view(S, n, C)
     pieces = [X]
     for s_ in sups:
@@ -1275,7 +1283,7 @@ def _from_g4(buf, which, slices, n):
 
 
 @pytest.mark.parametrize("n", [16, 207, 325])
-@pytest.mark.parametrize("mode", ["bn_gate", "bn_gate_tg4", "plain"])
+@pytest.mark.parametrize("mode", ["bn_gate", "bn_gate_tg4", "plain", "bn_gate_tg4_mlp", "plain_mlp"])
 def test_gcn_t16_bf16_backward(gpu, n, mode):
     """The bf16 16-node tile backward (gcn_bwd_t16_kernel<1024, true>: gwn_gcn_bwd_args.sup_g4b_t,
     split_planes 1) against fp64, kernel level (model.py:41-55 backward): the BN-backward prologue
@@ -1285,10 +1293,16 @@ def test_gcn_t16_bf16_backward(gpu, n, mode):
     epilogue (dfg from dxg + dskip and the saved (tanh f, sigmoid s)) or the plain dxg store.
     Bounds: against an fp64 evaluation of the same bf16-rounded operands (the arithmetic the kernel
     implements, fp32 accumulation the only difference) 2e-5 of each output's max magnitude (tg4: one
-    bf16 rounding, 2^-8); against the exact fp64 gradient 1e-2 (the forward test's bound)."""
+    bf16 rounding, 2^-8); against the exact fp64 gradient 1e-2 (the forward test's bound).
+    *_mlp: split_planes 2 (GWN_DTYPE_BF16_MLP), the channel maps on bf16 MFMA: every W_q^T y of the
+    emulation takes bf16(W_q), bf16(y); bound 3e-4 instead of 2e-5: an fp32 intermediate (e1, the
+    diffusion of dh) within its accumulation error of a bf16 rounding boundary rounds the other way
+    in the kernel than in fp64 (about 3e-4 of them, each one 2^-8 of one product of a 224-term sum)."""
     import ctypes
     from gwn_amd import _lib
     from test_gpu_model import _np_uniform
+    planes = 2 if mode.endswith("_mlp") else 1
+    mode = mode.replace("_mlp", "")
     torch.manual_seed(n + 11)
     C, K, S = 32, 3, 21
     NP = (n + 31) // 32 * 32
@@ -1344,7 +1358,7 @@ def test_gcn_t16_bf16_backward(gpu, n, mode):
         kw["tg4"] = tg4.data_ptr()
     gb = _lib.GcnBwdArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, P), ld_sup=NP, h=h.data_ptr(), ld_h=W,
                          w_mlp=wm.data_ptr(), dhcat=dhc.data_ptr(), ld_dhcat=W, adp_index=K - 1, accumulate_dadp=0,
-                         sup_t=ctypes.cast(arrT, P), skip_weight_grads=1, split_planes=1, sup_g4b_t=ctypes.cast(arrb, P),
+                         sup_t=ctypes.cast(arrT, P), skip_weight_grads=1, split_planes=planes, sup_g4b_t=ctypes.cast(arrb, P),
                          **kw)
     _lib.call("gwn_gcn_bwd", ctypes.byref(gb), _lib.stream())
     torch.cuda.synchronize()
@@ -1363,9 +1377,11 @@ def test_gcn_t16_bf16_backward(gpu, n, mode):
         dhr = dh.double().cpu()
     bf = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
     Wd = wm.double().cpu()
-    wq = lambda y, q: y @ Wd[:, q * C:(q + 1) * C]  # noqa: E731  (W_q^T applied to rows)
 
     def grads(rnd):
+        mr = rnd if planes == 2 else (lambda t: t)
+        Wm = mr(Wd)
+        wq = lambda y, q: mr(y) @ Wm[:, q * C:(q + 1) * C]  # noqa: E731  (W_q^T applied to rows)
         D = dhr.view(S, n, C)
         Db = rnd(D)
         dxg = wq(dhr, 0)
@@ -1396,20 +1412,21 @@ def test_gcn_t16_bf16_backward(gpu, n, mode):
         got_main, want_main, want_exact = dfg.cpu().numpy(), gate(emul[0]).numpy(), gate(exact[0]).numpy()
     else:
         got_main, want_main, want_exact = dhc[:, :C].cpu().numpy(), emul[0].numpy(), exact[0].numpy()
-    assert rel_err(got_main, want_main) <= 2e-5
+    tol = 2e-5 if planes == 1 else 3e-4
+    assert rel_err(got_main, want_main) <= tol
     assert rel_err(got_main, want_exact) <= 1e-2
     if tg4 is not None:
         for which, (em, ex) in enumerate(((emul[1], exact[1]), (emul[2], exact[2]))):
             got = _from_g4(tg4, which, S, n)
             assert torch.all(got[:, n:] == 0)  # the tiles' padding nodes
             got = got[:, :n].reshape(rows, C).numpy()
-            assert rel_err(got, em.numpy()) <= 2 ** -8 + 2e-5
+            assert rel_err(got, em.numpy()) <= 2 ** -8 + tol
             assert rel_err(got, ex.numpy()) <= 1e-2
         assert torch.all(dhc[:, C:3 * C] == 0)  # t1 / t2 went to tg4 only
     else:
         for j, (em, ex) in enumerate(((emul[1], exact[1]), (emul[2], exact[2]))):
             got = dhc[:, (1 + j) * C:(2 + j) * C].cpu().numpy()
-            assert rel_err(got, em.numpy()) <= 2e-5
+            assert rel_err(got, em.numpy()) <= tol
             assert rel_err(got, ex.numpy()) <= 1e-2
 
 
