@@ -1540,6 +1540,9 @@ __device__ __forceinline__ void t16_mlp(const float* m, int ld_m, const f32x4v* 
 // is the B operand as it stands: 2 MFMAs per piece instead of 16 f32 ones.  Forward M_p = W[:,
 // p-block]; backward M_p = its transpose (W^T applied to dh).
 typedef __bf16 bf16x8m __attribute__((ext_vector_type(8)));
+#ifndef GWN_T16B_X0_LDS
+#define GWN_T16B_X0_LDS 1  // bf16-mlp forward: piece 0 from the LDS image instead of fp32 rows
+#endif
 #ifndef GWN_T16_MLPB_SB
 #define GWN_T16_MLPB_SB 1
 #endif
@@ -1976,7 +1979,18 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
       f32x4v hacc[2];
       hacc[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
       hacc[1] = hacc[0];
-      {  // piece 0: the node features themselves (fp32)
+      if (MLPB && GWN_T16B_X0_LDS) {  // piece 0 = bf16(g): the staged image's column, no global read
+        const __bf16* xi = xs + w0 + j;
+        bf16x8m b0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          b0[e] = xi[(4 * g + e) * s16];
+          b0[4 + e] = xi[(16 + 4 * g + e) * s16];
+        }
+        t16_mlp_bp((const __bf16*)ws, 0, b0, lane, hacc);
+        if (a.xg4)  // t16_store_g4's layout, already bf16
+          *(bf16x8m*)((char*)a.xg4 + ((long)sl * nt + tile) * 1024 + lane * 16) = b0;
+      } else {  // piece 0: the node features themselves (fp32)
         f32x4v x0[2];
         t16_rows_global(hs_out, ldh, w0, n, lane, x0);
         mlp(0, x0, hacc);
