@@ -1541,7 +1541,7 @@ __device__ __forceinline__ void t16_mlp(const float* m, int ld_m, const f32x4v* 
 // p-block]; backward M_p = its transpose (W^T applied to dh).
 typedef __bf16 bf16x8m __attribute__((ext_vector_type(8)));
 #ifndef GWN_T16B_X0_LDS
-#define GWN_T16B_X0_LDS 1  // bf16-mlp forward: piece 0 from the LDS image instead of fp32 rows
+#define GWN_T16B_X0_LDS 1  // bf16 mlp: piece 0 (fwd) / dh (bwd) from the LDS image, not fp32 rows
 #endif
 #ifndef GWN_T16_MLPB_SB
 #define GWN_T16_MLPB_SB 1
@@ -1582,6 +1582,19 @@ __device__ __forceinline__ void t16_mlp_bp(const __bf16* maps, int p, const bf16
 }
 __device__ __forceinline__ void t16_mlp_b(const __bf16* maps, int p, const f32x4v* acc, int lane, f32x4v* hacc) {
   t16_mlp_bp(maps, p, t16_pack_b(acc), lane, hacc);
+}
+// node w0 + j's column of a channel-major bf16 image [32][s16] as t16_mlp_bp's B operand (channels
+// 4 g .. +3, 16 + 4 g .. +3): the bf16 mode's piece 0 / dh operand without re-reading fp32 rows
+__device__ __forceinline__ bf16x8m t16_img_col_b(const __bf16* img, int s16, int w0, int lane) {
+  const int g = lane >> 4, j = lane & 15;
+  const __bf16* xi = img + w0 + j;
+  bf16x8m b;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    b[e] = xi[(4 * g + e) * s16];
+    b[4 + e] = xi[(16 + 4 * g + e) * s16];
+  }
+  return b;
 }
 
 // both powers of one support for the wave's 16-node tile: acc[q][hf] (q = 0: G1, 1: G2) holds
@@ -1980,13 +1993,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
       hacc[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
       hacc[1] = hacc[0];
       if (MLPB && GWN_T16B_X0_LDS) {  // piece 0 = bf16(g): the staged image's column, no global read
-        const __bf16* xi = xs + w0 + j;
-        bf16x8m b0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          b0[e] = xi[(4 * g + e) * s16];
-          b0[4 + e] = xi[(16 + 4 * g + e) * s16];
-        }
+        const bf16x8m b0 = t16_img_col_b(xs, s16, w0, lane);
         t16_mlp_bp((const __bf16*)ws, 0, b0, lane, hacc);
         if (a.xg4)  // t16_store_g4's layout, already bf16
           *(bf16x8m*)((char*)a.xg4 + ((long)sl * nt + tile) * 1024 + lane * 16) = b0;
@@ -2290,7 +2297,11 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
       dx[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
       dx[1] = dx[0];
       const float* dh_rows = (a.bn_dy ? a.dh_out : a.dh) + row0 * CH;  // (BF: the fp32 rows)
-      {
+      // MLPB: the channel maps take bf16(dh), which is the staged image itself
+      const int s16b = t16b_s16(n);
+      if (MLPB && GWN_T16B_X0_LDS) {
+        t16_mlp_bp((const __bf16*)ws, 0, t16_img_col_b((const __bf16*)dhs, s16b, w0, lane), lane, dx);
+      } else {
         f32x4v d0[2];
         if (BF) t16_rows_global(dh_rows, CH, w0, n, lane, d0);
         else t16_rows(dhs, hs, w0, lane, d0);
@@ -2304,17 +2315,21 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
         mlp(2 + 2 * k, e[1], dx);
         if (k == a.adp_index) {  // t1 = W1^T dh + W2^T (A dh), t2 = W2^T dh
           f32x4v d0[2], tt[2];
-          if (BF) t16_rows_global(dh_rows, CH, w0, n, lane, d0);
+          bf16x8m db;
+          if (MLPB && GWN_T16B_X0_LDS) db = t16_img_col_b((const __bf16*)dhs, s16b, w0, lane);
+          else if (BF) t16_rows_global(dh_rows, CH, w0, n, lane, d0);
           else t16_rows(dhs, hs, w0, lane, d0);
           tt[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
           tt[1] = tt[0];
-          mlp(1 + 2 * k, d0, tt);
+          if (MLPB && GWN_T16B_X0_LDS) t16_mlp_bp((const __bf16*)ws, 1 + 2 * k, db, lane, tt);
+          else mlp(1 + 2 * k, d0, tt);
           mlp(2 + 2 * k, e[0], tt);
           if (BF && a.tg4) t16_store_g4(a.tg4, 0, a.slices, s, nt, tile, lane, tt);
           else t16_store(a.t1 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
           tt[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
           tt[1] = tt[0];
-          mlp(2 + 2 * k, d0, tt);
+          if (MLPB && GWN_T16B_X0_LDS) t16_mlp_bp((const __bf16*)ws, 2 + 2 * k, db, lane, tt);
+          else mlp(2 + 2 * k, d0, tt);
           if (BF && a.tg4) t16_store_g4(a.tg4, 1, a.slices, s, nt, tile, lane, tt);
           else t16_store(a.t2 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
         }
