@@ -307,8 +307,10 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
         # ridge (2.5 PF / 8 TB/s = 312 FLOP/B): the kernel is bounded by HBM, priced in bytes
         gbs = total_bytes / (total_ms / 1000.0) / 1e9
         t16b = getattr(acts, "g4bf_arr", None) is not None
-        kname = ("gcn_fwd_t16b_kernel<1024> (fused diffusion GCN forward, persistent 16-node tile waves, "
-                 "diffusion on bf16 MFMA operands, fp32 accumulation / mlp, 8 launches/step)" if t16b else
+        mlpb = getattr(acts, "planes", 1) == 2
+        kname = ("gcn_fwd_t16b_kernel<1024%s> (fused diffusion GCN forward, persistent 16-node tile waves, "
+                 "diffusion %s on bf16 MFMA operands, fp32 accumulation, 8 launches/step)"
+                 % ((", true", "and per-piece mlp") if mlpb else ("", "(mlp in fp32)")) if t16b else
                  "gcn_fwd_split_kernel<%d, 1, %d> (fused diffusion GCN forward, bf16 operands, 8 launches/step)"
                  % ((N + 31) // 32, (N + 31) // 32))
         traffic, mfma_busy, src = (pmc("pmc_bench_pems.json", "gcn_fwd_t16b_kernel" if t16b else "gcn_fwd_split_kernel")

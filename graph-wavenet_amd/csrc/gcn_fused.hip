@@ -1543,6 +1543,9 @@ typedef __bf16 bf16x8m __attribute__((ext_vector_type(8)));
 #ifndef GWN_T16B_X0_LDS
 #define GWN_T16B_X0_LDS 1  // bf16 mlp: piece 0 (fwd) / dh (bwd) from the LDS image, not fp32 rows
 #endif
+#ifndef GWN_T16B_PB_NT
+#define GWN_T16B_PB_NT 0  // bf16 piece stores: plain (write-back L2 merges the 8-B pieces into full lines: PEMS fwd HBM 171.6 -> 143.0 MB per launch, same time); 1 = non-temporal
+#endif
 #ifndef GWN_T16_MLPB_SB
 #define GWN_T16_MLPB_SB 1
 #endif
@@ -2015,8 +2018,13 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
             if (a.store_pieces && a.pb && w0 + j < n) {
               __bf16* bp = (__bf16*)a.pb + (row0 + w0 + j) * a.ld_pb + (2 * k + q) * CH + 4 * g;
               typedef __bf16 bf16x4p __attribute__((ext_vector_type(4)));
-              __builtin_nontemporal_store(bf16x4p{b[0], b[1], b[2], b[3]}, (bf16x4p*)bp);
-              __builtin_nontemporal_store(bf16x4p{b[4], b[5], b[6], b[7]}, (bf16x4p*)(bp + 16));
+              if (GWN_T16B_PB_NT) {
+                __builtin_nontemporal_store(bf16x4p{b[0], b[1], b[2], b[3]}, (bf16x4p*)bp);
+                __builtin_nontemporal_store(bf16x4p{b[4], b[5], b[6], b[7]}, (bf16x4p*)(bp + 16));
+              } else {
+                *(bf16x4p*)bp = bf16x4p{b[0], b[1], b[2], b[3]};
+                *(bf16x4p*)(bp + 16) = bf16x4p{b[4], b[5], b[6], b[7]};
+              }
               continue;
             }
           } else {
