@@ -309,7 +309,7 @@ typedef struct gwn_gcn_args {
    * persistent 16-node tile kernels run: one 16-wave workgroup per CU over an equal range of the
    * launch's 16-node tiles, each support fragment a 16-B load of four k-steps. */
   const float* const* sup_g4;
-  /* sup_g4b [2*nsup] (optional, bf16 operands: split_planes == 1): A_k and A_k^2 as
+  /* sup_g4b [2*nsup] (optional, bf16 operands: split_planes >= 1): A_k and A_k^2 as
    * gwn_support_g4_bf16 copies.  Given, the 16-node tile forward runs with the diffusion on bf16
    * MFMA operands (fp32 accumulation; the mlp, hop pieces, z and BN partials in fp32). */
   const void* const* sup_g4b;
@@ -354,7 +354,7 @@ long gwn_gcn_bn_partial_count(int rows, int n, int c, int nsup, int ld_sup);
 
 /* 1 iff the bf16 16-node tile gcn kernels (sup_g4b / sup_g4b_t) run for n nodes and nsup supports
  * (c == 32, their LDS fits, the t16 kernels not disabled by GWN_GCN_T16=0): the condition for
- * split_planes = 1 and for requesting xg4 / tg4 */
+ * split_planes >= 1 and for requesting xg4 / tg4 */
 int gwn_gcn_t16b_supported(int n, int nsup);
 
 /* Backward of gwn_gcn_fwd given dh (gradient w.r.t. the dropout output, i.e. dz with the
@@ -417,7 +417,7 @@ typedef struct gwn_gcn_bwd_args {
   /* sup_g4_t [2*nsup] (optional): A_k^T (index 2k) and (A_k^2)^T (2k+1) in the layout of
    * gwn_support_g4: the persistent 16-node tile backward, as gwn_gcn_args.sup_g4 */
   const float* const* sup_g4_t;
-  /* sup_g4b_t [2*nsup] (optional, bf16 operands: split_planes == 1): A_k^T and (A_k^2)^T as
+  /* sup_g4b_t [2*nsup] (optional, bf16 operands: split_planes >= 1): A_k^T and (A_k^2)^T as
    * gwn_support_g4_bf16 copies: the bf16 16-node tile backward (as sup_g4b of gwn_gcn_args) */
   const void* const* sup_g4b_t;
   /* tg4 (optional, the bf16 16-node tile kernel only): t1 / t2 of the adaptive support as bf16
