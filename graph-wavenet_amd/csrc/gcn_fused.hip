@@ -1883,8 +1883,15 @@ __device__ __forceinline__ void global_to_lds16_bf16(const float* src, long ld, 
 #define GWN_T16B_AHEAD 1  // 2: PEMS 23.65k vs 23.79k samples/s (not latency-bound on the fragments)
 #endif
 constexpr int T16B_AHEAD = GWN_T16B_AHEAD;  // support-fragment groups in flight ahead (1 or 2)
+// 12-wave bf16-mlp tile kernels (GWN_T16B_WAVES=12: 3 waves per SIMD, 168 registers): the fragment
+// ring one group deeper, the registers the 4th wave gave up paying for it
+#ifndef GWN_T16B_AHEAD12
+#define GWN_T16B_AHEAD12 2
+#endif
+__host__ __device__ constexpr int t16b_ahead(int maxt) { return maxt <= 768 ? GWN_T16B_AHEAD12 : T16B_AHEAD; }
 // both powers of one support on bf16 operands (acc as t16_diffuse); G1 / G2: gwn_support_g4_bf16
 // copies (block (kg, tile) = 64 lanes x 8 bf16)
+template <int AH = T16B_AHEAD>
 __device__ __forceinline__ void t16b_diffuse(const __bf16* img, const __bf16* G1, const __bf16* G2, int n, int tile,
                                              int lane, f32x4v (*acc)[2]) {
   const int g = lane >> 4, j = lane & 15;
@@ -1903,17 +1910,22 @@ __device__ __forceinline__ void t16b_diffuse(const __bf16* img, const __bf16* G1
     return __builtin_bit_cast(bf16x8b, __builtin_amdgcn_raw_buffer_load_b128(r, off(kg), 0, 0));
   };
   bf16x8b b1 = ld(r1, 0), b2 = ld(r2, 0);
-  bf16x8b c1 = T16B_AHEAD > 1 ? ld(r1, 1) : b1, c2 = T16B_AHEAD > 1 ? ld(r2, 1) : b2;
+  bf16x8b c1 = AH > 1 ? ld(r1, 1) : b1, c2 = AH > 1 ? ld(r2, 1) : b2;
+  bf16x8b d1 = AH > 2 ? ld(r1, 2) : b1, d2 = AH > 2 ? ld(r2, 2) : b2;
   bf16x8b a0 = *(const bf16x8b*)x0, a1 = *(const bf16x8b*)x1;
   for (int kg = 0; kg < nkg; ++kg) {
-    const bf16x8b nb1 = ld(r1, kg + T16B_AHEAD), nb2 = ld(r2, kg + T16B_AHEAD);
+    const bf16x8b nb1 = ld(r1, kg + AH), nb2 = ld(r2, kg + AH);
     const int nx = kg + 1 < nkg ? 32 * (kg + 1) : 32 * kg;
     const bf16x8b na0 = *(const bf16x8b*)(x0 + nx), na1 = *(const bf16x8b*)(x1 + nx);
     acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, acc[0][0], 0, 0, 0);
     acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc[0][1], 0, 0, 0);
     acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b2, acc[1][0], 0, 0, 0);
     acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b2, acc[1][1], 0, 0, 0);
-    if (T16B_AHEAD > 1) {
+    if (AH > 2) {
+      b1 = c1; b2 = c2;
+      c1 = d1; c2 = d2;
+      d1 = nb1; d2 = nb2;
+    } else if (AH > 1) {
       b1 = c1; b2 = c2;
       c1 = nb1; c2 = nb2;
     } else {
@@ -2008,7 +2020,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
       }
       for (int k = 0; k < a.nsup; ++k) {
         f32x4v acc[2][2];
-        t16b_diffuse(xs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, acc);
+        t16b_diffuse<t16b_ahead(MAXT)>(xs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, acc);
         if (a.xg4 && k == a.xg4_k) t16_store_g4(a.xg4, 1, a.slices, sl, nt, tile, lane, acc[0]);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -2317,7 +2329,7 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
       }
       for (int k = 0; k < a.nsup; ++k) {
         f32x4v e[2][2];
-        if (BF) t16b_diffuse((const __bf16*)dhs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, e);
+        if (BF) t16b_diffuse<t16b_ahead(MAXT)>((const __bf16*)dhs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, e);
         else t16_diffuse(dhs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, e);
         mlp(1 + 2 * k, e[0], dx);
         mlp(2 + 2 * k, e[1], dx);
@@ -2681,6 +2693,11 @@ static bool fold_last_enabled() {
   const char* e = getenv("GWN_BN_FOLD_LAST");
   return e && e[0] == '1';
 }
+// GWN_T16B_WAVES=12: the bf16-mlp tile kernels as 12-wave workgroups (t16b_ahead)
+static bool t16b_waves12() {
+  const char* e = getenv("GWN_T16B_WAVES");
+  return e && e[0] == '1' && e[1] == '2';
+}
 
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded, hipStream_t s) {
   *folded = false;
@@ -2734,6 +2751,8 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
                                   T16_LDS_MAX);
         (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b_kernel<1024, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
+        (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b_kernel<768, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
         attr_b = true;
       }
       const int nt = (g->n + 15) / 16;
@@ -2751,7 +2770,9 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
       a.ksplit = 1;
       a.bn_slots = (int)gwn_bn_part_slots(slices);
       if (fold_here) a.fold = *g->bn_fold;
-      if (g->split_planes == 2) gcn_fwd_t16b_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      if (g->split_planes == 2 && t16b_waves12() && !fold_here)
+        gcn_fwd_t16b_kernel<768, true><<<grid, 768, lds, s>>>(a, p, maximg);
+      else if (g->split_planes == 2) gcn_fwd_t16b_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       else gcn_fwd_t16b_kernel<1024><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       GWN_CHECK_LAUNCH();
       *folded = fold_here;
@@ -2864,6 +2885,8 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
       if (!attr_b) {
         (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<1024, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
+        (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<768, true, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
         (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<1024, true, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
         attr_b = true;
@@ -2881,7 +2904,8 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
       PowSup p = {};
       for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = (const float*)g->sup_g4b_t[k];
       a.ksplit = 1;
-      if (g->split_planes == 2) gcn_bwd_t16_kernel<1024, true, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      if (g->split_planes == 2 && t16b_waves12()) gcn_bwd_t16_kernel<768, true, true><<<grid, 768, lds, s>>>(a, p, maximg);
+      else if (g->split_planes == 2) gcn_bwd_t16_kernel<1024, true, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       else gcn_bwd_t16_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       GWN_CHECK_LAUNCH();
       return GWN_OK;
