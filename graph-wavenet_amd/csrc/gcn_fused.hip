@@ -1067,6 +1067,9 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_pow_kernel(const FusedFwd a, 
 // ---------------------------------------------------------------------------------------------
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int T16_RING = 4;   // k-steps (4 support rows each) of support fragments in flight
+#ifndef GWN_T16_PIECE_NT
+#define GWN_T16_PIECE_NT 1  // fp32 hop-piece stores of the 16-node tile forward non-temporal (0: plain)
+#endif
 constexpr int T16_WAVES = 16; // waves of a t16 workgroup (one workgroup per CU, persistent over a tile range)
 constexpr int T16_MAXIMG = 4; // slice images a workgroup holds at once (LDS permitting)
 // Tile order within a phase: slice-major (wave w takes every 16th tile).  GWN_T16_COLMAJOR=1:
@@ -1779,7 +1782,8 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
             float* dp = hs_out + (long)(w0 + j) * ldh + (1 + 2 * k + q) * CH + 4 * g;
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
-              if (nt_ok) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
+              if (nt_ok && GWN_T16_PIECE_NT) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
+              else if (nt_ok) *(f32x4v*)(dp + 16 * hf) = acc[q][hf];
               else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) dp[16 * hf + e] = acc[q][hf][e];
@@ -2057,7 +2061,8 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
             float* dp = hs_out + (long)(w0 + j) * ldh + (1 + 2 * k + q) * CH + 4 * g;
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
-              if (nt_ok) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
+              if (nt_ok && GWN_T16_PIECE_NT) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
+              else if (nt_ok) *(f32x4v*)(dp + 16 * hf) = acc[q][hf];
               else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) dp[16 * hf + e] = acc[q][hf][e];
