@@ -192,7 +192,9 @@ def main():
             "data": "synthetic (%s, seeded; random-init weights)"
                     % ("METR-LA tensor format" if not cfg["dense"] else "METR-LA tensor format, dense random graph"),
             "config": {"workload": cfg["workload"].format(
-                           dtype="bf16 MFMA operands with fp32 accumulation in the diffusion GCN" if bf16 else "fp32"),
+                           dtype=("bf16 MFMA operands with fp32 accumulation in the diffusion GCN (%s)"
+                                  % ("diffusion and per-piece mlp" if os.environ.get("GWN_BF16_MLP", "1") != "0"
+                                     else "diffusion; mlp in fp32")) if bf16 else "fp32"),
                        "global_batch": B * world, "nodes": N, "seq_len": T,
                        "parallelism": "dp%d" % world if world > 1 else "single"},
             "mae12": round(mae12, 6), "mae12_oracle_f64": round(mae12_ref, 6),
