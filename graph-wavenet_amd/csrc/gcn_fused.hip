@@ -1067,6 +1067,9 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_pow_kernel(const FusedFwd a, 
 // ---------------------------------------------------------------------------------------------
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int T16_RING = 4;   // k-steps (4 support rows each) of support fragments in flight
+#ifndef GWN_T16_GATE_PF
+#define GWN_T16_GATE_PF 0  // 1: the backward's gate rows pulled into L2 at tile start (measured: PEMS bwd -10 us, METR +6 us)
+#endif
 #ifndef GWN_T16_PIECE_NT
 #define GWN_T16_PIECE_NT 1  // fp32 hop-piece stores of the 16-node tile forward non-temporal (0: plain)
 #endif
@@ -2285,6 +2288,11 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
     else t16_mlp(ws + piece * CH * LDW16, LDW16, x, lane, out);
   };
   const T16Range rg = t16_range(a.slices, nt);
+  const __amdgpu_buffer_rsrc_t gate_rf = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.fg, (short)0, (int)min((long)a.slices * n * 2 * CH * 4, 0x7fffffffL), 0x00020000);
+  const __amdgpu_buffer_rsrc_t gate_rd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.dskip, (short)0, a.dskip ? (int)min(max((long)a.slices * n - a.skip_row0, 0L) * a.ld_dskip * 4, 0x7fffffffL) : 0,
+      0x00020000);
   if (a.bn_dy && blockIdx.x == 0 && threadIdx.x < CH) {
     if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
     if (a.bn_dgamma) a.bn_dgamma[threadIdx.x] = a.bn_sums[CH + threadIdx.x];
@@ -2322,6 +2330,20 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
       dx[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
       dx[1] = dx[0];
       const float* dh_rows = (a.bn_dy ? a.dh_out : a.dh) + row0 * CH;  // (BF: the fp32 rows)
+      // the gate epilogue's rows pulled into L2 now (one 4-B load per 128-B line: lane (node k,
+      // part) -> fg line part 0 / 1, dskip line part 2), consumed by a no-op at the epilogue so the
+      // loads stay issued here: the epilogue's loads then hit L2 instead of waiting on HBM
+      int pf1 = 0, pf2 = 0;
+      if (GWN_T16_GATE_PF && a.dfg) {
+        const int k = lane >> 2, part = lane & 3, wk = w0 + k;
+        const long mk = row0 + wk;
+        const bool ok = wk < n;
+        const int ofg = (ok && part < 2) ? (int)((mk * 2 * CH + part * 32) * 4) : 0x7ffffff0;
+        const int ods = (ok && part == 2 && a.dskip && mk >= a.skip_row0)
+                            ? (int)((mk - a.skip_row0) * a.ld_dskip * 4) : 0x7ffffff0;
+        pf1 = (int)__builtin_amdgcn_raw_buffer_load_b32(gate_rf, ofg, 0, 0);
+        pf2 = (int)__builtin_amdgcn_raw_buffer_load_b32(gate_rd, ods, 0, 0);
+      }
       // MLPB: the channel maps take bf16(dh), which is the staged image itself
       const int s16b = t16b_s16(n);
       if (MLPB && GWN_T16B_X0_LDS) {
@@ -2364,6 +2386,7 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
         continue;
       }
       // gate backward (gate_bwd_kernel's arithmetic): g = dxg (+ dskip) -> dfg via (tanh f, sigmoid s)
+      if (GWN_T16_GATE_PF) asm volatile("" ::"v"(pf1), "v"(pf2));
       const int w = w0 + j;
       if (w >= n) continue;
       const long m = row0 + w;
