@@ -133,6 +133,10 @@ def main():
     eng.model.set_compute_dtype("bf16" if bf16 else "fp32")
     eng.broadcast_parameters(0)
     ex = eng.model.executor()
+    # the operand format the fused GCN kernels actually run (0: fp32, also when bf16 was requested
+    # for a shape without a bf16 tile kernel; 1: bf16 diffusion; 2: bf16 diffusion and mlp)
+    planes = ex.split_planes()
+    bf16 = planes > 0
     ex.seed.fill_(12345 + 7919 * rank)
 
     nb = 8 if N <= 512 else 2  # distinct resident batches, cycled
@@ -193,8 +197,8 @@ def main():
                     % ("METR-LA tensor format" if not cfg["dense"] else "METR-LA tensor format, dense random graph"),
             "config": {"workload": cfg["workload"].format(
                            dtype=("bf16 MFMA operands with fp32 accumulation in the diffusion GCN (%s)"
-                                  % ("diffusion and per-piece mlp" if os.environ.get("GWN_BF16_MLP", "1") != "0"
-                                     else "diffusion; mlp in fp32")) if bf16 else "fp32"),
+                                  % ("diffusion and per-piece mlp" if planes == 2 else "diffusion; mlp in fp32"))
+                           if bf16 else "fp32"),
                        "global_batch": B * world, "nodes": N, "seq_len": T,
                        "parallelism": "dp%d" % world if world > 1 else "single"},
             "mae12": round(mae12, 6), "mae12_oracle_f64": round(mae12_ref, 6),

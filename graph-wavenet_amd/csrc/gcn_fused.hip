@@ -1067,22 +1067,10 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_fwd_pow_kernel(const FusedFwd a, 
 // ---------------------------------------------------------------------------------------------
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int T16_RING = 4;   // k-steps (4 support rows each) of support fragments in flight
-#ifndef GWN_T16_GATE_PF
-#define GWN_T16_GATE_PF 0  // 1: the backward's gate rows pulled into L2 at tile start (measured: PEMS bwd -10 us, METR +6 us)
-#endif
-#ifndef GWN_T16_PIECE_NT
-#define GWN_T16_PIECE_NT 1  // fp32 hop-piece stores of the 16-node tile forward non-temporal (0: plain)
-#endif
 constexpr int T16_WAVES = 16; // waves of a t16 workgroup (one workgroup per CU, persistent over a tile range)
 constexpr int T16_MAXIMG = 4; // slice images a workgroup holds at once (LDS permitting)
-// Tile order within a phase: slice-major (wave w takes every 16th tile).  GWN_T16_COLMAJOR=1:
-// column-major (a node-tile column of every staged slice, slice fastest), so that the waves of
-// consecutive indices -- one per SIMD -- diffuse the same support column at once and share its
-// fragment loads in L1: measured slower (the fragment traffic from L2 is not what bounds it).
-#ifndef GWN_T16_COLMAJOR
-#define GWN_T16_COLMAJOR 0  // measured slower: METR 23.98k vs 24.99k, PEMS 22.95k vs 23.89k samples/s
-#endif
-constexpr bool T16_COLMAJOR = GWN_T16_COLMAJOR != 0;
+// Tile order within a phase: slice-major (wave w takes every 16th tile; a column-major order
+// sharing support fragments in L1 measured slower).
 
 // rows of a slice image: the tiles' rows, and the diffusion loop's reads (4 rows per k-step, one
 // k-step ahead, whole rings of T16_RING k-steps); rows >= n are zero
@@ -1095,15 +1083,9 @@ __host__ __device__ inline int t16_img_rows(int n) {
 // Slice image in LDS: two channel halves, each [rows][16] (no padding): lane (g, j) of the
 // diffusion's A-operand read (row 4 ks + g, channel 16 hf + j) hits bank 16 g + j of 64.  The
 // half stride hs = rows * 16 floats is a multiple of 64 (ds_read2st64 pairs the two halves).
-// the t16 kernels' 16-B output stores (z, dres / dh_out, dxg / t1 / t2, dfg): plain by default
-// (-DGWN_T16_NT=1: non-temporal)
-#ifndef GWN_T16_NT
-#define GWN_T16_NT 0  // measured: non-temporal 24.64k / 23.54k vs plain 24.79k / 23.67k samples/s (METR / PEMS)
-#endif
-__device__ __forceinline__ void t16_st4(float* p, float4 v) {
-  if (GWN_T16_NT) __builtin_nontemporal_store(f32x4v{v.x, v.y, v.z, v.w}, (f32x4v*)p);
-  else *(float4*)p = v;
-}
+// the t16 kernels' 16-B output stores (z, dres / dh_out, dxg / t1 / t2, dfg): plain (non-temporal
+// measured slower: 24.64k / 23.54k vs 24.79k / 23.67k samples/s METR / PEMS)
+__device__ __forceinline__ void t16_st4(float* p, float4 v) { *(float4*)p = v; }
 constexpr int LDW16 = 36;  // LDS row stride of the staged channel maps: lane groups g hit banks 16 g + j
 
 // LDS of a t16 workgroup: the channel maps of all 2K+1 pieces (32 x LDW16 floats each), the waves'
@@ -1112,18 +1094,12 @@ size_t t16_lds_bytes(int n, int nsup, int maximg) {
   return (size_t)((2 * nsup + 1) * CH * LDW16 + T16_WAVES * 3 * CH + maximg * t16_img_rows(n) * CH) * sizeof(float);
 }
 
-// the channel maps M_p[out][in] of pieces p < npieces into LDS as m[(p*32 + out)*LDW16 + in] (a
-// lane's four consecutive input channels one ds_read_b128 in t16_mlp), from the mlp weights W
-// [32][ld_w] (row = mlp output channel): forward M_p = W[:, p-block] (rows of W, 16-B loads);
-// backward M_p = W[:, p-block]^T (M_p[c][o] = W[o][p*32 + c]: strided 4-B loads)
-#ifndef GWN_T16_MLP128
-#define GWN_T16_MLP128 0  // 0: the round-3 layout m[(p*32 + in)*LDW16 + out], 16 ds_read_b32 per piece
-#endif
+// the channel maps M_p[out][in] of pieces p < npieces into LDS transposed, m[(p*32 + in)*LDW16 +
+// out] (t16_mlp's 16 ds_read_b32 per piece; the untransposed layout read as ds_read_b128 measured no
+// faster), from the mlp weights W [32][ld_w] (row = mlp output channel): forward M_p = W[:,
+// p-block] (strided 4-B loads), backward M_p = W[:, p-block]^T (rows of W, 16-B loads)
 __device__ __forceinline__ void t16_stage_maps(const float* w, int ld_w, bool backward, int npieces, float* dst) {
-  if (!GWN_T16_MLP128) {
-    backward = !backward;  // the transposed layout: the other gather
-  }
-  if (!backward) {
+  if (backward) {
     const int total = npieces * CH * 8;  // float4s
     for (int e = threadIdx.x; e < total; e += blockDim.x) {
       const int r = e >> 3, q = e & 7;  // r = p*32 + out
@@ -1219,30 +1195,15 @@ __device__ __forceinline__ float row16_sum(float x) {
 }
 
 // A wave's running BatchNorm partial over its tiles (Chan merge in tile order): lane (g, j) keeps
-// the 8 channels 16 (q >> 2) + 4 g + (q & 3) of its row group (lane j = 0 of a group is the one read)
-// GWN_T16_BN_LDS=1: the running partials live in the wave's BN slot of LDS (the flush's wpart
-// layout, updated by lane j == 0 of each row group) instead of 16 registers per lane (off: no gain)
-#ifndef GWN_T16_BN_LDS
-#define GWN_T16_BN_LDS 0  // 1: PEMS 23.79k vs 23.89k, METR equal (the freed registers buy nothing)
-#endif
-constexpr bool T16_BN_LDS = GWN_T16_BN_LDS != 0;
+// the 8 channels 16 (q >> 2) + 4 g + (q & 3) of its row group (lane j = 0 of a group is the one read;
+// keeping them in the wave's LDS slot instead measured no faster)
 struct BnRun {
-  float n, mean[T16_BN_LDS ? 1 : 8], m2[T16_BN_LDS ? 1 : 8];
-  float* wp;  // T16_BN_LDS: this wave's [3][32] slot of wpart (n, mean, M2 per channel)
+  float n, mean[8], m2[8];
 };
-// zero state; T16_BN_LDS: the wave clears its own slot (read back only by its own lanes before the
-// flush's barrier)
-__device__ __forceinline__ void bn_init(BnRun& bn, float* wpart) {
+__device__ __forceinline__ void bn_init(BnRun& bn, float*) {
   bn.n = 0.0f;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  bn.wp = wpart + wave * 3 * 32;
-  if (T16_BN_LDS) {
-    bn.wp[lane] = 0.0f;
-    if (lane < 32) bn.wp[64 + lane] = 0.0f;
-  } else {
 #pragma unroll
-    for (int q = 0; q < (T16_BN_LDS ? 1 : 8); ++q) bn.mean[q] = bn.m2[q] = 0.0f;
-  }
+  for (int q = 0; q < 8; ++q) bn.mean[q] = bn.m2[q] = 0.0f;
 }
 
 // z tile epilogue (fwd_tile_epilogue's arithmetic on the 16-node tile layout): bias, dropout,
@@ -1296,30 +1257,8 @@ __device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* ha
   const float cnt = (float)min(16, n - w0);
   const float inv = 1.0f / cnt;
   const float tot = bn.n + cnt;
-  if (T16_BN_LDS) {
-    float mq[8], qq[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      mq[q] = row16_sum(valid ? v[q] : 0.0f) * inv;
-      const float d = valid ? v[q] - mq[q] : 0.0f;
-      qq[q] = row16_sum(d * d);
-    }
-    if (j == 0) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int c = 16 * (q >> 2) + 4 * g + (q & 3);
-        const float om = bn.wp[CH + c], o2 = bn.wp[2 * CH + c];
-        const float dm = mq[q] - om;
-        bn.wp[CH + c] = om + dm * (cnt / tot);
-        bn.wp[2 * CH + c] = o2 + qq[q] + dm * dm * (bn.n * cnt / tot);
-        bn.wp[c] = tot;
-      }
-    }
-    bn.n = tot;
-    return;
-  }
-#pragma unroll
-  for (int q = 0; q < (T16_BN_LDS ? 1 : 8); ++q) {
+  for (int q = 0; q < 8; ++q) {
     const float mean = row16_sum(valid ? v[q] : 0.0f) * inv;
     const float d = valid ? v[q] - mean : 0.0f;
     const float m2 = row16_sum(d * d);
@@ -1332,20 +1271,6 @@ __device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* ha
 
 // the waves' running partials (wave order) -> the workgroup's BN partial, slot blockIdx.x
 __device__ void t16_bn_fold_last(const FusedFwd& a, float* lds, const float* wv, const float* bv);
-#ifndef GWN_FOLD_EXP
-#define GWN_FOLD_EXP 0
-#endif
-// GWN_FOLD_EXP == 3 (timing probe builds only): phase timestamps of the last workgroup written past
-// the grid's partial slots
-#if GWN_FOLD_EXP == 3
-#define FOLD_TS(a, k)                                                                                  \
-  do {                                                                                                 \
-    if (threadIdx.x == 0)                                                                              \
-      ((unsigned long long*)((a).bn_part + (long)gridDim.x * 3 * CH))[k] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define FOLD_TS(a, k) do {} while (0)
-#endif
 
 __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn, float* wpart) {
   if (a.bn_part == nullptr || a.x_out) return;
@@ -1362,10 +1287,10 @@ __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn,
     }
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
-  if (!T16_BN_LDS && j == 0) {  // (T16_BN_LDS: the slots already hold the running partials)
+  if (j == 0) {
     float* wp = wpart + wave * 3 * CH;
 #pragma unroll
-    for (int q = 0; q < (T16_BN_LDS ? 1 : 8); ++q) {
+    for (int q = 0; q < 8; ++q) {
       const int c = 16 * (q >> 2) + 4 * g + (q & 3);
       wp[c] = bn.n;
       wp[CH + c] = bn.mean[q];
@@ -1405,7 +1330,6 @@ __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn,
   }
   if (fold) {
     if (split_arrive(a.fold.arrive, gridDim.x, (int*)wpart)) {
-      FOLD_TS(a, 0);
       t16_bn_fold_last(a, wpart + 4, wv, bv);
     }
     return;
@@ -1449,8 +1373,6 @@ __device__ void t16_bn_fold_last(const FusedFwd& a, float* lds, const float* wv,
       n = nn;
     }
   }
-#pragma unroll
-  FOLD_TS(a, 1);
   for (int off = 16; off > 0; off >>= 1) {
     const double nb = __shfl_down(n, off, 32), mb = __shfl_down(mean, off, 32), qb = __shfl_down(m2, off, 32);
     if (sub < off && nb > 0.0) {
@@ -1475,7 +1397,6 @@ __device__ void t16_bn_fold_last(const FusedFwd& a, float* lds, const float* wv,
     lds[j] = sc;
   }
   if (threadIdx.x == 0 && f.num_batches_tracked) *f.num_batches_tracked += 1;
-  FOLD_TS(a, 2);
   if (!f.w_next) return;
   __syncthreads();
   // w_fold[row][k] = w_next[row][k] * scale[k % c]; b_fold[row] = b_next[row] + sum_k w_next[row][k] *
@@ -1491,52 +1412,30 @@ __device__ void t16_bn_fold_last(const FusedFwd& a, float* lds, const float* wv,
   for (int off = 8; off > 0; off >>= 1) s += __shfl_down(s, off, 16);
   const int row = threadIdx.x >> 4;
   if ((threadIdx.x & 15) == 0) f.b_fold[row] = f.b_next[row] + s;
-  if (GWN_FOLD_EXP == 3) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    FOLD_TS(a, 3);
-  }
 }
 
 // the channel map of one piece held in accumulators acc[hf] (register s = input channel
 // 16 hf + 4 g + s): hacc[oh] (output channel 16 oh + 4 g + r) += M x piece with the A operand
-// M[out][in] read as m[out * ld_m + in] (t16_stage_maps: forward the piece's block of W, backward
+// M[out][in] read as m[in * ld_m + out] (t16_stage_maps: forward the piece's block of W, backward
 // its transpose, i.e. W^T applied to dh)
 __device__ __forceinline__ void t16_mlp(const float* m, int ld_m, const f32x4v* acc, int lane, f32x4v* hacc) {
   const int g = lane >> 4, j = lane & 15;
-  if (!GWN_T16_MLP128) {
-    float wf[2][2][4];
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int oh = 0; oh < 2; ++oh) wf[hf][oh][s] = m[(16 * hf + 4 * g + s) * ld_m + 16 * oh + j];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int oh = 0; oh < 2; ++oh)
-          hacc[oh] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[hf][oh][s], acc[hf][s], hacc[oh], 0, 0, 0);
-    return;
-  }
-  float4 wq[2][2];  // [hf][oh]: M[16 oh + j][16 hf + 4 g .. + 3]
+  float wf[2][2][4];
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-    for (int oh = 0; oh < 2; ++oh) wq[hf][oh] = *(const float4*)(m + (16 * oh + j) * ld_m + 16 * hf + 4 * g);
-  // all four fragment reads in flight before the first product (one LDS latency)
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int oh = 0; oh < 2; ++oh) wf[hf][oh][s] = m[(16 * hf + 4 * g + s) * ld_m + 16 * oh + j];
+  // all fragment reads in flight before the first product (one LDS latency)
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int oh = 0; oh < 2; ++oh) {
-        const float wv = s == 0 ? wq[hf][oh].x : s == 1 ? wq[hf][oh].y : s == 2 ? wq[hf][oh].z : wq[hf][oh].w;
-        hacc[oh] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv, acc[hf][s], hacc[oh], 0, 0, 0);
-      }
+      for (int oh = 0; oh < 2; ++oh)
+        hacc[oh] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[hf][oh][s], acc[hf][s], hacc[oh], 0, 0, 0);
 }
 
 // bf16 mlp (gwn_dtype GWN_DTYPE_BF16_MLP, the bf16 tile kernels): a piece's channel map as
@@ -1546,15 +1445,6 @@ __device__ __forceinline__ void t16_mlp(const float* m, int ld_m, const f32x4v* 
 // is the B operand as it stands: 2 MFMAs per piece instead of 16 f32 ones.  Forward M_p = W[:,
 // p-block]; backward M_p = its transpose (W^T applied to dh).
 typedef __bf16 bf16x8m __attribute__((ext_vector_type(8)));
-#ifndef GWN_T16B_X0_LDS
-#define GWN_T16B_X0_LDS 1  // bf16 mlp: piece 0 (fwd) / dh (bwd) from the LDS image, not fp32 rows
-#endif
-#ifndef GWN_T16B_PB_NT
-#define GWN_T16B_PB_NT 0  // bf16 piece stores: plain (write-back L2 merges the 8-B pieces into full lines: PEMS fwd HBM 171.6 -> 143.0 MB per launch, same time); 1 = non-temporal
-#endif
-#ifndef GWN_T16_MLPB_SB
-#define GWN_T16_MLPB_SB 1
-#endif
 __device__ __forceinline__ int mlp_perm(int g, int e) { return e < 4 ? 4 * g + e : 16 + 4 * g + (e - 4); }
 __device__ __forceinline__ void t16_stage_maps_bf16(const float* w, int ld_w, bool backward, int npieces, __bf16* dst) {
   for (int t = threadIdx.x; t < npieces * 2 * 64; t += blockDim.x) {
@@ -1585,7 +1475,7 @@ __device__ __forceinline__ bf16x8m t16_pack_b(const f32x4v* acc) {
 __device__ __forceinline__ void t16_mlp_bp(const __bf16* maps, int p, const bf16x8m b, int lane, f32x4v* hacc) {
   const bf16x8m a0 = *(const bf16x8m*)(maps + ((p * 2 + 0) * 64 + lane) * 8);
   const bf16x8m a1 = *(const bf16x8m*)(maps + ((p * 2 + 1) * 64 + lane) * 8);
-  if (GWN_T16_MLPB_SB) __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_sched_barrier(0);
   hacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b, hacc[0], 0, 0, 0);
   hacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b, hacc[1], 0, 0, 0);
 }
@@ -1614,8 +1504,12 @@ __device__ __forceinline__ bf16x8m t16_img_col_b(const __bf16* img, int s16, int
 // (tools/t16_loop_probe.hip, 16 waves per CU: L1 / address processing per load instruction),
 // these at 0.93.  Fragments run one group (4 k-steps) ahead: the group's load pair is issued
 // before the previous group's products, so every wait is vmcnt(2).
-__device__ __forceinline__ void t16_diffuse(const float* img, int hs, const float* G1, const float* G2, int n, int tile,
-                                            int lane, f32x4v (*acc)[2]) {
+// S > 1: the wave diffuses S slice images (the same 16-node column of S slices) against the same
+// support fragments -- each 16-B fragment load feeds 4 S MFMAs, and the S slices' products are
+// independent chains (acc[s][q][hf]).
+template <int S>
+__device__ __forceinline__ void t16_diffuse_s(const float* const (&img)[S], int hs, const float* G1, const float* G2,
+                                              int n, int tile, int lane, f32x4v (&acc)[S][2][2]) {
   const int g = lane >> 4, j = lane & 15;
   const int nt = (n + 15) >> 4, nkg = nt;  // k-groups of 16 rows: ceil(n / 16), as the column tiles
   const int bytes = nkg * nt * 1024;
@@ -1628,10 +1522,18 @@ __device__ __forceinline__ void t16_diffuse(const float* img, int hs, const floa
   a2[0] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r2, off(0), 0, 0));
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int q = 0; q < 2; ++q) acc[q][0] = acc[q][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-  const float* xp = img + g * 16 + j;
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) acc[s][q][0] = acc[s][q][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  const float* xp[S];
   // image operands one k-step ahead: the LDS latency hides behind the current step's products
-  float xa = xp[0], xb = xp[hs];
+  float xa[S], xb[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    xp[s] = img[s] + g * 16 + j;
+    xa[s] = xp[s][0];
+    xb[s] = xp[s][hs];
+  }
   // group kg (fragments in buffer kg & 1); the next group's pair is requested first (past the
   // last group the offsets leave the buffer range: zeros, no traffic)
   auto group = [&](int kg, int bsel) {
@@ -1641,14 +1543,25 @@ __device__ __forceinline__ void t16_diffuse(const float* img, int hs, const floa
     for (int i = 0; i < 4; ++i) {
       const int ks = 4 * kg + i;
       // the image has 4 * nkp + 4 rows (t16_img_rows): step nkp's read stays inside
-      const float na = xp[4 * (ks + 1) * 16], nb = xp[hs + 4 * (ks + 1) * 16];
+      float na[S], nb[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        na[s] = xp[s][4 * (ks + 1) * 16];
+        nb[s] = xp[s][hs + 4 * (ks + 1) * 16];
+      }
       __builtin_amdgcn_sched_barrier(0);
-      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, a1[bsel][i], acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb, a1[bsel][i], acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, a2[bsel][i], acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb, a2[bsel][i], acc[1][1], 0, 0, 0);
-      xa = na;
-      xb = nb;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        acc[s][0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], a1[bsel][i], acc[s][0][0], 0, 0, 0);
+        acc[s][0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s], a1[bsel][i], acc[s][0][1], 0, 0, 0);
+        acc[s][1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], a2[bsel][i], acc[s][1][0], 0, 0, 0);
+        acc[s][1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s], a2[bsel][i], acc[s][1][1], 0, 0, 0);
+      }
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        xa[s] = na[s];
+        xb[s] = nb[s];
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -1658,6 +1571,35 @@ __device__ __forceinline__ void t16_diffuse(const float* img, int hs, const floa
     group(kg + 1, 1);
   }
   if (kg < nkg) group(kg, 0);
+}
+__device__ __forceinline__ void t16_diffuse(const float* img, int hs, const float* G1, const float* G2, int n, int tile,
+                                            int lane, f32x4v (&acc)[1][2][2]) {
+  const float* const im[1] = {img};
+  t16_diffuse_s<1>(im, hs, G1, G2, n, tile, lane, acc);
+}
+
+// t16_mlp for S slices' pieces with the same channel map (its fragments read once): x(s, hf) is
+// slice s's piece half hf, hacc[s] its output accumulators
+template <int S, typename X>
+__device__ __forceinline__ void t16_mlp_s(const float* m, int ld_m, X x, int lane, f32x4v (&hacc)[S][2]) {
+  const int g = lane >> 4, j = lane & 15;
+  float wf[2][2][4];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int oh = 0; oh < 2; ++oh) wf[hf][oh][s] = m[(16 * hf + 4 * g + s) * ld_m + 16 * oh + j];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int oh = 0; oh < 2; ++oh)
+#pragma unroll
+        for (int sp = 0; sp < S; ++sp)
+          hacc[sp][oh] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[hf][oh][s], x(sp, hf)[s], hacc[sp][oh], 0, 0, 0);
 }
 
 // the image rows of the wave's tile as B operands in the permuted channel order of t16_mlp
@@ -1699,20 +1641,10 @@ __device__ __forceinline__ void t16_store_g4(void* base, int which, int slices, 
   *(bf16x8g*)((char*)base + (((long)which * slices + slice) * nt + tile) * 1024 + lane * 16) = r;
 }
 
-// GWN_T16_PROBE builds (tools/exp/t16_probe.py only): per-workgroup s_memrealtime stamps into
-// kws (unused by the 16-node tile path): [block][20] = start, first phase staged, wave 0..15
-// loop end, after the BN flush
-#ifdef GWN_T16_PROBE
-#define T16_TS(a, k)                                                                            \
-  do {                                                                                          \
-    if ((threadIdx.x & 63) == 0 && (a).kws)                                                     \
-      ((unsigned long long*)(a).kws)[blockIdx.x * 20 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define T16_TS(a, k) do {} while (0)
-#endif
-
-template <int MAXT>
+// SPW slices per wave: the range is cut over slice GROUPS (SPW consecutive slices) x node tiles;
+// a wave's unit is one 16-node column of every slice of a group, the group's diffusions sharing
+// the support fragments (t16_diffuse_s) and its mlps the channel-map fragments (t16_mlp_s)
+template <int MAXT, int SPW>
 __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, const PowSup p, const int maximg) {
   extern __shared__ float lds[];
   const int n = a.n;
@@ -1724,8 +1656,9 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int nwaves = blockDim.x >> 6;
   const long ldh = a.ld_h;
-  const T16Range rg = t16_range(a.slices, nt);
-  if (threadIdx.x == 0) T16_TS(a, 0);
+  const int groups = (a.slices + SPW - 1) / SPW;
+  const int gimg = maximg / SPW;  // groups a phase holds
+  const T16Range rg = t16_range(groups, nt);
   BnRun bn;
   bn_init(bn, wpart);
   // the phase's slices staged in one pass (stage_rows4; the channel maps inside its first round
@@ -1733,9 +1666,10 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
   if (!h16) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
   for (long p0 = rg.tb; p0 < rg.te;) {
-    const int s0 = (int)(p0 / nt);
-    const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
-    const int s1 = (int)((p1 - 1) / nt);
+    const int q0 = (int)(p0 / nt);
+    const long p1 = min(rg.te, (long)(q0 + gimg) * nt);
+    const int q1 = (int)((p1 - 1) / nt);
+    const int s0 = q0 * SPW, s1 = min((q1 + 1) * SPW, a.slices) - 1;
     if (p0 != rg.tb) __syncthreads();  // the previous phase's images are released
     if (h16) {
       const bool maps = p0 == rg.tb;
@@ -1749,59 +1683,62 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
       for (int s = s0; s <= s1; ++s) global_to_lds16(a.h + (long)s * n * ldh, ldh, n, rows_img, imgs + (s - s0) * imgf);
     }
     __syncthreads();
-    if (threadIdx.x == 0 && p0 == rg.tb) T16_TS(a, 1);
-    const int nsl = s1 - s0 + 1;
-    const int span = T16_COLMAJOR ? nt * nsl : (int)(p1 - p0);
+    const int span = (int)(p1 - p0);
     for (int tp = wave; tp < span; tp += nwaves) {
-      long t;
-      if (T16_COLMAJOR) {  // column tp / nsl of slice s0 + tp % nsl
-        const int c = tp / nsl;
-        t = (long)(s0 + tp - c * nsl) * nt + c;
-        if (t < p0 || t >= p1) continue;
-      } else {
-        t = p0 + tp;
-      }
-      const int s = (int)(t / nt), tile = (int)(t - (long)s * nt);
-      const float* xs = imgs + (s - s0) * imgf;
-      const long row0 = (long)s * n;
-      float* hs_out = (float*)a.h + row0 * ldh;
-      const bool nt_ok = ((((uintptr_t)hs_out) & 15) | (ldh & 3)) == 0;
+      const long t = p0 + tp;
+      const int q = (int)(t / nt), tile = (int)(t - (long)q * nt);
       const int w0 = 16 * tile;
-      f32x4v hacc[2];
-      hacc[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-      hacc[1] = hacc[0];
+      int sl[SPW];
+      bool ok[SPW];
+      const float* xs[SPW];
+#pragma unroll
+      for (int s = 0; s < SPW; ++s) {
+        sl[s] = q * SPW + s;
+        ok[s] = sl[s] < a.slices;  // a short last group diffuses its first slice twice, stores once
+        xs[s] = imgs + ((ok[s] ? sl[s] : sl[0]) - s0) * imgf;
+      }
+      f32x4v hacc[SPW][2];
+#pragma unroll
+      for (int s = 0; s < SPW; ++s) hacc[s][0] = hacc[s][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
       {  // piece 0: the node features themselves
-        f32x4v x0[2];
-        t16_rows(xs, hs, w0, lane, x0);
-        t16_mlp(ws, LDW16, x0, lane, hacc);
+        f32x4v x0[SPW][2];
+#pragma unroll
+        for (int s = 0; s < SPW; ++s) t16_rows(xs[s], hs, w0, lane, x0[s]);
+        t16_mlp_s<SPW>(ws, LDW16, [&](int s, int hf) { return x0[s][hf]; }, lane, hacc);
       }
       for (int k = 0; k < a.nsup; ++k) {
-        f32x4v acc[2][2];  // [power][channel half]
-        t16_diffuse(xs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, acc);
+        f32x4v acc[SPW][2][2];  // [slice][power][channel half]
+        t16_diffuse_s<SPW>(xs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, acc);
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          t16_mlp(ws + (1 + 2 * k + q) * CH * LDW16, LDW16, acc[q], lane, hacc);
+        for (int pw = 0; pw < 2; ++pw) {
+          t16_mlp_s<SPW>(ws + (1 + 2 * k + pw) * CH * LDW16, LDW16, [&](int s, int hf) { return acc[s][pw][hf]; }, lane,
+                         hacc);
           if (a.store_pieces && w0 + j < n) {
-            float* dp = hs_out + (long)(w0 + j) * ldh + (1 + 2 * k + q) * CH + 4 * g;
 #pragma unroll
-            for (int hf = 0; hf < 2; ++hf) {
-              if (nt_ok && GWN_T16_PIECE_NT) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
-              else if (nt_ok) *(f32x4v*)(dp + 16 * hf) = acc[q][hf];
-              else {
+            for (int s = 0; s < SPW; ++s) {
+              if (!ok[s]) continue;
+              float* hs_out = (float*)a.h + (long)sl[s] * n * ldh;
+              const bool nt_ok = ((((uintptr_t)hs_out) & 15) | (ldh & 3)) == 0;
+              float* dp = hs_out + (long)(w0 + j) * ldh + (1 + 2 * k + pw) * CH + 4 * g;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) dp[16 * hf + e] = acc[q][hf][e];
+              for (int hf = 0; hf < 2; ++hf) {
+                if (nt_ok) __builtin_nontemporal_store(acc[s][pw][hf], (f32x4v*)(dp + 16 * hf));
+                else {
+#pragma unroll
+                  for (int e = 0; e < 4; ++e) dp[16 * hf + e] = acc[s][pw][hf][e];
+                }
               }
             }
           }
         }
       }
-      t16_epilogue(a, hacc, row0, w0, lane, n, bn);
+#pragma unroll
+      for (int s = 0; s < SPW; ++s)
+        if (ok[s]) t16_epilogue(a, hacc[s], (long)sl[s] * n, w0, lane, n, bn);
     }
     p0 = p1;
   }
-  T16_TS(a, 2 + wave);
   t16_bn_flush(a, bn, wpart);
-  if (threadIdx.x == 0) T16_TS(a, 18);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1886,16 +1823,9 @@ __device__ __forceinline__ void global_to_lds16_bf16(const float* src, long ld, 
   }
 }
 
-#ifndef GWN_T16B_AHEAD
-#define GWN_T16B_AHEAD 1  // 2: PEMS 23.65k vs 23.79k samples/s (not latency-bound on the fragments)
-#endif
-constexpr int T16B_AHEAD = GWN_T16B_AHEAD;  // support-fragment groups in flight ahead (1 or 2)
-// 12-wave bf16-mlp tile kernels (GWN_T16B_WAVES=12: 3 waves per SIMD, 168 registers): the fragment
-// ring one group deeper, the registers the 4th wave gave up paying for it
-#ifndef GWN_T16B_AHEAD12
-#define GWN_T16B_AHEAD12 2
-#endif
-__host__ __device__ constexpr int t16b_ahead(int maxt) { return maxt <= 768 ? GWN_T16B_AHEAD12 : T16B_AHEAD; }
+// support-fragment groups in flight ahead: one (two at 16 waves: PEMS 23.65k vs 23.79k samples/s;
+// 12-wave workgroups with a ring 2-3 groups deep: slower again)
+constexpr int T16B_AHEAD = 1;
 // both powers of one support on bf16 operands (acc as t16_diffuse); G1 / G2: gwn_support_g4_bf16
 // copies (block (kg, tile) = 64 lanes x 8 bf16)
 template <int AH = T16B_AHEAD>
@@ -1994,17 +1924,9 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
       for (int sl = s0; sl <= s1; ++sl) global_to_lds16_bf16(a.h + (long)sl * n * ldh, ldh, n, imgs + (sl - s0) * imgb);
     }
     __syncthreads();
-    const int nsl = s1 - s0 + 1;
-    const int span = T16_COLMAJOR ? nt * nsl : (int)(p1 - p0);
+    const int span = (int)(p1 - p0);
     for (int tp = wave; tp < span; tp += nwaves) {
-      long t;
-      if (T16_COLMAJOR) {  // column tp / nsl of slice s0 + tp % nsl
-        const int c = tp / nsl;
-        t = (long)(s0 + tp - c * nsl) * nt + c;
-        if (t < p0 || t >= p1) continue;
-      } else {
-        t = p0 + tp;
-      }
+      const long t = p0 + tp;
       const int sl = (int)(t / nt), tile = (int)(t - (long)sl * nt);
       const __bf16* xs = imgs + (sl - s0) * imgb;
       const long row0 = (long)sl * n;
@@ -2014,7 +1936,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
       f32x4v hacc[2];
       hacc[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
       hacc[1] = hacc[0];
-      if (MLPB && GWN_T16B_X0_LDS) {  // piece 0 = bf16(g): the staged image's column, no global read
+      if (MLPB) {  // piece 0 = bf16(g): the staged image's column, no global read
         const bf16x8m b0 = t16_img_col_b(xs, s16, w0, lane);
         t16_mlp_bp((const __bf16*)ws, 0, b0, lane, hacc);
         if (a.xg4)  // t16_store_g4's layout, already bf16
@@ -2027,7 +1949,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
       }
       for (int k = 0; k < a.nsup; ++k) {
         f32x4v acc[2][2];
-        t16b_diffuse<t16b_ahead(MAXT)>(xs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, acc);
+        t16b_diffuse(xs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, acc);
         if (a.xg4 && k == a.xg4_k) t16_store_g4(a.xg4, 1, a.slices, sl, nt, tile, lane, acc[0]);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -2036,14 +1958,11 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
             t16_mlp_bp((const __bf16*)ws, 1 + 2 * k + q, b, lane, hacc);
             if (a.store_pieces && a.pb && w0 + j < n) {
               __bf16* bp = (__bf16*)a.pb + (row0 + w0 + j) * a.ld_pb + (2 * k + q) * CH + 4 * g;
+              // plain stores: write-back L2 merges a node's 8-B pieces into full lines (non-temporal:
+              // 1.43x instead of 1.19x the algorithmic forward traffic at the same time)
               typedef __bf16 bf16x4p __attribute__((ext_vector_type(4)));
-              if (GWN_T16B_PB_NT) {
-                __builtin_nontemporal_store(bf16x4p{b[0], b[1], b[2], b[3]}, (bf16x4p*)bp);
-                __builtin_nontemporal_store(bf16x4p{b[4], b[5], b[6], b[7]}, (bf16x4p*)(bp + 16));
-              } else {
-                *(bf16x4p*)bp = bf16x4p{b[0], b[1], b[2], b[3]};
-                *(bf16x4p*)(bp + 16) = bf16x4p{b[4], b[5], b[6], b[7]};
-              }
+              *(bf16x4p*)bp = bf16x4p{b[0], b[1], b[2], b[3]};
+              *(bf16x4p*)(bp + 16) = bf16x4p{b[4], b[5], b[6], b[7]};
               continue;
             }
           } else {
@@ -2064,8 +1983,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
             float* dp = hs_out + (long)(w0 + j) * ldh + (1 + 2 * k + q) * CH + 4 * g;
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
-              if (nt_ok && GWN_T16_PIECE_NT) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
-              else if (nt_ok) *(f32x4v*)(dp + 16 * hf) = acc[q][hf];
+              if (nt_ok) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
               else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) dp[16 * hf + e] = acc[q][hf][e];
@@ -2288,11 +2206,6 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
     else t16_mlp(ws + piece * CH * LDW16, LDW16, x, lane, out);
   };
   const T16Range rg = t16_range(a.slices, nt);
-  const __amdgpu_buffer_rsrc_t gate_rf = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.fg, (short)0, (int)min((long)a.slices * n * 2 * CH * 4, 0x7fffffffL), 0x00020000);
-  const __amdgpu_buffer_rsrc_t gate_rd = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.dskip, (short)0, a.dskip ? (int)min(max((long)a.slices * n - a.skip_row0, 0L) * a.ld_dskip * 4, 0x7fffffffL) : 0,
-      0x00020000);
   if (a.bn_dy && blockIdx.x == 0 && threadIdx.x < CH) {
     if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
     if (a.bn_dgamma) a.bn_dgamma[threadIdx.x] = a.bn_sums[CH + threadIdx.x];
@@ -2311,17 +2224,9 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
       }
     });
     __syncthreads();
-    const int nsl = s1 - s0 + 1;
-    const int span = T16_COLMAJOR ? nt * nsl : (int)(p1 - p0);
+    const int span = (int)(p1 - p0);
     for (int tp = wave; tp < span; tp += nwaves) {
-      long t;
-      if (T16_COLMAJOR) {  // column tp / nsl of slice s0 + tp % nsl
-        const int c = tp / nsl;
-        t = (long)(s0 + tp - c * nsl) * nt + c;
-        if (t < p0 || t >= p1) continue;
-      } else {
-        t = p0 + tp;
-      }
+      const long t = p0 + tp;
       const int s = (int)(t / nt), tile = (int)(t - (long)s * nt);
       const float* dhs = imgs + (s - s0) * imgf;
       const long row0 = (long)s * n;
@@ -2330,23 +2235,9 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
       dx[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
       dx[1] = dx[0];
       const float* dh_rows = (a.bn_dy ? a.dh_out : a.dh) + row0 * CH;  // (BF: the fp32 rows)
-      // the gate epilogue's rows pulled into L2 now (one 4-B load per 128-B line: lane (node k,
-      // part) -> fg line part 0 / 1, dskip line part 2), consumed by a no-op at the epilogue so the
-      // loads stay issued here: the epilogue's loads then hit L2 instead of waiting on HBM
-      int pf1 = 0, pf2 = 0;
-      if (GWN_T16_GATE_PF && a.dfg) {
-        const int k = lane >> 2, part = lane & 3, wk = w0 + k;
-        const long mk = row0 + wk;
-        const bool ok = wk < n;
-        const int ofg = (ok && part < 2) ? (int)((mk * 2 * CH + part * 32) * 4) : 0x7ffffff0;
-        const int ods = (ok && part == 2 && a.dskip && mk >= a.skip_row0)
-                            ? (int)((mk - a.skip_row0) * a.ld_dskip * 4) : 0x7ffffff0;
-        pf1 = (int)__builtin_amdgcn_raw_buffer_load_b32(gate_rf, ofg, 0, 0);
-        pf2 = (int)__builtin_amdgcn_raw_buffer_load_b32(gate_rd, ods, 0, 0);
-      }
       // MLPB: the channel maps take bf16(dh), which is the staged image itself
       const int s16b = t16b_s16(n);
-      if (MLPB && GWN_T16B_X0_LDS) {
+      if (MLPB) {
         t16_mlp_bp((const __bf16*)ws, 0, t16_img_col_b((const __bf16*)dhs, s16b, w0, lane), lane, dx);
       } else {
         f32x4v d0[2];
@@ -2355,27 +2246,28 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
         mlp(0, d0, dx);
       }
       for (int k = 0; k < a.nsup; ++k) {
-        f32x4v e[2][2];
-        if (BF) t16b_diffuse<t16b_ahead(MAXT)>((const __bf16*)dhs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, e);
-        else t16_diffuse(dhs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, e);
+        f32x4v e1[1][2][2];
+        f32x4v (&e)[2][2] = e1[0];
+        if (BF) t16b_diffuse((const __bf16*)dhs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, e);
+        else t16_diffuse(dhs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, e1);
         mlp(1 + 2 * k, e[0], dx);
         mlp(2 + 2 * k, e[1], dx);
         if (k == a.adp_index) {  // t1 = W1^T dh + W2^T (A dh), t2 = W2^T dh
           f32x4v d0[2], tt[2];
           bf16x8m db;
-          if (MLPB && GWN_T16B_X0_LDS) db = t16_img_col_b((const __bf16*)dhs, s16b, w0, lane);
+          if (MLPB) db = t16_img_col_b((const __bf16*)dhs, s16b, w0, lane);
           else if (BF) t16_rows_global(dh_rows, CH, w0, n, lane, d0);
           else t16_rows(dhs, hs, w0, lane, d0);
           tt[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
           tt[1] = tt[0];
-          if (MLPB && GWN_T16B_X0_LDS) t16_mlp_bp((const __bf16*)ws, 1 + 2 * k, db, lane, tt);
+          if (MLPB) t16_mlp_bp((const __bf16*)ws, 1 + 2 * k, db, lane, tt);
           else mlp(1 + 2 * k, d0, tt);
           mlp(2 + 2 * k, e[0], tt);
           if (BF && a.tg4) t16_store_g4(a.tg4, 0, a.slices, s, nt, tile, lane, tt);
           else t16_store(a.t1 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
           tt[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
           tt[1] = tt[0];
-          if (MLPB && GWN_T16B_X0_LDS) t16_mlp_bp((const __bf16*)ws, 2 + 2 * k, db, lane, tt);
+          if (MLPB) t16_mlp_bp((const __bf16*)ws, 2 + 2 * k, db, lane, tt);
           else mlp(2 + 2 * k, d0, tt);
           if (BF && a.tg4) t16_store_g4(a.tg4, 1, a.slices, s, nt, tile, lane, tt);
           else t16_store(a.t2 + row0 * a.ld_t, a.ld_t, tt, w0, lane, n);
@@ -2386,7 +2278,6 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
         continue;
       }
       // gate backward (gate_bwd_kernel's arithmetic): g = dxg (+ dskip) -> dfg via (tanh f, sigmoid s)
-      if (GWN_T16_GATE_PF) asm volatile("" ::"v"(pf1), "v"(pf2));
       const int w = w0 + j;
       if (w >= n) continue;
       const long m = row0 + w;
@@ -2623,12 +2514,9 @@ void ensure_lds_attr(K kern) {
 // slice in LDS, hands off its partial sum and one of three runs the epilogue), so the split only pays
 // where the whole-slice launch leaves most CUs idle: 64 slices 63.5 -> 37.8 (fwd); 192 slices
 // 68 -> 78 / 67 -> 79; 448 slices 115 -> 147 / 111 -> 148; 640 slices 174 -> 212 / 167 -> 201.
-// Default: split when every unit gets a CU of its own (slices * nsup <= CUs); GWN_KSPLIT_SLICES
-// overrides with a slice-count threshold (0 = never split).
+// Split when every unit gets a CU of its own (slices * nsup <= CUs).
 int ksplit_max_slices(int nsup) {
   static int v = [] {
-    const char* e = getenv("GWN_KSPLIT_SLICES");
-    if (e) return atoi(e);
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -2685,22 +2573,31 @@ struct T16Plan {
   int grid, maximg;
   size_t lds;
 };
-T16Plan t16_plan(int n, int nsup, int slices) {
+// spw > 1 (the forward's slice groups): the units are groups of spw slices x tiles and maximg a
+// multiple of spw; not ok when one group's images do not fit.
+T16Plan t16_plan(int n, int nsup, int slices, int spw = 1) {
   T16Plan pl{false, 0, 0, 0};
   const size_t fixed = t16_lds_bytes(n, nsup, 0), img = t16_lds_bytes(n, nsup, 1) - fixed;
-  if (fixed + img > (size_t)T16_LDS_MAX || slices <= 0) return pl;
+  if (fixed + spw * img > (size_t)T16_LDS_MAX || slices <= 0) return pl;
   const int nt = (n + 15) / 16;
-  const long tiles = (long)slices * nt;
+  const long tiles = (long)((slices + spw - 1) / spw) * nt;
   pl.grid = (int)(tiles < gwn_device_cus() ? tiles : gwn_device_cus());
   const long per = (tiles + pl.grid - 1) / pl.grid;
-  const int span = (int)((per - 1 + nt - 1) / nt) + 1;  // slices a range of `per` tiles can touch
-  int maximg = (int)((T16_LDS_MAX - fixed) / img);
-  maximg = maximg < T16_MAXIMG ? maximg : T16_MAXIMG;
-  pl.maximg = maximg < span ? maximg : span;
+  const int span = (int)((per - 1 + nt - 1) / nt) + 1;  // groups a range of `per` units can touch
+  int gmax = (int)((T16_LDS_MAX - fixed) / (spw * img));
+  gmax = gmax < T16_MAXIMG / spw ? gmax : T16_MAXIMG / spw;
+  pl.maximg = spw * (gmax < span ? gmax : span);
   pl.lds = fixed + pl.maximg * img;
   if (pl.lds < 81 * 1024) pl.lds = 81 * 1024;
   pl.ok = true;
   return pl;
+}
+
+// slices per wave of the fp32 tile forward (experiment: GWN_T16_SPW, default 1)
+int t16_spw(int slices, int nt) {
+  const char* e = getenv("GWN_T16_SPW");
+  (void)slices; (void)nt;
+  return e ? atoi(e) : 1;  // 3: two slices per wave in 12-wave workgroups
 }
 
 // zero the BN partial slots [written, gwn_bn_part_slots(slices)) that a whole-slice kernel leaves
@@ -2720,11 +2617,6 @@ int bn_part_tail(float* bn_part, int slices, int c, hipStream_t s) {
 static bool fold_last_enabled() {
   const char* e = getenv("GWN_BN_FOLD_LAST");
   return e && e[0] == '1';
-}
-// GWN_T16B_WAVES=12: the bf16-mlp tile kernels as 12-wave workgroups (t16b_ahead)
-static bool t16b_waves12() {
-  const char* e = getenv("GWN_T16B_WAVES");
-  return e && e[0] == '1' && e[1] == '2';
 }
 
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded, hipStream_t s) {
@@ -2779,8 +2671,6 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
                                   T16_LDS_MAX);
         (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b_kernel<1024, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
-        (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b_kernel<768, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
         attr_b = true;
       }
       const int nt = (g->n + 15) / 16;
@@ -2798,9 +2688,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
       a.ksplit = 1;
       a.bn_slots = (int)gwn_bn_part_slots(slices);
       if (fold_here) a.fold = *g->bn_fold;
-      if (g->split_planes == 2 && t16b_waves12() && !fold_here)
-        gcn_fwd_t16b_kernel<768, true><<<grid, 768, lds, s>>>(a, p, maximg);
-      else if (g->split_planes == 2) gcn_fwd_t16b_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      if (g->split_planes == 2) gcn_fwd_t16b_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       else gcn_fwd_t16b_kernel<1024><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       GWN_CHECK_LAUNCH();
       *folded = fold_here;
@@ -2820,7 +2708,11 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
     ensure_lds_attr(gcn_fwd_fused_kernel<1024, true>);
     ensure_lds_attr(gcn_fwd_pow_kernel<512>);
     ensure_lds_attr(gcn_fwd_pow_kernel<1024>);
-    (void)hipFuncSetAttribute((const void*)gcn_fwd_t16_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gcn_fwd_t16_kernel<1024, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              T16_LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)gcn_fwd_t16_kernel<1024, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              T16_LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)gcn_fwd_t16_kernel<768, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               T16_LDS_MAX);
     attr_set = true;
   }
@@ -2839,7 +2731,14 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
     // partial slot (gwn_bn_part_slots)
     a.bn_slots = (int)gwn_bn_part_slots(slices);
     if (fold_here) a.fold = *g->bn_fold;
-    gcn_fwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
+    const T16Plan p2 = t16_plan(g->n, g->nsup, slices, 2);
+    const int spw = t16_spw(slices, (g->n + 15) / 16);
+    if (spw == 3 && p2.ok && !fold_here)
+      gcn_fwd_t16_kernel<768, 2><<<p2.grid, 768, p2.lds, s>>>(a, p, p2.maximg);
+    else if (spw == 2 && p2.ok)
+      gcn_fwd_t16_kernel<1024, 2><<<p2.grid, 64 * T16_WAVES, p2.lds, s>>>(a, p, p2.maximg);
+    else
+      gcn_fwd_t16_kernel<1024, 1><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
     GWN_CHECK_LAUNCH();
     *folded = fold_here;
     return GWN_OK;
@@ -2913,8 +2812,6 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
       if (!attr_b) {
         (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<1024, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
-        (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<768, true, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
         (void)hipFuncSetAttribute((const void*)gcn_bwd_t16_kernel<1024, true, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T16_LDS_MAX);
         attr_b = true;
@@ -2932,8 +2829,7 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
       PowSup p = {};
       for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = (const float*)g->sup_g4b_t[k];
       a.ksplit = 1;
-      if (g->split_planes == 2 && t16b_waves12()) gcn_bwd_t16_kernel<768, true, true><<<grid, 768, lds, s>>>(a, p, maximg);
-      else if (g->split_planes == 2) gcn_bwd_t16_kernel<1024, true, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      if (g->split_planes == 2) gcn_bwd_t16_kernel<1024, true, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       else gcn_bwd_t16_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       GWN_CHECK_LAUNCH();
       return GWN_OK;

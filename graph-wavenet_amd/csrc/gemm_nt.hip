@@ -19,10 +19,7 @@ namespace {
 constexpr int BK = 32;
 constexpr int LDK = BK + 4;      // LDS row stride (floats)
 constexpr int OOR = 0x7ffffff0;  // out-of-range byte offset
-#ifndef GWN_GEMM_NT_STORE_AUX
-#define GWN_GEMM_NT_STORE_AUX 2  // output stores non-temporal (head GEMMs 128.4 -> 123.0 us per METR step; 0: plain)
-#endif
-constexpr int NT_STORE_AUX = GWN_GEMM_NT_STORE_AUX;
+constexpr int NT_STORE_AUX = 2;  // output stores non-temporal (head GEMMs 128.4 -> 123.0 us per METR step)
 
 struct NtArgs {
   const float* A; long lda;

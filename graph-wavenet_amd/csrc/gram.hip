@@ -226,10 +226,6 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* part, int
 inline unsigned gram_reduce_blocks(int n) { return (unsigned)(((long)n * n + 63) / 64); }
 
 constexpr size_t GRAM_IMG = 96 * 36 * sizeof(float);  // LINES: a wave's [96][36] image
-bool gram_lines() {
-  const char* e = getenv("GWN_GRAM_LINES");  // 0: the fragment-shaped direct loads (A/B)
-  return !(e && e[0] == '0');
-}
 
 int gram_nsplit(int n, int slices) {
   const int nt = (n + 31) / 32;
@@ -432,12 +428,9 @@ int gwn_gram_dtype(const float* x1, const float* t1, const float* x2, const floa
   if (bf16) {
     if (g.npairs == 2) gram_kernel<2, true><<<blocks, 64, 0, s>>>(g);
     else gram_kernel<1, true><<<blocks, 64, 0, s>>>(g);
-  } else if (gram_lines()) {
+  } else {  // fp32: full-line operand loads restaged per wave (the fragment-shaped loads: 317 vs 264 us)
     if (g.npairs == 2) gram_kernel<2, false, true><<<blocks, 64, GRAM_IMG, s>>>(g);
     else gram_kernel<1, false, true><<<blocks, 64, GRAM_IMG, s>>>(g);
-  } else {
-    if (g.npairs == 2) gram_kernel<2><<<blocks, 64, 0, s>>>(g);
-    else gram_kernel<1><<<blocks, 64, 0, s>>>(g);
   }
   GWN_CHECK_LAUNCH();
   gram_reduce_kernel<<<gram_reduce_blocks(n), 256, 0, s>>>(ws, g.nsplit, n, 32 * g.nt, dA, ld_dA,
@@ -482,10 +475,6 @@ int gram_group_plan(int n, const int* slices, int nlayers, int* nsp) {
 // block (gram_kernel: ~2.2 GB of fragment traffic per METR step).  The K permutation of
 // gram_kernel: lane group q takes channels 8q .. 8q+7 (two ds_read_b128 per operand and tile), the
 // same on both operands.  Partials [CU][np16][np16], summed in a fixed order by gram_reduce_kernel.
-#ifndef GWN_GRAM_CU_DMA
-#define GWN_GRAM_CU_DMA 0  // 1: gram_cu_kernel stages by LDS-DMA (measured 211 vs 170 us with paired tiles)
-#endif
-constexpr bool GRAM_CU_DMA = GWN_GRAM_CU_DMA != 0;
 constexpr int GCU_LDR = 36;  // LDS row stride (floats): the 16 rows of a ds_read_b128 pass on distinct banks
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 constexpr int GCG_NB = 4;  // LDS step buffers: three steps' operands in flight
@@ -543,62 +532,24 @@ __global__ __launch_bounds__(1024) void gram_cu_kernel(const GramCu g) {
       }
     }
   };
-  // GWN_GRAM_CU_DMA: the step's rows by 16-B LDS-DMA loads instead (no staging registers),
-  // unpadded 128-B rows with 16-B chunk c of row r at position c ^ ((r >> 1) & 7) (conflict-free
-  // fragment reads); every wave issues the same count per step (padding loads into a sink)
-  const int opb = rows * 32, ninst = rows / 4, G = (ninst + 15) / 16;
-  auto issue = [&](int st, int b) {
-    int L = 0;
-    while (L + 1 < g.nlayers && st >= g.lsteps0[L + 1]) ++L;
-    const int ls = st - g.lsteps0[L], sl = ls >> 1, p = ls & 1;
-    const long base = (long)sl * g.n;
-    const __amdgpu_buffer_rsrc_t rx = rsrc(g.X[L][p] + base * g.ldx, (long)g.n * g.ldx * 4);
-    const __amdgpu_buffer_rsrc_t rt = rsrc(g.T[L][p] + base * g.ldt, (long)g.n * g.ldt * 4);
-    const int wv = __builtin_amdgcn_readfirstlane(wave), lr = lane >> 3, pos = lane & 7;
-    for (int k = 0; k < G; ++k) {
-      const int m = wv + 16 * k;
-      const bool isx = m < rows / 8;
-      const int r = (isx ? m : m - rows / 8) * 8 + lr, c = pos ^ ((r >> 1) & 7);
-      float* dst = m < ninst ? lds + b * 2 * opb + m * 256 : lds + 2 * 2 * opb;
-      const bool ok = m < ninst && r < g.n;
-      if (isx)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)dst, 16, ok ? (int)((r * g.ldx + 4 * c) * 4) : OOR, 0, 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_ptr_t)dst, 16, ok ? (int)((r * g.ldt + 4 * c) * 4) : OOR, 0, 0, 0);
-    }
-  };
+  // (LDS-DMA staging of the step rows, no staging registers, measured slower here: 195 vs 170 us --
+  // the fp32 step computes longer than the load latency, one register-staged step in flight suffices)
   auto frag = [&](const float* img, int t16, float4* f) {
-    if (GRAM_CU_DMA) {
-      const int r = 16 * t16 + i, sw = (r >> 1) & 7;
-      f[0] = *(const float4*)(img + r * 32 + 4 * ((2 * q) ^ sw));
-      f[1] = *(const float4*)(img + r * 32 + 4 * ((2 * q + 1) ^ sw));
-      return;
-    }
     const float* r = img + (16 * t16 + i) * GCU_LDR + 8 * q;
     f[0] = *(const float4*)r;
     f[1] = *(const float4*)(r + 4);
   };
-  if (GRAM_CU_DMA) {
-    if (st0 < st1) issue(st0, 0);
-  } else {
-    if (st0 < st1) {
-      stage_load(st0);
-      stage_store(0);
-    }
-    __syncthreads();
+  if (st0 < st1) {
+    stage_load(st0);
+    stage_store(0);
   }
+  __syncthreads();
   int buf = 0;
   for (int st = st0; st < st1; ++st) {
     const bool more = st + 1 < st1;
-    if (GRAM_CU_DMA) {
-      GCG_WAIT_VM(0);
-      __builtin_amdgcn_s_barrier();
-      if (more) issue(st + 1, buf ^ 1);
-    } else if (more) {
-      stage_load(st + 1);
-    }
-    const float* xi = lds + buf * 2 * (GRAM_CU_DMA ? opb : opf);
-    const float* ti_ = xi + (GRAM_CU_DMA ? opb : opf);
+    if (more) stage_load(st + 1);
+    const float* xi = lds + buf * 2 * opf;
+    const float* ti_ = xi + opf;
     // (the 16 waves of the CU hide the LDS latency: no in-wave prefetch, which would cost 8 of the
     // registers the accumulators need)
 #pragma unroll
@@ -614,10 +565,8 @@ __global__ __launch_bounds__(1024) void gram_cu_kernel(const GramCu g) {
         for (int kk = 0; kk < 8; ++kk) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv[kk], acc[u], 0, 0, 0);
       }
     }
-    if (!GRAM_CU_DMA) {
-      if (more) stage_store(buf ^ 1);
-      __syncthreads();
-    }
+    if (more) stage_store(buf ^ 1);
+    __syncthreads();
     buf ^= 1;
   }
   // D[v][w]: lane (q, i) holds rows 16 ti + 4 q + r, column 16 tj + i
@@ -738,8 +687,7 @@ bool gram_cu_ok(int n) {
   return n <= 256;
 }
 size_t gram_cu_lds(int n) {
-  return GRAM_CU_DMA ? (size_t)(2 * 2 * 16 * ((n + 15) / 16) * 32 + 256) * sizeof(float)  // + the sink
-                     : (size_t)2 * 2 * 16 * ((n + 15) / 16) * GCU_LDR * sizeof(float);
+  return (size_t)2 * 2 * 16 * ((n + 15) / 16) * GCU_LDR * sizeof(float);
 }
 }  // namespace
 
@@ -826,8 +774,7 @@ int gwn_gram_group(const gwn_gram_layer* layers, int nlayers, long ldx, long ldt
   GWN_DEBUG_RANGE(dA, ((long)(n - 1) * ld_dA + n) * 4, "gram_group dA");
   const int per_split = g.nt * ((g.nt + 1) / 2);
   const int blocks = ((g.nsplit + NXCD - 1) / NXCD) * NXCD * per_split;
-  if (gram_lines()) gram_kernel<2, false, true><<<blocks, 64, GRAM_IMG, s>>>(g);
-  else gram_kernel<2><<<blocks, 64, 0, s>>>(g);
+  gram_kernel<2, false, true><<<blocks, 64, GRAM_IMG, s>>>(g);
   GWN_CHECK_LAUNCH();
   gram_reduce_kernel<<<gram_reduce_blocks(n), 256, 0, s>>>(ws, g.nsplit, n, (int)np, dA, ld_dA, accumulate);
   GWN_CHECK_LAUNCH();

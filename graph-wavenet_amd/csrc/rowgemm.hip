@@ -46,13 +46,10 @@ constexpr int OOR = 0x7ffffff0;  // out-of-range byte offset
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
 }
-// cache policy of the output stores (measurement hook: -DGWN_ROWGEMM_STORE_AUX=2 non-temporal,
-// 16 write-through)
-#ifndef GWN_ROWGEMM_STORE_AUX
-#define GWN_ROWGEMM_STORE_AUX 2  // non-temporal: gated forward 133 -> 122 us per METR step (0: 133, 16: 121)
-#endif
+// output stores non-temporal (cache policy 2): gated forward 133 -> 122 us per METR step
+constexpr int ST_AUX = 2;
 __device__ __forceinline__ void st32(__amdgpu_buffer_rsrc_t r, int off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, GWN_ROWGEMM_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, ST_AUX);
 }
 __device__ __forceinline__ float ld32(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
@@ -62,19 +59,11 @@ __device__ __forceinline__ float ld32(__amdgpu_buffer_rsrc_t r, int off) {
 // g = cols 2c+1 (tile 1) — so every lane owns channel c = col of both and writes full rows:
 // xg[m][c] = tanh(f) * sigmoid(g) (128 B per row) and fg[m][2c .. 2c+1] = (tanh f, sigmoid g).
 // STORE: ntiles waves share a chunk, one 32-column tile each.
-#ifndef GWN_ROWGEMM_WPE
-#define GWN_ROWGEMM_WPE  // measurement hook: -DGWN_ROWGEMM_WPE='__attribute__((amdgpu_waves_per_eu(2)))'
-#endif
-// WLDS (default): the stationary weights stay in LDS ([row][2 KH + 4]: 2 KH + 4 = 4 mod 64, so the
-// 16 lanes of a ds_read_b128 pass hit distinct banks) and are read four k-steps at a time next to
-// the MFMAs, instead of 2 KH registers per lane: 228-288 registers (one wave per SIMD, every load
-// stall exposed) -> two waves per SIMD.  -DGWN_ROWGEMM_WLDS=0: weights in registers.
-#ifndef GWN_ROWGEMM_WLDS
-#define GWN_ROWGEMM_WLDS 1
-#endif
-constexpr bool WLDS = GWN_ROWGEMM_WLDS != 0;
+// The stationary weights stay in LDS ([row][2 KH + 4]: 2 KH + 4 = 4 mod 64, so the 16 lanes of a
+// ds_read_b128 pass hit distinct banks) and are read four k-steps at a time next to the MFMAs,
+// instead of 2 KH registers per lane (228-288 registers, one wave per SIMD) -> two waves per SIMD.
 template <int KH, bool GATE, bool BNSTAT, bool CENTER = false>
-__global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowGemm p) {
+__global__ __launch_bounds__(256) void rowgemm_kernel(const RowGemm p) {
   constexpr int NQ = KH / 4;  // float4 per lane per chunk
   constexpr int NT = GATE ? 2 : 1;
   const int lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
@@ -103,17 +92,13 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
   float4 a[NQ];
   int chunk = wave;
   load(chunk, a);
-  // stationary weights w[t][j] = B(half*KH + j, column of (t, col)): WLDS, staged once per block
-  // in LDS and read next to the MFMAs; else in registers -- GATE (B = w_fg[n][k], the fragment is a
-  // strided column) through LDS as Bt[n][k] (k contiguous) read with 16-B LDS loads, STORE (B(k, n)
-  // rows contiguous in n) by direct coalesced loads.
+  // stationary weights w[t][j] = B(half*KH + j, column of (t, col)), staged once per block in LDS
+  // (rows: GATE (t, col) -> t*32 + col holds output column 2 col + t; STORE: row n)
   constexpr int K = 2 * KH, LDT = K + 4;
-  float w[NT][WLDS ? 1 : KH];
   float bn[NT];
   extern __shared__ float4 bt4[];
-  const float* wrow[NT];  // WLDS: this lane's weight rows in LDS
-  if (WLDS) {
-    // rows: GATE (t, col) -> t*32 + col holds output column 2 col + t; STORE: row n
+  const float* wrow[NT];  // this lane's weight rows in LDS
+  {
     float* bt = (float*)bt4;
     const int N = GATE ? 64 : 32 * p.ntiles;
     for (int e = threadIdx.x; e < K * N; e += blockDim.x) {
@@ -127,33 +112,6 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
       wrow[t] = bt + (GATE ? t * 32 + col : 32 * tile + col) * LDT + half * KH;
       bn[t] = GATE ? p.bias[2 * col + t] : 0.0f;
     }
-  } else if (GATE) {
-    const int N = 64;
-    float* bt = (float*)bt4;
-    for (int e = threadIdx.x; e < K * N; e += blockDim.x) {
-      const int k = e % K, nn = e / K;
-      bt[nn * LDT + k] = p.B[(k % KH) * p.ldb_k + (k / KH) * p.ldb_tap + (long)nn * p.ldb_n];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int nb = 2 * col + t;
-      const float4* src = (const float4*)(bt + nb * LDT + half * KH);
-#pragma unroll
-      for (int q = 0; q < KH / 4; ++q) {
-        const float4 v = src[q];
-        if (!WLDS) {
-          w[t][(4 * q) % (WLDS ? 1 : KH)] = v.x; w[t][(4 * q + 1) % (WLDS ? 1 : KH)] = v.y;
-          w[t][(4 * q + 2) % (WLDS ? 1 : KH)] = v.z; w[t][(4 * q + 3) % (WLDS ? 1 : KH)] = v.w;
-        }
-      }
-      bn[t] = p.bias[nb];
-    }
-  } else {
-    const long nb = 32 * tile + col;
-#pragma unroll
-    for (int j = 0; j < KH; ++j) w[0][j % (WLDS ? 1 : KH)] = p.B[j * p.ldb_k + half * p.ldb_tap + nb * p.ldb_n];
-    bn[0] = 0.0f;
   }
   if (wave >= nwaves) return;  // after the block-wide staging barrier
   // CENTER (BatchNorm on load, gwn_batchnorm_fwd_fold): the column means are wave-uniform
@@ -200,13 +158,8 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
       float wq[NT][4];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        if (WLDS) {
-          const float4 v = *(const float4*)(wrow[t] + 4 * q);
-          wq[t][0] = v.x; wq[t][1] = v.y; wq[t][2] = v.z; wq[t][3] = v.w;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) wq[t][e] = w[t][(4 * q + e) % (WLDS ? 1 : KH)];
-        }
+        const float4 v = *(const float4*)(wrow[t] + 4 * q);
+        wq[t][0] = v.x; wq[t][1] = v.y; wq[t][2] = v.z; wq[t][3] = v.w;
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
@@ -225,7 +178,7 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
         typedef unsigned v2u __attribute__((ext_vector_type(2)));
         const v2u fgv = {__builtin_bit_cast(unsigned, f), __builtin_bit_cast(unsigned, g)};
         __builtin_amdgcn_raw_buffer_store_b64(fgv, rx, ok ? (int)((m * p.ld_aux + 2 * col) * 4) : OOR, 0,
-                                              GWN_ROWGEMM_STORE_AUX);
+                                              ST_AUX);
         if (skip_rows > 0)
           st32(rk, ok && m >= p.aux2_row0 ? (int)(((m - p.aux2_row0) * p.ld_aux2 + col) * 4) : OOR, xg);
       } else {
@@ -252,17 +205,11 @@ __global__ __launch_bounds__(256) GWN_ROWGEMM_WPE void rowgemm_kernel(const RowG
   }
 }
 
-// waves per CU of the gated TCN forward (GWN_ROWGEMM_GATE_WPC, default 8; its 168 registers allow 12)
-inline int gate_wpc() {
-  const char* e = getenv("GWN_ROWGEMM_GATE_WPC");
-  const int v = e ? atoi(e) : 8;
-  return v >= 4 && v <= 12 ? v : 8;
-}
-
+// 8 waves per CU (12 for the gated forward, which its 168 registers allow, measured no faster)
 inline int rowgemm_grid(int M, int ntiles, bool gate) {
   const int nchunks = (M + 31) / 32;
   int waves = nchunks * (gate ? 1 : ntiles);
-  const int cap = 256 * (gate ? gate_wpc() : 8);
+  const int cap = 256 * 8;
   if (waves > cap) waves = cap;
   return (waves + 3) / 4;  // 4 | 4*grid, so every tile gets grid*4/ntiles waves
 }
@@ -279,7 +226,7 @@ int launch(const RowGemm& p, hipStream_t s) {
   GWN_REQUIRE(!BNSTAT || (p.ntiles == 1 && p.ldc == 32), "rowgemm: BN statistics need N = ldc = 32");
   (void)nchunks;
   const int grid = rowgemm_grid(p.M, p.ntiles, GATE);
-  const size_t lds = (GATE || WLDS) ? (size_t)(GATE ? 64 : 32 * p.ntiles) * (2 * KH + 4) * sizeof(float) : 0;
+  const size_t lds = (size_t)(GATE ? 64 : 32 * p.ntiles) * (2 * KH + 4) * sizeof(float);
   rowgemm_kernel<KH, GATE, BNSTAT, CENTER><<<grid, 256, lds, s>>>(p);
   GWN_CHECK_LAUNCH();
   return GWN_OK;

@@ -52,10 +52,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long by
 // XB (the gcn mlp in bf16 mode, Kc = 224): column chunk 0 (32 fp32 columns, 8-B loads) from X, the
 // hop pieces from Xb as bf16 -- a 16-B load (8 columns per lane: 128) and an 8-B load (4: 64);
 // converted to fp32 in registers (exact), the same 14 output tiles as the fp32 form
-// H2 (WR = 4): the row groups summed through TWO LDS slots instead of four (groups 2, 3 into the
-// slots, added by groups 0, 1, whose sums the workgroup adds on the way out: (r0 + r2) + (r1 + r3)),
-// so that two workgroups fit a CU (GWN_WGRAD_2WG=1, the gcn-mlp shape)
-template <int JW, int NX16, int NX8, int WK, int PD, bool AFF, bool XB = false, bool H2 = false>
+// (two workgroups per CU for the gcn-mlp shape -- row groups summed through two LDS slots, 4 quads in
+// flight -- measured within noise)
+template <int JW, int NX16, int NX8, int WK, int PD, bool AFF, bool XB = false>
 __global__ __launch_bounds__(256) void wgrad_group_kernel(const WGroup G) {
   constexpr int J = 16 * JW;
   constexpr int KCG = 64 * NX16 + 32 * NX8;  // columns of a column group
@@ -192,12 +191,7 @@ __global__ __launch_bounds__(256) void wgrad_group_kernel(const WGroup G) {
   }
   // row-group partials through LDS: red[rg][j * KC + k], bias at red[rg][J*KC + j]
   constexpr int SLOT = J * KC + J;
-  static_assert(!H2 || WR == 4, "H2: four row groups");
-  float* my = red + (H2 ? (rg & 1) : rg) * SLOT;
-  // H2 pass 0: groups 2, 3 store; pass 1: groups 0, 1 add that and store the sum
-  for (int pass = 0; pass < (H2 ? 2 : 1); ++pass) {
-  if (H2 && pass == 1) __syncthreads();
-  if (H2 && (pass == 0) != (rg >= 2)) continue;
+  float* my = red + rg * SLOT;
 #pragma unroll
   for (int e = 0; e < JW; ++e)
 #pragma unroll
@@ -212,22 +206,20 @@ __global__ __launch_bounds__(256) void wgrad_group_kernel(const WGroup G) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = JW * (4 * q + r) + e;
-        // (H2 pass 1: the lane reads back exactly the element it then overwrites)
-        my[j * KC + k] = (H2 && pass == 1) ? acc[e][t][r] + my[j * KC + k] : acc[e][t][r];
+        my[j * KC + k] = acc[e][t][r];
       }
     }
   if (kg == 0 && q == 0) {
 #pragma unroll
     for (int e = 0; e < JW; ++e)
-      my[J * KC + JW * i + e] = (H2 && pass == 1) ? bsum[e] + my[J * KC + JW * i + e] : bsum[e];
-  }
+      my[J * KC + JW * i + e] = bsum[e];
   }
   __syncthreads();
   float* out = P.part + (long)b * SLOT;
   for (int o = threadIdx.x; o < SLOT; o += 256) {
     float v = red[o];
 #pragma unroll
-    for (int g = 1; g < (H2 ? 2 : WR); ++g) v += red[g * SLOT + o];
+    for (int g = 1; g < WR; ++g) v += red[g * SLOT + o];
     out[o] = v;
   }
 }
@@ -236,10 +228,10 @@ struct Shape {
   int J, Kt, ntaps;
 };
 
-template <int JW, int NX16, int NX8, int WK, int PD, bool XB = false, bool H2 = false>
+template <int JW, int NX16, int NX8, int WK, int PD, bool XB = false>
 int launch(const WGroup& g, bool aff, int blocks, size_t lds, hipStream_t s) {
-  auto k = aff ? wgrad_group_kernel<JW, NX16, NX8, WK, PD, true, false, H2>
-               : wgrad_group_kernel<JW, NX16, NX8, WK, PD, false, XB, H2>;
+  auto k = aff ? wgrad_group_kernel<JW, NX16, NX8, WK, PD, true, false>
+               : wgrad_group_kernel<JW, NX16, NX8, WK, PD, false, XB>;
   static bool attr[2] = {false, false};
   if (!attr[aff]) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -257,16 +249,9 @@ int shape_kind(int J, int Kt, int ntaps) {
   if (J == 32 && Kt == 512 && ntaps == 1) return 3;  // end_conv_2 (12 -> 32 padded rows), E = 512
   return 0;
 }
-static bool wgrad_2wg() {  // GWN_WGRAD_2WG=1: the gcn-mlp shape with two workgroups per CU (H2, PD 4)
-  static const bool on = [] {
-    const char* e = getenv("GWN_WGRAD_2WG");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
 size_t shape_lds(int kind) {
   switch (kind) {
-    case 1: return (size_t)(wgrad_2wg() ? 2 : 4) * (32 * 224 + 32) * 4;  // WR = 4 (H2: two slots)
+    case 1: return (size_t)4 * (32 * 224 + 32) * 4;  // WR = 4
     case 2: return (size_t)4 * (64 * 64 + 64) * 4;   // WR = 4
     case 3: return (size_t)1 * (32 * 512 + 32) * 4;  // WK = 4, WR = 1
     default: return 0;
@@ -350,23 +335,12 @@ extern "C" int gwn_wgrad_group(const gwn_wgrad_problem* probs, int nprob, int J,
     b0 += nb[p];
   }
   const size_t lds = shape_lds(kind);
-  // quads in flight per wave (A/B: GWN_WGRAD_DEEP=0 -> 4 / 6 / 6): the mlp launch holds one
-  // workgroup (one wave per SIMD) per CU, so its loads in flight are all the latency hiding it has
-  static const bool deep = [] {
-    const char* e = getenv("GWN_WGRAD_DEEP");
-    return !(e && e[0] == '0');
-  }();
+  // quads in flight per wave (8 / 10 / 10; 4 / 6 / 6 measured slower on the TCN shape: 87 vs 74 us
+  // per METR step): the mlp launch holds one workgroup (one wave per SIMD) per CU, so its loads in
+  // flight are all the latency hiding it has
   switch (kind) {
-    case 1:
-      if (wgrad_2wg())
-        return xb ? launch<2, 3, 1, 1, 4, true, true>(g, false, blocks, lds, s) : launch<2, 3, 1, 1, 4, false, true>(g, aff, blocks, lds, s);
-      if (deep) return xb ? launch<2, 3, 1, 1, 8, true>(g, false, blocks, lds, s) : launch<2, 3, 1, 1, 8>(g, aff, blocks, lds, s);
-      return xb ? launch<2, 3, 1, 1, 4, true>(g, false, blocks, lds, s) : launch<2, 3, 1, 1, 4>(g, aff, blocks, lds, s);
-    case 2:
-      if (deep) return launch<4, 0, 2, 1, 10>(g, aff, blocks, lds, s);
-      return launch<4, 0, 2, 1, 6>(g, aff, blocks, lds, s);
-    default:
-      if (deep) return launch<2, 2, 0, 4, 10>(g, aff, blocks, lds, s);
-      return launch<2, 2, 0, 4, 6>(g, aff, blocks, lds, s);
+    case 1: return xb ? launch<2, 3, 1, 1, 8, true>(g, false, blocks, lds, s) : launch<2, 3, 1, 1, 8>(g, aff, blocks, lds, s);
+    case 2: return launch<4, 0, 2, 1, 10>(g, aff, blocks, lds, s);
+    default: return launch<2, 2, 0, 4, 10>(g, aff, blocks, lds, s);
   }
 }

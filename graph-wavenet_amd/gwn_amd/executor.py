@@ -15,6 +15,7 @@ skip term reach the output, model.py:216-222, 238), E1 = relu(end_conv_1), Y = e
 """
 import ctypes
 import os
+import warnings
 from collections import OrderedDict
 
 import torch
@@ -322,13 +323,17 @@ class Executor:
         * else 0: the f32-MFMA kernels (the default: the reference's fp32 arithmetic).
         0 when the shape has no bf16 tile kernel (c != 32, n > 512, no supports, GWN_GCN_T16=0)."""
         cfg = self.cfg
-        if self.compute_dtype != "bf16" or not cfg.use_gcn or cfg.nsup < 1 or not cfg.square:
+        if self.compute_dtype != "bf16":
             return 0
-        if not self._t16_ok() or not self._fused_gcn():
-            return 0
-        if not _lib.load().gwn_gcn_t16b_supported(cfg.N, cfg.nsup):
-            return 0
-        return 2 if os.environ.get("GWN_BF16_MLP", "1") != "0" else 1
+        planes = 0
+        if (cfg.use_gcn and cfg.nsup >= 1 and cfg.square and self._t16_ok() and self._fused_gcn()
+                and _lib.load().gwn_gcn_t16b_supported(cfg.N, cfg.nsup)):
+            planes = 2 if os.environ.get("GWN_BF16_MLP", "1") != "0" else 1
+        if planes == 0 and not getattr(self, "_warned_bf16", False):
+            self._warned_bf16 = True
+            warnings.warn("gwn_amd: compute dtype bf16 requested, but this shape (C=%d, N=%d, %d supports) has no "
+                          "bf16 tile kernel: the diffusion GCN runs in fp32" % (cfg.C, cfg.N, cfg.nsup))
+        return planes
 
     def pk(self, name, buf=None):
         return self.layout.view(self.packed if buf is None else buf, name)
@@ -415,9 +420,14 @@ class Executor:
                 # grouped adaptive-support gradient (gwn_gram_group, fp32 mode): each layer keeps its
                 # t1 / t2 ([rows][96]: the gcn backward's dhcat with only columns 32..96 written)
                 if cfg.adp_live and cfg.use_gcn and os.environ.get("GWN_GRAM_GROUP", "1") != "0":
-                    sl = (ctypes.c_int * (L - 1))(*[rows_l[i] // N for i in range(L - 1)])
-                    s["tt_l"] = [e(rows_l[i], 3 * C) for i in range(L - 1)]
-                    s["ws_gram_group"] = e(int(lib.gwn_gram_group_workspace_floats(N, sl, L - 1)) + 16)
+                    # a launch takes at most GRAM_GL layers: deeper stacks run several launches, the
+                    # later ones accumulating (the workspace: the largest chunk's need)
+                    need = [int(lib.gwn_gram_group_workspace_floats(
+                        N, (ctypes.c_int * len(ch))(*[rows_l[i] // N for i in ch]), len(ch)))
+                        for ch in _layer_chunks(L - 1)]
+                    if min(need) > 0:
+                        s["tt_l"] = [e(rows_l[i], 3 * C) for i in range(L - 1)]
+                        s["ws_gram_group"] = e(max(need) + 16)
             if cfg.Cin <= 4 and 256 % C == 0:  # the start conv's weight gradient (narrow form)
                 s["part_start"] = e(max(1, lib.gwn_wgrad_partial_count(ts[0] * P, C, cfg.Cin)) * (C * cfg.Cin + C))
             if cfg.E % 32 == 0 and (cfg.OP // 32) * (cfg.E // 32) <= 16:  # end_conv_2's weight gradient
@@ -594,9 +604,11 @@ class Executor:
         # bf16 mode: every layer's adaptive-support gram in one gwn_gram_g4_group launch at the end
         # of the backward (GWN_GRAM_GROUP=0: one gwn_gram_g4_bf16 per layer)
         if gram_g4 and L >= 2 and getattr(acts, "ws_g4g", None) is None and os.environ.get("GWN_GRAM_GROUP", "1") != "0":
-            sl = (ctypes.c_int * (L - 1))(*[ts[i + 1] * P // N for i in range(L - 1)])
-            need = int(_lib.load().gwn_gram_g4_group_workspace_floats(N, sl, L - 1))
-            acts.ws_g4g = torch.empty(need + 16, device=self.device, dtype=F32) if need > 0 else False
+            need = [int(_lib.load().gwn_gram_g4_group_workspace_floats(
+                N, (ctypes.c_int * len(ch))(*[ts[i + 1] * P // N for i in ch]), len(ch)))
+                for ch in _layer_chunks(L - 1)]
+            acts.ws_g4g = (torch.empty(max(need) + 16, device=self.device, dtype=F32) if min(need) > 0
+                           else False)
         # bf16 mode: the hop pieces' only reader is then the grouped mlp weight gradient -- stored
         # as bf16 (half the bytes written here and read there); GWN_BF16_PIECES=0 keeps them fp32
         pieces_b = (gram_g4 and "group_mlp" in scr and self._group_ok() and self._defer_ok(scr)
@@ -1192,8 +1204,10 @@ class Executor:
                 h, t = acts.H[i].data_ptr(), sc["tt_l"][i].data_ptr()
                 lay.append(_lib.GramLayer(x1=h, t1=t + 4 * C, x2=h + 4 * (1 + 2 * adp_index) * C, t2=t + 8 * C,
                                           slices=ts[i + 1] * P // N))
-            lib.call("gwn_gram_group", (_lib.GramLayer * len(lay))(*lay), len(lay), cfg.W, 3 * C, N, ptr(sc["dadp"]),
-                     cfg.NP, 0, ptr(sc["ws_gram_group"]), st)
+            for c, ch in enumerate(_layer_chunks(len(lay))):
+                sub = [lay[i] for i in ch]
+                lib.call("gwn_gram_group", (_lib.GramLayer * len(sub))(*sub), len(sub), cfg.W, 3 * C, N,
+                         ptr(sc["dadp"]), cfg.NP, int(c > 0), ptr(sc["ws_gram_group"]), st)
         if gram_g4_group:
             lay = []
             for i in range(L - 1):
@@ -1201,8 +1215,10 @@ class Executor:
                 half = S * ((N + 15) // 16) * 1024  # bytes of one bf16 operand
                 x, t = acts.XG4[i].data_ptr(), acts.TG4[i].data_ptr()
                 lay.append(_lib.GramLayer(x1=x, t1=t, x2=x + half, t2=t + half, slices=S))
-            lib.call("gwn_gram_g4_group", (_lib.GramLayer * len(lay))(*lay), len(lay), N, ptr(sc["dadp"]), cfg.NP, 0,
-                     ptr(acts.ws_g4g), st)
+            for c, ch in enumerate(_layer_chunks(len(lay))):
+                sub = [lay[i] for i in ch]
+                lib.call("gwn_gram_g4_group", (_lib.GramLayer * len(sub))(*sub), len(sub), N, ptr(sc["dadp"]),
+                         cfg.NP, int(c > 0), ptr(acts.ws_g4g), st)
         if defer:
             for k in range(0, len(segs), 32):  # <= 32 segments per launch (include/gwn.h)
                 chunk = segs[k:k + 32]
@@ -1421,3 +1437,12 @@ def wgrad(dY, J, X, Kc, rows, out, ws, bias_out=None, ldy=None):
     column)."""
     ks = _ksplit(J, Kc, rows)
     gemm(dY, 1, ldy or J, X, Kc, 1, out, Kc, 1, M=J, N=Kc, K=rows, ksplit=ks, part=ws, ones_out=bias_out)
+
+
+GRAM_GL = 8  # layers of one grouped gram launch (gram.hip GL)
+
+
+def _layer_chunks(n):
+    """Layer indices 0..n-1 cut into consecutive chunks of at most GRAM_GL (one grouped gram
+    launch each; the later launches accumulate into the first's output)."""
+    return [list(range(i, min(n, i + GRAM_GL))) for i in range(0, n, GRAM_GL)]

@@ -268,8 +268,9 @@ typedef struct gwn_gcn_args {
    * kernels): GWN_DTYPE_BF16 (1): bf16 operands, fp32 accumulation (v_mfma_f32_16x16x32_bf16) on the
    * 16-node tile kernel -- the mixed-precision path of configs[2].  Needs c == 32, nsup >= 1,
    * sup_g4b, layout 0, shared supports and gwn_gcn_t16b_supported(n, nsup); GWN_ERR_ARG otherwise.
-   * The mlp, the hop pieces, z and the BN partials stay fp32.  GWN_DTYPE_BF16_MLP (2): the same,
-   * and the mlp takes bf16 operands too (the pieces and W rounded to bf16, fp32 accumulation). */
+   * The mlp operands, z and the BN partials stay fp32; the hop pieces are fp32 columns of h, or
+   * bf16 in pieces_bf16 when given.  GWN_DTYPE_BF16_MLP (2): the same, and the mlp takes bf16
+   * operands too (the pieces and W rounded to bf16, fp32 accumulation). */
   int split_planes;
   /* per-sample supports (the per-sample-graph variant, gcn2 model.py:57-80; sup_batch <= 1 = shared):
    * slice s = t*sup_batch + b diffuses with support k at sup[k] + b*sup_bstride (floats), same
@@ -311,7 +312,8 @@ typedef struct gwn_gcn_args {
   const float* const* sup_g4;
   /* sup_g4b [2*nsup] (optional, bf16 operands: split_planes >= 1): A_k and A_k^2 as
    * gwn_support_g4_bf16 copies.  Given, the 16-node tile forward runs with the diffusion on bf16
-   * MFMA operands (fp32 accumulation; the mlp, hop pieces, z and BN partials in fp32). */
+   * MFMA operands (fp32 accumulation; the mlp on bf16 operands with GWN_DTYPE_BF16_MLP, else fp32;
+   * the hop pieces fp32 in h or bf16 in pieces_bf16; z and BN partials fp32). */
   const void* const* sup_g4b;
   /* xg4 (optional, the bf16 16-node tile kernel only: gwn_gcn_t16b_supported): X (the node
    * features, piece 0) and support xg4_support's hop-1 piece also written as bf16 in

@@ -102,3 +102,44 @@ def test_g17_diff_g_without_supports(gpu):
     _check_grads(m, {k[len("grad_f64/"):]: v for k, v in sub.items() if k.startswith("grad_f64/")}, "dgres")
     # the gcn mlps exist (gcn_bool) but never run: no gradient, as under reference autograd
     assert all(p.grad is None for n, p in m.named_parameters() if n.startswith("gconv."))
+
+
+@pytest.mark.parametrize("path", ["autograd", "trainer"])
+def test_deep_stack_gram_chunks(gpu, path):
+    """blocks=4, layers=3 at C=32: 11 adaptive-support gram layers, more than one
+    grouped gram launch takes (8), run as two launches, the second accumulating -- gradients against
+    the fp64 oracle like every other C=32 model test."""
+    from gwn_amd import synthetic, util
+    from gwn_amd.engine import trainer
+    from gwn_amd.model import gwnet
+    from oracle import gwnet_oracle as orc
+    n, B = 40, 2
+    adj = synthetic.random_sensor_graph(n, density=0.2, seed=11)
+    sups = synthetic.double_transition(adj)
+    x, y = synthetic.synthetic_batch(B, n, 12, seed=12)
+    torch.manual_seed(7)
+    dsups = [torch.tensor(a, device=gpu) for a in sups]
+    if path == "autograd":
+        m = gwnet(gpu, n, 0.0, supports=dsups, blocks=4, layers=3)
+        sd0 = {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()}
+        m.train()
+        out = m(torch.nn.functional.pad(torch.tensor(x, device=gpu), (1, 0, 0, 0)))
+        loss = _loss(out, y, gpu)
+        loss.backward()
+    else:
+        eng = trainer(util.StandardScaler(54.4, 19.5), 2, 12, n, 32, 0.0, 0.0, 0.0, gpu, dsups, True, True, None,
+                      4, 3)
+        m = eng.model
+        sd0 = {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()}
+        eng.clip = None
+        # the trainer's own x layout (train.py:244-247): [B, Cin, N, T] transposed views
+        met = eng.train(torch.tensor(x, device=gpu), torch.tensor(y, device=gpu))
+    torch.cuda.synchronize()
+    cfg = orc.Cfg(n, blocks=4, layers=3)
+    ref_out, ref_met, ref_g, _ = orc.grads(sd0, sups, x, y, cfg, 54.4, 19.5)
+    if path == "autograd":
+        assert rel_err(out.detach().cpu().numpy(), ref_out.numpy()) <= 1e-4
+        assert abs(loss.item() - ref_met[0]) <= 1e-4 * abs(ref_met[0])
+    else:
+        assert abs(met[0] - ref_met[0]) <= 1e-4 * abs(ref_met[0])
+    _check_grads(m, {k: v.numpy() for k, v in ref_g.items()}, "deep_" + path)

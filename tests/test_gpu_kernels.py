@@ -1430,20 +1430,25 @@ def test_gcn_t16_bf16_backward(gpu, n, mode):
             assert rel_err(got, ex.numpy()) <= 1e-2
 
 
-@pytest.mark.parametrize("shape", ["mlp", "tcn", "e2"])
+@pytest.mark.parametrize("shape", ["mlp", "mlp_xb", "tcn", "e2"])
 def test_wgrad_group_vs_fp64(gpu, shape):
     """gwn_wgrad_group (the deferred weight gradients of several layers in one launch, then
     gwn_reduce_partials) against fp64, per problem: the gcn mlp of 7 layers (J = 32, Kc = 224,
     the METR-LA row counts scaled down, ragged), the gated TCN of 8 layers (J = 64, two taps
     d*P apart, BatchNorm affine on load, identity affine for the first), end_conv_2 on its 32-row
-    padded gradient (J = 32, Kc = 512, one problem).  Bound per element: an fp32 FMA chain over the
-    rows, |err| <= 2^-22 R sum|dY||X|.  A second launch is bitwise identical (fixed-order sums)."""
+    padded gradient (J = 32, Kc = 512, one problem).  mlp_xb: the bf16 mode's mlp form
+    -- columns 0..31 fp32 from X, the hop pieces (columns 32..223) from a bf16 matrix Xb with
+    ldxb = 200 (> 192: the row pitch is exercised) -- against fp64 on the same bf16 values.  Bound
+    per element: an fp32 FMA chain over the rows, |err| <= 2^-22 R sum|dY||X|.  A second launch is
+    bitwise identical (fixed-order sums)."""
     import ctypes
     from gwn_amd import _lib
     lib = _lib.load()
-    torch.manual_seed({"mlp": 1, "tcn": 2, "e2": 3}[shape])
+    torch.manual_seed({"mlp": 1, "mlp_xb": 4, "tcn": 2, "e2": 3}[shape])
     P = 207 * 3
-    if shape == "mlp":
+    xb = shape == "mlp_xb"
+    ldxb = 200
+    if shape in ("mlp", "mlp_xb"):
         J, Kt, ntaps, Ts = 32, 224, 1, [12, 10, 9, 7, 6, 4, 3]
     elif shape == "tcn":
         J, Kt, ntaps, Ts = 64, 32, 2, [12, 10, 9, 7, 6, 4, 3, 1]
@@ -1459,6 +1464,8 @@ def test_wgrad_group_vs_fp64(gpu, shape):
         if shape == "e2":
             dY[:, 12:] = 0.0  # the padded output gradient
         X = torch.randn(x_rows, Kt, dtype=torch.float64) * 2 + 1
+        if xb:  # the pieces as the kernel sees them: bf16 values
+            X[:, 32:] = X[:, 32:].to(torch.bfloat16).double()
         aff = None
         if shape == "tcn":
             aff = (torch.zeros(Kt), torch.ones(Kt), torch.zeros(Kt)) if p == 0 else \
@@ -1472,12 +1479,19 @@ def test_wgrad_group_vs_fp64(gpu, shape):
         dYd, Xd = dY.float().to(gpu), X.float().to(gpu)
         affd = [a.float().to(gpu) for a in aff] if aff is not None else [None] * 3
         part = torch.full((nb[p] * (J * Kt * ntaps + J),), float("nan"), device=gpu)
-        keep.append((dYd, Xd, affd, part))
+        Xbd = None
+        if xb:  # Xb[r][k - 32] = X[r][k] (bf16), the fp32 X keeps garbage past column 32
+            Xbd = torch.zeros(x_rows, ldxb, dtype=torch.bfloat16)
+            Xbd[:, :Kt - 32] = X[:, 32:].to(torch.bfloat16)
+            Xbd = Xbd.to(gpu)
+            Xd[:, 32:] = float("nan")
+        keep.append((dYd, Xd, affd, part, Xbd))
         probs.append(_lib.WgradProblem(dY=dYd.data_ptr(), ldy=J, X=Xd.data_ptr(), ldx=Kt, x_rows=X.shape[0], shift=shift,
                                        x_mean=affd[0].data_ptr() if aff is not None else None,
                                        x_scale=affd[1].data_ptr() if aff is not None else None,
                                        x_shift=affd[2].data_ptr() if aff is not None else None,
-                                       part=part.data_ptr(), R=R))
+                                       part=part.data_ptr(), R=R,
+                                       Xb=Xbd.data_ptr() if xb else None, ldxb=ldxb if xb else 0))
     arr = (_lib.WgradProblem * len(probs))(*probs)
     Kc = Kt * ntaps
     outs = []

@@ -418,3 +418,36 @@ def test_num_batches_tracked_counts_train_forwards(gpu):
         dg(xd, None, None).sum().backward()
     torch.cuda.synchronize()
     assert [int(b.num_batches_tracked) for b in dg.bn] == [2] * len(dg.bn)
+
+
+def test_sync_check_debug_mode(gpu):
+    """GWN_SYNC_CHECK (the debugging aid, gwn_set_sync_check): every launch synchronised and every
+    operand / workspace range checked against its device allocation.  A train-mode forward +
+    backward runs clean under it and gives the same bits as without it."""
+    from gwn_amd import _lib, synthetic, util
+    from gwn_amd.model import gwnet
+    n = 40
+    sups = synthetic.double_transition(synthetic.random_sensor_graph(n, density=0.2, seed=3))
+    x, y = synthetic.synthetic_batch(2, n, 12, seed=5)
+
+    def run():
+        torch.manual_seed(999)
+        m = gwnet(gpu, n, 0.0, supports=[torch.tensor(a, device=gpu) for a in sups])
+        m.train()
+        out = m(torch.nn.functional.pad(torch.tensor(x, device=gpu), (1, 0, 0, 0)))
+        loss = util.masked_mae(out.transpose(1, 3) * 19.5 + 54.4, torch.tensor(y, device=gpu).unsqueeze(1), 0.0)
+        loss.backward()
+        torch.cuda.synchronize()
+        return out.detach().cpu(), {k: p.grad.detach().cpu() for k, p in m.named_parameters() if p.grad is not None}
+
+    ref_out, ref_g = run()
+    lib = _lib.load()
+    lib.gwn_set_sync_check(1)
+    try:
+        out, g = run()
+    finally:
+        lib.gwn_set_sync_check(0)
+    assert torch.equal(out, ref_out)
+    assert set(g) == set(ref_g)
+    for k in g:
+        assert torch.equal(g[k], ref_g[k]), k
