@@ -1504,12 +1504,8 @@ __device__ __forceinline__ bf16x8m t16_img_col_b(const __bf16* img, int s16, int
 // (tools/t16_loop_probe.hip, 16 waves per CU: L1 / address processing per load instruction),
 // these at 0.93.  Fragments run one group (4 k-steps) ahead: the group's load pair is issued
 // before the previous group's products, so every wait is vmcnt(2).
-// S > 1: the wave diffuses S slice images (the same 16-node column of S slices) against the same
-// support fragments -- each 16-B fragment load feeds 4 S MFMAs, and the S slices' products are
-// independent chains (acc[s][q][hf]).
-template <int S>
-__device__ __forceinline__ void t16_diffuse_s(const float* const (&img)[S], int hs, const float* G1, const float* G2,
-                                              int n, int tile, int lane, f32x4v (&acc)[S][2][2]) {
+__device__ __forceinline__ void t16_diffuse(const float* img, int hs, const float* G1, const float* G2, int n, int tile,
+                                            int lane, f32x4v (*acc)[2]) {
   const int g = lane >> 4, j = lane & 15;
   const int nt = (n + 15) >> 4, nkg = nt;  // k-groups of 16 rows: ceil(n / 16), as the column tiles
   const int bytes = nkg * nt * 1024;
@@ -1522,18 +1518,10 @@ __device__ __forceinline__ void t16_diffuse_s(const float* const (&img)[S], int 
   a2[0] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r2, off(0), 0, 0));
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int s = 0; s < S; ++s)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) acc[s][q][0] = acc[s][q][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-  const float* xp[S];
+  for (int q = 0; q < 2; ++q) acc[q][0] = acc[q][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  const float* xp = img + g * 16 + j;
   // image operands one k-step ahead: the LDS latency hides behind the current step's products
-  float xa[S], xb[S];
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    xp[s] = img[s] + g * 16 + j;
-    xa[s] = xp[s][0];
-    xb[s] = xp[s][hs];
-  }
+  float xa = xp[0], xb = xp[hs];
   // group kg (fragments in buffer kg & 1); the next group's pair is requested first (past the
   // last group the offsets leave the buffer range: zeros, no traffic)
   auto group = [&](int kg, int bsel) {
@@ -1543,25 +1531,14 @@ __device__ __forceinline__ void t16_diffuse_s(const float* const (&img)[S], int 
     for (int i = 0; i < 4; ++i) {
       const int ks = 4 * kg + i;
       // the image has 4 * nkp + 4 rows (t16_img_rows): step nkp's read stays inside
-      float na[S], nb[S];
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        na[s] = xp[s][4 * (ks + 1) * 16];
-        nb[s] = xp[s][hs + 4 * (ks + 1) * 16];
-      }
+      const float na = xp[4 * (ks + 1) * 16], nb = xp[hs + 4 * (ks + 1) * 16];
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        acc[s][0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], a1[bsel][i], acc[s][0][0], 0, 0, 0);
-        acc[s][0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s], a1[bsel][i], acc[s][0][1], 0, 0, 0);
-        acc[s][1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], a2[bsel][i], acc[s][1][0], 0, 0, 0);
-        acc[s][1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s], a2[bsel][i], acc[s][1][1], 0, 0, 0);
-      }
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        xa[s] = na[s];
-        xb[s] = nb[s];
-      }
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, a1[bsel][i], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb, a1[bsel][i], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, a2[bsel][i], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb, a2[bsel][i], acc[1][1], 0, 0, 0);
+      xa = na;
+      xb = nb;
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -1571,35 +1548,6 @@ __device__ __forceinline__ void t16_diffuse_s(const float* const (&img)[S], int 
     group(kg + 1, 1);
   }
   if (kg < nkg) group(kg, 0);
-}
-__device__ __forceinline__ void t16_diffuse(const float* img, int hs, const float* G1, const float* G2, int n, int tile,
-                                            int lane, f32x4v (&acc)[1][2][2]) {
-  const float* const im[1] = {img};
-  t16_diffuse_s<1>(im, hs, G1, G2, n, tile, lane, acc);
-}
-
-// t16_mlp for S slices' pieces with the same channel map (its fragments read once): x(s, hf) is
-// slice s's piece half hf, hacc[s] its output accumulators
-template <int S, typename X>
-__device__ __forceinline__ void t16_mlp_s(const float* m, int ld_m, X x, int lane, f32x4v (&hacc)[S][2]) {
-  const int g = lane >> 4, j = lane & 15;
-  float wf[2][2][4];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int oh = 0; oh < 2; ++oh) wf[hf][oh][s] = m[(16 * hf + 4 * g + s) * ld_m + 16 * oh + j];
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int oh = 0; oh < 2; ++oh)
-#pragma unroll
-        for (int sp = 0; sp < S; ++sp)
-          hacc[sp][oh] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[hf][oh][s], x(sp, hf)[s], hacc[sp][oh], 0, 0, 0);
 }
 
 // the image rows of the wave's tile as B operands in the permuted channel order of t16_mlp
@@ -1641,10 +1589,11 @@ __device__ __forceinline__ void t16_store_g4(void* base, int which, int slices, 
   *(bf16x8g*)((char*)base + (((long)which * slices + slice) * nt + tile) * 1024 + lane * 16) = r;
 }
 
-// SPW slices per wave: the range is cut over slice GROUPS (SPW consecutive slices) x node tiles;
-// a wave's unit is one 16-node column of every slice of a group, the group's diffusions sharing
-// the support fragments (t16_diffuse_s) and its mlps the channel-map fragments (t16_mlp_s)
-template <int MAXT, int SPW>
+// (Two slices per wave -- the same node column of two slices diffused against shared support
+// fragments, the channel-map fragments shared by both mlps -- measured slower at every layer shape:
+// 167 vs 159 us at 768 slices with 16 waves (51 registers spilled), 167 at 12 waves without spills;
+// profiles/r05/spw.)
+template <int MAXT>
 __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, const PowSup p, const int maximg) {
   extern __shared__ float lds[];
   const int n = a.n;
@@ -1656,9 +1605,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int nwaves = blockDim.x >> 6;
   const long ldh = a.ld_h;
-  const int groups = (a.slices + SPW - 1) / SPW;
-  const int gimg = maximg / SPW;  // groups a phase holds
-  const T16Range rg = t16_range(groups, nt);
+  const T16Range rg = t16_range(a.slices, nt);
   BnRun bn;
   bn_init(bn, wpart);
   // the phase's slices staged in one pass (stage_rows4; the channel maps inside its first round
@@ -1666,10 +1613,9 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
   if (!h16) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
   for (long p0 = rg.tb; p0 < rg.te;) {
-    const int q0 = (int)(p0 / nt);
-    const long p1 = min(rg.te, (long)(q0 + gimg) * nt);
-    const int q1 = (int)((p1 - 1) / nt);
-    const int s0 = q0 * SPW, s1 = min((q1 + 1) * SPW, a.slices) - 1;
+    const int s0 = (int)(p0 / nt);
+    const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
+    const int s1 = (int)((p1 - 1) / nt);
     if (p0 != rg.tb) __syncthreads();  // the previous phase's images are released
     if (h16) {
       const bool maps = p0 == rg.tb;
@@ -1686,55 +1632,40 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
     const int span = (int)(p1 - p0);
     for (int tp = wave; tp < span; tp += nwaves) {
       const long t = p0 + tp;
-      const int q = (int)(t / nt), tile = (int)(t - (long)q * nt);
+      const int s = (int)(t / nt), tile = (int)(t - (long)s * nt);
+      const float* xs = imgs + (s - s0) * imgf;
+      const long row0 = (long)s * n;
+      float* hs_out = (float*)a.h + row0 * ldh;
+      const bool nt_ok = ((((uintptr_t)hs_out) & 15) | (ldh & 3)) == 0;
       const int w0 = 16 * tile;
-      int sl[SPW];
-      bool ok[SPW];
-      const float* xs[SPW];
-#pragma unroll
-      for (int s = 0; s < SPW; ++s) {
-        sl[s] = q * SPW + s;
-        ok[s] = sl[s] < a.slices;  // a short last group diffuses its first slice twice, stores once
-        xs[s] = imgs + ((ok[s] ? sl[s] : sl[0]) - s0) * imgf;
-      }
-      f32x4v hacc[SPW][2];
-#pragma unroll
-      for (int s = 0; s < SPW; ++s) hacc[s][0] = hacc[s][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      f32x4v hacc[2];
+      hacc[0] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      hacc[1] = hacc[0];
       {  // piece 0: the node features themselves
-        f32x4v x0[SPW][2];
-#pragma unroll
-        for (int s = 0; s < SPW; ++s) t16_rows(xs[s], hs, w0, lane, x0[s]);
-        t16_mlp_s<SPW>(ws, LDW16, [&](int s, int hf) { return x0[s][hf]; }, lane, hacc);
+        f32x4v x0[2];
+        t16_rows(xs, hs, w0, lane, x0);
+        t16_mlp(ws, LDW16, x0, lane, hacc);
       }
       for (int k = 0; k < a.nsup; ++k) {
-        f32x4v acc[SPW][2][2];  // [slice][power][channel half]
-        t16_diffuse_s<SPW>(xs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, acc);
+        f32x4v acc[2][2];  // [power][channel half]
+        t16_diffuse(xs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, acc);
 #pragma unroll
-        for (int pw = 0; pw < 2; ++pw) {
-          t16_mlp_s<SPW>(ws + (1 + 2 * k + pw) * CH * LDW16, LDW16, [&](int s, int hf) { return acc[s][pw][hf]; }, lane,
-                         hacc);
+        for (int q = 0; q < 2; ++q) {
+          t16_mlp(ws + (1 + 2 * k + q) * CH * LDW16, LDW16, acc[q], lane, hacc);
           if (a.store_pieces && w0 + j < n) {
+            float* dp = hs_out + (long)(w0 + j) * ldh + (1 + 2 * k + q) * CH + 4 * g;
 #pragma unroll
-            for (int s = 0; s < SPW; ++s) {
-              if (!ok[s]) continue;
-              float* hs_out = (float*)a.h + (long)sl[s] * n * ldh;
-              const bool nt_ok = ((((uintptr_t)hs_out) & 15) | (ldh & 3)) == 0;
-              float* dp = hs_out + (long)(w0 + j) * ldh + (1 + 2 * k + pw) * CH + 4 * g;
+            for (int hf = 0; hf < 2; ++hf) {
+              if (nt_ok) __builtin_nontemporal_store(acc[q][hf], (f32x4v*)(dp + 16 * hf));
+              else {
 #pragma unroll
-              for (int hf = 0; hf < 2; ++hf) {
-                if (nt_ok) __builtin_nontemporal_store(acc[s][pw][hf], (f32x4v*)(dp + 16 * hf));
-                else {
-#pragma unroll
-                  for (int e = 0; e < 4; ++e) dp[16 * hf + e] = acc[s][pw][hf][e];
-                }
+                for (int e = 0; e < 4; ++e) dp[16 * hf + e] = acc[q][hf][e];
               }
             }
           }
         }
       }
-#pragma unroll
-      for (int s = 0; s < SPW; ++s)
-        if (ok[s]) t16_epilogue(a, hacc[s], (long)sl[s] * n, w0, lane, n, bn);
+      t16_epilogue(a, hacc, row0, w0, lane, n, bn);
     }
     p0 = p1;
   }
@@ -1999,6 +1930,147 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
   t16_bn_flush(a, bn, wpart);
 }
 
+// Two slices per wave in the bf16-mlp forward (the same node column of slices 2q and 2q + 1): at
+// N = 325 the single-slice kernel streams ~66 KB of support fragments per tile from L2 (~17 TB/s,
+// the L2's shared-rows rate), so each fragment load here feeds both slices' MFMAs.
+__device__ __forceinline__ void t16b_diffuse2(const __bf16* imgA, const __bf16* imgB, const __bf16* G1,
+                                              const __bf16* G2, int n, int tile, int lane, f32x4v (*accA)[2],
+                                              f32x4v (*accB)[2]) {
+  const int g = lane >> 4, j = lane & 15;
+  const int nt = (n + 15) >> 4, nkg = (n + 31) >> 5, s16 = t16b_s16(n);
+  const int bytes = nkg * nt * 1024;
+  const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc((void*)G1, (short)0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc((void*)G2, (short)0, bytes, 0x00020000);
+  auto off = [&](int kg) { return ((kg * nt + tile) * 64 + lane) * 16; };
+  const __bf16* xa0 = imgA + j * s16 + 8 * g;
+  const __bf16* xa1 = imgA + (16 + j) * s16 + 8 * g;
+  const __bf16* xb0 = imgB + j * s16 + 8 * g;
+  const __bf16* xb1 = imgB + (16 + j) * s16 + 8 * g;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) accA[q][0] = accA[q][1] = accB[q][0] = accB[q][1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  auto ld = [&](const __amdgpu_buffer_rsrc_t& r, int kg) {
+    return __builtin_bit_cast(bf16x8b, __builtin_amdgcn_raw_buffer_load_b128(r, off(kg), 0, 0));
+  };
+  bf16x8b b1 = ld(r1, 0), b2 = ld(r2, 0);
+  for (int kg = 0; kg < nkg; ++kg) {
+    const bf16x8b nb1 = ld(r1, kg + 1), nb2 = ld(r2, kg + 1);
+    const bf16x8b pa0 = *(const bf16x8b*)(xa0 + 32 * kg), pa1 = *(const bf16x8b*)(xa1 + 32 * kg);
+    const bf16x8b pb0 = *(const bf16x8b*)(xb0 + 32 * kg), pb1 = *(const bf16x8b*)(xb1 + 32 * kg);
+    accA[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa0, b1, accA[0][0], 0, 0, 0);
+    accA[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa1, b1, accA[0][1], 0, 0, 0);
+    accB[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pb0, b1, accB[0][0], 0, 0, 0);
+    accB[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pb1, b1, accB[0][1], 0, 0, 0);
+    accA[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa0, b2, accA[1][0], 0, 0, 0);
+    accA[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa1, b2, accA[1][1], 0, 0, 0);
+    accB[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pb0, b2, accB[1][0], 0, 0, 0);
+    accB[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pb1, b2, accB[1][1], 0, 0, 0);
+    b1 = nb1;
+    b2 = nb2;
+  }
+}
+
+// t16_mlp_bp for two slices with one read of the map's A fragments
+__device__ __forceinline__ void t16_mlp_bp2(const __bf16* maps, int p, const bf16x8m bA, const bf16x8m bB, int lane,
+                                            f32x4v* haccA, f32x4v* haccB) {
+  const bf16x8m a0 = *(const bf16x8m*)(maps + ((p * 2 + 0) * 64 + lane) * 8);
+  const bf16x8m a1 = *(const bf16x8m*)(maps + ((p * 2 + 1) * 64 + lane) * 8);
+  __builtin_amdgcn_sched_barrier(0);
+  haccA[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bA, haccA[0], 0, 0, 0);
+  haccB[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bB, haccB[0], 0, 0, 0);
+  haccA[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bA, haccA[1], 0, 0, 0);
+  haccB[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bB, haccB[1], 0, 0, 0);
+}
+
+// the bf16-mlp forward over slice pairs: units = (pair, node tile) in pair-major order, cut into
+// equal ranges per CU; a phase holds maximg (even) slices
+template <int MAXT>
+__global__ __launch_bounds__(MAXT) void gcn_fwd_t16b2_kernel(const FusedFwd a, const PowSup p, const int maximg) {
+  extern __shared__ float lds[];
+  const int n = a.n;
+  const int nt = (n + 15) >> 4;
+  const int s16 = t16b_s16(n), imgb = CH * s16;
+  float* ws = lds;
+  float* wpart = ws + (2 * a.nsup + 1) * CH * LDW16;
+  __bf16* imgs = (__bf16*)(wpart + T16_WAVES * 3 * CH);
+  const __bf16* maps = (const __bf16*)ws;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  const int nwaves = blockDim.x >> 6;
+  const long ldh = a.ld_h;
+  const int pairs = (a.slices + 1) / 2;
+  const T16Range rg = t16_range(pairs, nt);
+  BnRun bn;
+  bn_init(bn, wpart);
+  for (long p0 = rg.tb; p0 < rg.te;) {
+    const int q0 = (int)(p0 / nt);
+    const long p1 = min(rg.te, (long)(q0 + maximg / 2) * nt);
+    const int q1 = (int)((p1 - 1) / nt);
+    const int s0 = 2 * q0, s1 = min(2 * q1 + 2, a.slices) - 1;
+    if (p0 != rg.tb) __syncthreads();
+    const bool first = p0 == rg.tb;
+    stage_bf16_octets(a.h + (long)s0 * n * ldh, ldh, n, s16, s1 - s0 + 1, imgs, imgb, [&] {
+      if (first) t16_stage_maps_bf16(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, (__bf16*)ws);
+    });
+    __syncthreads();
+    const int span = (int)(p1 - p0);
+    for (int tp = wave; tp < span; tp += nwaves) {
+      const long t = p0 + tp;
+      const int q = (int)(t / nt), tile = (int)(t - (long)q * nt);
+      const int sA = 2 * q, sB = 2 * q + 1;
+      const bool okB = sB < a.slices;  // an odd last slice: B diffuses A's image, stores nothing
+      const __bf16* xsA = imgs + (sA - s0) * imgb;
+      const __bf16* xsB = okB ? imgs + (sB - s0) * imgb : xsA;
+      const long rowA = (long)sA * n, rowB = (long)sB * n;
+      const int w0 = 16 * tile;
+      f32x4v haccA[2], haccB[2];
+      haccA[0] = haccA[1] = haccB[0] = haccB[1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      {
+        const bf16x8m bA = t16_img_col_b(xsA, s16, w0, lane), bB = t16_img_col_b(xsB, s16, w0, lane);
+        t16_mlp_bp2(maps, 0, bA, bB, lane, haccA, haccB);
+        if (a.xg4) {
+          *(bf16x8m*)((char*)a.xg4 + ((long)sA * nt + tile) * 1024 + lane * 16) = bA;
+          if (okB) *(bf16x8m*)((char*)a.xg4 + ((long)sB * nt + tile) * 1024 + lane * 16) = bB;
+        }
+      }
+      for (int k = 0; k < a.nsup; ++k) {
+        f32x4v accA[2][2], accB[2][2];
+        t16b_diffuse2(xsA, xsB, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, accA, accB);
+        if (a.xg4 && k == a.xg4_k) {
+          t16_store_g4(a.xg4, 1, a.slices, sA, nt, tile, lane, accA[0]);
+          if (okB) t16_store_g4(a.xg4, 1, a.slices, sB, nt, tile, lane, accB[0]);
+        }
+#pragma unroll
+        for (int pw = 0; pw < 2; ++pw) {
+          const bf16x8m bA = t16_pack_b(accA[pw]), bB = t16_pack_b(accB[pw]);
+          t16_mlp_bp2(maps, 1 + 2 * k + pw, bA, bB, lane, haccA, haccB);
+          if (a.store_pieces && a.pb && w0 + j < n) {
+            typedef __bf16 bf16x4p __attribute__((ext_vector_type(4)));
+            __bf16* bpA = (__bf16*)a.pb + (rowA + w0 + j) * a.ld_pb + (2 * k + pw) * CH + 4 * g;
+            *(bf16x4p*)bpA = bf16x4p{bA[0], bA[1], bA[2], bA[3]};
+            *(bf16x4p*)(bpA + 16) = bf16x4p{bA[4], bA[5], bA[6], bA[7]};
+            if (okB) {
+              __bf16* bpB = (__bf16*)a.pb + (rowB + w0 + j) * a.ld_pb + (2 * k + pw) * CH + 4 * g;
+              *(bf16x4p*)bpB = bf16x4p{bB[0], bB[1], bB[2], bB[3]};
+              *(bf16x4p*)(bpB + 16) = bf16x4p{bB[4], bB[5], bB[6], bB[7]};
+            }
+          } else if (a.store_pieces && w0 + j < n) {  // fp32 pieces into h
+            float* dA = (float*)a.h + (rowA + w0 + j) * ldh + (1 + 2 * k + pw) * CH + 4 * g;
+            float* dB = (float*)a.h + (rowB + w0 + j) * ldh + (1 + 2 * k + pw) * CH + 4 * g;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+              __builtin_nontemporal_store(accA[pw][hf], (f32x4v*)(dA + 16 * hf));
+              if (okB) __builtin_nontemporal_store(accB[pw][hf], (f32x4v*)(dB + 16 * hf));
+            }
+          }
+        }
+      }
+      t16_epilogue(a, haccA, rowA, w0, lane, n, bn);
+      if (okB) t16_epilogue(a, haccB, rowB, w0, lane, n, bn);
+    }
+    p0 = p1;
+  }
+  t16_bn_flush(a, bn, wpart);
+}
+
 // Backward on 16-node tiles: the forward's structure with the dh image (BN-backward prologue),
 // the transposed supports A_k^T and (A_k^2)^T (so D = A dh, A^2 dh) and the channel map W^T:
 //   dxg = W_0^T dh + sum_k W_{1+2k}^T (A_k dh) + W_{2+2k}^T (A_k^2 dh)
@@ -2246,10 +2318,9 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
         mlp(0, d0, dx);
       }
       for (int k = 0; k < a.nsup; ++k) {
-        f32x4v e1[1][2][2];
-        f32x4v (&e)[2][2] = e1[0];
+        f32x4v e[2][2];
         if (BF) t16b_diffuse((const __bf16*)dhs, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, e);
-        else t16_diffuse(dhs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, e1);
+        else t16_diffuse(dhs, hs, p.g4[2 * k], p.g4[2 * k + 1], n, tile, lane, e);
         mlp(1 + 2 * k, e[0], dx);
         mlp(2 + 2 * k, e[1], dx);
         if (k == a.adp_index) {  // t1 = W1^T dh + W2^T (A dh), t2 = W2^T dh
@@ -2573,31 +2644,22 @@ struct T16Plan {
   int grid, maximg;
   size_t lds;
 };
-// spw > 1 (the forward's slice groups): the units are groups of spw slices x tiles and maximg a
-// multiple of spw; not ok when one group's images do not fit.
-T16Plan t16_plan(int n, int nsup, int slices, int spw = 1) {
+T16Plan t16_plan(int n, int nsup, int slices) {
   T16Plan pl{false, 0, 0, 0};
   const size_t fixed = t16_lds_bytes(n, nsup, 0), img = t16_lds_bytes(n, nsup, 1) - fixed;
-  if (fixed + spw * img > (size_t)T16_LDS_MAX || slices <= 0) return pl;
+  if (fixed + img > (size_t)T16_LDS_MAX || slices <= 0) return pl;
   const int nt = (n + 15) / 16;
-  const long tiles = (long)((slices + spw - 1) / spw) * nt;
+  const long tiles = (long)slices * nt;
   pl.grid = (int)(tiles < gwn_device_cus() ? tiles : gwn_device_cus());
   const long per = (tiles + pl.grid - 1) / pl.grid;
-  const int span = (int)((per - 1 + nt - 1) / nt) + 1;  // groups a range of `per` units can touch
-  int gmax = (int)((T16_LDS_MAX - fixed) / (spw * img));
-  gmax = gmax < T16_MAXIMG / spw ? gmax : T16_MAXIMG / spw;
-  pl.maximg = spw * (gmax < span ? gmax : span);
+  const int span = (int)((per - 1 + nt - 1) / nt) + 1;  // slices a range of `per` tiles can touch
+  int maximg = (int)((T16_LDS_MAX - fixed) / img);
+  maximg = maximg < T16_MAXIMG ? maximg : T16_MAXIMG;
+  pl.maximg = maximg < span ? maximg : span;
   pl.lds = fixed + pl.maximg * img;
   if (pl.lds < 81 * 1024) pl.lds = 81 * 1024;
   pl.ok = true;
   return pl;
-}
-
-// slices per wave of the fp32 tile forward (experiment: GWN_T16_SPW, default 1)
-int t16_spw(int slices, int nt) {
-  const char* e = getenv("GWN_T16_SPW");
-  (void)slices; (void)nt;
-  return e ? atoi(e) : 1;  // 3: two slices per wave in 12-wave workgroups
 }
 
 // zero the BN partial slots [written, gwn_bn_part_slots(slices)) that a whole-slice kernel leaves
@@ -2688,7 +2750,31 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
       a.ksplit = 1;
       a.bn_slots = (int)gwn_bn_part_slots(slices);
       if (fold_here) a.fold = *g->bn_fold;
-      if (g->split_planes == 2) gcn_fwd_t16b_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      const char* spw_e = getenv("GWN_T16B_SPW");  // experiment: two slices per wave
+      const int slices2 = (slices + 1) / 2;
+      const long units2 = (long)slices2 * nt;
+      const int grid2 = (int)(units2 < gwn_device_cus() ? units2 : gwn_device_cus());
+      const long per2 = (units2 + grid2 - 1) / grid2;
+      int gmax2 = (int)((T16_LDS_MAX - fixed) / (2 * img));
+      gmax2 = gmax2 < T16_MAXIMG / 2 ? gmax2 : T16_MAXIMG / 2;
+      const int span2 = (int)((per2 - 1 + nt - 1) / nt) + 1;
+      const int maximg2 = 2 * (gmax2 < span2 ? gmax2 : span2);
+      const bool h16 = ((((uintptr_t)a.h) & 15) | (a.ld_h & 3)) == 0;
+      if (g->split_planes == 2 && spw_e && (spw_e[0] == '2' || spw_e[0] == '3') && gmax2 >= 1 && h16 && !fold_here) {
+        static bool attr2 = false;
+        if (!attr2) {
+          (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b2_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    T16_LDS_MAX);
+          (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b2_kernel<768>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    T16_LDS_MAX);
+          attr2 = true;
+        }
+        size_t lds2 = fixed + maximg2 * img;
+        if (lds2 < 81 * 1024) lds2 = 81 * 1024;
+        if (spw_e[0] == '3') gcn_fwd_t16b2_kernel<768><<<grid2, 768, lds2, s>>>(a, p, maximg2);
+        else gcn_fwd_t16b2_kernel<1024><<<grid2, 64 * T16_WAVES, lds2, s>>>(a, p, maximg2);
+      } else if (g->split_planes == 2)
+        gcn_fwd_t16b_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       else gcn_fwd_t16b_kernel<1024><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       GWN_CHECK_LAUNCH();
       *folded = fold_here;
@@ -2708,11 +2794,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
     ensure_lds_attr(gcn_fwd_fused_kernel<1024, true>);
     ensure_lds_attr(gcn_fwd_pow_kernel<512>);
     ensure_lds_attr(gcn_fwd_pow_kernel<1024>);
-    (void)hipFuncSetAttribute((const void*)gcn_fwd_t16_kernel<1024, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              T16_LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)gcn_fwd_t16_kernel<1024, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              T16_LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)gcn_fwd_t16_kernel<768, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gcn_fwd_t16_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               T16_LDS_MAX);
     attr_set = true;
   }
@@ -2731,14 +2813,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
     // partial slot (gwn_bn_part_slots)
     a.bn_slots = (int)gwn_bn_part_slots(slices);
     if (fold_here) a.fold = *g->bn_fold;
-    const T16Plan p2 = t16_plan(g->n, g->nsup, slices, 2);
-    const int spw = t16_spw(slices, (g->n + 15) / 16);
-    if (spw == 3 && p2.ok && !fold_here)
-      gcn_fwd_t16_kernel<768, 2><<<p2.grid, 768, p2.lds, s>>>(a, p, p2.maximg);
-    else if (spw == 2 && p2.ok)
-      gcn_fwd_t16_kernel<1024, 2><<<p2.grid, 64 * T16_WAVES, p2.lds, s>>>(a, p, p2.maximg);
-    else
-      gcn_fwd_t16_kernel<1024, 1><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
+    gcn_fwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
     GWN_CHECK_LAUNCH();
     *folded = fold_here;
     return GWN_OK;

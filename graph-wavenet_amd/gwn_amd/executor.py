@@ -1030,6 +1030,9 @@ class Executor:
         side = self._side_stream() if overlap else None
 
         def head_wgrad(dY, J, X, Kc, w, b, ldy=None):
+            # (the head's weight gradients on a second stream beside its input gradients, joined
+            # before the deferred reduction, measured slower: 24.4-24.7k vs 25.0k samples/s,
+            # profiles/r05/head_side)
             if not overlap:
                 wgrad(dY, J, X, Kc, rows_f, w, ws, b, ldy=ldy)
                 return

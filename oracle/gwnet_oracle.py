@@ -133,6 +133,61 @@ def bf16_round(t):
     return t.to(torch.bfloat16).to(t.dtype)
 
 
+class Bf16Pins:
+    """Rounding-boundary pinning of the bf16 emulation (gradient / forward gates of the bf16 mode).
+
+    Rounding an fp32-computed value v = exact + err (|err| <= band) to bf16 and rounding exact itself
+    differ when exact lies within band of a rounding boundary (the midpoint of two adjacent bf16
+    numbers) -- or, for values so small that band exceeds their ulp, by a few ulps; the difference
+    propagates as a ~2^-8 relative change of one operand.  Like the ReLU / |.| branch pinning
+    (module docstring), the emulation can take the rounding the HIP run took, element by element,
+    where it is such a tie: |hip - exact| <= half an ulp of hip + band (what rounding a value
+    within band of exact can give):
+      * supports: the HIP run's fp32 A_k and A_k^2 (``sup``: [(A, A2), ...] in support order) are
+        checked against the exact ones (max-rel <= ``sup_tol``) and rounded to bf16 in their place;
+      * the gcn input g (``g[i]``: the layer's fp32 g, NCHW): bf16(g_hip) is adopted as above with
+        band = ``g_band`` * max|g| (the fp32 error the layers below leave in g);
+      * the hop pieces (``pieces[i]``: the bf16 pieces the HIP run stored, NCHW [B, 2K*C, N, T]):
+        adopted with band = ``piece_band`` * sum|terms| (the fp32 accumulation error bound of the
+        diffusion sum, sum|terms| = |rnd(g)| diffused through |rnd(A)|).
+    Every difference that is not such a tie is counted in ``report`` as a violation (the tests
+    require none); adopted ties are counted too."""
+
+    def __init__(self, sup=None, g=None, pieces=None, sup_tol=1e-5, g_band=2.0 ** -16, piece_band=2.0 ** -19):
+        self.sup, self.g, self.pieces = sup, g or {}, pieces or {}
+        self.sup_tol, self.g_band, self.piece_band = sup_tol, g_band, piece_band
+        self.report = {"g_adopted": 0, "g_bad": 0, "piece_adopted": 0, "piece_bad": 0, "sup_err": 0.0}
+
+    def adopt(self, own_b, exact, hip_b, band, tag):
+        """own_b = bf16(exact); hip_b = the HIP run's bf16 value: hip_b where it is a rounding tie."""
+        diff = own_b != hip_b
+        if not bool(diff.any()):
+            return own_b
+        _, e = torch.frexp(hip_b)  # hip = m 2^e, 0.5 <= |m| < 1: a bf16 ulp there is 2^(e - 8)
+        half_ulp = torch.ldexp(torch.ones_like(hip_b), e - 9)
+        reach = (hip_b - exact).abs() / (half_ulp + band)  # <= 1: a rounding of some value within band of exact
+        tie = reach <= 1.0
+        ok = diff & tie
+        bad = diff & ~tie
+        self.report[tag + "_adopted"] += int(ok.sum())
+        self.report[tag + "_bad"] += int(bad.sum())
+        if bool(bad.any()):  # the first few, for the failure message: (exact, hip, reach)
+            det = list(zip(exact[bad].tolist()[:4], hip_b[bad].tolist()[:4], reach[bad].tolist()[:4]))
+            self.report.setdefault(tag + "_bad_detail", []).extend(det)
+        return torch.where(ok, hip_b, own_b)
+
+    def supports(self, sups):
+        """the bf16 operands [(rnd(A), rnd(A^2))] of the HIP run's supports (checked)."""
+        out = []
+        for a, (ha, ha2) in zip(sups, self.sup):
+            a2 = a @ a
+            for ex, h in ((a, ha), (a2, ha2)):
+                e = float((h.to(ex.dtype) - ex).abs().max() / ex.abs().max())
+                self.report["sup_err"] = max(self.report["sup_err"], e)
+            out.append((bf16_round(ha.to(a.dtype)), bf16_round(ha2.to(a.dtype))))
+        return out
+
+
 class _GcnBf16(torch.autograd.Function):
     """sum_q W_q . piece_q of gcn.forward (model.py:41-55, without the bias) in libgwn's bf16 mode
     (csrc/gcn_fused.hip gcn_fwd_t16b_kernel / gcn_bwd_t16_kernel<., true>, gram.hip
@@ -149,15 +204,41 @@ class _GcnBf16(torch.autograd.Function):
     backward (dg, t1, t2) -> mrnd(W_q)^T mrnd(y); dW stays exact.  None = exact mlp (GWN_BF16_MLP=0)."""
 
     @staticmethod
-    def forward(ctx, g, w, rnd, mrnd, *sups):
-        gb = rnd(g)
+    def forward(ctx, g, w, rnd, mrnd, pin, *sups):
+        # pin: (Bf16Pins, layer) -- take the HIP run's roundings where they are ties (Bf16Pins)
+        pins, layer = pin if pin is not None else (None, None)
+        C = g.shape[1]
+        if pins is not None and rnd is bf16_round:
+            sr = pins.supports(sups)
+            gb = rnd(g)
+            if layer in pins.g:
+                gb = pins.adopt(gb, g, bf16_round(pins.g[layer].to(g.dtype)), pins.g_band * float(g.abs().max()), "g")
+        else:
+            sr = [(rnd(a), rnd(a @ a)) for a in sups]
+            gb = rnd(g)
         pieces = [g]
-        for a in sups:
-            pieces += [diffuse(gb, rnd(a)), diffuse(gb, rnd(a @ a))]
+        for ra, ra2 in sr:
+            pieces += [diffuse(gb, ra), diffuse(gb, ra2)]
         h = torch.cat(pieces, dim=1)
+        hb = None  # the bf16-stored hop pieces (the mlp operand in mlp mode, dW's operand)
+        if pins is not None and rnd is bf16_round and layer in pins.pieces:
+            hp = pins.pieces[layer].to(g.dtype)
+            parts = []
+            for k, (ra, ra2) in enumerate(sr):
+                for q, m in enumerate((ra, ra2)):
+                    pi = 1 + 2 * k + q
+                    ex = h[:, pi * C:(pi + 1) * C]
+                    terms = diffuse(gb.abs(), m.abs())
+                    parts.append(pins.adopt(bf16_round(ex), ex, hp[:, (pi - 1) * C:pi * C],
+                                            pins.piece_band * terms, "piece"))
+            hb = torch.cat(parts, dim=1)
         ctx.rnd, ctx.mrnd = rnd, mrnd
+        ctx.sr, ctx.gb, ctx.hb = sr, gb, hb
         ctx.save_for_backward(g, w, h, *sups)
-        return pointwise(h, w) if mrnd is None else pointwise(mrnd(h), mrnd(w))
+        if mrnd is None:
+            return pointwise(h, w)
+        hm = mrnd(h) if hb is None else torch.cat([gb if mrnd is bf16_round else mrnd(g), hb], dim=1)
+        return pointwise(hm, mrnd(w))
 
     @staticmethod
     def backward(ctx, dy):
@@ -170,30 +251,32 @@ class _GcnBf16(torch.autograd.Function):
         def wt(q, y):  # W_q^T y over the channel axis (the mlp's operand rounding)
             return torch.einsum("oi,bont->bint", wm[:, q * C:(q + 1) * C], mr(y))
 
-        hb = torch.cat([h[:, :C], rnd(h[:, C:])], dim=1)  # the bf16-stored hop pieces
+        pb = rnd(h[:, C:]) if ctx.hb is None else ctx.hb
+        hb = torch.cat([h[:, :C], pb], dim=1)  # the bf16-stored hop pieces
         dw = torch.einsum("bont,bint->oi", dy, hb).reshape(w.shape)
         dyb = rnd(dy)
         dg = wt(0, dy)
         dsups = []
         for k, a in enumerate(sups):
+            ra, ra2 = ctx.sr[k]
             # (A y)[v] = sum_w A[v][w] y[w] = diffuse(y, A^T)
-            e1 = diffuse(dyb, rnd(a).t())
-            e2 = diffuse(dyb, rnd(a @ a).t())
+            e1 = diffuse(dyb, ra.t())
+            e2 = diffuse(dyb, ra2.t())
             dg = dg + wt(1 + 2 * k, e1) + wt(2 + 2 * k, e2)
             da = None
-            if ctx.needs_input_grad[4 + k]:
+            if ctx.needs_input_grad[5 + k]:
                 t1 = wt(1 + 2 * k, dy) + wt(2 + 2 * k, e1)
                 t2 = wt(2 + 2 * k, dy)
-                x1 = h[:, (1 + 2 * k) * C:(2 + 2 * k) * C]
-                da = torch.einsum("bcvt,bcwt->vw", rnd(g), rnd(t1)) + torch.einsum("bcvt,bcwt->vw", rnd(x1), rnd(t2))
+                x1b = pb[:, 2 * k * C:(2 * k + 1) * C]
+                da = torch.einsum("bcvt,bcwt->vw", ctx.gb, rnd(t1)) + torch.einsum("bcvt,bcwt->vw", x1b, rnd(t2))
             dsups.append(da)
-        return (dg, dw, None, None, *dsups)
+        return (dg, dw, None, None, None, *dsups)
 
 
-def gcn_bf16(g, w, sups, rnd=bf16_round, mrnd=None):
+def gcn_bf16(g, w, sups, rnd=bf16_round, mrnd=None, pin=None):
     """libgwn's bf16-mode gcn products (_GcnBf16): sum_q W_q piece_q, no bias; mrnd = the mlp's
-    operand rounding (None: exact mlp)."""
-    return _GcnBf16.apply(g, w, rnd, mrnd, *sups)
+    operand rounding (None: exact mlp); pin = (Bf16Pins, layer index) or None."""
+    return _GcnBf16.apply(g, w, rnd, mrnd, pin, *sups)
 
 
 def pointwise(x, w, bias=None):
@@ -235,11 +318,12 @@ def _relu(x, masks, key):
     return x * masks[key].to(x.dtype)
 
 
-def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, masks=None, record=None):
+def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, masks=None, record=None, pins=None):
     """gwnet forward.  p: dict of parameter tensors (state_dict names); supports: list of [N,N]
     fixed supports; x: [B, Cin, N, T]; bn_state: dict name->buffer updated in train mode;
     masks: optional ReLU branches {"skip": [B,S,N,T_f], "e1": [B,E,N,T_f]} (module docstring);
-    record: optional dict that receives the head's pre-activations "skip" and "e1" (detached)."""
+    record: optional dict that receives the head's pre-activations "skip" and "e1" (detached);
+    pins: optional Bf16Pins (bf16 emulation only: the HIP run's rounding ties)."""
     t = x.shape[-1]
     if t < cfg.receptive_field:
         x = torch.nn.functional.pad(x, (cfg.receptive_field - t, 0, 0, 0))
@@ -257,7 +341,8 @@ def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, ma
         skip = s if skip is None else s + skip[..., -s.shape[-1]:]
         if cfg.use_gcn and getattr(cfg, "gcn_bf16", False):
             h = gcn_bf16(g, p["gconv.%d.mlp.mlp.weight" % i], sups,
-                         mrnd=bf16_round if getattr(cfg, "gcn_bf16_mlp", False) else None) \
+                         mrnd=bf16_round if getattr(cfg, "gcn_bf16_mlp", False) else None,
+                         pin=(pins, i) if pins is not None else None) \
                 + p["gconv.%d.mlp.mlp.bias" % i].view(1, -1, 1, 1)
             if training and cfg.dropout > 0:
                 m = dropout_masks[i] if dropout_masks is not None else \
@@ -305,18 +390,18 @@ def masked_metrics(pred, real, null_val=0.0, sign=None):
 
 
 def engine_loss(p, supports, x, real_val, cfg, scaler_mean, scaler_std, bn_state=None, training=True, masks=None,
-                record=None):
+                record=None, pins=None):
     """engine.py:41-51 up to the loss: pad 1, forward, inverse scale, masked MAE.
     masks: optional branches (module docstring; "sign": [B,1,N,T_out] of pred - real)."""
     x = torch.nn.functional.pad(x, (1, 0, 0, 0))
-    out = forward(p, supports, x, cfg, training, bn_state, masks=masks, record=record)
+    out = forward(p, supports, x, cfg, training, bn_state, masks=masks, record=record, pins=pins)
     pred = out.transpose(1, 3) * scaler_std + scaler_mean
     real = real_val.unsqueeze(1)
     mae, mape, rmse = masked_metrics(pred, real, sign=None if masks is None else masks.get("sign"))
     return out, mae, mape, rmse
 
 
-def grads(sd, supports, x, real_val, cfg, scaler_mean, scaler_std, dtype=F64, masks=None, record=None):
+def grads(sd, supports, x, real_val, cfg, scaler_mean, scaler_std, dtype=F64, masks=None, record=None, pins=None):
     """Per-parameter gradients of the engine loss (train mode); params that do not reach the
     output get no entry (the reference leaves their .grad None).  masks: optional branch pinning
     (module docstring)."""
@@ -325,7 +410,7 @@ def grads(sd, supports, x, real_val, cfg, scaler_mean, scaler_std, dtype=F64, ma
     bn = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in sd.items() if "running" in k}
     sups = [torch.tensor(np.asarray(a), dtype=dtype) for a in supports]
     out, mae, mape, rmse = engine_loss(p, sups, torch.tensor(x, dtype=dtype), torch.tensor(real_val, dtype=dtype),
-                                       cfg, scaler_mean, scaler_std, bn, masks=masks, record=record)
+                                       cfg, scaler_mean, scaler_std, bn, masks=masks, record=record, pins=pins)
     names = list(p.keys())
     gs = torch.autograd.grad(mae, [p[n] for n in names], allow_unused=True)
     g = {n: gi for n, gi in zip(names, gs) if gi is not None}

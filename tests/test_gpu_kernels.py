@@ -1481,7 +1481,7 @@ def test_wgrad_group_vs_fp64(gpu, shape):
         part = torch.full((nb[p] * (J * Kt * ntaps + J),), float("nan"), device=gpu)
         Xbd = None
         if xb:  # Xb[r][k - 32] = X[r][k] (bf16), the fp32 X keeps garbage past column 32
-            Xbd = torch.zeros(x_rows, ldxb, dtype=torch.bfloat16)
+            Xbd = torch.zeros(X.shape[0], ldxb, dtype=torch.bfloat16)
             Xbd[:, :Kt - 32] = X[:, 32:].to(torch.bfloat16)
             Xbd = Xbd.to(gpu)
             Xd[:, 32:] = float("nan")
