@@ -73,11 +73,15 @@ def _worker(rank, world, port, out_q):
 
 
 def _captured_dp(eng):
-    """Steps 2.. replayed the data-parallel graphs: one entry (g0, g1, g2, ...) with g2 present."""
+    """Steps 2.. replayed the data-parallel graphs: one entry (g0, (g1, g1b), g2, ...) with g2
+    present; returns "split" when the backward is two graphs (the early range's all-reduce beside
+    the second, engine.trainer._overlap_hook), "whole" for one, False otherwise."""
     if len(eng._graphs) != 1:
         return False
-    g0, g1, g2 = list(eng._graphs.values())[0][:3]
-    return g0 is not None and g1 is not None and g2 is not None
+    g0, (g1, g1b), g2 = list(eng._graphs.values())[0][:3]
+    if g0 is None or g1 is None or g2 is None:
+        return False
+    return "split" if g1b is not None else "whole"
 
 
 def _expected_step1(sd, gmean, lr=1e-3, wd=1e-4, clip=5.0, b1=0.9, b2=0.999, eps=1e-8):
@@ -118,7 +122,7 @@ def test_gpu_ddp_two_ranks_captured_step(gpu):
     exp = _expected_step1(sd, ref)
     for r in range(world):
         grads, p1, p3, captured = res[r]
-        assert captured, "steps 2-3 did not take the two-graph data-parallel path"
+        assert captured == "split", "steps 2-3 did not take the split data-parallel path (%s)" % captured
         assert set(grads) == set(ref), sorted(set(grads) ^ set(ref))
         for k, v in ref.items():
             if k.endswith("mlp.bias"):
@@ -152,10 +156,11 @@ def _headline_setup(dev, seed_x):
     return eng, torch.tensor(x, device=dev), torch.tensor(y, device=dev)
 
 
-def _headline_worker(rank, world, port, out_q):
+def _headline_worker(rank, world, port, out_q, overlap="1"):
     for p in (PKG, ROOT):
         if p not in sys.path:
             sys.path.insert(0, p)
+    os.environ["GWN_DP_OVERLAP"] = overlap
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
@@ -173,7 +178,10 @@ def _headline_worker(rank, world, port, out_q):
         torch.distributed.destroy_process_group()
 
 
-def test_gpu_ddp_headline_shape_equals_mean_of_single_runs(gpu):
+@pytest.mark.parametrize("overlap", ["1", "0"])
+def test_gpu_ddp_headline_shape_equals_mean_of_single_runs(gpu, overlap):
+    """overlap 1 (default): end_conv_1's gradient all-reduced on a side stream while the layers'
+    backward runs (the step split into g1 / g1b around it); 0: one all-reduce after the backward."""
     # the two shards trained by single-process HIP trainers (no process group in this process)
     singles = []
     for r in range(2):
@@ -187,7 +195,7 @@ def test_gpu_ddp_headline_shape_equals_mean_of_single_runs(gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_headline_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_headline_worker, args=(r, world, port, q, overlap)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -203,7 +211,7 @@ def test_gpu_ddp_headline_shape_equals_mean_of_single_runs(gpu):
     scale = float(np.max(np.abs(mean)))
     for r in range(world):
         g1, p3, captured = res[r]
-        assert captured, "steps 2-3 did not take the g0 -> g1 -> all-reduce -> g2 path"
+        assert captured == ("split" if overlap == "1" else "whole"), (captured, overlap)
         diff = float(np.max(np.abs(g1.astype(np.float64) - mean)))
         assert diff <= 1e-6 * scale, (r, diff, scale)
         assert np.all(np.isfinite(p3))

@@ -211,15 +211,24 @@ def test_g7_data_parallel_shards(gpu):
 
 
 # ------------------------------------------------------------------------------------------------
+def _mix32(h):
+    M = np.uint32
+    h = h ^ (h >> M(16))
+    h = h * M(0x7FEB352D)
+    h = h ^ (h >> M(15))
+    h = h * M(0x846CA68B)
+    return h ^ (h >> M(16))
+
+
 def _np_uniform(seed, salt, idx):
     """numpy restatement of gwn_uniform (csrc/gwn_internal.h) to rebuild libgwn's dropout masks."""
     with np.errstate(over="ignore"):
-        M = np.uint64
-        z = M(seed) + M(0x9E3779B97F4A7C15) * M(salt + 1) + idx.astype(np.uint64) * M(0xD1B54A32D192ED03)
-        z = (z ^ (z >> M(30))) * M(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> M(27))) * M(0x94D049BB133111EB)
-        z = z ^ (z >> M(31))
-    return (z >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+        M = np.uint32
+        seed = int(seed) & ((1 << 64) - 1)
+        key = _mix32(np.array(seed & 0xFFFFFFFF, dtype=M)
+                     ^ _mix32(np.array(seed >> 32, dtype=M) + M(0x9E3779B9) * M((int(salt) + 1) & 0xFFFFFFFF)))
+        h = _mix32(idx.astype(np.uint64).astype(M) * M(0x9E3779B1) + key)
+    return (h >> M(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
 
 
 def test_dropout_forward_backward_exact_masks(gpu):
