@@ -1194,9 +1194,10 @@ __device__ __forceinline__ float row16_sum(float x) {
   return x;
 }
 
-// A wave's running BatchNorm partial over its tiles (Chan merge in tile order): lane (g, j) keeps
-// the 8 channels 16 (q >> 2) + 4 g + (q & 3) of its row group (lane j = 0 of a group is the one read;
-// keeping them in the wave's LDS slot instead measured no faster)
+// A lane's running BatchNorm partial over the nodes it held in the wave's tiles (Welford, tile
+// order): lane (g, j) keeps the 8 channels 16 (q >> 2) + 4 g + (q & 3) of node j of each tile.  The
+// 16 lanes of a row group are merged once, at the flush (t16_bn_lanes) -- not per tile, which cost
+// two 4-step DPP reductions per channel and tile.
 struct BnRun {
   float n, mean[8], m2[8];
 };
@@ -1253,28 +1254,85 @@ __device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* ha
     }
     if (valid) t16_st4(dst + m * CH + c0, make_float4(v[4 * oh], v[4 * oh + 1], v[4 * oh + 2], v[4 * oh + 3]));
   }
-  if (a.bn_part == nullptr || a.x_out) return;
-  const float cnt = (float)min(16, n - w0);
-  const float inv = 1.0f / cnt;
-  const float tot = bn.n + cnt;
+  if (a.bn_part == nullptr || a.x_out || !valid) return;
+  bn.n += 1.0f;
+  const float inv = 1.0f / bn.n;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const float mean = row16_sum(valid ? v[q] : 0.0f) * inv;
-    const float d = valid ? v[q] - mean : 0.0f;
-    const float m2 = row16_sum(d * d);
-    const float dm = mean - bn.mean[q];
-    bn.mean[q] += dm * (cnt / tot);
-    bn.m2[q] += m2 + dm * dm * (bn.n * cnt / tot);
+    const float d = v[q] - bn.mean[q];
+    bn.mean[q] = fmaf(d, inv, bn.mean[q]);
+    bn.m2[q] = fmaf(d, v[q] - bn.mean[q], bn.m2[q]);
+  }
+}
+
+// the 16 lanes of each row group merged (Chan, rotations by 8, 4, 2, 1 within the row): lane j = 0
+// of a group then holds the group's partial (each lane merges in its own order; lane 0's is fixed)
+template <int CTRL>
+__device__ __forceinline__ float row_ror(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ void bn_lane_step(BnRun& bn) {
+  const float nb = row_ror<CTRL>(bn.n);
+  const float tot = bn.n + nb;
+  const float wb = tot > 0.0f ? nb / tot : 0.0f, wab = tot > 0.0f ? bn.n * nb / tot : 0.0f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float mb = row_ror<CTRL>(bn.mean[q]), qb = row_ror<CTRL>(bn.m2[q]);
+    const float d = mb - bn.mean[q];
+    bn.mean[q] = fmaf(d, wb, bn.mean[q]);
+    bn.m2[q] = bn.m2[q] + qb + d * d * wab;
   }
   bn.n = tot;
+}
+__device__ __forceinline__ void t16_bn_lanes(BnRun& bn) {
+  bn_lane_step<0x128>(bn);  // row_ror 8, 4, 2, 1
+  bn_lane_step<0x124>(bn);
+  bn_lane_step<0x122>(bn);
+  bn_lane_step<0x121>(bn);
 }
 
 // the waves' running partials (wave order) -> the workgroup's BN partial, slot blockIdx.x
 __device__ void t16_bn_fold_last(const FusedFwd& a, float* lds, const float* wv, const float* bv);
 
+// group g = blockIdx.x % GWN_BN_GROUPS: its last workgroup to arrive (group_arrive[g]) merges the
+// group's write-through channel-major partials (t16_bn_flush) in ascending block order, in double,
+// into group_part[g][3][c]; with fewer workgroups than groups, workgroup 0 writes the empty ones
+__device__ void t16_bn_group(const FusedFwd& a, float* lds) {
+  constexpr int G = GWN_BN_GROUPS;
+  const int g = blockIdx.x % G, parts = gridDim.x;
+  if (blockIdx.x == 0 && parts < G)
+    for (int e = threadIdx.x; e < (G - parts) * 3 * CH; e += blockDim.x) a.fold.group_part[parts * 3 * CH + e] = 0.0f;
+  const int members = (parts - g + G - 1) / G;
+  if (!split_arrive(a.fold.group_arrive + g, members, (int*)lds)) return;
+  if (threadIdx.x >= CH) return;
+  const int c = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.bn_part, (short)0, 3 * CH * parts * 4, 0x00020000);
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int b = g; b < parts; b += G) {
+    const int o = (c * parts + b) * 4;
+    const double nb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, SC1));
+    const double mb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o + CH * parts * 4, 0, SC1));
+    const double qb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o + 2 * CH * parts * 4, 0, SC1));
+    if (nb <= 0.0) continue;
+    const double nn = n + nb, d = mb - mean, w = nb / nn;
+    mean += d * w;
+    m2 += qb + d * d * n * w;
+    n = nn;
+  }
+  float* gp = a.fold.group_part + (long)g * 3 * CH;
+  gp[c] = (float)n;
+  gp[CH + c] = (float)mean;
+  gp[2 * CH + c] = (float)m2;
+}
+
 __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn, float* wpart) {
   if (a.bn_part == nullptr || a.x_out) return;
-  const bool fold = a.fold.arrive != nullptr;
+  // group: the workgroup partials merged into GWN_BN_GROUPS group partials (gwn_bn_fold.group_part)
+  // by the last workgroup of each group (blockIdx.x % groups); the consumer finalizes them
+  const bool group = a.fold.group_part != nullptr;
+  const bool fold = a.fold.arrive != nullptr && !group;
   // fold: the next TCN's weights (w_next[2c][2c], four per thread) and the products of the bias
   // fold do not depend on the statistics: loaded before the hand-off
   float wv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, bv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1287,14 +1345,16 @@ __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn,
     }
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  BnRun bl = bn;
+  t16_bn_lanes(bl);
   if (j == 0) {
     float* wp = wpart + wave * 3 * CH;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int c = 16 * (q >> 2) + 4 * g + (q & 3);
-      wp[c] = bn.n;
-      wp[CH + c] = bn.mean[q];
-      wp[2 * CH + c] = bn.m2[q];
+      wp[c] = bl.n;
+      wp[CH + c] = bl.mean[q];
+      wp[2 * CH + c] = bl.m2[q];
     }
   }
   __syncthreads();
@@ -1312,7 +1372,7 @@ __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn,
       nn = tot;
     }
     float* sp = a.bn_part + (long)blockIdx.x * 3 * CH;
-    if (fold) {
+    if (fold || group) {
       // write-through (read by another XCD's workgroup in the same launch), channel-major
       // [3][c][gridDim.x] so that the last workgroup's loads of 32 consecutive slots are one line
       const int parts = gridDim.x;
@@ -1327,6 +1387,10 @@ __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn,
       sp[CH + c] = mean;
       sp[2 * CH + c] = m2;
     }
+  }
+  if (group) {
+    t16_bn_group(a, wpart);
+    return;
   }
   if (fold) {
     if (split_arrive(a.fold.arrive, gridDim.x, (int*)wpart)) {
@@ -2705,7 +2769,8 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
   a.fold = gwn_bn_fold{};
   // the t16 kernels' last-workgroup finalize (their 1024-thread workgroups map 32 channels x 32
   // partial lanes, and the 64 x 64 folded weights four per thread)
-  const bool fold_here = g->bn_fold && bn_part && !a.x_out && fold_last_enabled();
+  const bool group = g->bn_fold && g->bn_fold->group_part && bn_part && !a.x_out;
+  const bool fold_here = g->bn_fold && bn_part && !a.x_out && (group || fold_last_enabled());
   GWN_REQUIRE(g->ksplit == 0 || g->ksplit == 1 || g->ksplit == g->nsup, "gcn_fwd: ksplit must be 0, 1 or nsup");
   GWN_REQUIRE(!a.res_scale == !a.res_shift && !a.res_scale == !a.res_mean,
               "gcn_fwd (fused): residual_mean, residual_scale and residual_shift go together");
