@@ -1295,44 +1295,9 @@ __device__ __forceinline__ void t16_bn_lanes(BnRun& bn) {
 // the waves' running partials (wave order) -> the workgroup's BN partial, slot blockIdx.x
 __device__ void t16_bn_fold_last(const FusedFwd& a, float* lds, const float* wv, const float* bv);
 
-// group g = blockIdx.x % GWN_BN_GROUPS: its last workgroup to arrive (group_arrive[g]) merges the
-// group's write-through channel-major partials (t16_bn_flush) in ascending block order, in double,
-// into group_part[g][3][c]; with fewer workgroups than groups, workgroup 0 writes the empty ones
-__device__ void t16_bn_group(const FusedFwd& a, float* lds) {
-  constexpr int G = GWN_BN_GROUPS;
-  const int g = blockIdx.x % G, parts = gridDim.x;
-  if (blockIdx.x == 0 && parts < G)
-    for (int e = threadIdx.x; e < (G - parts) * 3 * CH; e += blockDim.x) a.fold.group_part[parts * 3 * CH + e] = 0.0f;
-  const int members = (parts - g + G - 1) / G;
-  if (!split_arrive(a.fold.group_arrive + g, members, (int*)lds)) return;
-  if (threadIdx.x >= CH) return;
-  const int c = threadIdx.x;
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.bn_part, (short)0, 3 * CH * parts * 4, 0x00020000);
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int b = g; b < parts; b += G) {
-    const int o = (c * parts + b) * 4;
-    const double nb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, SC1));
-    const double mb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o + CH * parts * 4, 0, SC1));
-    const double qb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, o + 2 * CH * parts * 4, 0, SC1));
-    if (nb <= 0.0) continue;
-    const double nn = n + nb, d = mb - mean, w = nb / nn;
-    mean += d * w;
-    m2 += qb + d * d * n * w;
-    n = nn;
-  }
-  float* gp = a.fold.group_part + (long)g * 3 * CH;
-  gp[c] = (float)n;
-  gp[CH + c] = (float)mean;
-  gp[2 * CH + c] = (float)m2;
-}
-
 __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn, float* wpart) {
   if (a.bn_part == nullptr || a.x_out) return;
-  // group: the workgroup partials merged into GWN_BN_GROUPS group partials (gwn_bn_fold.group_part)
-  // by the last workgroup of each group (blockIdx.x % groups); the consumer finalizes them
-  const bool group = a.fold.group_part != nullptr;
-  const bool fold = a.fold.arrive != nullptr && !group;
+  const bool fold = a.fold.arrive != nullptr;
   // fold: the next TCN's weights (w_next[2c][2c], four per thread) and the products of the bias
   // fold do not depend on the statistics: loaded before the hand-off
   float wv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, bv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1372,7 +1337,7 @@ __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn,
       nn = tot;
     }
     float* sp = a.bn_part + (long)blockIdx.x * 3 * CH;
-    if (fold || group) {
+    if (fold) {
       // write-through (read by another XCD's workgroup in the same launch), channel-major
       // [3][c][gridDim.x] so that the last workgroup's loads of 32 consecutive slots are one line
       const int parts = gridDim.x;
@@ -1387,10 +1352,6 @@ __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn,
       sp[CH + c] = mean;
       sp[2 * CH + c] = m2;
     }
-  }
-  if (group) {
-    t16_bn_group(a, wpart);
-    return;
   }
   if (fold) {
     if (split_arrive(a.fold.arrive, gridDim.x, (int*)wpart)) {
@@ -2769,8 +2730,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
   a.fold = gwn_bn_fold{};
   // the t16 kernels' last-workgroup finalize (their 1024-thread workgroups map 32 channels x 32
   // partial lanes, and the 64 x 64 folded weights four per thread)
-  const bool group = g->bn_fold && g->bn_fold->group_part && bn_part && !a.x_out;
-  const bool fold_here = g->bn_fold && bn_part && !a.x_out && (group || fold_last_enabled());
+  const bool fold_here = g->bn_fold && bn_part && !a.x_out && fold_last_enabled();
   GWN_REQUIRE(g->ksplit == 0 || g->ksplit == 1 || g->ksplit == g->nsup, "gcn_fwd: ksplit must be 0, 1 or nsup");
   GWN_REQUIRE(!a.res_scale == !a.res_shift && !a.res_scale == !a.res_mean,
               "gcn_fwd (fused): residual_mean, residual_scale and residual_shift go together");
@@ -2815,7 +2775,9 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
       a.ksplit = 1;
       a.bn_slots = (int)gwn_bn_part_slots(slices);
       if (fold_here) a.fold = *g->bn_fold;
-      const char* spw_e = getenv("GWN_T16B_SPW");  // experiment: two slices per wave
+      // the bf16-mlp forward takes two slices per wave (12-wave workgroups, 168 registers): PEMS
+      // forward 63 -> 58 us per launch, 25.8k -> 26.4k samples/s (profiles/r05/welford_hash); with
+      // 16 waves it spills (76 us)
       const int slices2 = (slices + 1) / 2;
       const long units2 = (long)slices2 * nt;
       const int grid2 = (int)(units2 < gwn_device_cus() ? units2 : gwn_device_cus());
@@ -2825,19 +2787,16 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
       const int span2 = (int)((per2 - 1 + nt - 1) / nt) + 1;
       const int maximg2 = 2 * (gmax2 < span2 ? gmax2 : span2);
       const bool h16 = ((((uintptr_t)a.h) & 15) | (a.ld_h & 3)) == 0;
-      if (g->split_planes == 2 && spw_e && (spw_e[0] == '2' || spw_e[0] == '3') && gmax2 >= 1 && h16 && !fold_here) {
+      if (g->split_planes == 2 && gmax2 >= 1 && h16 && !fold_here) {
         static bool attr2 = false;
         if (!attr2) {
-          (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b2_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    T16_LDS_MAX);
           (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b2_kernel<768>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     T16_LDS_MAX);
           attr2 = true;
         }
         size_t lds2 = fixed + maximg2 * img;
         if (lds2 < 81 * 1024) lds2 = 81 * 1024;
-        if (spw_e[0] == '3') gcn_fwd_t16b2_kernel<768><<<grid2, 768, lds2, s>>>(a, p, maximg2);
-        else gcn_fwd_t16b2_kernel<1024><<<grid2, 64 * T16_WAVES, lds2, s>>>(a, p, maximg2);
+        gcn_fwd_t16b2_kernel<768><<<grid2, 768, lds2, s>>>(a, p, maximg2);
       } else if (g->split_planes == 2)
         gcn_fwd_t16b_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       else gcn_fwd_t16b_kernel<1024><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);

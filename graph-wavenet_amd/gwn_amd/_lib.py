@@ -48,21 +48,7 @@ class TcnArgs(ctypes.Structure):
         ("skipcat", c_void_p), ("ld_skip", c_long), ("skip_row0", c_int),
         ("x_mean", c_void_p),
         ("ntaps", c_int), ("c_out", c_int),
-        ("bn", c_void_p),
     ]
-
-
-class BnStats(ctypes.Structure):
-    _fields_ = [
-        ("group_part", c_void_p),
-        ("gamma", c_void_p), ("beta", c_void_p), ("running_mean", c_void_p), ("running_var", c_void_p),
-        ("momentum", c_float), ("eps", c_float),
-        ("save_mean", c_void_p), ("save_rstd", c_void_p), ("scale", c_void_p),
-        ("num_batches_tracked", c_void_p),
-    ]
-
-
-BN_GROUPS = 8  # include/gwn.h GWN_BN_GROUPS
 
 
 class TcnBwdArgs(ctypes.Structure):
@@ -91,7 +77,6 @@ class BnFold(ctypes.Structure):
         ("w_next", c_void_p), ("b_next", c_void_p), ("w_fold", c_void_p), ("b_fold", c_void_p),
         ("num_batches_tracked", c_void_p),
         ("arrive", c_void_p),
-        ("group_part", c_void_p), ("group_arrive", c_void_p),
     ]
 
 

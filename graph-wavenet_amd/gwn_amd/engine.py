@@ -141,6 +141,33 @@ class trainer():
         self._norm_ready = not self._distributed()
         ex.unpack_grads(self.optimizer.grad_flat, self.optimizer._ws if self._norm_ready else None)
 
+    def _early_range(self, acts):
+        """Data parallel: the flat gradient range final after the backward's head stage
+        (Executor.early_grad_range), whose all-reduce overlaps the layers' backward; None in a
+        single process, with the side-stream weight gradients of GWN_OVERLAP, or without one.
+        GWN_DP_OVERLAP=0: one all-reduce of the whole gradient after the backward."""
+        ex = self.model._executor
+        if not self._distributed() or ex._overlap_ok(acts) or os.environ.get("GWN_DP_OVERLAP", "1") == "0":
+            return None
+        return ex.early_grad_range()
+
+    def _backward_split(self, acts, dout, between):
+        """The backward in two parts around between(): the head stage plus the gather of the early
+        gradient range, then the layers and the gather of the rest (data parallel only)."""
+        ex = self.model._executor
+        a, b = self._early_range(acts)
+        gf = self.optimizer.grad_flat
+        stages = ex.backward_stages(acts, dout)
+        next(stages)
+        ex.unpack_grads_range(gf, a, b)
+        between(1)
+        for _ in stages:
+            pass
+        ex.unpack_grads_range(gf, 0, a)
+        ex.unpack_grads_range(gf, b, ex.layout.flat_total)
+        self._norm_ready = False
+        between(2)
+
     def _phase_loss(self, input, real_val, training):
         """pad -> forward -> masked loss (+ its gradient); returns (metrics, saved state, dout)."""
         model = self.model
@@ -222,8 +249,12 @@ class trainer():
             self._capture(key, input, real_val)
             return self._replay(key, input, real_val)
         self._eager_runs[key] = self._eager_runs.get(key, 0) + 1
-        m = self._phase_grads(input, real_val, True)
-        self._allreduce_grads()
+        m, acts, dout = self._phase_loss(input, real_val, True)
+        if self._early_range(acts) is not None:
+            self._backward_split(acts, dout, self._overlap_hook())
+        else:
+            self._phase_backward(acts, dout)
+            self._allreduce_grads()
         self._phase_update()
         return m
 
@@ -239,17 +270,35 @@ class trainer():
         with torch.cuda.graph(g0):
             m, acts, dout = self._phase_loss(sx, sy, True)
         g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1, pool=g0.pool()):
-            self._phase_backward(acts, dout)
-            if not self._distributed():
-                self._phase_update()
+        g1b = None
+        if self._early_range(acts) is not None:
+            # data parallel: the backward in two graphs; between them the early range's all-reduce
+            # is issued on a side stream, beside the second graph (_replay)
+            g1b = torch.cuda.CUDAGraph()
+            ctx = [torch.cuda.graph(g1, pool=g0.pool())]
+            ctx[0].__enter__()
+
+            def between(part):
+                if part == 1:
+                    ctx[0].__exit__(None, None, None)
+                    ctx[0] = torch.cuda.graph(g1b, pool=g0.pool())
+                    ctx[0].__enter__()
+                else:
+                    ctx[0].__exit__(None, None, None)
+
+            self._backward_split(acts, dout, between)
+        else:
+            with torch.cuda.graph(g1, pool=g0.pool()):
+                self._phase_backward(acts, dout)
+                if not self._distributed():
+                    self._phase_update()
         g2 = None
         if self._distributed():
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2, pool=g0.pool()):
                 self._phase_update()
         # acts (and the scratch dy the loss wrote) live on; the entry keeps them referenced
-        self._graphs[key] = (g0, g1, g2, sx, sy, m, (acts, dout))
+        self._graphs[key] = (g0, (g1, g1b), g2, sx, sy, m, (acts, dout))
 
     def _replay(self, key, input, real_val):
         g0, g1, g2, sx, sy, m, _ = self._graphs[key]
@@ -263,11 +312,54 @@ class trainer():
             self._host_metrics[:3].copy_(m[:3], non_blocking=True)
             self._metrics_ready.record()
             self._metrics_early = True
+        g1, g1b = g1
         g1.replay()
-        if g2 is not None:
+        if g1b is not None:
+            hook = self._overlap_hook()
+            hook(1)
+            g1b.replay()
+            hook(2)
+            g2.replay()
+        elif g2 is not None:
             self._allreduce_grads()
             g2.replay()
         return m
+
+    def _overlap_hook(self):
+        """between(part) for _backward_split in a data-parallel step: part 1 (after the head stage
+        and the early range's gather) starts that range's all-reduce on a side stream; part 2 (after
+        the rest of the backward) all-reduces the rest on the current stream and joins the side
+        stream, so clip + Adam see every averaged gradient."""
+        ex = self.model._executor
+        a, b = ex.early_grad_range()
+        gf = self.optimizer.grad_flat
+        if getattr(self, "_dp_side", None) is None:
+            self._dp_side = torch.cuda.Stream(device=gf.device)
+        side = self._dp_side
+        main = torch.cuda.current_stream()
+
+        def between(part):
+            if part == 1:
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self._allreduce(gf[a:b])
+            else:
+                if a > 0:
+                    self._allreduce(gf[:a])
+                if b < gf.numel():
+                    self._allreduce(gf[b:])
+                main.wait_stream(side)
+
+        return between
+
+    @staticmethod
+    def _allreduce(g):
+        dist = torch.distributed
+        if dist.get_backend() == "nccl":
+            dist.all_reduce(g, op=dist.ReduceOp.AVG)
+        else:
+            dist.all_reduce(g, op=dist.ReduceOp.SUM)
+            g.div_(dist.get_world_size())
 
     def _allreduce_grads(self):
         """Data parallel (one process per GPU): average the flat gradient over ranks with ONE

@@ -989,6 +989,33 @@ class Executor:
         """Gradients of every active parameter into self.gpacked (kernel layout).  dout: the output
         gradient [B, O, N, T_f], or None when scratch "dy" already holds it in row layout
         (gwn_masked_loss_rows)."""
+        for _ in self.backward_stages(acts, dout):
+            pass
+
+    def early_grad_range(self):
+        """The flat range [a, b) whose gradients are final after the head stage of the backward
+        (backward_stages' first yield): end_conv_1's weight and bias (written at once by its
+        weight-gradient GEMM, the largest single gradient: 131.6k of the ~300k floats at METR-LA).
+        None when they are not contiguous or not active."""
+        lay = self.layout
+        w, b = lay.flat_off.get("end_conv_1.weight"), lay.flat_off.get("end_conv_1.bias")
+        if w is None or b is None:
+            return None
+        a0, a1 = w[0], w[0] + int(torch.Size(w[1]).numel())
+        if b[0] != a1:
+            return None
+        return a0, a1 + int(torch.Size(b[1]).numel())
+
+    def unpack_grads_range(self, gflat, a, b):
+        """unpack_grads for flat entries [a, b) only."""
+        if b > a:
+            _lib.call("gwn_gather", ptr(self.gpacked), self.uidx.data_ptr() + 4 * a, gflat.data_ptr() + 4 * a, b - a,
+                      _lib.stream())
+
+    def backward_stages(self, acts, dout):
+        """backward as a generator: it yields once after the head (end_conv_2 / end_conv_1 / skip
+        convs: early_grad_range is final then), so a data-parallel trainer can start that range's
+        all-reduce while the layers' backward runs; the rest completes when the generator ends."""
         cfg = self.cfg
         C, D, N, L, S, E, O = cfg.C, cfg.D, cfg.N, cfg.L, cfg.S, cfg.E, cfg.O
         B, ts, P = acts.B, acts.ts, acts.P
@@ -1079,6 +1106,7 @@ class Executor:
             gemm_nt(sc["dsk"], S, self.pk("skip_wT"), S, sc["dskipcat"], L * D, rows_f, L * D, S)
         else:
             gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * D, 1, sc["dskipcat"], L * D, 1, M=rows_f, N=L * D, K=S)
+        yield "head"
         side_done = {}
         dnext = None
         bufs = [sc["dxa"], sc["dxb"]]

@@ -184,22 +184,7 @@ typedef struct gwn_tcn_args {
    * c_out (resp. 2*c_out) channels.  0 = the defaults ntaps 2, c_out c.  Non-default values run
    * the generic GEMM path (no x_mean fold). */
   int ntaps, c_out;
-  /* bn (optional, c == 32 row-GEMM path, x_mean NULL): x holds the PRE-BatchNorm z of the layer
-   * below and bn its statistics as GWN_BN_GROUPS group partials (gwn_bn_fold.group_part): every
-   * workgroup finalizes them itself (merge, mean / rstd, scale = gamma * rstd) and applies the
-   * BatchNorm on load -- z centred, the scale and beta folded into w_fg / b_fg, which are then the
-   * RAW weights -- and workgroup 0 writes save_mean / save_rstd / scale, the running statistics
-   * and num_batches_tracked (gwn_batchnorm_fwd_fold's outputs): no finalize launch between the
-   * gcn and the next TCN. */
-  const struct gwn_bn_stats* bn;
 } gwn_tcn_args;
-typedef struct gwn_bn_stats {
-  const float* group_part;
-  const float* gamma; const float* beta; float* running_mean; float* running_var;
-  float momentum; float eps;
-  float* save_mean; float* save_rstd; float* scale;
-  long long* num_batches_tracked;
-} gwn_bn_stats;
 /* fg may be NULL when no backward follows (inference; c == 32 row-GEMM path): the (tanh, sigmoid)
  * pairs are then not stored. */
 int gwn_gated_tcn_fwd(const gwn_tcn_args* a, hipStream_t stream);
@@ -347,12 +332,7 @@ typedef struct gwn_gcn_args {
   const struct gwn_bn_fold* bn_fold;
 } gwn_gcn_args;
 /* gwn_batchnorm_fwd_fold's arguments (same meaning) for gwn_gcn_args.bn_fold, plus arrive: one
- * device int, zero before the first launch and left zero by every launch (the workgroup count).
- * group_part (optional): instead of the finalize, the launch only merges its BatchNorm partials
- * into GWN_BN_GROUPS group partials group_part[g][3][c] (n, mean, M2; groups without rows written
- * empty) -- the statistics are then finalized by their consumer, the next gated TCN
- * (gwn_tcn_args.bn) -- using the GWN_BN_GROUPS device ints at group_arrive (zero before the first
- * launch, left zero); every other field but gamma (unused) may then be NULL. */
+ * device int, zero before the first launch and left zero by every launch (the workgroup count). */
 typedef struct gwn_bn_fold {
   const float* gamma; const float* beta; float* running_mean; float* running_var;
   float momentum; float eps;
@@ -360,9 +340,7 @@ typedef struct gwn_bn_fold {
   const float* w_next; const float* b_next; float* w_fold; float* b_fold;
   long long* num_batches_tracked;
   int* arrive;
-  float* group_part; int* group_arrive;
 } gwn_bn_fold;
-#define GWN_BN_GROUPS 8
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
  * accumulators, residual + dropout + BN partials in the epilogue).  In that case the supports
