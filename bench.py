@@ -244,7 +244,7 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
     idempotent) as one captured HIP graph between HIP events on the launch stream; achieved =
     algorithmic FLOP / time,
     where the algorithmic FLOP of a call = slices * (K*order*2*C*N^2 + 2*(2K+1)*C*C*N) (SURVEY.md
-    Appendix A)."""
+    Appendix A), plus slices * N * 2*(2C)^2 when the call carries the layer's gated TCN."""
     import ctypes
     from gwn_amd import _lib
     ex = eng.model._executor
@@ -291,6 +291,12 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
             # stats) stores no hop pieces
             piece_b = 0 if ga.no_pieces else 2 * K * (2.0 if ga.pieces_bf16 else 4.0)
             total_bytes += slices * N * C * (4.0 * 3 + piece_b + (4.0 if ga.xg4 else 0.0))
+            if ga.tcn:
+                # the layer's gated TCN inside the launch (gwn_gcn_args.tcn): 2C x 2C per row, and
+                # its tap-0 input in and (tanh, sigmoid) pairs out (the xg it writes replaces the
+                # xg read; tap 1 is the residual row)
+                total_flop += slices * N * 2.0 * (2 * C) * (2 * C)
+                total_bytes += slices * N * C * (4.0 + 8.0)
             count += 1
     avg_us = 1000.0 * total_ms / count
     achieved = total_flop / (total_ms / 1000.0) / 1e12

@@ -57,6 +57,13 @@ struct FusedFwd {
   void* xg4; int xg4_k;  // bf16 t16 kernel: X and support xg4_k's hop 1 in the tiled activation layout
   void* pb; long ld_pb;  // bf16 t16 kernel: the hop pieces as bf16 [rows][ld_pb] instead of h's columns
   gwn_bn_fold fold;      // t16 kernels: BN finalize + fold by the last workgroup (fold.arrive != NULL)
+  // f32 t16 forward: the layer's gated TCN computed in the phase staging (gwn_gcn_args.tcn; x NULL =
+  // off): xg = tanh(f) sigmoid(g) of taps x[r], x[r + tap_rows] (minus mean) straight into the
+  // slice images, and to h's piece 0, fg and the skip rows
+  struct {
+    const float* x; const float* mean; const float* w; const float* b; float* fg; float* skip;
+    long tap_rows, x_rows, ld_skip, skip_row0;
+  } tcn;
 };
 
 struct FusedBwd {
@@ -1090,8 +1097,14 @@ constexpr int LDW16 = 36;  // LDS row stride of the staged channel maps: lane gr
 
 // LDS of a t16 workgroup: the channel maps of all 2K+1 pieces (32 x LDW16 floats each), the waves'
 // BN partials [16][3][32], and maximg slice images
-size_t t16_lds_bytes(int n, int nsup, int maximg) {
-  return (size_t)((2 * nsup + 1) * CH * LDW16 + T16_WAVES * 3 * CH + maximg * t16_img_rows(n) * CH) * sizeof(float);
+// fused TCN (FusedFwd.tcn): the region of the waves' BN partials (used only by the final flush)
+// first holds the TCN weights [64 outputs in MFMA-tile order][LDT_TCN], the input means and the biases
+constexpr int LDT_TCN = 68;  // 2c + 4: a ds_read_b128 pass of 16 rows hits distinct banks
+constexpr int T16_TCN_REGION = 64 * LDT_TCN + 32 + 64 + 16;  // + the TCN's pointers / sizes (TcnLds)
+__host__ __device__ constexpr int t16_region(bool tcn) { return tcn ? T16_TCN_REGION : T16_WAVES * 3 * CH; }
+static_assert(T16_TCN_REGION >= T16_WAVES * 3 * CH, "the TCN region holds the BN partials' space");
+size_t t16_lds_bytes(int n, int nsup, int maximg, bool tcn = false) {
+  return (size_t)((2 * nsup + 1) * CH * LDW16 + t16_region(tcn) + maximg * t16_img_rows(n) * CH) * sizeof(float);
 }
 
 // the channel maps M_p[out][in] of pieces p < npieces into LDS transposed, m[(p*32 + in)*LDW16 +
@@ -1614,6 +1627,146 @@ __device__ __forceinline__ void t16_store_g4(void* base, int which, int slices, 
   *(bf16x8g*)((char*)base + (((long)which * slices + slice) * nt + tile) * 1024 + lane * 16) = r;
 }
 
+// ---- the gated TCN fused into the f32 tile forward's staging (FusedFwd.tcn) ----
+// xg[r][c] = tanh(f) sigmoid(g) with (f, g)[r] = w_fg [x[r] | x[r + tap_rows]] + b_fg (model.py:
+// 206-212; rowgemm.hip's gwn_rowgemm_tcn_fwd computes the same as a separate launch).  One unit = a
+// 16-node group of one output slice on v_mfma_f32_16x16x4_f32, in the transposed orientation
+//   D[o][w] = sum_k W[o][k] X[w][k]        (M = 64 gate outputs in four 16-row tiles, N = nodes)
+// with the contraction permuted so that lane group g takes k = 16 g + kk at step kk: its B operand
+// is 16 contiguous floats of its node's row (tap g >> 1, channels 16 (g & 1) ..), its A operand 16
+// contiguous floats of a weight row (ds_read_b128 x 4).  Tile t of the outputs holds channel
+// 16 (t >> 1) + i's filter (t even) or gate (t odd) row, so lane (g, j) ends with f and g of the
+// same four channels 16 hf + 4 g + r of node w0 + j: the gate is elementwise in registers, and
+// the result is a float4 of the two-half slice image as it stands.
+
+// the TCN's pointers and sizes as the staging reads them: parked in LDS with the weights, so that
+// they do not hold scalar registers through the tile loop (which then spilled)
+struct TcnLds {
+  const float* x; float* fg; float* skip; float* h;
+  long tap_rows, ld_skip, skip_row0;
+  int x_bytes, ld_h;
+};
+static_assert(sizeof(TcnLds) <= 16 * sizeof(float), "TcnLds in its LDS slot");
+__device__ __forceinline__ const TcnLds* tcn_lds(const float* tw) { return (const TcnLds*)(tw + 64 * LDT_TCN + 96); }
+template <typename T>
+__device__ __forceinline__ T tcn_uniform(const T& v) {  // an LDS-held value as a wave-uniform scalar
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte values");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+  } else {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffff)), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __builtin_bit_cast(T, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+  }
+}
+
+// the TCN weights (rows in MFMA-tile order), input means and biases into the staging region
+__device__ __forceinline__ void t16_tcn_stage_weights(const FusedFwd& a, float* tw) {
+  for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
+    const int ti = e >> 6, k = e & 63, t = ti >> 4, i = ti & 15;
+    const int o = 2 * (16 * (t >> 1) + i) + (t & 1);
+    tw[ti * LDT_TCN + k] = a.tcn.w[o * 64 + k];
+  }
+  if (threadIdx.x < 32) tw[64 * LDT_TCN + threadIdx.x] = a.tcn.mean ? a.tcn.mean[threadIdx.x] : 0.0f;
+  if (threadIdx.x < 64) tw[64 * LDT_TCN + 32 + threadIdx.x] = a.tcn.b[threadIdx.x];
+  if (threadIdx.x == 0) {
+    TcnLds* t = (TcnLds*)(tw + 64 * LDT_TCN + 96);
+    t->x = a.tcn.x; t->fg = a.tcn.fg; t->skip = a.tcn.skip; t->h = (float*)a.h;
+    t->tap_rows = a.tcn.tap_rows; t->ld_skip = a.tcn.ld_skip; t->skip_row0 = a.tcn.skip_row0;
+    t->x_bytes = (int)(a.tcn.x_rows * CH * 4); t->ld_h = (int)a.ld_h;
+  }
+}
+
+// the unit's input rows: lane (g, j) loads node w0 + j's 16 channels of k-group g
+__device__ __forceinline__ void t16_tcn_load(const TcnLds* tp, int s, int w0, int lane, int n, float4* xq) {
+  const int g = lane >> 4, node = w0 + (lane & 15);
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)tcn_uniform(tp->x), (short)0, tcn_uniform(tp->x_bytes), 0x00020000);
+  const long row = (long)s * n + node + (g >> 1) * tcn_uniform(tp->tap_rows);
+  const int off = node < n ? (int)((row * CH + 16 * (g & 1)) * 4) : 0x7ffffff0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) xq[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 16 * q, 0));
+}
+
+// one unit: the products, the gate, the image rows (zero past n) and the global outputs
+__device__ __forceinline__ void t16_tcn_unit(const float* tw, const float4* xq, float* img, int hs, int s, int w0,
+                                             int lane, int n) {
+  const TcnLds* tp = tcn_lds(tw);
+  const int g = lane >> 4, j = lane & 15, node = w0 + j;
+  const bool valid = node < n;
+  const float* mu = tw + 64 * LDT_TCN + 16 * (g & 1);
+  float xv[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 m = *(const float4*)(mu + 4 * q);
+    xv[4 * q] = xq[q].x - m.x; xv[4 * q + 1] = xq[q].y - m.y;
+    xv[4 * q + 2] = xq[q].z - m.z; xv[4 * q + 3] = xq[q].w - m.w;
+  }
+  const float* bias = tw + 64 * LDT_TCN + 32;
+  const long row = (long)s * n + node;
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    // the half's filter and gate tiles (t = 2 hf, 2 hf + 1), then its gate: one half live at a time
+    f32x4v acc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const float* wr = tw + (16 * (2 * hf + u) + j) * LDT_TCN + 16 * g;
+      float wf[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *(const float4*)(wr + 4 * q);
+        wf[4 * q] = v.x; wf[4 * q + 1] = v.y; wf[4 * q + 2] = v.z; wf[4 * q + 3] = v.w;
+      }
+      acc[u] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[kk], xv[kk], acc[u], 0, 0, 0);
+    }
+    const int c0 = 16 * hf + 4 * g;
+    f32x4v xg, f0, f1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float tf = gwn_gate_tanh(acc[0][r] + bias[2 * (c0 + r)]);
+      const float sg = gwn_gate_sigmoid(acc[1][r] + bias[2 * (c0 + r) + 1]);
+      xg[r] = tf * sg;
+      if (r < 2) { f0[2 * r] = tf; f0[2 * r + 1] = sg; }
+      else { f1[2 * r - 4] = tf; f1[2 * r - 3] = sg; }
+    }
+    *(f32x4v*)(img + hf * hs + node * 16 + 4 * g) = valid ? xg : f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    if (valid) {
+      __builtin_nontemporal_store(xg, (f32x4v*)(tcn_uniform(tp->h) + row * tcn_uniform(tp->ld_h) + c0));
+      float* fg = tcn_uniform(tp->fg);
+      if (fg) {
+        __builtin_nontemporal_store(f0, (f32x4v*)(fg + row * 2 * CH + 2 * c0));
+        __builtin_nontemporal_store(f1, (f32x4v*)(fg + row * 2 * CH + 2 * c0 + 4));
+      }
+      float* skip = tcn_uniform(tp->skip);
+      const long srow0 = tcn_uniform(tp->skip_row0);
+      if (skip && row >= srow0)
+        __builtin_nontemporal_store(xg, (f32x4v*)(skip + (row - srow0) * tcn_uniform(tp->ld_skip) + c0));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// a phase's slice images from the TCN: units (slice, 16-node group) dealt to the waves, each
+// unit's rows loaded one unit ahead; the image rows past the last group are zeroed
+__device__ __forceinline__ void t16_tcn_stage(int n, const float* tw, float* imgs, int imgf, int hs, int rows_img,
+                                              int s0, int nsl, int lane, int wave, int nwaves) {
+  const int nt = (n + 15) >> 4, units = nsl * nt;
+  const TcnLds* tp = tcn_lds(tw);
+  for (int u = wave; u < units; u += nwaves) {
+    const int sl = u / nt, w0 = 16 * (u - sl * nt);
+    float4 xq[4];
+    t16_tcn_load(tp, s0 + sl, w0, lane, n, xq);
+    t16_tcn_unit(tw, xq, imgs + sl * imgf, hs, s0 + sl, w0, lane, n);
+  }
+  const int pad = rows_img - 16 * nt;  // rows past the groups: zero (both halves)
+  for (int e = threadIdx.x; e < nsl * pad * 8; e += blockDim.x) {
+    const int sl = e / (pad * 8), rem = e - sl * pad * 8, w = 16 * nt + (rem >> 3), q = rem & 7;
+    *(float4*)(imgs + sl * imgf + (q >> 2) * hs + w * 16 + 4 * (q & 3)) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+}
+
 // (Two slices per wave -- the same node column of two slices diffused against shared support
 // fragments, the channel-map fragments shared by both mlps -- measured slower at every layer shape:
 // 167 vs 159 us at 768 slices with 16 waves (51 registers spilled), 167 at 12 waves without spills;
@@ -1626,7 +1779,8 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   const int rows_img = t16_img_rows(n), hs = rows_img * 16, imgf = rows_img * CH;
   float* ws = lds;
   float* wpart = ws + (2 * a.nsup + 1) * CH * LDW16;
-  float* imgs = wpart + T16_WAVES * 3 * CH;
+  const bool tcn = a.tcn.x != nullptr;
+  float* imgs = wpart + t16_region(tcn);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int nwaves = blockDim.x >> 6;
   const long ldh = a.ld_h;
@@ -1634,15 +1788,19 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   BnRun bn;
   bn_init(bn, wpart);
   // the phase's slices staged in one pass (stage_rows4; the channel maps inside its first round
-  // trip), else slice by slice
+  // trip), else slice by slice; with the fused TCN computed from its inputs (the TCN weights in
+  // the BN partials' region until the final flush)
   const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
-  if (!h16) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
+  if (!h16 || tcn) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
+  if (tcn) t16_tcn_stage_weights(a, wpart);
   for (long p0 = rg.tb; p0 < rg.te;) {
     const int s0 = (int)(p0 / nt);
     const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
     const int s1 = (int)((p1 - 1) / nt);
-    if (p0 != rg.tb) __syncthreads();  // the previous phase's images are released
-    if (h16) {
+    if (p0 != rg.tb || tcn) __syncthreads();  // the previous phase's images released (TCN: weights staged)
+    if (tcn) {
+      t16_tcn_stage(n, wpart, imgs, imgf, hs, rows_img, s0, s1 - s0 + 1, lane, wave, nwaves);
+    } else if (h16) {
       const bool maps = p0 == rg.tb;
       stage_rows4<8>(
           a.h + (long)s0 * n * ldh, ldh, n, rows_img, s1 - s0 + 1,
@@ -2669,9 +2827,9 @@ struct T16Plan {
   int grid, maximg;
   size_t lds;
 };
-T16Plan t16_plan(int n, int nsup, int slices) {
+T16Plan t16_plan(int n, int nsup, int slices, bool tcn = false) {
   T16Plan pl{false, 0, 0, 0};
-  const size_t fixed = t16_lds_bytes(n, nsup, 0), img = t16_lds_bytes(n, nsup, 1) - fixed;
+  const size_t fixed = t16_lds_bytes(n, nsup, 0, tcn), img = t16_lds_bytes(n, nsup, 1, tcn) - fixed;
   if (fixed + img > (size_t)T16_LDS_MAX || slices <= 0) return pl;
   const int nt = (n + 15) / 16;
   const long tiles = (long)slices * nt;
@@ -2698,6 +2856,28 @@ int bn_part_tail(float* bn_part, int slices, int c, hipStream_t s) {
 }
 
 }  // namespace
+
+// gwn_gcn_args.tcn runs inside the f32 16-node tile forward (else gwn_gcn_fwd issues it as its own
+// launch first): c = 32, two taps, c_out = 32, xg = h's piece 0, 16-B aligned operands, the launch
+// would take that kernel (with the TCN's LDS region), and it has at least a slice per CU: every
+// workgroup computes the TCN of all the slices its tile range touches, so with less than a slice
+// per CU most of that work is redundant (METR: the layers of 192 and 64 slices ran 4 and 1 us
+// slower fused, those of >= 256 slices 2-6 us faster; step 25.04k -> 25.26k samples/s same-box,
+// profiles/r05/tcn_fused)
+bool gwn_gcn_tcn_fusable(const gwn_gcn_args* g) {
+  const gwn_tcn_args* t = g->tcn;
+  if (!t) return false;
+  auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
+  const int slices = g->rows / g->n, nwt = (g->n + 31) / 32;
+  return t->c == CH && (t->ntaps == 0 || t->ntaps == 2) && (t->c_out == 0 || t->c_out == CH) &&
+         t->xg == g->h && t->ld_xg == g->ld_h && (long)(t->t_in - t->dilation) * t->P == g->rows && t->dilation > 0 &&
+         al(t->x) && t->w_fg && t->b_fg && (!t->fg || al(t->fg)) &&
+         (!t->skipcat || (al(t->skipcat) && (t->ld_skip & 3) == 0)) && g->c == CH &&
+         (g->c_out == 0 || g->c_out == CH) && gwn_gcn_fused_eligible(g->c, g->n, g->nsup, g->ld_sup) &&
+         al(g->h) && (g->ld_h & 3) == 0 && g->split_planes == 0 && g->sup_g4 && g->sup_batch <= 1 && g->nsup > 0 &&
+         g->layout == 0 && t16_enabled() && (pick_ksplit(g, slices, nwt) <= 1 || g->ksplit != g->nsup) &&
+         slices >= gwn_device_cus() && t16_plan(g->n, g->nsup, slices, true).ok;
+}
 
 // GWN_BN_FOLD_LAST=1: the 16-node tile kernels run gwn_gcn_args.bn_fold in their last workgroup
 // (off by default: measured break-even); else it is a separate launch
@@ -2728,6 +2908,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
   a.xg4 = g->xg4; a.xg4_k = g->xg4_support;
   a.pb = g->pieces_bf16; a.ld_pb = g->ld_pb;
   a.fold = gwn_bn_fold{};
+  a.tcn = {};
   // the t16 kernels' last-workgroup finalize (their 1024-thread workgroups map 32 channels x 32
   // partial lanes, and the 64 x 64 folded weights four per thread)
   const bool fold_here = g->bn_fold && bn_part && !a.x_out && fold_last_enabled();
@@ -2825,11 +3006,19 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
   const int slices = g->rows / g->n;
   a.ksplit = pick_ksplit(g, slices, nwt);
   const int grid = a.ksplit > 1 ? (slices + 7) / 8 * 8 * a.ksplit : slices;
-  const T16Plan pl = t16_plan(g->n, g->nsup, slices);
+  const bool tcn = g->tcn != nullptr;
+  GWN_REQUIRE(!tcn || gwn_gcn_tcn_fusable(g), "gcn_fwd (fused): tcn given where it cannot be fused");
+  const T16Plan pl = t16_plan(g->n, g->nsup, slices, tcn);
   // (the t16 ranges already cut small launches finely: the support split runs only when forced)
   if (g->sup_g4 && a.sup_batch <= 1 && g->nsup > 0 && (a.ksplit <= 1 || g->ksplit != g->nsup) && g->layout == 0 &&
       t16_enabled() && pl.ok) {
     GWN_REQUIRE(g->w_mlp_t, "gcn_fwd (16-node tiles): w_mlp_t (the transposed mlp weights) is required with sup_g4");
+    if (tcn) {
+      const gwn_tcn_args* t = g->tcn;
+      a.tcn.x = t->x; a.tcn.mean = t->x_mean; a.tcn.w = t->w_fg; a.tcn.b = t->b_fg; a.tcn.fg = t->fg;
+      a.tcn.skip = t->skipcat; a.tcn.ld_skip = t->ld_skip; a.tcn.skip_row0 = t->skip_row0;
+      a.tcn.tap_rows = (long)t->dilation * t->P; a.tcn.x_rows = (long)t->t_in * t->P;
+    }
     PowSup p = {};
     for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = g->sup_g4[k];
     a.ksplit = 1;

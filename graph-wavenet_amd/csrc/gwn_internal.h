@@ -52,6 +52,7 @@ int gwn_gemm_launch(const GemmParams& p, hipStream_t stream);
 bool gwn_gcn_fused_eligible(int c, int n, int nsup, int ld_sup);
 // *folded: the launch also ran g->bn_fold (the 16-node tile kernels' last-workgroup finalize)
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded, hipStream_t s);
+bool gwn_gcn_tcn_fusable(const gwn_gcn_args* g);
 int gwn_device_cus();  // compute units of the current device (cached)
 // BatchNorm partial slots of a gwn_gcn_fwd launch over `slices` slices (every slot written)
 long gwn_bn_part_slots(int slices);
@@ -78,6 +79,11 @@ constexpr int GWN_ROWGEMM_MAX_PARTS = 2048;  // waves of one rowgemm launch (8 p
 // differentiates the same mask: a 32-bit key of (seed, salt) (uniform per launch), then per element
 // the lowbias32 finaliser (two multiplies) of idx * phi + key -- 32-bit arithmetic throughout (the
 // splitmix64 form it replaces spent ~30 VALU ops per element on 64-bit multiplies).  idx < 2^32.
+// Branch-free gate nonlinearities of the gated TCN (model.py:206-212) on v_exp_f32 / v_rcp_f32:
+// absolute error ~1e-7 (a few ulp of 1); the row-GEMM TCN and the gcn-fused TCN share them.
+__device__ __forceinline__ float gwn_gate_sigmoid(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+__device__ __forceinline__ float gwn_gate_tanh(float x) { return 1.0f - 2.0f * __frcp_rn(__expf(2.0f * x) + 1.0f); }
+
 __host__ __device__ inline unsigned gwn_mix32(unsigned h) {
   h ^= h >> 16;
   h *= 0x7FEB352Du;

@@ -1198,6 +1198,17 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   }
   const int c = a->c, n = a->n;
   const int co = a->c_out > 0 ? a->c_out : c;
+  gwn_gcn_args local;
+  if (a->tcn) {
+    GWN_REQUIRE(a->tcn->xg == a->h && a->tcn->ld_xg == a->ld_h, "gcn_fwd: tcn must write xg into h (ld_xg = ld_h)");
+    if (!gwn_gcn_tcn_fusable(a)) {  // the TCN as its own launch, then the diffusion without it
+      const int rc = gwn_gated_tcn_fwd(a->tcn, s);
+      if (rc) return rc;
+      local = *a;
+      local.tcn = nullptr;
+      a = &local;
+    }
+  }
   bool folded = false;
   int rc = (co == c && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup))
                ? gwn_gcn_fused_fwd_launch(a, a->bn_partials, &folded, s)

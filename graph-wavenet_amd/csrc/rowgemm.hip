@@ -31,10 +31,9 @@ struct RowGemm {
   const float* center;                                           // CENTER: A[.][h*a_tap + j] - center[j]
 };
 
-// Branch-free gate nonlinearities on v_exp_f32 / v_rcp_f32: absolute error ~1e-7 (a few ulp of
-// 1), which is what the parity tolerance sees (errors are measured against max |value|).
-__device__ __forceinline__ float sigmoidf_(float x) { return __frcp_rn(1.0f + __expf(-x)); }
-__device__ __forceinline__ float tanhf_(float x) { return 1.0f - 2.0f * __frcp_rn(__expf(2.0f * x) + 1.0f); }
+// gate nonlinearities: gwn_gate_sigmoid / gwn_gate_tanh (gwn_internal.h)
+__device__ __forceinline__ float sigmoidf_(float x) { return gwn_gate_sigmoid(x); }
+__device__ __forceinline__ float tanhf_(float x) { return gwn_gate_tanh(x); }
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
 // Each wave walks 32-row chunks (grid stride).  Every global access goes through a buffer

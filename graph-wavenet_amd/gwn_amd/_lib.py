@@ -106,6 +106,7 @@ class GcnArgs(ctypes.Structure):
         ("xg4", c_void_p), ("xg4_support", c_int),
         ("pieces_bf16", c_void_p), ("ld_pb", c_long),
         ("bn_fold", ctypes.POINTER(BnFold)),
+        ("tcn", ctypes.POINTER(TcnArgs)),
     ]
 
 

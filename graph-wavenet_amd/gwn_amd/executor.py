@@ -579,14 +579,6 @@ class Executor:
         acts.planes = planes
         if not training:
             acts.g4bt_arr = None
-        # the last layer's gcn + bn only update bn[L-1]'s running statistics (their output is dead,
-        # model.py:225-236): GWN_TAIL_OVERLAP=1 runs them on a second stream beside the head GEMMs
-        # (the head needs only the skip sum), joined before the forward returns.  Off by default:
-        # measured 17,843 vs 17,854 samples/s (round 2) -- the head GEMMs already fill the chip
-        tail_side = (training and L > 1 and os.environ.get("GWN_TAIL_OVERLAP", "0") != "0"
-                     and torch.cuda.is_available() and x.is_cuda)
-        main = torch.cuda.current_stream() if tail_side else None
-        tail_done = None
         # train mode: BatchNorm i is applied on load by its consumers (TCN weights of layer i+1
         # folded, residual affine in gcn epilogue i+1, affine in the TCN weight gradient) instead
         # of materialising bn(z) (one HBM pass and one launch fewer per layer)
@@ -626,18 +618,9 @@ class Executor:
                               xg=ptr(acts.H[i]), ld_xg=cfg.W, fg=ptr(acts.FG[i]),
                               skipcat=acts.skipcat.data_ptr() + 4 * i * cfg.D, ld_skip=L * cfg.D,
                               skip_row0=(ts[i + 1] - tf) * P, ntaps=cfg.K, c_out=cfg.D)
-            lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), st)
             if i == L - 1 and not training:
+                lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), st)
                 continue  # the last gcn / bn output is dead in eval (only skip reaches the output)
-            side_ctx = None
-            if tail_side and i == L - 1:
-                side = self._side_stream()
-                ev = torch.cuda.Event()
-                ev.record(main)
-                side.wait_event(ev)
-                side_ctx = torch.cuda.stream(side)
-                side_ctx.__enter__()
-                st = _lib.stream()
             drop = float(self.dropout) if (training and cfg.use_gcn) else 0.0
             xg4 = None
             if gram_g4 and i < L - 1:
@@ -666,6 +649,9 @@ class Executor:
                               split_planes=planes, **self.ksplit_fields(scr))
             if pieces_b and i < L - 1:
                 ga.pieces_bf16, ga.ld_pb = acts.HB[i].data_ptr(), 2 * cfg.nsup * cfg.D
+            # the gated TCN rides on the gcn call (gwn_gcn_args.tcn: inside the f32 tile kernel's
+            # staging where it runs, else its own launch issued by gwn_gcn_fwd)
+            ga.tcn = ctypes.pointer(ta)
             rm, rv, mom, eps, nbt = bn_bufs[i]
             if fold:
                 # the BN finalize + fold into the next TCN rides on the gcn launch (gwn_gcn_args.bn_fold:
@@ -693,19 +679,12 @@ class Executor:
                 lib.call("gwn_batchnorm_fwd", ptr(acts.Z[i]), rows, C, ptr(self.pk("bn_g%d" % i)),
                          ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps, 0,
                          ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(ws), st)
-            if side_ctx is not None:
-                tail_done = torch.cuda.Event()
-                tail_done.record(torch.cuda.current_stream())
-                side_ctx.__exit__(None, None, None)
-                st = _lib.stream()
         rows_f = tf * P
         self._head_fwd(acts.skipcat, acts.skr, acts.e1, acts.y, rows_f, ws)
         out = None
         if want_out:
             out = torch.empty(B, cfg.O, N, tf, device=self.device, dtype=F32)
             lib.call("gwn_to_nchw", ptr(acts.y), B, cfg.O, N, tf, ptr(out), st)
-        if tail_done is not None:
-            main.wait_event(tail_done)
         return out, acts
 
     def _bn_parts(self, rows):

@@ -286,8 +286,7 @@ typedef struct gwn_gcn_args {
    * whose partial mlp sums [np][c] go to ksplit_ws; the last of them to finish (ksplit_count[slice],
    * a device counter that is zero on entry and left zero) adds them in support order and runs the
    * epilogue.  Finer work units for layers with too few slices to occupy the chip (a unit costs
-   * about half a slice, so auto splits only when slices * nsup <= CUs; GWN_KSPLIT_SLICES = a slice
-   * threshold overrides; with sup_g4 given the persistent 16-node tile kernels, which already cut
+   * about half a slice, so auto splits only when slices * nsup <= CUs; with sup_g4 given the persistent 16-node tile kernels, which already cut
    * every launch into equal per-CU tile ranges, take precedence over the auto split).  ksplit: 0 = auto,
    * 1 = off, nsup = always.  ksplit_ws: gwn_gcn_ksplit_ws_floats(rows, n, nsup) floats,
    * ksplit_count: rows / n ints; NULL = no split. */
@@ -330,6 +329,13 @@ typedef struct gwn_gcn_args {
    * the persistent 16-node tile kernels run it in their last workgroup to finish instead (partials
    * written through in a private channel-major order: bn_partials' content is then unspecified). */
   const struct gwn_bn_fold* bn_fold;
+  /* tcn (optional): the layer's gated TCN (gwn_gated_tcn_fwd's arguments, its xg = h and ld_xg =
+   * ld_h: the TCN writes piece 0 of h) run by this call before the diffusion.  When the f32 16-node
+   * tile forward runs (c == 32, two taps, c_out == c, 16-B aligned x / h / fg / skipcat, split_planes
+   * 0, sup_g4 given) it is computed inside that kernel's staging -- the slice images come straight
+   * from x, and xg, fg and the skip rows are written from there -- otherwise it is issued as its own
+   * launch first.  The caller then does not call gwn_gated_tcn_fwd. */
+  const struct gwn_tcn_args* tcn;
 } gwn_gcn_args;
 /* gwn_batchnorm_fwd_fold's arguments (same meaning) for gwn_gcn_args.bn_fold, plus arrive: one
  * device int, zero before the first launch and left zero by every launch (the workgroup count). */

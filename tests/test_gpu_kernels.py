@@ -697,6 +697,95 @@ def test_gcn_fused_schedules_agree(gpu, n, monkeypatch):
             assert rel_err(a_.cpu().numpy(), b_.cpu().numpy()) <= 2e-6
 
 
+@pytest.mark.parametrize("n,B,t_out,d", [(207, 32, 8, 2), (37, 64, 5, 1), (207, 8, 3, 1)])
+def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d):
+    """gwn_gcn_args.tcn: the gated TCN (model.py:206-212) computed inside the f32 16-node tile
+    forward's staging (>= a slice per CU) against the same layer as two calls (gwn_gated_tcn_fwd,
+    then gwn_gcn_fwd): xg (piece 0 of h), the (tanh, sigmoid) pairs, the skip rows, the hop pieces,
+    z and the BN statistics agree to the fp32 floor (the products summed in another order), and xg
+    matches fp64.  The last case has fewer slices than CUs: the TCN is then its own launch inside
+    gwn_gcn_fwd and everything is bitwise the two-call result.  BatchNorm on load: x is a pre-BN z
+    (centred by x_mean, weights folded) as in the training step."""
+    import ctypes
+    from gwn_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(n + B + d)
+    C, K = 32, 3
+    NP = (n + 31) // 32 * 32
+    W = (2 * K + 1) * C
+    P = B * n
+    t_in = t_out + d
+    S = t_out * B
+    rows = S * n
+    sups = []
+    for _ in range(K):
+        s_ = torch.zeros(NP, NP, device=gpu)
+        s_[:n, :n] = torch.rand(n, n, device=gpu) / n
+        sups.append(s_)
+    supT = [s_.t().contiguous() for s_ in sups]
+    sq = _squares(gpu, sups)
+    arr = (ctypes.c_void_p * K)(*[s_.data_ptr() for s_ in sups])
+    arr2 = (ctypes.c_void_p * K)(*[q[0].data_ptr() for q in sq])
+    g4f, _ = _g4s(gpu, n, sups, sq, supT)
+    PP = ctypes.POINTER(ctypes.c_void_p)
+    x = torch.randn(t_in * P, C, device=gpu) * 2 + 3
+    xmean = torch.randn(C, device=gpu) + 3
+    wfg = torch.randn(2 * C, 2 * C, device=gpu) * 0.15
+    bfg = torch.randn(2 * C, device=gpu) * 0.1
+    wm = torch.randn(C, W, device=gpu) * 0.1
+    wmt = wm.t().contiguous()
+    bm = torch.randn(C, device=gpu)
+    seed = torch.zeros(1, device=gpu, dtype=torch.int64)
+    ld_skip = 3 * C
+    skip_row0 = (t_out - 1) * P
+    nparts = int(lib.gwn_gcn_bn_partial_count(rows, n, C, K, NP))
+    outs = {}
+    for fused in (False, True):
+        h = torch.full((rows, W), float("nan"), device=gpu)
+        fg = torch.full((rows, 2 * C), float("nan"), device=gpu)
+        skip = torch.full((rows - skip_row0, ld_skip), float("nan"), device=gpu)
+        z = torch.empty(rows, C, device=gpu)
+        bnp = torch.full((nparts * 3 * C,), float("nan"), device=gpu)
+        ta = _lib.TcnArgs(x=x.data_ptr(), t_in=t_in, P=P, c=C, dilation=d, w_fg=wfg.data_ptr(), b_fg=bfg.data_ptr(),
+                          xg=h.data_ptr(), ld_xg=W, fg=fg.data_ptr(), skipcat=skip.data_ptr(), ld_skip=ld_skip,
+                          skip_row0=skip_row0, x_mean=xmean.data_ptr())
+        ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, PP), ld_sup=NP, h=h.data_ptr(), ld_h=W,
+                          w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(), residual=x.data_ptr() + 4 * d * P * C,
+                          z=z.data_ptr(), seed_ptr=seed.data_ptr(), salt=0, drop_p=0.0, bn_partials=bnp.data_ptr(),
+                          sup2=ctypes.cast(arr2, PP), w_mlp_t=wmt.data_ptr(), sup_g4=g4f[1])
+        if fused:
+            ga.tcn = ctypes.pointer(ta)
+        else:
+            _lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), _lib.stream())
+        _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
+        torch.cuda.synchronize()
+        outs[fused] = (h, fg, skip[:, :C], z, _bn_all(bnp, rows, n, C, K, NP))
+    (h0, fg0, sk0, z0, st0), (h1, fg1, sk1, z1, st1) = outs[False], outs[True]
+    if S < _cus():
+        for a_, b_ in zip(outs[False], outs[True]):
+            assert torch.equal(a_, b_)
+        return
+    # fp64 truth of xg
+    xd = (x.double() - xmean.double()).cpu()
+    f = torch.cat([xd[:rows], xd[d * P:d * P + rows]], dim=1) @ wfg.double().cpu().t() + bfg.double().cpu()
+    xg_ref = torch.tanh(f[:, 0::2]) * torch.sigmoid(f[:, 1::2])
+    # (the fp32 floor of 64-term sums of ~5-magnitude products, as the row-GEMM TCN's tests: 5e-6)
+    assert rel_err(h0[:, :C].cpu().numpy(), xg_ref.numpy()) <= 5e-6
+    assert rel_err(h1[:, :C].cpu().numpy(), xg_ref.numpy()) <= 5e-6
+    assert rel_err(h1[:, :C].cpu().numpy(), h0[:, :C].cpu().numpy()) <= 5e-6
+    assert rel_err(fg1.cpu().numpy(), fg0.cpu().numpy()) <= 5e-6
+    assert torch.equal(sk1, h1[skip_row0:, :C])
+    assert rel_err(h1.cpu().numpy(), h0.cpu().numpy()) <= 5e-6
+    assert rel_err(z1.cpu().numpy(), z0.cpu().numpy()) <= 5e-6
+    assert torch.equal(st1[:, 0], st0[:, 0])
+    assert rel_err(st1[:, 1].numpy(), st0[:, 1].numpy()) <= 1e-5
+    assert rel_err(st1[:, 2].numpy(), st0[:, 2].numpy()) <= 1e-5
+
+
+def _cus():
+    return torch.cuda.get_device_properties(0).multi_processor_count
+
+
 @pytest.mark.parametrize("pw", [False, True])
 def test_gcn_split_many_slices_bn_prologue_gate_epilogue(gpu, pw):
     """The support split at scale: 80 slices (10 groups of 8 workgroups per support)
