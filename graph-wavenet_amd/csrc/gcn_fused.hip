@@ -56,7 +56,6 @@ struct FusedFwd {
   int bn_slots;  // t16 kernels: BN partial slots to write (those past the grid get count 0)
   void* xg4; int xg4_k;  // bf16 t16 kernel: X and support xg4_k's hop 1 in the tiled activation layout
   void* pb; long ld_pb;  // bf16 t16 kernel: the hop pieces as bf16 [rows][ld_pb] instead of h's columns
-  gwn_bn_fold fold;      // t16 kernels: BN finalize + fold by the last workgroup (fold.arrive != NULL)
   // f32 t16 forward: the layer's gated TCN computed in the phase staging (gwn_gcn_args.tcn; x NULL =
   // off): xg = tanh(f) sigmoid(g) of taps x[r], x[r + tap_rows] (minus mean) straight into the
   // slice images, and to h's piece 0, fg and the skip rows
@@ -1193,20 +1192,6 @@ __device__ __forceinline__ void stage_rows4(const float* src, long ld, int n, in
   }
 }
 
-// x += (x rotated by 8, 4, 2, 1 lanes within its 16-lane row): the row sum in every lane (each lane
-// in its own order; callers take lane 0 of the row: deterministic)
-__device__ __forceinline__ float row16_sum(float x) {
-  int v = __builtin_bit_cast(int, x);
-  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false));
-  v = __builtin_bit_cast(int, x);
-  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false));
-  v = __builtin_bit_cast(int, x);
-  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x122, 0xF, 0xF, false));
-  v = __builtin_bit_cast(int, x);
-  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x121, 0xF, 0xF, false));
-  return x;
-}
-
 // A lane's running BatchNorm partial over the nodes it held in the wave's tiles (Welford, tile
 // order): lane (g, j) keeps the 8 channels 16 (q >> 2) + 4 g + (q & 3) of node j of each tile.  The
 // 16 lanes of a row group are merged once, at the flush (t16_bn_lanes) -- not per tile, which cost
@@ -1306,22 +1291,8 @@ __device__ __forceinline__ void t16_bn_lanes(BnRun& bn) {
 }
 
 // the waves' running partials (wave order) -> the workgroup's BN partial, slot blockIdx.x
-__device__ void t16_bn_fold_last(const FusedFwd& a, float* lds, const float* wv, const float* bv);
-
 __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn, float* wpart) {
   if (a.bn_part == nullptr || a.x_out) return;
-  const bool fold = a.fold.arrive != nullptr;
-  // fold: the next TCN's weights (w_next[2c][2c], four per thread) and the products of the bias
-  // fold do not depend on the statistics: loaded before the hand-off
-  float wv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, bv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  if (fold && a.fold.w_next) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = (4 * threadIdx.x + e) & (2 * CH - 1);  // column tap*c + ci of row threadIdx.x / 16
-      wv[e] = a.fold.w_next[4 * threadIdx.x + e];
-      bv[e] = wv[e] * a.fold.beta[k & (CH - 1)];
-    }
-  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   BnRun bl = bn;
   t16_bn_lanes(bl);
@@ -1350,106 +1321,13 @@ __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn,
       nn = tot;
     }
     float* sp = a.bn_part + (long)blockIdx.x * 3 * CH;
-    if (fold) {
-      // write-through (read by another XCD's workgroup in the same launch), channel-major
-      // [3][c][gridDim.x] so that the last workgroup's loads of 32 consecutive slots are one line
-      const int parts = gridDim.x;
-      const __amdgpu_buffer_rsrc_t r =
-          __builtin_amdgcn_make_buffer_rsrc((void*)a.bn_part, (short)0, 3 * CH * parts * 4, 0x00020000);
-      const int o = (c * parts + blockIdx.x) * 4;
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, nn), r, o, 0, SC1);
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mean), r, o + CH * parts * 4, 0, SC1);
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m2), r, o + 2 * CH * parts * 4, 0, SC1);
-    } else {
-      sp[c] = nn;
-      sp[CH + c] = mean;
-      sp[2 * CH + c] = m2;
-    }
-  }
-  if (fold) {
-    if (split_arrive(a.fold.arrive, gridDim.x, (int*)wpart)) {
-      t16_bn_fold_last(a, wpart + 4, wv, bv);
-    }
-    return;
+    sp[c] = nn;
+    sp[CH + c] = mean;
+    sp[2 * CH + c] = m2;
   }
   // the slots past the grid (gwn_bn_part_slots: at least one per slice) hold no rows
   for (long slot = blockIdx.x + gridDim.x; slot < a.bn_slots; slot += gridDim.x)
     if (threadIdx.x < 3 * CH) a.bn_part[slot * 3 * CH + threadIdx.x] = 0.0f;
-}
-
-// gwn_batchnorm_fwd_fold (bn_finalize_fold_kernel's arithmetic) by the launch's last workgroup on
-// its gridDim.x channel-major partials (1024 threads): channel j's partials are merged by the 32 lanes of one
-// half-wave (slots sub, sub + 32, ... sequentially, in double), then down a fixed shuffle tree;
-// wv / bv: this thread's four elements of w_next (row tid / 16) and their products with beta
-__device__ void t16_bn_fold_last(const FusedFwd& a, float* lds, const float* wv, const float* bv) {
-  static_assert(T16_WAVES * 64 == 32 * CH && T16_WAVES * 64 * 4 == 4 * CH * CH, "fold: 1024 threads, c = 32");
-  const gwn_bn_fold& f = a.fold;
-  const int j = threadIdx.x >> 5, sub = threadIdx.x & 31;
-  const int parts = gridDim.x;
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.bn_part, (short)0, parts * 3 * CH * 4, 0x00020000);
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  constexpr int U = 8;
-  for (int i0 = sub; i0 < parts; i0 += 32 * U) {
-    float nbv[U], mbv[U], qbv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + 32 * u;
-      const bool ok = i < parts;  // else an out-of-range offset: zero
-      const int off = (j * parts + i) * 4;  // channel-major [3][c][parts] (t16_bn_flush)
-      nbv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, ok ? off : 0x7ffffff0, 0, SC1));
-      mbv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, ok ? off + CH * parts * 4 : 0x7ffffff0, 0, SC1));
-      qbv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, ok ? off + 2 * CH * parts * 4 : 0x7ffffff0, 0, SC1));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const double nb = nbv[u];
-      if (nb <= 0.0) continue;
-      const double nn = n + nb, delta = (double)mbv[u] - mean, w = nb / nn;
-      mean += delta * w;
-      m2 += (double)qbv[u] + delta * delta * n * w;
-      n = nn;
-    }
-  }
-  for (int off = 16; off > 0; off >>= 1) {
-    const double nb = __shfl_down(n, off, 32), mb = __shfl_down(mean, off, 32), qb = __shfl_down(m2, off, 32);
-    if (sub < off && nb > 0.0) {
-      const double nn = n + nb, delta = mb - mean, w = nb / nn;
-      mean += delta * w;
-      m2 += qb + delta * delta * n * w;
-      n = nn;
-    }
-  }
-  if (sub == 0) {
-    const double var = (n > 0.0) ? m2 / n : 0.0;
-    const float rs = (float)(1.0 / sqrt(var + (double)f.eps));
-    f.save_mean[j] = (float)mean;
-    f.save_rstd[j] = rs;
-    if (f.running_mean) {
-      const double unbiased = (n > 1.0) ? m2 / (n - 1.0) : var;
-      f.running_mean[j] = (float)((1.0 - f.momentum) * f.running_mean[j] + f.momentum * mean);
-      f.running_var[j] = (float)((1.0 - f.momentum) * f.running_var[j] + f.momentum * unbiased);
-    }
-    const float sc = rs * f.gamma[j];  // bn(z) = (z - mean) * sc + beta
-    f.scale[j] = sc;
-    lds[j] = sc;
-  }
-  if (threadIdx.x == 0 && f.num_batches_tracked) *f.num_batches_tracked += 1;
-  if (!f.w_next) return;
-  __syncthreads();
-  // w_fold[row][k] = w_next[row][k] * scale[k % c]; b_fold[row] = b_next[row] + sum_k w_next[row][k] *
-  // beta[k % c] (the 16 threads of a row: four products each, then a fixed shuffle tree)
-  float s = 0.0f;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int k = (4 * threadIdx.x + e) & (2 * CH - 1);
-    f.w_fold[4 * threadIdx.x + e] = wv[e] * lds[k & (CH - 1)];
-    s += bv[e];
-  }
-#pragma unroll
-  for (int off = 8; off > 0; off >>= 1) s += __shfl_down(s, off, 16);
-  const int row = threadIdx.x >> 4;
-  if ((threadIdx.x & 15) == 0) f.b_fold[row] = f.b_next[row] + s;
 }
 
 // the channel map of one piece held in accumulators acc[hf] (register s = input channel
@@ -2660,92 +2538,6 @@ __global__ __launch_bounds__(MAXT, 4) void gcn_bwd_pow_kernel(const FusedBwd a, 
   else acc_to_global(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
 }
 
-// C = A A and C^T for a padded support A [np][ld] (zero outside [n][n], so C is too): one
-// 4-wave workgroup per 32 x 32 output tile on v_mfma_f32_32x32x2_f32, each wave a quarter of K
-// (np / 2 k-steps, a multiple of 16) with its operands loaded four k-steps ahead; the four partial
-// tiles are added in wave order through LDS.  Also A^T when at != nullptr.
-// element (r, c) of a padded support into its gwn_support_g4 copy (r, c < 16 * nt)
-__device__ __forceinline__ void g4_put(float* dst, int nt, int r, int c, float v) {
-  if (r < 16 * nt && c < 16 * nt)
-    dst[((long)((r >> 4) * nt + (c >> 4)) * 64 + 16 * (r & 3) + (c & 15)) * 4 + ((r & 15) >> 2)] = v;
-}
-
-// A^2, (A^2)^T and optionally A^T of a padded support; with g4, also the gwn_support_g4 copies of
-// A and A^2 (g4 + 0 / 1 * g4_stride) and, with g4_count == 4, of A^T and (A^2)^T (2 / 3) -- the
-// adaptive support's per-step preparation in one launch
-__global__ __launch_bounds__(256) void support_square_kernel(const float* A, int np, int ld, float* C, float* CT,
-                                                             float* AT, float* g4, long g4_stride, int g4_nt,
-                                                             int g4_count) {
-  __shared__ float red[4][32][33];
-  const int ti = blockIdx.y * 32, tj = blockIdx.x * 32;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5, col = lane & 31;
-  const int per = np / 8;  // k-steps per wave (np / 2 in all), a multiple of 4
-  f32x16 acc = zero16();
-  // D[i][j] = sum_k A[ti + i][k] A[k][tj + j]: A operand lane (half, col) = A[ti + col][2 ks + half]
-  const float* ar = A + (long)(ti + col) * ld + half;
-  const float* br = A + (long)half * ld + tj + col;
-  for (int ks = wave * per; ks < (wave + 1) * per; ks += 4) {
-    float a[4], b[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      a[j] = ar[2 * (ks + j)];
-      b[j] = br[(long)2 * (ks + j) * ld];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) red[wave][crow(r, half)][col] = acc[r];
-  __syncthreads();
-  for (int e = threadIdx.x; e < 1024; e += 256) {
-    const int i = e >> 5, j = e & 31;  // C row-major: coalesced rows
-    C[(long)(ti + i) * ld + tj + j] = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
-    const int jt = e >> 5, it = e & 31;  // C^T rows: C[. ][jt] down the column
-    CT[(long)(tj + jt) * ld + ti + it] = ((red[0][it][jt] + red[1][it][jt]) + red[2][it][jt]) + red[3][it][jt];
-    if (g4) {
-      const float v = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
-      g4_put(g4 + g4_stride, g4_nt, ti + i, tj + j, v);
-      if (g4_count == 4) g4_put(g4 + 3 * g4_stride, g4_nt, tj + j, ti + i, v);
-    }
-  }
-  if (AT || g4) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < 1024; e += 256) red[0][e >> 5][e & 31] = A[(long)(ti + (e >> 5)) * ld + tj + (e & 31)];
-    __syncthreads();
-    for (int e = threadIdx.x; e < 1024; e += 256) {
-      if (AT) AT[(long)(tj + (e >> 5)) * ld + ti + (e & 31)] = red[0][e & 31][e >> 5];
-      if (g4) {
-        const int i = e >> 5, j = e & 31;
-        g4_put(g4, g4_nt, ti + i, tj + j, red[0][i][j]);
-        if (g4_count == 4) g4_put(g4 + 2 * g4_stride, g4_nt, tj + j, ti + i, red[0][i][j]);
-      }
-    }
-  }
-}
-
-__global__ void pad_copy_kernel(const float* src, int n, int ld_src, float* dst, int ld_dst, int np,
-                                int transpose, long src_bstride = 0, long dst_bstride = 0) {
-  __shared__ float tile[32][33];
-  src += blockIdx.z * src_bstride;  // batched: blockIdx.z walks the matrices
-  dst += blockIdx.z * dst_bstride;
-  const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
-  for (int r = ty; r < 32; r += 8) {
-    const int i = by + r, j = bx + tx;
-    tile[r][tx] = (i < n && j < n) ? src[(long)i * ld_src + j] : 0.0f;
-  }
-  __syncthreads();
-  for (int r = ty; r < 32; r += 8) {
-    if (transpose) {
-      const int i = bx + r, j = by + tx;
-      if (i < np && j < np) dst[(long)i * ld_dst + j] = tile[tx][r];
-    } else {
-      const int i = by + r, j = bx + tx;
-      if (i < np && j < np) dst[(long)i * ld_dst + j] = tile[r][tx];
-    }
-  }
-}
-
 size_t fused_lds_bytes(int n) {
   const int np = (n + 31) / 32 * 32;
   return (size_t)2 * np * LDR * sizeof(float);
@@ -2879,15 +2671,7 @@ bool gwn_gcn_tcn_fusable(const gwn_gcn_args* g) {
          slices >= gwn_device_cus() && t16_plan(g->n, g->nsup, slices, true).ok;
 }
 
-// GWN_BN_FOLD_LAST=1: the 16-node tile kernels run gwn_gcn_args.bn_fold in their last workgroup
-// (off by default: measured break-even); else it is a separate launch
-static bool fold_last_enabled() {
-  const char* e = getenv("GWN_BN_FOLD_LAST");
-  return e && e[0] == '1';
-}
-
-int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded, hipStream_t s) {
-  *folded = false;
+int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
   const int nwt = (g->n + 31) / 32;
   GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_fwd (fused): supports must be padded to 32*ceil(n/32)");
   GWN_REQUIRE(g->layout == 0 || g->layout == 1, "gcn_fwd (fused): layout must be 0 or 1 (one wave per node tile)");
@@ -2907,11 +2691,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
   a.ksplit = 1; a.slices = g->rows / g->n; a.kws = g->ksplit_ws; a.kcnt = g->ksplit_count; a.bn_slots = 0;
   a.xg4 = g->xg4; a.xg4_k = g->xg4_support;
   a.pb = g->pieces_bf16; a.ld_pb = g->ld_pb;
-  a.fold = gwn_bn_fold{};
   a.tcn = {};
-  // the t16 kernels' last-workgroup finalize (their 1024-thread workgroups map 32 channels x 32
-  // partial lanes, and the 64 x 64 folded weights four per thread)
-  const bool fold_here = g->bn_fold && bn_part && !a.x_out && fold_last_enabled();
   GWN_REQUIRE(g->ksplit == 0 || g->ksplit == 1 || g->ksplit == g->nsup, "gcn_fwd: ksplit must be 0, 1 or nsup");
   GWN_REQUIRE(!a.res_scale == !a.res_shift && !a.res_scale == !a.res_mean,
               "gcn_fwd (fused): residual_mean, residual_scale and residual_shift go together");
@@ -2955,7 +2735,6 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
       for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = (const float*)g->sup_g4b[k];
       a.ksplit = 1;
       a.bn_slots = (int)gwn_bn_part_slots(slices);
-      if (fold_here) a.fold = *g->bn_fold;
       // the bf16-mlp forward takes two slices per wave (12-wave workgroups, 168 registers): PEMS
       // forward 63 -> 58 us per launch, 25.8k -> 26.4k samples/s (profiles/r05/welford_hash); with
       // 16 waves it spills (76 us)
@@ -2968,7 +2747,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
       const int span2 = (int)((per2 - 1 + nt - 1) / nt) + 1;
       const int maximg2 = 2 * (gmax2 < span2 ? gmax2 : span2);
       const bool h16 = ((((uintptr_t)a.h) & 15) | (a.ld_h & 3)) == 0;
-      if (g->split_planes == 2 && gmax2 >= 1 && h16 && !fold_here) {
+      if (g->split_planes == 2 && gmax2 >= 1 && h16) {
         static bool attr2 = false;
         if (!attr2) {
           (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b2_kernel<768>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2982,7 +2761,6 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
         gcn_fwd_t16b_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       else gcn_fwd_t16b_kernel<1024><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
       GWN_CHECK_LAUNCH();
-      *folded = fold_here;
       return GWN_OK;
     }
   }
@@ -3025,10 +2803,8 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, bool* folded
     // 16-node tile waves, one workgroup per CU over an equal tile range; it writes every BN
     // partial slot (gwn_bn_part_slots)
     a.bn_slots = (int)gwn_bn_part_slots(slices);
-    if (fold_here) a.fold = *g->bn_fold;
     gcn_fwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
     GWN_CHECK_LAUNCH();
-    *folded = fold_here;
     return GWN_OK;
   }
   if (g->sup2 && a.sup_batch <= 1 && g->nsup > 0) {
@@ -3199,114 +2975,6 @@ extern "C" long gwn_gcn_bn_partial_count(int rows, int n, int c, int nsup, int l
   (void)c; (void)nsup; (void)ld_sup;
   if (rows <= 0 || n <= 0 || rows % n) return 0;
   return gwn_bn_part_slots(rows / n);  // max(slices, CUs): every path writes all of them
-}
-
-extern "C" int gwn_support_square(const float* a, int np, int ld, float* a2, float* a2_t, float* a_t, hipStream_t s) {
-  return gwn_support_square_g4(a, np, ld, a2, a2_t, a_t, 0, nullptr, 0, 0, s);
-}
-
-extern "C" int gwn_support_square_g4(const float* a, int np, int ld, float* a2, float* a2_t, float* a_t, int n,
-                                     float* g4, long g4_stride, int g4_count, hipStream_t s) {
-  GWN_REQUIRE(a && a2 && a2_t && np > 0 && np % 32 == 0 && ld >= np, "support_square: np must be a multiple of 32");
-  GWN_REQUIRE(!g4 || (n > 0 && (n + 31) / 32 * 32 <= np && (g4_count == 2 || g4_count == 4) &&
-                      g4_stride >= gwn_support_g4_floats(n)),
-              "support_square_g4: needs n <= np, g4_count 2 or 4 and g4_stride >= gwn_support_g4_floats(n)");
-  dim3 grid(np / 32, np / 32);
-  support_square_kernel<<<grid, 256, 0, s>>>(a, np, ld, a2, a2_t, a_t, g4, g4_stride, g4 ? (n + 15) / 16 : 0,
-                                             g4_count);
-  GWN_CHECK_LAUNCH();
-  return GWN_OK;
-}
-
-namespace {
-struct G4Src {
-  const float* src[32];
-};
-// one 256-thread block per (1-KiB block = (k-group, tile), copy): thread e writes float e of the block
-__global__ __launch_bounds__(256) void support_g4_kernel(G4Src gs, int nt, int ld, float* dst, long dst_stride) {
-  const int blk = blockIdx.x, c = blockIdx.y;
-  const int kg = blk / nt, t = blk - kg * nt;
-  const int e = threadIdx.x, lane = e >> 2, i = e & 3, g = lane >> 4, j = lane & 15;
-  dst[(long)c * dst_stride + (long)blk * 256 + e] = gs.src[c][(long)(16 * kg + 4 * i + g) * ld + 16 * t + j];
-}
-}  // namespace
-
-extern "C" long gwn_support_g4_floats(int n) {
-  const long nt = (n + 15) / 16;
-  return n > 0 ? nt * nt * 256 : 0;
-}
-
-extern "C" int gwn_support_g4(const float* const* src, int count, int n, int ld, float* dst, long dst_stride,
-                              hipStream_t s) {
-  GWN_REQUIRE(src && dst && n > 0 && count > 0 && count <= 32 && ld >= (n + 31) / 32 * 32 &&
-                  dst_stride >= gwn_support_g4_floats(n),
-              "support_g4: needs 1..32 padded [np][ld] supports (ld >= 32*ceil(n/32)) and dst_stride >= "
-              "gwn_support_g4_floats(n)");
-  G4Src gs = {};
-  for (int c = 0; c < count; ++c) gs.src[c] = src[c];
-  const int nt = (n + 15) / 16;
-  support_g4_kernel<<<dim3(nt * nt, count), 256, 0, s>>>(gs, nt, ld, dst, dst_stride);
-  GWN_CHECK_LAUNCH();
-  return GWN_OK;
-}
-
-namespace {
-// bf16 copy: one 512-thread block per (32-row k-group, 16-column tile, copy): thread e writes element
-// e of the block, lane e >> 3's k-step row 8 (lane >> 4) + (e & 7)
-__global__ __launch_bounds__(512) void support_g4_bf16_kernel(G4Src gs, int nt, int ld, __bf16* dst, long dst_stride) {
-  const int blk = blockIdx.x, c = blockIdx.y;
-  const int kg = blk / nt, t = blk - kg * nt;
-  const int e = threadIdx.x, lane = e >> 3, i = e & 7;
-  dst[(long)c * dst_stride + (long)blk * 512 + e] =
-      (__bf16)gs.src[c][(long)(32 * kg + 8 * (lane >> 4) + i) * ld + 16 * t + (lane & 15)];
-}
-}  // namespace
-
-extern "C" long gwn_support_g4_bf16_elems(int n) {
-  const long nt = (n + 15) / 16, nkg = (n + 31) / 32;
-  return n > 0 ? nkg * nt * 512 : 0;
-}
-
-extern "C" int gwn_support_g4_bf16(const float* const* src, int count, int n, int ld, void* dst, long dst_stride,
-                                   hipStream_t s) {
-  GWN_REQUIRE(src && dst && n > 0 && count > 0 && count <= 32 && ld >= (n + 31) / 32 * 32 &&
-                  dst_stride >= gwn_support_g4_bf16_elems(n) && dst_stride % 8 == 0,
-              "support_g4_bf16: needs 1..32 padded [np][ld] supports (ld >= 32*ceil(n/32)) and dst_stride >= "
-              "gwn_support_g4_bf16_elems(n), a multiple of 8");
-  G4Src gs = {};
-  for (int c = 0; c < count; ++c) gs.src[c] = src[c];
-  const int nt = (n + 15) / 16, nkg = (n + 31) / 32;
-  support_g4_bf16_kernel<<<dim3(nkg * nt, count), 512, 0, s>>>(gs, nt, ld, (__bf16*)dst, dst_stride);
-  GWN_CHECK_LAUNCH();
-  return GWN_OK;
-}
-
-extern "C" int gwn_transpose(const float* src, int n, int ld_src, float* dst, int ld_dst, hipStream_t s) {
-  GWN_REQUIRE(n > 0, "transpose: bad shape");
-  dim3 grid((n + 31) / 32, (n + 31) / 32);
-  pad_copy_kernel<<<grid, 256, 0, s>>>(src, n, ld_src, dst, ld_dst, n, 1);
-  GWN_CHECK_LAUNCH();
-  return GWN_OK;
-}
-
-extern "C" int gwn_pad_square(const float* src, int n, int ld_src, float* dst, int np, int ld_dst, int transpose,
-                              hipStream_t s) {
-  GWN_REQUIRE(n > 0 && np >= n && ld_dst >= np, "pad_square: bad shape");
-  dim3 grid((np + 31) / 32, (np + 31) / 32);
-  pad_copy_kernel<<<grid, 256, 0, s>>>(src, n, ld_src, dst, ld_dst, np, transpose);
-  GWN_CHECK_LAUNCH();
-  return GWN_OK;
-}
-
-extern "C" int gwn_pad_square_batched(const float* src, int batch, long src_bstride, int n, int ld_src, float* dst,
-                                      int np, int ld_dst, long dst_bstride, int transpose, hipStream_t s) {
-  GWN_REQUIRE(n > 0 && np >= n && ld_dst >= np && batch > 0 && batch <= 65535 && src_bstride >= (long)n * ld_src &&
-                  dst_bstride >= (long)np * ld_dst,
-              "pad_square_batched: bad shape");
-  dim3 grid((np + 31) / 32, (np + 31) / 32, batch);
-  pad_copy_kernel<<<grid, 256, 0, s>>>(src, n, ld_src, dst, ld_dst, np, transpose, src_bstride, dst_bstride);
-  GWN_CHECK_LAUNCH();
-  return GWN_OK;
 }
 
 // the bf16 16-node tile kernels run for (n, nsup) (c == 32, sup_g4b / sup_g4b_t given, layout 0)

@@ -1190,9 +1190,9 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   const gwn_bn_fold* f = a->bn_fold;
   if (f) {
     const int co = a->c_out > 0 ? a->c_out : a->c;
-    GWN_REQUIRE(co == 32 && a->bn_partials && !a->bn_out && f->arrive && f->gamma && f->beta && f->save_mean &&
-                    f->save_rstd && f->scale,
-                "gcn_fwd: bn_fold needs c_out == 32, bn_partials, no bn_out, arrive, gamma / beta and the outputs");
+    GWN_REQUIRE(co == 32 && a->bn_partials && !a->bn_out && f->gamma && f->beta && f->save_mean && f->save_rstd &&
+                    f->scale,
+                "gcn_fwd: bn_fold needs c_out == 32, bn_partials, no bn_out, gamma / beta and the outputs");
     GWN_REQUIRE(!f->w_next || (f->b_next && f->w_fold && f->b_fold && f->w_fold != f->w_next),
                 "gcn_fwd: bn_fold.w_next needs b_next, w_fold, b_fold (w_fold not aliasing w_next)");
   }
@@ -1209,11 +1209,10 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
       a = &local;
     }
   }
-  bool folded = false;
   int rc = (co == c && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup))
-               ? gwn_gcn_fused_fwd_launch(a, a->bn_partials, &folded, s)
+               ? gwn_gcn_fused_fwd_launch(a, a->bn_partials, s)
                : gcn_fwd_unfolded(a, s);
-  if (rc || !f || folded) return rc;
+  if (rc || !f) return rc;
   return gwn_batchnorm_fwd_fold(a->bn_partials, (int)gwn_bn_part_slots(a->rows / n), co, f->gamma, f->beta,
                                 f->running_mean, f->running_var, f->momentum, f->eps, f->save_mean, f->save_rstd,
                                 f->scale, f->w_next, f->b_next, f->w_fold, f->b_fold, f->num_batches_tracked, s);

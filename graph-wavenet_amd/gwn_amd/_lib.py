@@ -76,7 +76,6 @@ class BnFold(ctypes.Structure):
         ("save_mean", c_void_p), ("save_rstd", c_void_p), ("scale", c_void_p),
         ("w_next", c_void_p), ("b_next", c_void_p), ("w_fold", c_void_p), ("b_fold", c_void_p),
         ("num_batches_tracked", c_void_p),
-        ("arrive", c_void_p),
     ]
 
 

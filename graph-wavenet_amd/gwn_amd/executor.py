@@ -373,8 +373,6 @@ class Executor:
             "bnsums": e(2 * C),  # BN-backward statistics handed from a layer's TCN backward to the next
             # BN partials of one layer: gwn_gcn_bn_partial_count slots (>= one per slice)
             "bnpart": e(self._bn_parts(ts[0] * B * N) * 3 * C),
-            # per-layer arrival counters of the gcn forward's in-launch BN finalize (gwn_bn_fold.arrive)
-            "bnarrive": torch.zeros(L, device=self.device, dtype=torch.int32),
         }
         lib = _lib.load()
         need = [
@@ -665,7 +663,7 @@ class Executor:
                                  b_next=ptr(self.pk("fg_b%d" % (i + 1))) if nxt else None,
                                  w_fold=acts.w_fold[i + 1].data_ptr() if nxt else None,
                                  b_fold=acts.b_fold[i + 1].data_ptr() if nxt else None,
-                                 num_batches_tracked=ptr(nbt), arrive=scr["bnarrive"].data_ptr() + 4 * i)
+                                 num_batches_tracked=ptr(nbt))
                 ga.bn_fold = ctypes.pointer(bf)
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing

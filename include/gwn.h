@@ -325,9 +325,7 @@ typedef struct gwn_gcn_args {
   void* pieces_bf16; long ld_pb;
   /* bn_fold (optional, train mode, c == 32, bn_partials given): gwn_batchnorm_fwd_fold on this
    * launch's partials, issued by gwn_gcn_fwd itself (a second launch on the same stream); the
-   * caller then does not call gwn_batchnorm_fwd_fold.  With GWN_BN_FOLD_LAST=1 in the environment
-   * the persistent 16-node tile kernels run it in their last workgroup to finish instead (partials
-   * written through in a private channel-major order: bn_partials' content is then unspecified). */
+   * caller then does not call gwn_batchnorm_fwd_fold. */
   const struct gwn_bn_fold* bn_fold;
   /* tcn (optional): the layer's gated TCN (gwn_gated_tcn_fwd's arguments, its xg = h and ld_xg =
    * ld_h: the TCN writes piece 0 of h) run by this call before the diffusion.  When the f32 16-node
@@ -337,15 +335,13 @@ typedef struct gwn_gcn_args {
    * launch first.  The caller then does not call gwn_gated_tcn_fwd. */
   const struct gwn_tcn_args* tcn;
 } gwn_gcn_args;
-/* gwn_batchnorm_fwd_fold's arguments (same meaning) for gwn_gcn_args.bn_fold, plus arrive: one
- * device int, zero before the first launch and left zero by every launch (the workgroup count). */
+/* gwn_batchnorm_fwd_fold's arguments (same meaning) for gwn_gcn_args.bn_fold */
 typedef struct gwn_bn_fold {
   const float* gamma; const float* beta; float* running_mean; float* running_var;
   float momentum; float eps;
   float* save_mean; float* save_rstd; float* scale;
   const float* w_next; const float* b_next; float* w_fold; float* b_fold;
   long long* num_batches_tracked;
-  int* arrive;
 } gwn_bn_fold;
 /* c == 32, n <= 512 and ld_sup >= np = 32*ceil(n/32): one fused launch (gcn_fused.hip: node
  * features LDS-resident through the whole diffusion chain, mlp accumulated from the MFMA
