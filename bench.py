@@ -257,6 +257,15 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
     for i in sorted(acts.gcn_args):
         ga = type(acts.gcn_args[i]).from_buffer_copy(acts.gcn_args[i])
         ga.bn_fold = None
+        if ga.tcn and ga.tcn.contents.bn:
+            # the fused TCN's BatchNorm finalize stays in (it is this launch's work) but without
+            # the running statistics / num_batches_tracked updates: the replay leaves the model as is
+            ta = type(ga.tcn.contents).from_buffer_copy(ga.tcn.contents)
+            bfp = _lib.BnFold.from_buffer_copy(_lib.BnFold.from_address(ta.bn))
+            bfp.running_mean = bfp.running_var = bfp.num_batches_tracked = None
+            ta.bn = ctypes.addressof(bfp)
+            ta._bn_keep = bfp
+            ga.tcn = ctypes.pointer(ta)
         launches.append(ga)
     # the 8 launches captured in one HIP graph (as the training step replays them: no host launch
     # overhead between kernels) and replayed `rounds` times between one event pair on the stream;

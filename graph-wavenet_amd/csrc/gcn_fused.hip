@@ -59,9 +59,15 @@ struct FusedFwd {
   // f32 t16 forward: the layer's gated TCN computed in the phase staging (gwn_gcn_args.tcn; x NULL =
   // off): xg = tanh(f) sigmoid(g) of taps x[r], x[r + tap_rows] (minus mean) straight into the
   // slice images, and to h's piece 0, fg and the skip rows
+  // with bn (bn.part != NULL): x is the layer below's pre-BN z and its BatchNorm is finalized
+  // from bn.part in every workgroup (gwn_tcn_args.bn): w / b are then the raw weights
   struct {
     const float* x; const float* mean; const float* w; const float* b; float* fg; float* skip;
     long tap_rows, x_rows, ld_skip, skip_row0;
+    struct {
+      const float* part; int nparts; const float* gamma; const float* beta; float* rm; float* rv; float mom, eps;
+      float* save_mean; float* save_rstd; float* scale; float* w_fold; float* b_fold; long long* nbt;
+    } bn;
   } tcn;
 };
 
@@ -1099,7 +1105,10 @@ constexpr int LDW16 = 36;  // LDS row stride of the staged channel maps: lane gr
 // fused TCN (FusedFwd.tcn): the region of the waves' BN partials (used only by the final flush)
 // first holds the TCN weights [64 outputs in MFMA-tile order][LDT_TCN], the input means and the biases
 constexpr int LDT_TCN = 68;  // 2c + 4: a ds_read_b128 pass of 16 rows hits distinct banks
-constexpr int T16_TCN_REGION = 64 * LDT_TCN + 32 + 64 + 16;  // + the TCN's pointers / sizes (TcnLds)
+// region layout: weights [64][LDT_TCN], input means [32], biases [64], the TCN's pointers / sizes
+// (TcnLds, 16 floats), BatchNorm scales [32]
+constexpr int TW_MEAN = 64 * LDT_TCN, TW_BIAS = TW_MEAN + 32, TW_PAR = TW_BIAS + 64, TW_SCALE = TW_PAR + 16;
+constexpr int T16_TCN_REGION = TW_SCALE + 32;
 __host__ __device__ constexpr int t16_region(bool tcn) { return tcn ? T16_TCN_REGION : T16_WAVES * 3 * CH; }
 static_assert(T16_TCN_REGION >= T16_WAVES * 3 * CH, "the TCN region holds the BN partials' space");
 size_t t16_lds_bytes(int n, int nsup, int maximg, bool tcn = false) {
@@ -1209,7 +1218,10 @@ __device__ __forceinline__ void bn_init(BnRun& bn, float*) {
 // residual (BN of the layer below applied on load), z or eval-BN output store; the tile's BN
 // partial merged into the wave's running one
 __device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* hacc, long row0, int w0, int lane,
-                                             int n, BnRun& bn) {
+                                             int n, BnRun& bn, const float* res_mean = nullptr,
+                                             const float* res_scale = nullptr) {
+  if (!res_mean) res_mean = a.res_mean;
+  if (!res_scale) res_scale = a.res_scale;
   const int g = lane >> 4, j = lane & 15;
   const int w = w0 + j;
   const bool valid = w < n;
@@ -1227,8 +1239,8 @@ __device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* ha
     const float* rv = (const float*)&rq;
     float4 mq, sq, hq;
     if (a.res_scale) {
-      mq = *(const float4*)(a.res_mean + c0);
-      sq = *(const float4*)(a.res_scale + c0);
+      mq = *(const float4*)(res_mean + c0);
+      sq = *(const float4*)(res_scale + c0);
       hq = *(const float4*)(a.res_shift + c0);
     }
 #pragma unroll
@@ -1525,7 +1537,7 @@ struct TcnLds {
   int x_bytes, ld_h;
 };
 static_assert(sizeof(TcnLds) <= 16 * sizeof(float), "TcnLds in its LDS slot");
-__device__ __forceinline__ const TcnLds* tcn_lds(const float* tw) { return (const TcnLds*)(tw + 64 * LDT_TCN + 96); }
+__device__ __forceinline__ const TcnLds* tcn_lds(const float* tw) { return (const TcnLds*)(tw + TW_PAR); }
 template <typename T>
 __device__ __forceinline__ T tcn_uniform(const T& v) {  // an LDS-held value as a wave-uniform scalar
   static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte values");
@@ -1538,17 +1550,114 @@ __device__ __forceinline__ T tcn_uniform(const T& v) {  // an LDS-held value as 
   }
 }
 
-// the TCN weights (rows in MFMA-tile order), input means and biases into the staging region
-__device__ __forceinline__ void t16_tcn_stage_weights(const FusedFwd& a, float* tw) {
-  for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
-    const int ti = e >> 6, k = e & 63, t = ti >> 4, i = ti & 15;
-    const int o = 2 * (16 * (t >> 1) + i) + (t & 1);
-    tw[ti * LDT_TCN + k] = a.tcn.w[o * 64 + k];
+// the layer below's BatchNorm from its partials (gwn_tcn_args.bn), in every workgroup: thread (sub,
+// c) merges slots sub, sub + 32, ... of channel c in double (coalesced rows), the 32 subs meet in
+// scratch (LDS, 3 KiB floats x 4) and channel c's thread merges them in order -> mean and scale =
+// gamma * rstd at tw[TW_MEAN] / tw[TW_SCALE]; workgroup 0 writes gwn_batchnorm_fwd_fold's outputs
+// but w_fold / b_fold (t16_tcn_stage_weights).  Every workgroup computes bit-identical values.
+__device__ __forceinline__ void t16_tcn_bn_finalize(const FusedFwd& a, float* tw, float* scratch) {
+  const auto& f = a.tcn.bn;
+  const int c = threadIdx.x & 31, sub = threadIdx.x >> 5, nsub = blockDim.x >> 5;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  auto merge = [&](double nb, double mb, double qb) {
+    if (nb <= 0.0) return;
+    const double nn = n + nb, d = mb - mean, w = nb / nn;
+    mean += d * w;
+    m2 += qb + d * d * n * w;
+    n = nn;
+  };
+  constexpr int U = 4;
+  for (int i0 = sub; i0 < f.nparts; i0 += U * nsub) {
+    float nb[U], mb[U], qb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * nsub;
+      const float* pp = f.part + (long)(i < f.nparts ? i : 0) * 3 * CH;
+      nb[u] = i < f.nparts ? pp[c] : 0.0f;
+      mb[u] = pp[CH + c];
+      qb[u] = pp[2 * CH + c];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) merge(nb[u], mb[u], qb[u]);
   }
-  if (threadIdx.x < 32) tw[64 * LDT_TCN + threadIdx.x] = a.tcn.mean ? a.tcn.mean[threadIdx.x] : 0.0f;
-  if (threadIdx.x < 64) tw[64 * LDT_TCN + 32 + threadIdx.x] = a.tcn.b[threadIdx.x];
+  scratch[(sub * 3) * CH + c] = (float)n;
+  scratch[(sub * 3 + 1) * CH + c] = (float)mean;
+  scratch[(sub * 3 + 2) * CH + c] = (float)m2;
+  __syncthreads();
+  if (threadIdx.x < CH) {
+    n = mean = m2 = 0.0;
+    for (int q = 0; q < nsub; ++q) merge(scratch[(q * 3) * CH + c], scratch[(q * 3 + 1) * CH + c], scratch[(q * 3 + 2) * CH + c]);
+    const double var = n > 0.0 ? m2 / n : 0.0;
+    const float rs = (float)(1.0 / sqrt(var + (double)f.eps));
+    const float sc = rs * f.gamma[c];  // bn(z) = (z - mean) * sc + beta
+    tw[TW_MEAN + c] = (float)mean;
+    tw[TW_SCALE + c] = sc;
+    if (blockIdx.x == 0) {
+      f.save_mean[c] = (float)mean;
+      f.save_rstd[c] = rs;
+      f.scale[c] = sc;
+      if (f.rm) {
+        const double unbiased = n > 1.0 ? m2 / (n - 1.0) : var;
+        f.rm[c] = (float)((1.0 - f.mom) * f.rm[c] + f.mom * mean);
+        f.rv[c] = (float)((1.0 - f.mom) * f.rv[c] + f.mom * unbiased);
+      }
+      if (c == 0 && f.nbt) *f.nbt += 1;
+    }
+  }
+  __syncthreads();
+}
+
+// the TCN weights (rows in MFMA-tile order), input means and biases into the staging region; with
+// bn, first the finalize (scratch: the channel maps' LDS, staged afterwards), then the weights
+// folded (w * scale, b + w beta; workgroup 0 also writes w_fold / b_fold)
+__device__ __forceinline__ void t16_tcn_stage_weights(const FusedFwd& a, float* tw, float* scratch) {
+  static_assert(T16_WAVES * 64 == 1024, "the staging maps 64 x 64 weights four per thread");
+  const bool bn = a.tcn.bn.part != nullptr;
+  // the raw weights and the bias-fold operands do not depend on the statistics: loaded first, so
+  // their latency overlaps the finalize's
+  float wr[4], wb[4], bb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = threadIdx.x + 1024 * q, ti = e >> 6, k = e & 63, t = ti >> 4, i = ti & 15;
+    wr[q] = a.tcn.w[(2 * (16 * (t >> 1) + i) + (t & 1)) * 64 + k];
+  }
+  const int bo = threadIdx.x >> 4, bpart = threadIdx.x & 15;  // bias fold: 16 threads per output
+  if (bn) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      wb[q] = a.tcn.w[bo * 64 + 4 * bpart + q];
+      bb[q] = a.tcn.bn.beta[(4 * bpart + q) & 31];
+    }
+    t16_tcn_bn_finalize(a, tw, scratch);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = threadIdx.x + 1024 * q, ti = e >> 6, k = e & 63, t = ti >> 4, i = ti & 15;
+    float w = wr[q];
+    if (bn) {
+      w *= tw[TW_SCALE + (k & 31)];
+      if (blockIdx.x == 0) a.tcn.bn.w_fold[(2 * (16 * (t >> 1) + i) + (t & 1)) * 64 + k] = w;
+    }
+    tw[ti * LDT_TCN + k] = w;
+  }
+  if (bn) {
+    // b_fold[o] = b[o] + sum_k w[o][k] beta[k % 32]: 16 threads per output, 4 k each, fixed tree
+    float acc = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc = fmaf(wb[q], bb[q], acc);
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
+    if (bpart == 0) {
+      const float b = a.tcn.b[bo] + acc;
+      tw[TW_BIAS + bo] = b;
+      if (blockIdx.x == 0) a.tcn.bn.b_fold[bo] = b;
+    }
+  } else {
+    if (threadIdx.x < 32) tw[TW_MEAN + threadIdx.x] = a.tcn.mean ? a.tcn.mean[threadIdx.x] : 0.0f;
+    if (threadIdx.x < 64) tw[TW_BIAS + threadIdx.x] = a.tcn.b[threadIdx.x];
+  }
   if (threadIdx.x == 0) {
-    TcnLds* t = (TcnLds*)(tw + 64 * LDT_TCN + 96);
+    TcnLds* t = (TcnLds*)(tw + TW_PAR);
     t->x = a.tcn.x; t->fg = a.tcn.fg; t->skip = a.tcn.skip; t->h = (float*)a.h;
     t->tap_rows = a.tcn.tap_rows; t->ld_skip = a.tcn.ld_skip; t->skip_row0 = a.tcn.skip_row0;
     t->x_bytes = (int)(a.tcn.x_rows * CH * 4); t->ld_h = (int)a.ld_h;
@@ -1572,7 +1681,7 @@ __device__ __forceinline__ void t16_tcn_unit(const float* tw, const float4* xq, 
   const TcnLds* tp = tcn_lds(tw);
   const int g = lane >> 4, j = lane & 15, node = w0 + j;
   const bool valid = node < n;
-  const float* mu = tw + 64 * LDT_TCN + 16 * (g & 1);
+  const float* mu = tw + TW_MEAN + 16 * (g & 1);
   float xv[16];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -1580,7 +1689,7 @@ __device__ __forceinline__ void t16_tcn_unit(const float* tw, const float4* xq, 
     xv[4 * q] = xq[q].x - m.x; xv[4 * q + 1] = xq[q].y - m.y;
     xv[4 * q + 2] = xq[q].z - m.z; xv[4 * q + 3] = xq[q].w - m.w;
   }
-  const float* bias = tw + 64 * LDT_TCN + 32;
+  const float* bias = tw + TW_BIAS;
   const long row = (long)s * n + node;
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
@@ -1670,7 +1779,12 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   // the BN partials' region until the final flush)
   const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
   if (!h16 || tcn) t16_stage_maps(a.w_mlp, a.ld_w, false, 2 * a.nsup + 1, ws);
-  if (tcn) t16_tcn_stage_weights(a, wpart);
+  if (tcn) t16_tcn_stage_weights(a, wpart, imgs);  // (the finalize's scratch: the free image space)
+  // the residual's BatchNorm (the layer below's, finalized above when the TCN carries it: this
+  // launch's workgroup 0 writes the global copies, so every workgroup reads its own)
+  const bool bnk = tcn && a.tcn.bn.part != nullptr;
+  const float* res_mean = bnk ? wpart + TW_MEAN : a.res_mean;
+  const float* res_scale = bnk ? wpart + TW_SCALE : a.res_scale;
   for (long p0 = rg.tb; p0 < rg.te;) {
     const int s0 = (int)(p0 / nt);
     const long p1 = min(rg.te, (long)(s0 + maximg) * nt);
@@ -1726,7 +1840,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
           }
         }
       }
-      t16_epilogue(a, hacc, row0, w0, lane, n, bn);
+      t16_epilogue(a, hacc, row0, w0, lane, n, bn, res_mean, res_scale);
     }
     p0 = p1;
   }
@@ -2656,6 +2770,13 @@ int bn_part_tail(float* bn_part, int slices, int c, hipStream_t s) {
 // per CU most of that work is redundant (METR: the layers of 192 and 64 slices ran 4 and 1 us
 // slower fused, those of >= 256 slices 2-6 us faster; step 25.04k -> 25.26k samples/s same-box,
 // profiles/r05/tcn_fused)
+// the in-kernel finalize's merge: 32 channels x (blockDim / 32) slot lanes, exchanged through the
+// image space before the first phase is staged
+constexpr size_t T16_BN_SCRATCH = 3 * (64 * T16_WAVES / 32) * CH * sizeof(float);
+static bool bn_scratch_ok(int n, int nsup, int slices) {
+  const T16Plan pl = t16_plan(n, nsup, slices, true);
+  return pl.ok && pl.lds >= t16_lds_bytes(n, nsup, 0, true) + T16_BN_SCRATCH;
+}
 bool gwn_gcn_tcn_fusable(const gwn_gcn_args* g) {
   const gwn_tcn_args* t = g->tcn;
   if (!t) return false;
@@ -2668,7 +2789,11 @@ bool gwn_gcn_tcn_fusable(const gwn_gcn_args* g) {
          (g->c_out == 0 || g->c_out == CH) && gwn_gcn_fused_eligible(g->c, g->n, g->nsup, g->ld_sup) &&
          al(g->h) && (g->ld_h & 3) == 0 && g->split_planes == 0 && g->sup_g4 && g->sup_batch <= 1 && g->nsup > 0 &&
          g->layout == 0 && t16_enabled() && (pick_ksplit(g, slices, nwt) <= 1 || g->ksplit != g->nsup) &&
-         slices >= gwn_device_cus() && t16_plan(g->n, g->nsup, slices, true).ok;
+         slices >= gwn_device_cus() && t16_plan(g->n, g->nsup, slices, true).ok &&
+         (!t->bn || (t->bn_partials && t->bn_nparts > 0 && t->bn->w_next && t->bn->b_next && t->bn->w_fold &&
+                     t->bn->b_fold && t->bn->gamma && t->bn->beta && t->bn->save_mean && t->bn->save_rstd &&
+                     t->bn->scale && bn_scratch_ok(g->n, g->nsup, slices) &&
+                     (!g->residual_mean || (g->residual_mean == t->bn->save_mean && g->residual_scale == t->bn->scale))));
 }
 
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
@@ -2796,6 +2921,12 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
       a.tcn.x = t->x; a.tcn.mean = t->x_mean; a.tcn.w = t->w_fg; a.tcn.b = t->b_fg; a.tcn.fg = t->fg;
       a.tcn.skip = t->skipcat; a.tcn.ld_skip = t->ld_skip; a.tcn.skip_row0 = t->skip_row0;
       a.tcn.tap_rows = (long)t->dilation * t->P; a.tcn.x_rows = (long)t->t_in * t->P;
+      if (t->bn) {  // the layer below's BatchNorm finalized in the launch (raw weights folded there)
+        const gwn_bn_fold* f = t->bn;
+        a.tcn.mean = nullptr; a.tcn.w = f->w_next; a.tcn.b = f->b_next;
+        a.tcn.bn = {t->bn_partials, t->bn_nparts, f->gamma, f->beta, f->running_mean, f->running_var, f->momentum,
+                    f->eps, f->save_mean, f->save_rstd, f->scale, f->w_fold, f->b_fold, f->num_batches_tracked};
+      }
     }
     PowSup p = {};
     for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = g->sup_g4[k];

@@ -1072,6 +1072,22 @@ int gwn_start_conv_fwd(const float* x, long sb, long sc, long sn, long st, int B
 // ---------------------------------------------------------------------------------------------
 int gwn_gated_tcn_fwd(const gwn_tcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->c > 0 && a->P > 0 && a->ntaps >= 0 && a->c_out >= 0, "gated_tcn_fwd: bad shape");
+  if (a->bn) {  // the layer below's BatchNorm finalized first (its own launch), then the folded TCN
+    const gwn_bn_fold* f = a->bn;
+    GWN_REQUIRE(a->c == 32 && a->bn_partials && a->bn_nparts > 0 && f->w_next && f->b_next && f->w_fold && f->b_fold &&
+                    f->w_fold != f->w_next && f->gamma && f->beta && f->save_mean && f->save_rstd && f->scale,
+                "gated_tcn_fwd: bn needs c == 32, bn_partials / bn_nparts, and bn's weights, outputs and w_fold / b_fold");
+    int rc = gwn_batchnorm_fwd_fold(a->bn_partials, a->bn_nparts, a->c, f->gamma, f->beta, f->running_mean,
+                                    f->running_var, f->momentum, f->eps, f->save_mean, f->save_rstd, f->scale,
+                                    f->w_next, f->b_next, f->w_fold, f->b_fold, f->num_batches_tracked, s);
+    if (rc) return rc;
+    gwn_tcn_args t = *a;
+    t.bn = nullptr;
+    t.x_mean = f->save_mean;
+    t.w_fg = f->w_fold;
+    t.b_fg = f->b_fold;
+    return gwn_gated_tcn_fwd(&t, s);
+  }
   const int taps = a->ntaps > 0 ? a->ntaps : 2, co = a->c_out > 0 ? a->c_out : a->c;
   GWN_REQUIRE(a->t_in > a->dilation * (taps - 1), "gated_tcn_fwd: input shorter than the receptive field");
   GWN_REQUIRE(a->c % 16 == 0 && co % 16 == 0, "gated_tcn_fwd: channels must be multiples of 16");

@@ -48,6 +48,7 @@ class TcnArgs(ctypes.Structure):
         ("skipcat", c_void_p), ("ld_skip", c_long), ("skip_row0", c_int),
         ("x_mean", c_void_p),
         ("ntaps", c_int), ("c_out", c_int),
+        ("bn", c_void_p), ("bn_partials", c_void_p), ("bn_nparts", c_int),
     ]
 
 

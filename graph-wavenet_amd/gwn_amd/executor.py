@@ -373,6 +373,9 @@ class Executor:
             "bnsums": e(2 * C),  # BN-backward statistics handed from a layer's TCN backward to the next
             # BN partials of one layer: gwn_gcn_bn_partial_count slots (>= one per slice)
             "bnpart": e(self._bn_parts(ts[0] * B * N) * 3 * C),
+            # layer i's partials are finalized by layer i+1's TCN (gwn_tcn_args.bn) while layer i+1's
+            # gcn writes its own: alternate buffers
+            "bnpart2": e(self._bn_parts(ts[0] * B * N) * 3 * C),
         }
         lib = _lib.load()
         need = [
@@ -568,7 +571,7 @@ class Executor:
         lib.call("gwn_start_conv_fwd", ptr(x), sx[0], sx[1], sx[2], sx[3], B, cin, N, t_in, ts[0],
                  ptr(self.pk("start_w")), ptr(self.pk("start_b")), C, ptr(acts.X[0]), ptr(acts.xin), st)
         scr = self.scratch(B, ts)
-        ws, bnpart = scr["ws"], scr["bnpart"]
+        ws, bnparts = scr["ws"], (scr["bnpart"], scr["bnpart2"])
         planes = self.split_planes() if sup_batch <= 1 else 0
         acts.g4bt_arr = None
         # (shared supports only: planes is 0 for per-sample graphs, whose padded stacks are fresh per call)
@@ -616,6 +619,21 @@ class Executor:
                               xg=ptr(acts.H[i]), ld_xg=cfg.W, fg=ptr(acts.FG[i]),
                               skipcat=acts.skipcat.data_ptr() + 4 * i * cfg.D, ld_skip=L * cfg.D,
                               skip_row0=(ts[i + 1] - tf) * P, ntaps=cfg.K, c_out=cfg.D)
+            if fold and i > 0:
+                # BatchNorm i-1 (train mode) finalized by this TCN from layer i-1's partials: inside
+                # the fused gcn launch every workgroup merges them (no finalize launch), else
+                # gwn_gated_tcn_fwd issues gwn_batchnorm_fwd_fold first (gwn_tcn_args.bn)
+                rm_, rv_, mom_, eps_, nbt_ = bn_bufs[i - 1]
+                bfp = _lib.BnFold(gamma=ptr(self.pk("bn_g%d" % (i - 1))), beta=ptr(self.pk("bn_b%d" % (i - 1))),
+                                  running_mean=ptr(rm_), running_var=ptr(rv_), momentum=mom_, eps=eps_,
+                                  save_mean=ptr(acts.mean[i - 1]), save_rstd=ptr(acts.rstd[i - 1]),
+                                  scale=acts.bn_scale[i - 1].data_ptr(),
+                                  w_next=ptr(self.pk("fg_w%d" % i)), b_next=ptr(self.pk("fg_b%d" % i)),
+                                  w_fold=acts.w_fold[i].data_ptr(), b_fold=acts.b_fold[i].data_ptr(),
+                                  num_batches_tracked=ptr(nbt_))
+                ta.bn, ta.bn_partials = ctypes.addressof(bfp), ptr(bnparts[(i - 1) % 2])
+                ta.bn_nparts = self._bn_parts(ts[i] * P)
+                ta._bn_keep = bfp  # (ctypes keeps no reference through the c_void_p field)
             if i == L - 1 and not training:
                 lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), st)
                 continue  # the last gcn / bn output is dead in eval (only skip reaches the output)
@@ -634,7 +652,7 @@ class Executor:
                               w_mlp=ptr(self.pk("mlp_w%d" % i)), b_mlp=ptr(self.pk("mlp_b%d" % i)),
                               residual=xin + 4 * sh * P * C, z=ptr(acts.Z[i]),
                               seed_ptr=ptr(acts.seed), salt=i, drop_p=drop,
-                              bn_partials=ptr(bnpart) if training else None,
+                              bn_partials=ptr(bnparts[i % 2]) if training else None,
                               # the last layer's gcn output only feeds bn[L-1]'s running statistics:
                               # no backward reads its hop pieces
                               no_pieces=1 if i == L - 1 and self._fused_gcn() else 0,
@@ -651,26 +669,20 @@ class Executor:
             # staging where it runs, else its own launch issued by gwn_gcn_fwd)
             ga.tcn = ctypes.pointer(ta)
             rm, rv, mom, eps, nbt = bn_bufs[i]
-            if fold:
-                # the BN finalize + fold into the next TCN rides on the gcn launch (gwn_gcn_args.bn_fold:
-                # its last workgroup merges the partials on the 16-node tile kernels)
-                nxt = i + 1 < L
+            if fold and i == L - 1:
+                # the last BatchNorm (its output dead but for the running statistics): finalized by
+                # the gcn call (gwn_gcn_args.bn_fold, a second launch); the others by the next TCN
                 bf = _lib.BnFold(gamma=ptr(self.pk("bn_g%d" % i)), beta=ptr(self.pk("bn_b%d" % i)),
                                  running_mean=ptr(rm), running_var=ptr(rv), momentum=mom, eps=eps,
                                  save_mean=ptr(acts.mean[i]), save_rstd=ptr(acts.rstd[i]),
-                                 scale=acts.bn_scale[i].data_ptr(),
-                                 w_next=ptr(self.pk("fg_w%d" % (i + 1))) if nxt else None,
-                                 b_next=ptr(self.pk("fg_b%d" % (i + 1))) if nxt else None,
-                                 w_fold=acts.w_fold[i + 1].data_ptr() if nxt else None,
-                                 b_fold=acts.b_fold[i + 1].data_ptr() if nxt else None,
-                                 num_batches_tracked=ptr(nbt))
+                                 scale=acts.bn_scale[i].data_ptr(), num_batches_tracked=ptr(nbt))
                 ga.bn_fold = ctypes.pointer(bf)
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
             if fold:
                 pass  # done by the gcn launch
             elif training:
-                lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnpart), self._bn_parts(rows),
+                lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnparts[i % 2]), self._bn_parts(rows),
                          ptr(self.pk("bn_g%d" % i)), ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps,
                          ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(nbt), st)
             else:

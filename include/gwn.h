@@ -184,6 +184,15 @@ typedef struct gwn_tcn_args {
    * c_out (resp. 2*c_out) channels.  0 = the defaults ntaps 2, c_out c.  Non-default values run
    * the generic GEMM path (no x_mean fold). */
   int ntaps, c_out;
+  /* bn (optional, c == 32 row-GEMM / fused path, training): x holds the PRE-BatchNorm z of the
+   * layer below and its BatchNorm is finalized by this call -- bn_partials [bn_nparts][3][c]
+   * (gwn_gcn_fwd's partials of that layer) merged into the statistics, and every output of
+   * gwn_batchnorm_fwd_fold written (save_mean / save_rstd / scale, the running statistics,
+   * num_batches_tracked advanced once, w_fold / b_fold from bn->w_next / b_next = this TCN's raw
+   * weights) -- then the TCN applied with them (x_mean, w_fg and b_fg are ignored).  Inside the
+   * f32 16-node tile forward (gwn_gcn_args.tcn) every workgroup merges the partials itself: no
+   * finalize launch; elsewhere gwn_batchnorm_fwd_fold runs first as its own launch. */
+  const struct gwn_bn_fold* bn; const float* bn_partials; int bn_nparts;
 } gwn_tcn_args;
 /* fg may be NULL when no backward follows (inference; c == 32 row-GEMM path): the (tanh, sigmoid)
  * pairs are then not stored. */

@@ -697,19 +697,23 @@ def test_gcn_fused_schedules_agree(gpu, n, monkeypatch):
             assert rel_err(a_.cpu().numpy(), b_.cpu().numpy()) <= 2e-6
 
 
+@pytest.mark.parametrize("bn", [False, True])
 @pytest.mark.parametrize("n,B,t_out,d", [(207, 32, 8, 2), (37, 64, 5, 1), (207, 8, 3, 1)])
-def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d):
+def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn):
     """gwn_gcn_args.tcn: the gated TCN (model.py:206-212) computed inside the f32 16-node tile
     forward's staging (>= a slice per CU) against the same layer as two calls (gwn_gated_tcn_fwd,
     then gwn_gcn_fwd): xg (piece 0 of h), the (tanh, sigmoid) pairs, the skip rows, the hop pieces,
     z and the BN statistics agree to the fp32 floor (the products summed in another order), and xg
     matches fp64.  The last case has fewer slices than CUs: the TCN is then its own launch inside
-    gwn_gcn_fwd and everything is bitwise the two-call result.  BatchNorm on load: x is a pre-BN z
-    (centred by x_mean, weights folded) as in the training step."""
+    gwn_gcn_fwd and everything is bitwise the two-call result.  x is a pre-BN z (model.py:234-236,
+    train mode): plain, its BatchNorm applied on load (x_mean, folded weights); with bn, that
+    BatchNorm finalized by the TCN itself from [nparts][3][c] partials (gwn_tcn_args.bn: in every
+    workgroup of the fused launch, or gwn_batchnorm_fwd_fold first): its outputs (mean, rstd,
+    scale, running statistics, num_batches_tracked, w_fold, b_fold) against fp64 as well."""
     import ctypes
     from gwn_amd import _lib
     lib = _lib.load()
-    torch.manual_seed(n + B + d)
+    torch.manual_seed(n + B + d + bn)
     C, K = 32, 3
     NP = (n + 31) // 32 * 32
     W = (2 * K + 1) * C
@@ -728,7 +732,7 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d):
     arr2 = (ctypes.c_void_p * K)(*[q[0].data_ptr() for q in sq])
     g4f, _ = _g4s(gpu, n, sups, sq, supT)
     PP = ctypes.POINTER(ctypes.c_void_p)
-    x = torch.randn(t_in * P, C, device=gpu) * 2 + 3
+    x = torch.randn(t_in * P, C, device=gpu) * 2 + 3 + torch.randn(C, device=gpu)
     xmean = torch.randn(C, device=gpu) + 3
     wfg = torch.randn(2 * C, 2 * C, device=gpu) * 0.15
     bfg = torch.randn(2 * C, device=gpu) * 0.1
@@ -739,6 +743,17 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d):
     ld_skip = 3 * C
     skip_row0 = (t_out - 1) * P
     nparts = int(lib.gwn_gcn_bn_partial_count(rows, n, C, K, NP))
+    # the layer below's BatchNorm partials over x's rows: 300 ragged chunks, some empty
+    xr = x.double().cpu()
+    cuts = sorted(set([0, xr.shape[0]] + torch.randint(0, xr.shape[0], (297,)).tolist()))
+    bpl = torch.zeros(len(cuts) - 1 + 3, 3, C, dtype=torch.float64)
+    for q, (lo, hi) in enumerate(zip(cuts[:-1], cuts[1:])):
+        if hi > lo:
+            blk = xr[lo:hi]
+            bpl[q, 0], bpl[q, 1] = hi - lo, blk.mean(0)
+            bpl[q, 2] = ((blk - blk.mean(0)) ** 2).sum(0)
+    bparts = bpl.float().to(gpu).contiguous()
+    gamma, beta = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu)
     outs = {}
     for fused in (False, True):
         h = torch.full((rows, W), float("nan"), device=gpu)
@@ -749,25 +764,60 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d):
         ta = _lib.TcnArgs(x=x.data_ptr(), t_in=t_in, P=P, c=C, dilation=d, w_fg=wfg.data_ptr(), b_fg=bfg.data_ptr(),
                           xg=h.data_ptr(), ld_xg=W, fg=fg.data_ptr(), skipcat=skip.data_ptr(), ld_skip=ld_skip,
                           skip_row0=skip_row0, x_mean=xmean.data_ptr())
+        res_aff = {}
+        bo = None
+        if bn:
+            bo = dict(mean=torch.full((C,), float("nan"), device=gpu), rstd=torch.full((C,), float("nan"), device=gpu),
+                      scale=torch.full((C,), float("nan"), device=gpu), rm=torch.zeros(C, device=gpu) + 0.5,
+                      rv=torch.ones(C, device=gpu), nbt=torch.full((1,), 3, device=gpu, dtype=torch.int64),
+                      wf=torch.full_like(wfg, float("nan")), bf=torch.full_like(bfg, float("nan")))
+            bfp = _lib.BnFold(gamma=gamma.data_ptr(), beta=beta.data_ptr(), running_mean=bo["rm"].data_ptr(),
+                              running_var=bo["rv"].data_ptr(), momentum=0.1, eps=1e-5, save_mean=bo["mean"].data_ptr(),
+                              save_rstd=bo["rstd"].data_ptr(), scale=bo["scale"].data_ptr(), w_next=wfg.data_ptr(),
+                              b_next=bfg.data_ptr(), w_fold=bo["wf"].data_ptr(), b_fold=bo["bf"].data_ptr(),
+                              num_batches_tracked=bo["nbt"].data_ptr())
+            ta.bn, ta.bn_partials, ta.bn_nparts = ctypes.addressof(bfp), bparts.data_ptr(), bparts.shape[0]
+            ta.x_mean = None
+            res_aff = dict(residual_mean=bo["mean"].data_ptr(), residual_scale=bo["scale"].data_ptr(),
+                           residual_shift=beta.data_ptr())
         ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, PP), ld_sup=NP, h=h.data_ptr(), ld_h=W,
                           w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(), residual=x.data_ptr() + 4 * d * P * C,
                           z=z.data_ptr(), seed_ptr=seed.data_ptr(), salt=0, drop_p=0.0, bn_partials=bnp.data_ptr(),
-                          sup2=ctypes.cast(arr2, PP), w_mlp_t=wmt.data_ptr(), sup_g4=g4f[1])
+                          sup2=ctypes.cast(arr2, PP), w_mlp_t=wmt.data_ptr(), sup_g4=g4f[1], **res_aff)
         if fused:
             ga.tcn = ctypes.pointer(ta)
         else:
             _lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), _lib.stream())
         _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
         torch.cuda.synchronize()
-        outs[fused] = (h, fg, skip[:, :C], z, _bn_all(bnp, rows, n, C, K, NP))
-    (h0, fg0, sk0, z0, st0), (h1, fg1, sk1, z1, st1) = outs[False], outs[True]
+        outs[fused] = (h, fg, skip[:, :C], z, _bn_all(bnp, rows, n, C, K, NP)) + (
+            tuple(bo[k] for k in ("mean", "rstd", "scale", "rm", "rv", "nbt", "wf", "bf")) if bn else ())
+    (h0, fg0, sk0, z0, st0), (h1, fg1, sk1, z1, st1) = outs[False][:5], outs[True][:5]
     if S < _cus():
         for a_, b_ in zip(outs[False], outs[True]):
             assert torch.equal(a_, b_)
         return
-    # fp64 truth of xg
-    xd = (x.double() - xmean.double()).cpu()
-    f = torch.cat([xd[:rows], xd[d * P:d * P + rows]], dim=1) @ wfg.double().cpu().t() + bfg.double().cpu()
+    # fp64 truth of xg (and of the BatchNorm the TCN finalized)
+    if bn:
+        mu, var = xr.mean(0), xr.var(0, unbiased=False)
+        rstd = 1.0 / torch.sqrt(var + 1e-5)
+        sc = rstd * gamma.double().cpu()
+        for k, (mean_, rstd_, scale_, rm_, rv_, nbt_, wf_, bf_) in ((k, outs[k][5:]) for k in (False, True)):
+            assert rel_err(mean_.cpu().numpy(), mu.numpy()) <= 1e-6
+            assert rel_err(rstd_.cpu().numpy(), rstd.numpy()) <= 1e-6
+            assert rel_err(scale_.cpu().numpy(), sc.numpy()) <= 1e-6
+            assert rel_err(rm_.cpu().numpy(), (0.45 + 0.1 * mu).numpy()) <= 1e-6
+            assert rel_err(rv_.cpu().numpy(), (0.9 + 0.1 * xr.var(0, unbiased=True)).numpy()) <= 1e-6
+            assert int(nbt_.item()) == 4
+            assert rel_err(wf_.cpu().numpy(), (wfg.double().cpu() * sc.repeat(2)[None, :]).numpy()) <= 1e-6
+            bref = bfg.double().cpu() + wfg.double().cpu() @ beta.double().cpu().repeat(2)
+            assert rel_err(bf_.cpu().numpy(), bref.numpy()) <= 1e-6
+        xd = ((xr - mu) * sc + beta.double().cpu())
+        W_ = wfg.double().cpu()
+        f = torch.cat([xd[:rows], xd[d * P:d * P + rows]], dim=1) @ W_.t() + bfg.double().cpu()
+    else:
+        xd = (xr - xmean.double().cpu())
+        f = torch.cat([xd[:rows], xd[d * P:d * P + rows]], dim=1) @ wfg.double().cpu().t() + bfg.double().cpu()
     xg_ref = torch.tanh(f[:, 0::2]) * torch.sigmoid(f[:, 1::2])
     # (the fp32 floor of 64-term sums of ~5-magnitude products, as the row-GEMM TCN's tests: 5e-6)
     assert rel_err(h0[:, :C].cpu().numpy(), xg_ref.numpy()) <= 5e-6
