@@ -11,7 +11,7 @@ FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result ${EXT
 OBJ="$(mktemp -d)"
 trap 'rm -rf "$OBJ"' EXIT
 pids=()
-for f in gemm gemm_nt ops gcn_fused supports rowgemm gram wgrad wgrad_group infer bigdiff; do
+for f in gemm gemm_nt ops gcn_fused gcn_slice supports rowgemm gram wgrad wgrad_group infer bigdiff; do
   "$HIPCC" $FLAGS -c -o "$OBJ/$f.o" "$SRC/$f.hip" &
   pids+=($!)
   while [ "$(jobs -rp | wc -l)" -ge "${JOBS:-8}" ]; do sleep 0.2; done
