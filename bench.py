@@ -315,12 +315,13 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
         # over this bench (tools/gpu.sh pmc:<cfg> + tools/pmc_summary.py: separate --pmc runs for
         # FETCH_SIZE, WRITE_SIZE and the SQ counters; FETCH x2 per the gfx950 correction)
         # (the newest round's committed passes)
-        for rnd in ("r04", "r03"):
+        for rnd in ("r05/final", "r04", "r03"):
             path = os.path.join(ROOT, "profiles", rnd, name)
             if os.path.exists(path):
                 with open(path) as f:
                     rec = json.load(f).get(key, {})
-                return rec.get("hbm_bytes_per_dispatch"), rec.get("mfma_busy_frac"), "profiles/%s/%s" % (rnd, name)
+                if rec:
+                    return rec.get("hbm_bytes_per_dispatch"), rec.get("mfma_busy_frac"), "profiles/%s/%s" % (rnd, name)
         return None, None, None
 
     if bf16:
@@ -329,13 +330,15 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
         gbs = total_bytes / (total_ms / 1000.0) / 1e9
         t16b = getattr(acts, "g4bf_arr", None) is not None
         mlpb = getattr(acts, "planes", 1) == 2
-        kname = ("gcn_fwd_t16b_kernel<1024%s> (fused diffusion GCN forward, persistent 16-node tile waves, "
-                 "diffusion %s on bf16 MFMA operands, fp32 accumulation, 8 launches/step)"
-                 % ((", true", "and per-piece mlp") if mlpb else ("", "(mlp in fp32)")) if t16b else
-                 "gcn_fwd_split_kernel<%d, 1, %d> (fused diffusion GCN forward, bf16 operands, 8 launches/step)"
-                 % ((N + 31) // 32, (N + 31) // 32))
-        traffic, mfma_busy, src = (pmc("pmc_bench_pems.json", "gcn_fwd_t16b_kernel" if t16b else "gcn_fwd_split_kernel")
-                                   if N == 325 else (None,) * 3)
+        kname = ("gcn_fwd_t16b2_kernel<768> (fused diffusion GCN forward, persistent 16-node tile waves, two "
+                 "slices per wave, diffusion and per-piece mlp on bf16 MFMA operands, fp32 accumulation, "
+                 "8 launches/step)" if mlpb else
+                 "gcn_fwd_t16b_kernel<1024> (fused diffusion GCN forward, persistent 16-node tile waves, diffusion "
+                 "on bf16 MFMA operands (mlp in fp32), fp32 accumulation, 8 launches/step)") if t16b else \
+            ("gcn_fwd_split_kernel<%d, 1, %d> (fused diffusion GCN forward, bf16 operands, 8 launches/step)"
+             % ((N + 31) // 32, (N + 31) // 32))
+        pkey = ("gcn_fwd_t16b2_kernel" if mlpb else "gcn_fwd_t16b_kernel") if t16b else "gcn_fwd_split_kernel"
+        traffic, mfma_busy, src = pmc("pmc_bench_pems.json", pkey) if N == 325 else (None,) * 3
         return {"kernel": kname,
                 "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
@@ -347,7 +350,8 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
     traffic, mfma_busy, src = pmc("pmc_bench_metr.json", "gcn_fwd_t16_kernel") if t16 and N == 207 else (None,) * 3
     if fused:
         kname = (("gcn_fwd_t16_kernel<1024> (fused diffusion GCN forward, power schedule, persistent 16-node "
-                  "tile waves: one workgroup per CU over an equal tile range" if t16 else
+                  "tile waves: one workgroup per CU over an equal tile range; the layer's gated TCN and the "
+                  "layer below's BatchNorm finalize in its staging where >= a slice per CU" if t16 else
                   "gcn_fwd_pow_kernel<512> (fused diffusion GCN forward, power schedule")
                  + ", 8 launches/step)" if ex._pow_ok(1) else "gcn_fwd_fused_kernel<512, true> (fused diffusion GCN forward, chained hops, "
                                        "8 launches/step)")
