@@ -698,8 +698,12 @@ def test_gcn_fused_schedules_agree(gpu, n, monkeypatch):
 
 
 @pytest.mark.parametrize("bn", [False, True])
-@pytest.mark.parametrize("n,B,t_out,d", [(207, 32, 8, 2), (37, 64, 5, 1), (207, 8, 3, 1)])
-def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn):
+@pytest.mark.parametrize("n,B,t_out,d,planes", [(207, 32, 8, 2, 0), (37, 64, 5, 1, 0), (207, 8, 3, 1, 0),
+                                                (325, 32, 8, 1, 2)])
+# (planes 2: the bf16-mlp pair forward, where the TCN stays a separate launch -- fused there it was
+#  7.5 % slower per PEMS step, profiles/r05/tcn_fused -- so both sides of the comparison are the
+#  two-launch path and must agree bitwise)
+def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn, planes):
     """gwn_gcn_args.tcn: the gated TCN (model.py:206-212) computed inside the f32 16-node tile
     forward's staging (>= a slice per CU) against the same layer as two calls (gwn_gated_tcn_fwd,
     then gwn_gcn_fwd): xg (piece 0 of h), the (tanh, sigmoid) pairs, the skip rows, the hop pieces,
@@ -709,7 +713,8 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn):
     train mode): plain, its BatchNorm applied on load (x_mean, folded weights); with bn, that
     BatchNorm finalized by the TCN itself from [nparts][3][c] partials (gwn_tcn_args.bn: in every
     workgroup of the fused launch, or gwn_batchnorm_fwd_fold first): its outputs (mean, rstd,
-    scale, running statistics, num_batches_tracked, w_fold, b_fold) against fp64 as well."""
+    scale, running statistics, num_batches_tracked, w_fold, b_fold) against fp64 as well.  planes 2:
+    the bf16-mlp pair forward (configs[2]), which takes the TCN as its own launch."""
     import ctypes
     from gwn_amd import _lib
     lib = _lib.load()
@@ -732,6 +737,15 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn):
     arr2 = (ctypes.c_void_p * K)(*[q[0].data_ptr() for q in sq])
     g4f, _ = _g4s(gpu, n, sups, sq, supT)
     PP = ctypes.POINTER(ctypes.c_void_p)
+    extra = dict(sup_g4=g4f[1])
+    if planes:
+        el = lib.gwn_support_g4_bf16_elems(n)
+        mats = [m for s_, q in zip(sups, sq) for m in (s_, q[0])]
+        g4bf = torch.zeros(len(mats), el // 2, device=gpu)
+        srcb = (ctypes.c_void_p * len(mats))(*[m.data_ptr() for m in mats])
+        _lib.call("gwn_support_g4_bf16", ctypes.cast(srcb, PP), len(mats), n, NP, g4bf.data_ptr(), el, _lib.stream())
+        arrb = (ctypes.c_void_p * len(mats))(*[g4bf[i].data_ptr() for i in range(len(mats))])
+        extra = dict(split_planes=planes, sup_g4b=ctypes.cast(arrb, PP))
     x = torch.randn(t_in * P, C, device=gpu) * 2 + 3 + torch.randn(C, device=gpu)
     xmean = torch.randn(C, device=gpu) + 3
     wfg = torch.randn(2 * C, 2 * C, device=gpu) * 0.15
@@ -783,7 +797,7 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn):
         ga = _lib.GcnArgs(rows=rows, n=n, c=C, nsup=K, sup=ctypes.cast(arr, PP), ld_sup=NP, h=h.data_ptr(), ld_h=W,
                           w_mlp=wm.data_ptr(), b_mlp=bm.data_ptr(), residual=x.data_ptr() + 4 * d * P * C,
                           z=z.data_ptr(), seed_ptr=seed.data_ptr(), salt=0, drop_p=0.0, bn_partials=bnp.data_ptr(),
-                          sup2=ctypes.cast(arr2, PP), w_mlp_t=wmt.data_ptr(), sup_g4=g4f[1], **res_aff)
+                          sup2=ctypes.cast(arr2, PP), w_mlp_t=wmt.data_ptr(), **extra, **res_aff)
         if fused:
             ga.tcn = ctypes.pointer(ta)
         else:
@@ -793,7 +807,7 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn):
         outs[fused] = (h, fg, skip[:, :C], z, _bn_all(bnp, rows, n, C, K, NP)) + (
             tuple(bo[k] for k in ("mean", "rstd", "scale", "rm", "rv", "nbt", "wf", "bf")) if bn else ())
     (h0, fg0, sk0, z0, st0), (h1, fg1, sk1, z1, st1) = outs[False][:5], outs[True][:5]
-    if S < _cus():
+    if S < _cus() or planes:
         for a_, b_ in zip(outs[False], outs[True]):
             assert torch.equal(a_, b_)
         return
@@ -825,11 +839,12 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn):
     assert rel_err(h1[:, :C].cpu().numpy(), h0[:, :C].cpu().numpy()) <= 5e-6
     assert rel_err(fg1.cpu().numpy(), fg0.cpu().numpy()) <= 5e-6
     assert torch.equal(sk1, h1[skip_row0:, :C])
-    assert rel_err(h1.cpu().numpy(), h0.cpu().numpy()) <= 5e-6
-    assert rel_err(z1.cpu().numpy(), z0.cpu().numpy()) <= 5e-6
+    floor = 5e-6 if not planes else 1e-2  # (bf16: a tie rounded the other way moves a piece by 1 ulp)
+    assert rel_err(h1.cpu().numpy(), h0.cpu().numpy()) <= max(floor, 5e-6)
+    assert rel_err(z1.cpu().numpy(), z0.cpu().numpy()) <= floor
     assert torch.equal(st1[:, 0], st0[:, 0])
-    assert rel_err(st1[:, 1].numpy(), st0[:, 1].numpy()) <= 1e-5
-    assert rel_err(st1[:, 2].numpy(), st0[:, 2].numpy()) <= 1e-5
+    assert rel_err(st1[:, 1].numpy(), st0[:, 1].numpy()) <= max(floor, 1e-5)
+    assert rel_err(st1[:, 2].numpy(), st0[:, 2].numpy()) <= max(floor, 1e-5)
 
 
 def _cus():
