@@ -138,6 +138,9 @@ def main():
     planes = ex.split_planes()
     bf16 = planes > 0
     ex.seed.fill_(12345 + 7919 * rank)
+    # the dominant kernel's own clock stamps (measure_dominant), captured into the step's graphs
+    # with the rest of the step: two stores per workgroup and launch
+    ex.launch_clock = True
 
     nb = 8 if N <= 512 else 2  # distinct resident batches, cycled
     xs, ys = [], []
@@ -157,6 +160,9 @@ def main():
 
     for i in range(args.warmup):
         eng.train(xs[i % nb], ys[i % nb])
+    clocks = [a for k, a in eng._acts.items() if k[2]]
+    for ck in (getattr(clocks[0], "CLK", {}) if clocks else {}).values():
+        ck.zero_()  # (a kernel path that stamps nothing leaves zeros)
     barrier()
     t0 = time.perf_counter()
     last = None
@@ -186,7 +192,7 @@ def main():
     mae12 = float(np.mean(maes))
     mae12_ref = oracle_mae12(eng, sups_np, xt, yt, N, T) if rank == 0 else None
 
-    roof = measure_dominant(eng, dev, bf16=bf16)
+    roof = measure_dominant(eng, dev, bf16=bf16, steps=args.steps)
     result = None
     if rank == 0:
         result = {
@@ -235,42 +241,11 @@ def rank_timing(elapsed, world, rank, dev):
                            "rank_seconds_min": round(min(per_rank), 6), "rank_seconds_max": round(max(per_rank), 6)}
 
 
-def measure_dominant(eng, dev, rounds=5, bf16=False):
-    """The dominant kernel is the diffusion graph convolution forward (gwn_gcn_fwd: 3 supports x 2
-    hops of 'ncvl,vw->ncwl' + the 224->32 mlp + residual + dropout + BN partials, one call per
-    layer, 8 per step; for N <= 512 ONE fused launch, gcn_fwd_t16_kernel; the BN finalize + fold
-    its bn_fold argument issues after it is left out of the replay).  Replay
-    exactly the last training step's 8 calls (same arguments and buffers; the replay is
-    idempotent) as one captured HIP graph between HIP events on the launch stream; achieved =
-    algorithmic FLOP / time,
-    where the algorithmic FLOP of a call = slices * (K*order*2*C*N^2 + 2*(2K+1)*C*C*N) (SURVEY.md
-    Appendix A), plus slices * N * 2*(2C)^2 when the call carries the layer's gated TCN."""
+def replay_ms(launches, rounds):
+    """The launches captured in one HIP graph (no host launch overhead between kernels) and
+    replayed `rounds` times between one HIP event pair on the launch stream (ms)."""
     import ctypes
     from gwn_amd import _lib
-    ex = eng.model._executor
-    acts = [a for k, a in eng._acts.items() if k[2]][0]
-    cfg = ex.cfg
-    C, N, K = cfg.C, cfg.N, cfg.nsup
-    # the gcn launches alone: the step's BN finalize that gwn_gcn_fwd issues after each (bn_fold,
-    # a separate ~8 us launch) is not part of this kernel (copies: the step's own args stay intact)
-    launches = []
-    for i in sorted(acts.gcn_args):
-        ga = type(acts.gcn_args[i]).from_buffer_copy(acts.gcn_args[i])
-        ga.bn_fold = None
-        if ga.tcn and ga.tcn.contents.bn:
-            # the fused TCN's BatchNorm finalize stays in (it is this launch's work) but without
-            # the running statistics / num_batches_tracked updates: the replay leaves the model as is
-            ta = type(ga.tcn.contents).from_buffer_copy(ga.tcn.contents)
-            bfp = _lib.BnFold.from_buffer_copy(_lib.BnFold.from_address(ta.bn))
-            bfp.running_mean = bfp.running_var = bfp.num_batches_tracked = None
-            ta.bn = ctypes.addressof(bfp)
-            ta._bn_keep = bfp
-            ga.tcn = ctypes.pointer(ta)
-        launches.append(ga)
-    # the 8 launches captured in one HIP graph (as the training step replays them: no host launch
-    # overhead between kernels) and replayed `rounds` times between one event pair on the stream;
-    # per-launch events had added ~10 us of event overhead, and host-issued launches ~12 us of
-    # Python/ctypes issue time, to each ~80-90 us kernel
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -283,13 +258,84 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
             _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    total_ms, total_flop, total_bytes, count = 0.0, 0.0, 0.0, 0
     e0.record()
     for _ in range(rounds):
         graph.replay()
     e1.record()
     torch.cuda.synchronize()
-    total_ms = e0.elapsed_time(e1)
+    return e0.elapsed_time(e1)
+
+
+def clock_spans(acts):
+    """Durations (us) of the last timed step's gcn forward launches from the kernels' own device
+    clock stamps (gwn_gcn_args.clock: every workgroup's start and end on the device wall clock;
+    each launch overwrites the previous step's): launch i lasts max(end) - min(start) over its
+    workgroups.  None where a layer's kernel path stamps nothing (only the 16-node tile forward
+    kernels do)."""
+    from gwn_amd import _lib
+    khz = _lib.load().gwn_wall_clock_khz()
+    ck = getattr(acts, "CLK", {})
+    if khz <= 0 or not ck or sorted(ck) != sorted(acts.gcn_args):
+        return None
+    spans = []
+    for i in sorted(ck):
+        c = ck[i].cpu().numpy().reshape(-1, 2)
+        g = int((c[:, 1] > 0).sum())  # the launch's workgroups, slots [0, g)
+        if g == 0 or (c[:g] <= 0).any() or (c[g:] != 0).any():
+            return None
+        spans.append(float(c[:g, 1].max() - c[:g, 0].min()) * 1000.0 / khz)
+    return spans if min(spans) > 0 else None
+
+
+def measure_dominant(eng, dev, rounds=5, bf16=False, steps=None):
+    """The dominant kernel is the diffusion graph convolution forward (gwn_gcn_fwd: 3 supports x 2
+    hops of 'ncvl,vw->ncwl' + the 224->32 mlp + residual + dropout + BN partials, one call per
+    layer, 8 per step; for N <= 512 ONE fused launch, gcn_fwd_t16_kernel).  Timing: the kernel's
+    own device clock stamps in the last timed step's launches (clock_spans: the training step as
+    timed, no replay); where the kernel records none, exactly the last training step's 8 calls
+    (same arguments and buffers; idempotent) replayed as one captured HIP graph between HIP events
+    on the launch stream.  Either way only the gcn kernel: the BN finalize + fold its bn_fold
+    argument issues after it, and the TCN it issues before it where it does not fuse it, are left
+    out.  achieved = algorithmic FLOP / time, where the algorithmic FLOP of a call = slices *
+    (K*order*2*C*N^2 + 2*(2K+1)*C*C*N), plus slices * N * 2*(2C)^2 when the
+    kernel runs the layer's gated TCN itself (gwn_gcn_tcn_fused; where it does not -- bf16, or
+    fewer slices than CUs -- the TCN is its own rowgemm launch)."""
+    import ctypes
+    from gwn_amd import _lib
+    ex = eng.model._executor
+    acts = [a for k, a in eng._acts.items() if k[2]][0]
+    cfg = ex.cfg
+    C, N, K = cfg.C, cfg.N, cfg.nsup
+    # the gcn launches alone (copies: the step's own args stay intact)
+    launches = []
+    for i in sorted(acts.gcn_args):
+        ga = type(acts.gcn_args[i]).from_buffer_copy(acts.gcn_args[i])
+        ga.bn_fold = None
+        ga.clock = None
+        if ga.tcn and not _lib.load().gwn_gcn_tcn_fused(ctypes.byref(ga)):
+            ga.tcn = None  # its TCN (and BN finalize) run as launches of their own: not this kernel's work
+        if ga.tcn and ga.tcn.contents.bn:
+            # the fused TCN's BatchNorm finalize stays in (it is this launch's work) but without
+            # the running statistics / num_batches_tracked updates: the replay leaves the model as is
+            ta = type(ga.tcn.contents).from_buffer_copy(ga.tcn.contents)
+            bfp = _lib.BnFold.from_buffer_copy(_lib.BnFold.from_address(ta.bn))
+            bfp.running_mean = bfp.running_var = bfp.num_batches_tracked = None
+            ta.bn = ctypes.addressof(bfp)
+            ta._bn_keep = bfp
+            ga.tcn = ctypes.pointer(ta)
+        launches.append(ga)
+    spans = clock_spans(acts) if steps else None
+    if spans is not None:
+        timing = ("device wall-clock stamps of every workgroup (start, end) in the last timed step's %d "
+                  "launches, inside the step's graphs" % len(launches))
+        total_ms = sum(spans) / 1000.0
+        rounds = 1
+        timing = {"method": timing, "launch_us": [round(x, 2) for x in spans]}
+    else:
+        timing = "captured-graph replay of the last step's %d launches x %d, HIP events" % (len(launches), rounds)
+        total_ms = replay_ms(launches, rounds)
+        timing = {"method": timing}
+    total_flop, total_bytes, count = 0.0, 0.0, 0
     for _ in range(rounds):
         for ga in launches:
             slices = ga.rows // N
@@ -324,6 +370,20 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
                     return rec.get("hbm_bytes_per_dispatch"), rec.get("mfma_busy_frac"), "profiles/%s/%s" % (rnd, name)
         return None, None, None
 
+    def rocprof_avg(name, key):
+        # the same kernel's average dispatch duration in the committed rocprofv3 --kernel-trace --stats
+        # run of this bench (tools/gpu.sh stats:<cfg>): its packet timestamps also hold the dispatch
+        # before the first workgroup and the end-of-kernel release after the last
+        import csv
+        for rnd in ("r05/final", "r04", "r03"):
+            path = os.path.join(ROOT, "profiles", rnd, name)
+            if os.path.exists(path):
+                with open(path) as f:
+                    for r in csv.DictReader(f):
+                        if key + "<" in r["Name"]:
+                            return round(float(r["AverageNs"]) / 1000.0, 3), "profiles/%s/%s" % (rnd, name)
+        return None, None
+
     if bf16:
         # bf16 operands: arithmetic intensity (~80 FLOP/B algorithmic) sits far below the bf16
         # ridge (2.5 PF / 8 TB/s = 312 FLOP/B): the kernel is bounded by HBM, priced in bytes
@@ -339,15 +399,20 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
              % ((N + 31) // 32, (N + 31) // 32))
         pkey = ("gcn_fwd_t16b2_kernel" if mlpb else "gcn_fwd_t16b_kernel") if t16b else "gcn_fwd_split_kernel"
         traffic, mfma_busy, src = pmc("pmc_bench_pems.json", pkey) if N == 325 else (None,) * 3
+        timing["rocprof_avg_us"], timing["rocprof_source"] = (rocprof_avg("pems_kernel_stats.csv", pkey)
+                                                              if N == 325 else (None, None))
         return {"kernel": kname,
                 "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
                 "pmc_mfma_busy_frac": mfma_busy,
                 "mfma_tflops": round(achieved, 3), "mfma_peak_bf16": BF16_PEAK_TFLOPS,
                 "avg_launch_us": round(avg_us, 3), "flop_per_launch_avg": round(total_flop / count, 1),
-                "algorithmic_bytes_per_launch": round(total_bytes / count), "launches_timed": count}
+                "algorithmic_bytes_per_launch": round(total_bytes / count), "launches_timed": count,
+                "timing": timing}
     t16 = fused and ex._pow_ok(1) and os.environ.get("GWN_GCN_T16", "1") != "0"
     traffic, mfma_busy, src = pmc("pmc_bench_metr.json", "gcn_fwd_t16_kernel") if t16 and N == 207 else (None,) * 3
+    timing["rocprof_avg_us"], timing["rocprof_source"] = (rocprof_avg("metr_kernel_stats.csv", "gcn_fwd_t16_kernel")
+                                                          if t16 and N == 207 else (None, None))
     if fused:
         kname = (("gcn_fwd_t16_kernel<1024> (fused diffusion GCN forward, power schedule, persistent 16-node "
                   "tile waves: one workgroup per CU over an equal tile range; the layer's gated TCN and the "
@@ -364,7 +429,7 @@ def measure_dominant(eng, dev, rounds=5, bf16=False):
             "pmc_mfma_busy_frac": mfma_busy,
             "avg_launch_us": round(avg_us, 3), "flop_per_launch_avg": round(total_flop / count, 1),
             "algorithmic_bytes_per_launch": round(total_bytes / count),
-            "launches_timed": count}
+            "launches_timed": count, "timing": timing}
 
 
 def oracle_mae12(eng, sups_np, xt, yt, N, T):

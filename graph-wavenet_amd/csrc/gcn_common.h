@@ -48,6 +48,7 @@ struct FusedFwd {
       float* save_mean; float* save_rstd; float* scale; float* w_fold; float* b_fold; long long* nbt;
     } bn;
   } tcn;
+  unsigned long long* clk;  // gwn_gcn_args.clock (NULL: off)
 };
 
 struct FusedBwd {

@@ -294,6 +294,18 @@ __device__ __forceinline__ void t16_bn_flush(const FusedFwd& a, const BnRun& bn,
     if (threadIdx.x < 3 * CH) a.bn_part[slot * 3 * CH + threadIdx.x] = 0.0f;
 }
 
+// gwn_gcn_args.clock: the workgroup's (start, end) device wall clock into slot blockIdx.x, each a
+// plain store (no atomic, no load: nothing waits on memory and nothing is held in registers across
+// the kernel); every launch overwrites the call site's slots
+__device__ __forceinline__ void t16_clock_start(const FusedFwd& a) {
+  if (a.clk != nullptr && threadIdx.x == 0) a.clk[2 * blockIdx.x] = wall_clock64();
+}
+__device__ __forceinline__ void t16_clock_end(const FusedFwd& a) {
+  if (a.clk == nullptr) return;
+  __syncthreads();
+  if (threadIdx.x == 0) a.clk[2 * blockIdx.x + 1] = wall_clock64();
+}
+
 // the channel map of one piece held in accumulators acc[hf] (register s = input channel
 // 16 hf + 4 g + s): hacc[oh] (output channel 16 oh + 4 g + r) += M x piece with the A operand
 // M[out][in] read as m[in * ld_m + out] (t16_stage_maps: forward the piece's block of W, backward
@@ -726,6 +738,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   const T16Range rg = t16_range(a.slices, nt);
   BnRun bn;
   bn_init(bn, wpart);
+  t16_clock_start(a);
   // the phase's slices staged in one pass (stage_rows4; the channel maps inside its first round
   // trip), else slice by slice; with the fused TCN computed from its inputs (the TCN weights in
   // the BN partials' region until the final flush)
@@ -797,6 +810,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
     p0 = p1;
   }
   t16_bn_flush(a, bn, wpart);
+  t16_clock_end(a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -957,6 +971,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
   const T16Range rg = t16_range(a.slices, nt);
   BnRun bn;
   bn_init(bn, wpart);
+  t16_clock_start(a);
   const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
   // the channel maps: f32 for t16_mlp, or bf16 MFMA operands for t16_mlp_b (MLPB)
   auto stage_maps = [&] {
@@ -1055,6 +1070,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
     p0 = p1;
   }
   t16_bn_flush(a, bn, wpart);
+  t16_clock_end(a);
 }
 
 // Two slices per wave in the bf16-mlp forward (the same node column of slices 2q and 2q + 1): at
@@ -1127,6 +1143,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b2_kernel(const FusedFwd a, c
   const T16Range rg = t16_range(pairs, nt);
   BnRun bn;
   bn_init(bn, wpart);
+  t16_clock_start(a);
   for (long p0 = rg.tb; p0 < rg.te;) {
     const int q0 = (int)(p0 / nt);
     const long p1 = min(rg.te, (long)(q0 + maximg / 2) * nt);
@@ -1196,6 +1213,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b2_kernel(const FusedFwd a, c
     p0 = p1;
   }
   t16_bn_flush(a, bn, wpart);
+  t16_clock_end(a);
 }
 
 // Backward on 16-node tiles: the forward's structure with the dh image (BN-backward prologue),
@@ -1545,6 +1563,13 @@ static bool t16_enabled() {
   return !(e && e[0] == '0');
 }
 
+extern "C" int gwn_wall_clock_khz(void) {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess)
+    return 0;
+  return khz;
+}
+
 int gwn_device_cus() {
   static int v = [] {
     int dev = 0, cus = 0;
@@ -1621,6 +1646,8 @@ bool gwn_gcn_tcn_fusable(const gwn_gcn_args* g) {
                      (!g->residual_mean || (g->residual_mean == t->bn->save_mean && g->residual_scale == t->bn->scale))));
 }
 
+extern "C" int gwn_gcn_tcn_fused(const gwn_gcn_args* a) { return a && a->tcn && gwn_gcn_tcn_fusable(a) ? 1 : 0; }
+
 int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
   const int nwt = (g->n + 31) / 32;
   GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_fwd (fused): supports must be padded to 32*ceil(n/32)");
@@ -1642,6 +1669,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
   a.xg4 = g->xg4; a.xg4_k = g->xg4_support;
   a.pb = g->pieces_bf16; a.ld_pb = g->ld_pb;
   a.tcn = {};
+  a.clk = g->clock;
   GWN_REQUIRE(g->ksplit == 0 || g->ksplit == 1 || g->ksplit == g->nsup, "gcn_fwd: ksplit must be 0, 1 or nsup");
   GWN_REQUIRE(!a.res_scale == !a.res_shift && !a.res_scale == !a.res_mean,
               "gcn_fwd (fused): residual_mean, residual_scale and residual_shift go together");

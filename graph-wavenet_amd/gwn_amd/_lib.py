@@ -107,6 +107,7 @@ class GcnArgs(ctypes.Structure):
         ("pieces_bf16", c_void_p), ("ld_pb", c_long),
         ("bn_fold", ctypes.POINTER(BnFold)),
         ("tcn", ctypes.POINTER(TcnArgs)),
+        ("clock", c_void_p),
     ]
 
 
@@ -200,6 +201,8 @@ _SIGS = [
     ("gwn_nconv2_adj_grad", c_int, [c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                     c_long, c_int, c_void_p]),
     ("gwn_gcn_fwd", c_int, [ctypes.POINTER(GcnArgs), c_void_p]),
+    ("gwn_gcn_tcn_fused", c_int, [ctypes.POINTER(GcnArgs)]),
+    ("gwn_wall_clock_khz", c_int, []),
     ("gwn_gcn_bn_partial_count", c_long, [c_int, c_int, c_int, c_int, c_int]),
     ("gwn_gcn_t16b_supported", c_int, [c_int, c_int]),
     ("gwn_gcn_bwd", c_int, [ctypes.POINTER(GcnBwdArgs), c_void_p]),

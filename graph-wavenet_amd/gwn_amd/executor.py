@@ -297,6 +297,9 @@ class Executor:
         self.compute_dtype = getattr(model, "compute_dtype", "fp32")
         self.device = None
         self._scratch = {}
+        # instrumentation (bench.py): the training gcn forward launches store their workgroups' device
+        # clock stamps (gwn_gcn_args.clock, per layer in acts.CLK)
+        self.launch_clock = False
 
     # ---------------------------------------------------------------------------------------
     def bind(self, device):
@@ -593,7 +596,7 @@ class Executor:
                    and _lib.load().gwn_gcn_t16b_supported(N, cfg.nsup) == 1)
         acts.gram_g4 = gram_g4
         if getattr(acts, "XG4", None) is None:
-            acts.XG4, acts.TG4 = {}, {}
+            acts.XG4, acts.TG4, acts.CLK = {}, {}, {}
         # bf16 mode: every layer's adaptive-support gram in one gwn_gram_g4_group launch at the end
         # of the backward (GWN_GRAM_GROUP=0: one gwn_gram_g4_bf16 per layer)
         if gram_g4 and L >= 2 and getattr(acts, "ws_g4g", None) is None and os.environ.get("GWN_GRAM_GROUP", "1") != "0":
@@ -668,6 +671,11 @@ class Executor:
             # the gated TCN rides on the gcn call (gwn_gcn_args.tcn: inside the f32 tile kernel's
             # staging where it runs, else its own launch issued by gwn_gcn_fwd)
             ga.tcn = ctypes.pointer(ta)
+            if training and self.launch_clock:
+                if acts.CLK.get(i) is None:
+                    cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+                    acts.CLK[i] = torch.zeros(2 * cus, device=self.device, dtype=torch.int64)
+                ga.clock = ptr(acts.CLK[i])
             rm, rv, mom, eps, nbt = bn_bufs[i]
             if fold and i == L - 1:
                 # the last BatchNorm (its output dead but for the running statistics): finalized by
@@ -678,9 +686,9 @@ class Executor:
                                  scale=acts.bn_scale[i].data_ptr(), num_batches_tracked=ptr(nbt))
                 ga.bn_fold = ctypes.pointer(bf)
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
-            acts.gcn_args[i] = ga  # kept for bench.py's per-kernel replay timing
+            acts.gcn_args[i] = ga  # kept for bench.py's per-kernel timing
             if fold:
-                pass  # done by the gcn launch
+                pass  # the BatchNorm finalize rides on the next TCN / this gcn call
             elif training:
                 lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnparts[i % 2]), self._bn_parts(rows),
                          ptr(self.pk("bn_g%d" % i)), ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps,

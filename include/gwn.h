@@ -343,6 +343,11 @@ typedef struct gwn_gcn_args {
    * from x, and xg, fg and the skip rows are written from there -- otherwise it is issued as its own
    * launch first.  The caller then does not call gwn_gated_tcn_fwd. */
   const struct gwn_tcn_args* tcn;
+  /* clock (optional, instrumentation): the 16-node tile forward kernels store each workgroup's
+   * device wall clock (gwn_wall_clock_khz ticks) at its start and end, clock[2*wg] and
+   * clock[2*wg + 1] (wg < CUs: one workgroup per CU); each launch overwrites the previous one's.
+   * Other forward paths write nothing (the caller zeroes it first to tell). */
+  unsigned long long* clock;
 } gwn_gcn_args;
 /* gwn_batchnorm_fwd_fold's arguments (same meaning) for gwn_gcn_args.bn_fold */
 typedef struct gwn_bn_fold {
@@ -358,6 +363,11 @@ typedef struct gwn_bn_fold {
  * must be [np][ld_sup] and ZERO outside [n][n] (gwn_pad_square makes such copies).
  * Otherwise: 2K nconv GEMMs + one mlp GEMM. */
 int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t stream);
+/* 1 iff gwn_gcn_fwd runs a->tcn (and its BatchNorm finalize, tcn->bn) inside its own kernel, 0 when
+ * it issues them as separate launches first (or a->tcn is NULL) */
+int gwn_gcn_tcn_fused(const gwn_gcn_args* a);
+/* the device wall clock's rate (kHz) that gwn_gcn_args.clock counts in */
+int gwn_wall_clock_khz(void);
 /* number of BatchNorm partial slots gwn_gcn_fwd writes to bn_partials ([slots][3][c]):
  * max(rows/n, CUs of the device).  Every path writes all of them (slots that hold no rows get
  * count 0): the whole-slice kernels one per slice, the persistent 16-node tile kernels one per

@@ -714,7 +714,8 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn, planes):
     BatchNorm finalized by the TCN itself from [nparts][3][c] partials (gwn_tcn_args.bn: in every
     workgroup of the fused launch, or gwn_batchnorm_fwd_fold first): its outputs (mean, rstd,
     scale, running statistics, num_batches_tracked, w_fold, b_fold) against fp64 as well.  planes 2:
-    the bf16-mlp pair forward (configs[2]), which takes the TCN as its own launch."""
+    the bf16-mlp pair forward (configs[2]), which takes the TCN as its own launch.  The fused call
+    also carries gwn_gcn_args.clock (bench.py's timing): every workgroup's (start, end) stamped."""
     import ctypes
     from gwn_amd import _lib
     lib = _lib.load()
@@ -800,6 +801,8 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn, planes):
                           sup2=ctypes.cast(arr2, PP), w_mlp_t=wmt.data_ptr(), **extra, **res_aff)
         if fused:
             ga.tcn = ctypes.pointer(ta)
+            clk = torch.zeros(2 * _cus(), device=gpu, dtype=torch.int64)
+            ga.clock = clk.data_ptr()  # the instrumentation rides along (results compared as ever)
         else:
             _lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), _lib.stream())
         _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
@@ -807,6 +810,13 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn, planes):
         outs[fused] = (h, fg, skip[:, :C], z, _bn_all(bnp, rows, n, C, K, NP)) + (
             tuple(bo[k] for k in ("mean", "rstd", "scale", "rm", "rv", "nbt", "wf", "bf")) if bn else ())
     (h0, fg0, sk0, z0, st0), (h1, fg1, sk1, z1, st1) = outs[False][:5], outs[True][:5]
+    # gwn_gcn_args.clock: every workgroup of the tile launch stamped (start, end), slots [0, grid)
+    c = clk.cpu().reshape(-1, 2)
+    g = int((c[:, 1] > 0).sum())
+    assert 0 < g <= _cus() and bool((c[:g] > 0).all()) and bool((c[g:] == 0).all())
+    assert bool((c[:g, 1] >= c[:g, 0]).all())
+    span_ms = float(c[:g, 1].max() - c[:g, 0].min()) / lib.gwn_wall_clock_khz()
+    assert 0 < span_ms < 1000
     if S < _cus() or planes:
         for a_, b_ in zip(outs[False], outs[True]):
             assert torch.equal(a_, b_)
