@@ -181,6 +181,8 @@ _SIGS = [
     ("gwn_gemm", c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     ("gwn_gemm_nt", c_int, [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int,
                             c_void_p, c_int, c_void_p, c_long, c_void_p]),
+    ("gwn_gemm_nt_bf16", c_int, [c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_int,
+                                 c_void_p, c_int, c_void_p, c_long, c_void_p]),
     ("gwn_gemm_workspace_floats", c_long, [c_int, c_int, c_int]),
     ("gwn_nconv", c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,
                           c_int, c_int, c_int, c_void_p]),
@@ -216,6 +218,8 @@ _SIGS = [
     ("gwn_wgrad_partials", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_long, c_int, c_int, c_long, c_int,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gwn_reduce_partials", c_int, [ctypes.POINTER(ReduceSeg), c_int, c_void_p]),
+    ("gwn_wgrad_bf16_partial_count", c_int, [c_int, c_int, c_int]),
+    ("gwn_wgrad_bf16_partials", c_int, [c_void_p, c_long, c_int, c_void_p, c_long, c_int, c_int, c_void_p, c_void_p]),
     ("gwn_wgrad_group_supported", c_int, [c_int, c_int, c_int]),
     ("gwn_gram_group_workspace_floats", c_long, [c_int, ctypes.POINTER(c_int), c_int]),
     ("gwn_gram_group", c_int, [ctypes.POINTER(GramLayer), c_int, c_long, c_long, c_int, c_void_p, c_int, c_int,

@@ -847,10 +847,11 @@ class Executor:
         L, C = cfg.L, cfg.D  # the skip convs read the gated (dilation-channel) outputs
         acts = _HeadBufs(skipcat, skr, e1, y)
         if self._head_nt():
+            hb = self.head_bf16()
             gemm_nt(acts.skipcat, L * C, self.pk("skip_w"), L * C, acts.skr, cfg.S, rows_f, cfg.S, L * C,
-                    bias=self.pk("skip_bsum"), relu=1)
+                    bias=self.pk("skip_bsum"), relu=1, bf16=hb)
             gemm_nt(acts.skr, cfg.S, self.pk("e1_w"), cfg.S, acts.e1, cfg.E, rows_f, cfg.E, cfg.S,
-                    bias=self.pk("e1_b"), relu=1)
+                    bias=self.pk("e1_b"), relu=1, bf16=hb)
             gemm_nt(acts.e1, cfg.E, self.pk("e2_w"), cfg.E, acts.y, cfg.O, rows_f, cfg.O, cfg.E,
                     bias=self.pk("e2_b"))
         else:
@@ -1067,6 +1068,24 @@ class Executor:
                 wgrad(dY, J, X, Kc, rows_f, w, sc["ws_side"], b, ldy=ldy)
 
         nt = self._head_nt()
+        hb = nt and self.head_bf16()
+
+        def head_wgrad_bf16(dY, J, X, Kc, w, b, key, now=False):
+            # the bf16 mode: partials on bf16 operands (gwn_wgrad_bf16_partials), reduced with the
+            # deferred ones at the end of the backward, else (or now: end_conv_1, final at the head
+            # stage's yield, early_grad_range) right away
+            n = _lib.load().gwn_wgrad_bf16_partial_count(rows_f, J, Kc)
+            part = sc.get(key)
+            if part is None or part.numel() < n * (J * Kc + J):
+                part = sc[key] = torch.empty(n * (J * Kc + J), device=self.device, dtype=F32)
+            lib.call("gwn_wgrad_bf16_partials", ptr(dY), J, J, ptr(X), Kc, Kc, rows_f, ptr(part), st)
+            seg = _lib.ReduceSeg(part=ptr(part), nparts=n, part_stride=J * Kc + J, J=J, Kc=Kc, out=ptr(w), ld_out=Kc,
+                                 out2=ptr(b), db_off=J * Kc)
+            if defer and not now:
+                segs.append(seg)
+            else:
+                lib.call("gwn_reduce_partials", (_lib.ReduceSeg * 1)(seg), 1, st)
+
         # end_conv_2: its weight gradient from the 32-column padded output gradient on the row
         # reduction kernel (deferred), else the split-K GEMM
         if defer and "part_e2g" in sc:  # one-problem gwn_wgrad_group (4 column groups per workgroup)
@@ -1091,16 +1110,22 @@ class Executor:
             gemm(sc["dy"], OP, 1, self.pk("e2_w"), E, 1, sc["de1"], E, 1, M=rows_f, N=E, K=O,
                  epi=2, mask=acts.e1, ldmask=E)
         # end_conv_1
-        head_wgrad(sc["de1"], E, acts.skr, S, self.gk("e1_w"), self.gk("e1_b"))
+        if hb:
+            head_wgrad_bf16(sc["de1"], E, acts.skr, S, self.gk("e1_w"), self.gk("e1_b"), "part_hb_e1", now=True)
+        else:
+            head_wgrad(sc["de1"], E, acts.skr, S, self.gk("e1_w"), self.gk("e1_b"))
         if nt:
-            gemm_nt(sc["de1"], E, self.pk("e1_wT"), E, sc["dsk"], S, rows_f, S, E, mask=acts.skr, ldmask=S)
+            gemm_nt(sc["de1"], E, self.pk("e1_wT"), E, sc["dsk"], S, rows_f, S, E, mask=acts.skr, ldmask=S, bf16=hb)
         else:
             gemm(sc["de1"], E, 1, self.pk("e1_w"), S, 1, sc["dsk"], S, 1, M=rows_f, N=S, K=E,
                  epi=2, mask=acts.skr, ldmask=S)
         # skip convs
-        head_wgrad(sc["dsk"], S, acts.skipcat, L * D, self.gk("skip_w"), self.gk("skip_bsum"))
+        if hb:
+            head_wgrad_bf16(sc["dsk"], S, acts.skipcat, L * D, self.gk("skip_w"), self.gk("skip_bsum"), "part_hb_skip")
+        else:
+            head_wgrad(sc["dsk"], S, acts.skipcat, L * D, self.gk("skip_w"), self.gk("skip_bsum"))
         if nt:
-            gemm_nt(sc["dsk"], S, self.pk("skip_wT"), S, sc["dskipcat"], L * D, rows_f, L * D, S)
+            gemm_nt(sc["dsk"], S, self.pk("skip_wT"), S, sc["dskipcat"], L * D, rows_f, L * D, S, bf16=hb)
         else:
             gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * D, 1, sc["dskipcat"], L * D, 1, M=rows_f, N=L * D, K=S)
         yield "head"
@@ -1269,6 +1294,15 @@ class Executor:
         cfg = self.cfg
         return (os.environ.get("GWN_HEAD_NT", "1") != "0"
                 and all(v % 4 == 0 for v in (cfg.O, cfg.S, cfg.E, cfg.L * cfg.D)))
+
+    def head_bf16(self):
+        """The bf16 mode's head (split_planes 2, configs[2]): the skip convs' and end_conv_1's GEMMs,
+        their input gradients (gwn_gemm_nt_bf16) and weight gradients (gwn_wgrad_bf16_partials) on
+        bf16 operands, fp32 in and out, fp32 sums; end_conv_2 (12 outputs) and the bias gradients
+        stay fp32."""
+        cfg = self.cfg
+        return (self._head_nt() and self.split_planes() == 2 and cfg.S % 128 == 0 and cfg.E % 128 == 0
+                and (cfg.L * cfg.D) % 128 == 0)
 
     def _fuse_ok(self, acts):
         cfg = self.cfg
@@ -1453,10 +1487,10 @@ def gemm(A, lda_m, lda_k, B, ldb_k, ldb_n, Cout, ldc_m, ldc_n, M, N, K, bias=Non
     _lib.call("gwn_gemm", ctypes.byref(d), _lib.stream())
 
 
-def gemm_nt(A, lda, B, ldb, Cout, ldc, M, N, K, bias=None, relu=0, mask=None, ldmask=0):
-    """Cout[m][n] = epi(sum_k A[m][k] B[n][k])  (gwn_gemm_nt)."""
-    _lib.call("gwn_gemm_nt", ptr(A), lda, ptr(B), ldb, ptr(Cout), ldc, M, N, K, ptr(bias), relu, ptr(mask),
-              ldmask, _lib.stream())
+def gemm_nt(A, lda, B, ldb, Cout, ldc, M, N, K, bias=None, relu=0, mask=None, ldmask=0, bf16=False):
+    """Cout[m][n] = epi(sum_k A[m][k] B[n][k])  (gwn_gemm_nt; bf16: gwn_gemm_nt_bf16's bf16 operands)."""
+    _lib.call("gwn_gemm_nt_bf16" if bf16 else "gwn_gemm_nt", ptr(A), lda, ptr(B), ldb, ptr(Cout), ldc, M, N, K,
+              ptr(bias), relu, ptr(mask), ldmask, _lib.stream())
 
 
 def wgrad(dY, J, X, Kc, rows, out, ws, bias_out=None, ldy=None):

@@ -98,6 +98,11 @@ long gwn_gemm_workspace_floats(int M, int N, int ksplit);
  * A [M][lda], B [N][ldb] K-contiguous, K / lda / ldb multiples of 4, A and B 16-B aligned. */
 int gwn_gemm_nt(const float* A, long lda, const float* B, long ldb, float* C, long ldc, int M, int N, int K,
                 const float* bias, int relu, const float* mask, long ldmask, hipStream_t stream);
+/* gwn_gemm_nt on bf16 operands (the bf16 compute mode's head, configs[2]): A and B rounded to bf16
+ * (round to nearest even) as they are read, products summed in fp32; fp32 in and out, the same
+ * epilogue.  N a multiple of 64. */
+int gwn_gemm_nt_bf16(const float* A, long lda, const float* B, long ldb, float* C, long ldc, int M, int N, int K,
+                     const float* bias, int relu, const float* mask, long ldmask, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * nconv (model.py:12-14): einsum('ncvl,vw->ncwl', x, A), i.e. for every slice s
@@ -493,6 +498,13 @@ int gwn_wgrad_partials(const float* dY, long ldy, int J, const float* X, long ld
                        long shift, int R, const float* x_mean, const float* x_scale, const float* x_shift, float* part,
                        hipStream_t stream);
 int gwn_reduce_partials(const gwn_reduce_seg* segs, int nseg, hipStream_t stream);
+/* Weight-gradient partials on bf16 operands (the bf16 compute mode's head, end_conv_1 and the skip
+ * convs): part[c][j*Kc + k] = sum over chunk c's rows r of bf16(dY[r][j]) bf16(X[r][k]) (fp32 sums),
+ * part[c][J*Kc + j] = sum_r dY[r][j] (fp32), for the gwn_wgrad_bf16_partial_count(R, J, Kc) row
+ * chunks; gwn_reduce_partials sums them (part_stride J*Kc + J).  J, Kc multiples of 128. */
+int gwn_wgrad_bf16_partial_count(int R, int J, int Kc);
+int gwn_wgrad_bf16_partials(const float* dY, long ldy, int J, const float* X, long ldx, int Kc, int R, float* part,
+                            hipStream_t stream);
 
 /* Grouped weight gradients: the gwn_wgrad_bn problem for the same weight shape of up to 8 layers
  * in ONE launch (the deferred gcn-mlp or gated-TCN weight gradients of a whole backward).  Problem

@@ -27,7 +27,9 @@ of every gcn take bf16-rounded operands (node features, A and A^2 forward; the m
 gradient and A, A^2 in the backward) with exact accumulation, the adaptive support's gradient
 takes bf16-rounded operands, and the mlp, its weight gradient and every other layer stay exact
 (``gcn_bf16``, a custom autograd node); ``gcn_bf16_mlp=True`` also rounds the per-piece mlp's
-operands (weights, pieces, backward inputs) as the default bf16 mode does.  The HIP path accumulates in fp32 instead, so a test can
+operands (weights, pieces, backward inputs) as the default bf16 mode does; ``head_bf16=True`` the
+head's skip convs and end_conv_1 (their inputs and weights, and the operands of their input and
+weight gradients; end_conv_2 and the bias gradients stay exact: ``_HeadLin``) as that mode's head does.  The HIP path accumulates in fp32 instead, so a test can
 hold it to the fp32 rounding floor around this reference rather than to the bf16 distance from
 the exact model.
 
@@ -51,7 +53,7 @@ class Cfg:
 
     def __init__(self, num_nodes, nfixed=2, gcn_bool=True, addaptadj=True, in_dim=2, out_dim=12, nhid=32,
                  skip=None, end=None, blocks=4, layers=2, dropout=0.0, kernel_size=2, dilation_channels=None,
-                 first_dilation=1, gcn_bf16=False, gcn_bf16_mlp=False):
+                 first_dilation=1, gcn_bf16=False, gcn_bf16_mlp=False, head_bf16=False):
         self.N, self.nfixed = num_nodes, nfixed
         self.gcn_bool, self.addaptadj = gcn_bool, addaptadj
         self.Cin, self.O, self.C = in_dim, out_dim, nhid
@@ -62,6 +64,7 @@ class Cfg:
         self.kernel_size = kernel_size
         self.gcn_bf16 = gcn_bf16  # libgwn's bf16 mode (module docstring)
         self.gcn_bf16_mlp = gcn_bf16_mlp  # ... with the per-piece mlp on bf16 operands too (_GcnBf16)
+        self.head_bf16 = head_bf16  # ... and the skip convs / end_conv_1 on bf16 operands (_HeadLin)
         # gwnet_diff_G starts every block at dilation 4 (model.py:291)
         self.dilations = [first_dilation * 2 ** j for _ in range(blocks) for j in range(layers)]
         # model.py:130-157: every layer adds (kernel_size - 1) * 2^j -- the reference counts from
@@ -153,10 +156,19 @@ class Bf16Pins:
     Every difference that is not such a tie is counted in ``report`` as a violation (the tests
     require none); adopted ties are counted too."""
 
-    def __init__(self, sup=None, g=None, pieces=None, sup_tol=1e-5, g_band=2.0 ** -16, piece_band=2.0 ** -19):
+    def __init__(self, sup=None, g=None, pieces=None, sup_tol=1e-5, g_band=2.0 ** -16, piece_band=2.0 ** -19,
+                 skr=None, head_band=2.0 ** -19, head_dy=None, head_dband=2.0 ** -18):
         self.sup, self.g, self.pieces = sup, g or {}, pieces or {}
         self.sup_tol, self.g_band, self.piece_band = sup_tol, g_band, piece_band
-        self.report = {"g_adopted": 0, "g_bad": 0, "piece_adopted": 0, "piece_bad": 0, "sup_err": 0.0}
+        # the head (head_bf16): the HIP run's fp32 relu(skip) (end_conv_1's operand, NCHW [B, S, N, T_f]),
+        # adopted with band = head_band * sum|terms| of the skip sum; its backward's bf16 operands
+        # head_dy["de1"] (end_conv_1's output gradient) and head_dy["dsk"] (the skip sum's), adopted
+        # with band = head_dband * max|dy| (the fp32 error of short sums, generously)
+        self.skr, self.head_band = skr, head_band
+        self.head_dy, self.head_dband = head_dy or {}, head_dband
+        self.report = {"g_adopted": 0, "g_bad": 0, "piece_adopted": 0, "piece_bad": 0, "sup_err": 0.0,
+                       "skr_adopted": 0, "skr_bad": 0, "de1_adopted": 0, "de1_bad": 0, "dsk_adopted": 0,
+                       "dsk_bad": 0}
 
     def adopt(self, own_b, exact, hip_b, band, tag):
         """own_b = bf16(exact); hip_b = the HIP run's bf16 value: hip_b where it is a rounding tie."""
@@ -273,6 +285,61 @@ class _GcnBf16(torch.autograd.Function):
         return (dg, dw, None, None, None, *dsups)
 
 
+class _HeadLin(torch.autograd.Function):
+    """pointwise(xb, rnd(w)): one of the bf16 mode's head GEMMs (csrc/gemm_nt.hip gwn_gemm_nt_bf16:
+    a skip conv, end_conv_1; model.py:216-222, 238), xb = bf16(x) with the HIP run's ties (Bf16Pins).
+    Backward on bf16 operands as well: the input gradient rnd(w)^T rnd(dy) (the transposed-weight
+    gwn_gemm_nt_bf16), the weight gradient rnd(dy) (x) xb (gwn_wgrad_bf16_partials, the same bf16
+    activations as the forward); the bias gradients (outside) stay exact sums."""
+
+    @staticmethod
+    def forward(ctx, x, w, xb, dpin=None):
+        # dpin: (Bf16Pins, "de1" | "dsk") -- the HIP run's rounding ties of the output gradient
+        ctx.save_for_backward(xb, w)
+        ctx.dpin = dpin
+        return pointwise(xb, bf16_round(w))
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, w = ctx.saved_tensors
+        wr = bf16_round(w.reshape(w.shape[0], -1))
+        dyb = bf16_round(dy)
+        if ctx.dpin is not None:
+            pins, key = ctx.dpin
+            if key in pins.head_dy:
+                hip = bf16_round(pins.head_dy[key].to(dy.dtype))
+                dyb = pins.adopt(dyb, dy, hip, pins.head_dband * float(dy.abs().max()), key)
+        dx = torch.einsum("oi,bont->bint", wr, dyb)
+        dw = torch.einsum("bont,bint->oi", dyb, xb).reshape(w.shape)
+        return dx, dw, None, None
+
+
+def _head_bf16(p, gs, tf, masks, pins):
+    """skip sum -> relu -> end_conv_1 of the bf16 mode (Cfg.head_bf16): the skip convs over the
+    layers' gated outputs at the last tf steps and end_conv_1 as _HeadLin (bf16 operands, exact
+    sums), the bf16 roundings of g and of relu(skip) pinned to the HIP run's ties where given.
+    Returns (skip, e1) pre-activations."""
+    skip, terms = None, None
+    for i, g in enumerate(gs):
+        gl = g[..., -tf:]
+        gb = bf16_round(gl)
+        if pins is not None and i in pins.g:
+            gb = pins.adopt(gb, gl, bf16_round(pins.g[i][..., -tf:].to(gl.dtype)), pins.g_band * float(g.abs().max()), "g")
+        w = p["skip_convs.%d.weight" % i]
+        s = _HeadLin.apply(gl, w, gb.detach(), (pins, "dsk") if pins is not None else None) \
+            + p["skip_convs.%d.bias" % i].view(1, -1, 1, 1)
+        skip = s if skip is None else skip + s
+        t = pointwise(gb.abs(), bf16_round(w).abs())
+        terms = t if terms is None else terms + t
+    sk = _relu(skip, masks, "skip")
+    skb = bf16_round(sk)
+    if pins is not None and pins.skr is not None:
+        skb = pins.adopt(skb, sk, bf16_round(pins.skr.to(sk.dtype)), pins.head_band * terms.detach(), "skr")
+    e1 = _HeadLin.apply(sk, p["end_conv_1.weight"], skb.detach(), (pins, "de1") if pins is not None else None) \
+        + p["end_conv_1.bias"].view(1, -1, 1, 1)
+    return skip, e1
+
+
 def gcn_bf16(g, w, sups, rnd=bf16_round, mrnd=None, pin=None):
     """libgwn's bf16-mode gcn products (_GcnBf16): sum_q W_q piece_q, no bias; mrnd = the mlp's
     operand rounding (None: exact mlp); pin = (Bf16Pins, layer index) or None."""
@@ -332,13 +399,18 @@ def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, ma
     if cfg.use_gcn and cfg.adaptive:
         sups.append(adaptive_adjacency(p["nodevec1"], p["nodevec2"]))
     skip = None
+    head_b = getattr(cfg, "head_bf16", False)
+    gs = []  # (head_bf16: the gated outputs, for _head_bf16)
     for i, d in enumerate(cfg.dilations):
         res = h
         filt = torch.tanh(dilated_conv(res, p["filter_convs.%d.weight" % i], p["filter_convs.%d.bias" % i], d))
         gate = torch.sigmoid(dilated_conv(res, p["gate_convs.%d.weight" % i], p["gate_convs.%d.bias" % i], d))
         g = filt * gate
-        s = pointwise(g, p["skip_convs.%d.weight" % i], p["skip_convs.%d.bias" % i])
-        skip = s if skip is None else s + skip[..., -s.shape[-1]:]
+        if head_b:
+            gs.append(g)
+        else:
+            s = pointwise(g, p["skip_convs.%d.weight" % i], p["skip_convs.%d.bias" % i])
+            skip = s if skip is None else s + skip[..., -s.shape[-1]:]
         if cfg.use_gcn and getattr(cfg, "gcn_bf16", False):
             h = gcn_bf16(g, p["gconv.%d.mlp.mlp.weight" % i], sups,
                          mrnd=bf16_round if getattr(cfg, "gcn_bf16_mlp", False) else None,
@@ -365,7 +437,10 @@ def forward(p, supports, x, cfg, training, bn_state=None, dropout_masks=None, ma
         rm = bn_state["bn.%d.running_mean" % i] if bn_state is not None else None
         rv = bn_state["bn.%d.running_var" % i] if bn_state is not None else None
         h = batchnorm(h, p["bn.%d.weight" % i], p["bn.%d.bias" % i], rm, rv, training)
-    e1 = pointwise(_relu(skip, masks, "skip"), p["end_conv_1.weight"], p["end_conv_1.bias"])
+    if head_b:
+        skip, e1 = _head_bf16(p, gs, h.shape[-1], masks, pins)
+    else:
+        e1 = pointwise(_relu(skip, masks, "skip"), p["end_conv_1.weight"], p["end_conv_1.bias"])
     if record is not None:
         record["skip"], record["e1"] = skip.detach(), e1.detach()
     return pointwise(_relu(e1, masks, "e1"), p["end_conv_2.weight"], p["end_conv_2.bias"])

@@ -16,10 +16,14 @@ Tolerances:
   operands are not pinned), median <= 5e-5 (measured 7-9e-6).  Before the tie pinning a tie moved
   the forward 1.3-1.6e-4 and gradients up to 1.3e-3 (round 4's 4e-4 / 2e-3 gates).
 * the report: the distance from the reference's own f64 run (the bf16 distance itself) is printed
-  and held to the loose bounds of rounds 2-3 (forward 2e-2, gradients 0.1 each / 5e-2 median).
+  and held to loose bounds (forward 2e-2; gradients: the reference's own distance under autocast,
+  REPORT_WORST / REPORT_MEDIAN -- rounds 2-4 held 0.1 / 5e-2 before the head went to bf16 operands:
+  measured then ~0.05 / 0.03, now ~0.10 / 0.05-0.07, sign flips of |pred - real| at B = 2-4).
   For scale: the reference itself under torch.autocast(bfloat16) (the oracle, CPU) is 7.5e-2 /
-  8.5e-2 median and 0.13 / 0.12 worst off the same f64 truth -- this path keeps the TCN, skip,
-  head and BN in fp32 and is ~2x closer.
+  8.5e-2 median and 0.13 / 0.12 worst off the same f64 truth -- this path keeps the TCN, BN,
+  end_conv_2 and every weight gradient of the head in fp32 and is ~2x closer.
+The head's skip convs and end_conv_1 (forward and input gradients) run on bf16 operands in this
+mode too (executor.head_bf16; the emulation's Cfg.head_bf16, its relu(skip) operand tie-pinned).
 Plus: the bf16 kernels against the fp32 kernels at N=16 (one node tile) and N=37 (two tiles), and
 the per-sample independence of a bf16 eval batch."""
 import numpy as np
@@ -42,32 +46,38 @@ def _trainer(gpu, g, n, dropout=0.0, nhid=32):
     return eng
 
 
+# the report bounds (bf16 distance from an f64 / fp32 run, tiny batches: sign flips of |pred - real|
+# dominate): the reference's own distance under torch.autocast(bfloat16) (module docstring),
+# worst 0.13 and median 0.085 -- this path stays inside it with the head on bf16 operands too
+REPORT_WORST, REPORT_MEDIAN = 0.13, 0.085
+
+
 def _check_grads(model, ref, tag, emul=None, gates=None):
-    """emul: the bf16-emulating oracle's gradients (the gate, 1e-3 norm-rel per tensor); ref: the
-    reference's f64 gradients (the report, loose bounds)."""
+    """emul: the bf16-emulating oracle's gradients (the gate, asserted first); ref: the reference's
+    f64 gradients (the report, loose bounds)."""
     got = {k: p.grad.detach().cpu().numpy() for k, p in model.named_parameters() if p.grad is not None}
     assert set(got) == set(ref), (tag, sorted(set(got) ^ set(ref)))
     scale = max(float(np.max(np.abs(v))) for v in ref.values())
-    errs, gate = [], {}
+    errs, gate = {}, {}
     for k, v in ref.items():
         if k.endswith("mlp.bias") or np.linalg.norm(v) == 0:
             # analytically zero (BN-cancelled): fp32 noise only
             assert float(np.max(np.abs(got[k]))) <= 1e-5 * scale, (tag, k)
             continue
-        e = norm_rel(got[k], v)
-        assert e <= 0.1, (tag, k, e)
-        errs.append(e)
+        errs[k] = norm_rel(got[k], v)
         if emul is not None:
             gate[k] = norm_rel(got[k], emul[k].numpy())
-    assert np.median(errs) <= 5e-2, (tag, np.median(errs))
+    fw = max(errs, key=errs.get)
     if emul is not None:
         worst = max(gate, key=gate.get)
-        print("%s: vs bf16 emulation worst %.2e (%s), median %.2e; vs f64 worst %.2e, median %.2e"
-              % (tag, gate[worst], worst, np.median(list(gate.values())), max(errs), np.median(errs)))
+        print("%s: vs bf16 emulation worst %.2e (%s), median %.2e; vs f64 worst %.2e (%s), median %.2e"
+              % (tag, gate[worst], worst, np.median(list(gate.values())), errs[fw], fw, np.median(list(errs.values()))))
         worst_gate, median_gate = gates or _grad_gates()
         for k, e in gate.items():
             assert e <= worst_gate, (tag, k, e)
         assert np.median(list(gate.values())) <= median_gate
+    assert errs[fw] <= REPORT_WORST, (tag, fw, errs[fw])
+    assert np.median(list(errs.values())) <= REPORT_MEDIAN, (tag, np.median(list(errs.values())))
 
 
 def _mlp_bf16():
@@ -120,13 +130,23 @@ def _pins(model, acts, n, B):
     sup.append((acts.adp[:n, :n].double().cpu(), acts.adp2b[:n, :n].double().cpu()))
     gs, pieces = {}, {}
     hbs = getattr(acts, "HB", None) if getattr(acts, "pieces_b", False) else None
-    for i in range(ex.cfg.L - 1):  # (the last layer's gcn does not reach the output)
+    head = ex.head_bf16()
+    for i in range(ex.cfg.L):  # (the last layer's gcn does not reach the output: its g only the skip)
+        if i == ex.cfg.L - 1:
+            if head:
+                gs[i] = nchw(acts.H[i][:, :C].contiguous(), C)
+            break
         gs[i] = nchw(acts.H[i][:, :C].contiguous(), C)
         if hbs is not None:
             pieces[i] = nchw(hbs[i].view(torch.bfloat16).float(), hbs[i].shape[1])
         else:
             pieces[i] = nchw(acts.H[i][:, C:].contiguous().to(torch.bfloat16).float(), acts.H[i].shape[1] - C)
-    return orc.Bf16Pins(sup=sup, g=gs, pieces=pieces)
+    skr = nchw(acts.skr, acts.skr.shape[1]) if head else None  # the head's bf16 operand (ex.head_bf16)
+    head_dy = {}
+    if head and getattr(acts, "training", False):  # its backward's: end_conv_1's / the skip sum's output gradients
+        sc = ex.scratch(B, acts.ts)
+        head_dy = {"de1": nchw(sc["de1"], sc["de1"].shape[1]), "dsk": nchw(sc["dsk"], sc["dsk"].shape[1])}
+    return orc.Bf16Pins(sup=sup, g=gs, pieces=pieces, skr=skr, head_dy=head_dy)
 
 
 def _emulated(g, n, x, y=None, masks=None, pins=None):  # noqa: C901
@@ -135,7 +155,7 @@ def _emulated(g, n, x, y=None, masks=None, pins=None):  # noqa: C901
     GWN_BF16_MLP=0 (executor.split_planes: the library's mode 2 / mode 1)."""
     from oracle import gwnet_oracle as orc
     sd = state_dict_of(g)
-    cfg = orc.Cfg(n, gcn_bf16=True, gcn_bf16_mlp=_mlp_bf16())
+    cfg = orc.Cfg(n, gcn_bf16=True, gcn_bf16_mlp=_mlp_bf16(), head_bf16=_mlp_bf16())
     if y is None:
         p = {k: torch.tensor(v, dtype=torch.float64) for k, v in sd.items() if "running" not in k and "num_batches" not in k}
         bn = {k: torch.tensor(v, dtype=torch.float64) for k, v in sd.items() if "running" in k}
@@ -165,7 +185,7 @@ def test_bf16_eval_forward(gpu, name, n, xkey, okey):
     pins = _pins(m, acts, n, xd.shape[0])
     emu = _emulated(g, n, g[xkey], pins=pins).numpy()
     rep = pins.report
-    assert rep["g_bad"] == 0 and rep["piece_bad"] == 0 and rep["sup_err"] <= 1e-5, rep
+    assert rep["g_bad"] == 0 and rep["piece_bad"] == 0 and rep["skr_bad"] == 0 and rep["sup_err"] <= 1e-5, rep
     e_emu, e_full, e_f64 = (rel_err(out.cpu().numpy(), emu), rel_err(full.cpu().numpy(), emu),
                             rel_err(out.cpu().numpy(), g[okey]))
     print("bf16 eval forward N=%d: vs pinned bf16 emulation %.2e (full schedule %.2e; ties adopted: g %d, "
@@ -189,9 +209,10 @@ def test_bf16_train_step_grads(gpu, name, n, pre):
     pins = _pins(eng.model, acts, n, B)
     eout, emet, egr = _emulated(g, n, g[pre + "x"], g[pre + "y"], masks=_branches(eng, n, g[pre + "y"]), pins=pins)
     rep = pins.report
-    print("%s: bf16 ties adopted: g %d, pieces %d; not ties: g %d, pieces %d; supports max-rel %.1e"
-          % (name, rep["g_adopted"], rep["piece_adopted"], rep["g_bad"], rep["piece_bad"], rep["sup_err"]))
-    assert rep["g_bad"] == 0 and rep["piece_bad"] == 0 and rep["sup_err"] <= 1e-5, rep
+    print("%s: bf16 ties adopted: g %d, pieces %d, skr %d, de1 %d, dsk %d; supports max-rel %.1e"
+          % (name, rep["g_adopted"], rep["piece_adopted"], rep["skr_adopted"], rep["de1_adopted"], rep["dsk_adopted"],
+             rep["sup_err"]))
+    assert all(rep[k + "_bad"] == 0 for k in ("g", "piece", "skr", "de1", "dsk")) and rep["sup_err"] <= 1e-5, rep
     out = acts.y.detach().cpu().double().view(B, n, -1)  # [B, N, T_out] rows (b, n)
     e_fwd = rel_err(out.numpy(), eout[:, :, :, 0].permute(0, 2, 1).numpy())
     print("%s: train-mode output vs pinned emulation %.2e" % (name, e_fwd))
@@ -212,7 +233,10 @@ def test_bf16_train_step_grads(gpu, name, n, pre):
 @pytest.mark.parametrize("n", [16, 37])
 def test_bf16_vs_fp32_kernels_small_graphs(gpu, n):
     """One- and two-tile graphs (every node-tile count has its own instantiation): a train step
-    with dropout 0.3 in bf16 against fp32 on identical inputs and masks, same tolerances."""
+    with dropout 0.3 in bf16 against fp32 on identical inputs and masks -- a sanity bound on the bf16
+    distance (the parity gates are the emulation tests above): worst 0.2, median REPORT_MEDIAN
+    (measured with the bf16 head: N=16 0.103 / 0.060, N=37 0.140 (bn.2.weight) -- B = 4 samples,
+    sign flips of |pred - real|)."""
     from gwn_amd import synthetic, util
     from gwn_amd.engine import trainer
     adj = synthetic.random_sensor_graph(n, density=0.3, seed=n)
@@ -233,9 +257,10 @@ def test_bf16_vs_fp32_kernels_small_graphs(gpu, n):
         if k.endswith("mlp.bias") or np.linalg.norm(v) == 0:
             continue
         e = norm_rel(res[1][1][k], v)
-        assert e <= 0.1, (n, k, e)
+        assert e <= 0.2, (n, k, e)
         errs.append(e)
-    assert np.median(errs) <= 5e-2
+    print("bf16 vs fp32 kernels N=%d: worst %.2e, median %.2e" % (n, max(errs), np.median(errs)))
+    assert np.median(errs) <= REPORT_MEDIAN
 
 
 def test_bf16_eval_batch_is_per_sample(gpu):

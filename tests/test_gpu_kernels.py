@@ -456,6 +456,75 @@ def test_gemm_nt(gpu, M, N, K, epi):
     assert float((got[:, :N] - ref).abs().max()) / scale <= 2e-6
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 64, 256), (777, 256, 256), (20800, 512, 256), (20800, 256, 512),
+                                   (300, 192, 36), (129, 64, 4)])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu", "mask"])
+def test_gemm_nt_bf16(gpu, M, N, K, epi):
+    """gwn_gemm_nt_bf16 (the bf16 mode's head GEMMs) vs fp64 of the bf16-rounded (RNE) operands:
+    the fp32 accumulation floor; ragged row tiles, K < one LDS tile, column tiles of 64 and 128;
+    columns of C beyond N untouched."""
+    from gwn_amd import _lib
+    torch.manual_seed(M + 5 * N + 11 * K)
+    A = torch.randn(M, K) * 3
+    Bm = torch.randn(N, K)
+    bias = torch.randn(N, dtype=torch.float64)
+    mask = torch.randn(M, N, dtype=torch.float64)
+    rb = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
+    ref = rb(A) @ rb(Bm).t()
+    if epi == "bias_relu":
+        ref = torch.clamp(ref + bias, min=0.0)
+    elif epi == "mask":
+        ref = torch.where(mask > 0, ref, torch.zeros_like(ref))
+    ldc = N + 4
+    Cd = torch.full((M, ldc), 7.0, device=gpu)
+    Ad, Bd = A.to(gpu), Bm.to(gpu)
+    bd, md = bias.float().to(gpu), mask.float().to(gpu)
+    _lib.call("gwn_gemm_nt_bf16", Ad.data_ptr(), K, Bd.data_ptr(), K, Cd.data_ptr(), ldc, M, N, K,
+              bd.data_ptr() if epi == "bias_relu" else None, 1 if epi == "bias_relu" else 0,
+              md.data_ptr() if epi == "mask" else None, N, _lib.stream())
+    torch.cuda.synchronize()
+    got = Cd.cpu().double()
+    assert torch.all(got[:, N:] == 7.0)
+    terms = rb(A).abs() @ rb(Bm).abs().t()  # fp32 accumulation error ~ 2^-24 sqrt(K) sum|terms|
+    assert float(((got[:, :N] - ref).abs() / (terms + 1e-30)).max()) <= 2e-6
+    # not the fp32 product: the operands really were rounded
+    if epi == "plain" and K >= 36:
+        assert float((got[:, :N] - A.double() @ Bm.double().t()).abs().max()) > 1e-4
+
+
+@pytest.mark.parametrize("R,J,Kc,pad", [(20800, 512, 256, 0), (13248, 256, 256, 4), (777, 256, 128, 0),
+                                        (100, 128, 128, 8)])
+def test_wgrad_bf16_partials(gpu, R, J, Kc, pad):
+    """gwn_wgrad_bf16_partials + gwn_reduce_partials (the bf16 mode's head weight gradients) vs fp64
+    of the bf16-rounded operands: dW = bf16(dY)^T bf16(X) at the fp32 accumulation floor, db = the
+    unrounded column sums of dY; ragged row chunks, padded leading dimensions."""
+    from gwn_amd import _lib
+    torch.manual_seed(R + J + Kc)
+    dY = torch.randn(R, J + pad) * 2
+    X = torch.rand(R, Kc + pad)
+    rb = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
+    ref = rb(dY[:, :J]).t() @ rb(X[:, :Kc])
+    terms = rb(dY[:, :J]).abs().t() @ rb(X[:, :Kc]).abs()
+    dbr = dY[:, :J].double().sum(0)
+    n = int(_lib.load().gwn_wgrad_bf16_partial_count(R, J, Kc))
+    assert n >= 1
+    part = torch.full((n * (J * Kc + J),), float("nan"), device=gpu)
+    dYd, Xd = dY.to(gpu), X.to(gpu)
+    out = torch.full((J, Kc + 3), 7.0, device=gpu)
+    db = torch.empty(J, device=gpu)
+    _lib.call("gwn_wgrad_bf16_partials", dYd.data_ptr(), J + pad, J, Xd.data_ptr(), Kc + pad, Kc, R, part.data_ptr(),
+              _lib.stream())
+    seg = _lib.ReduceSeg(part=part.data_ptr(), nparts=n, part_stride=J * Kc + J, J=J, Kc=Kc, out=out.data_ptr(),
+                         ld_out=Kc + 3, out2=db.data_ptr(), db_off=J * Kc)
+    _lib.call("gwn_reduce_partials", (_lib.ReduceSeg * 1)(seg), 1, _lib.stream())
+    torch.cuda.synchronize()
+    got = out.cpu().double()
+    assert torch.all(got[:, Kc:] == 7.0)
+    assert float(((got[:, :Kc] - ref).abs() / terms).max()) <= 2e-6
+    assert float((db.cpu().double() - dbr).abs().max() / dY[:, :J].double().abs().sum(0).max()) <= 2e-6
+    assert float((got[:, :Kc] - dY[:, :J].double().t() @ X[:, :Kc].double()).abs().max()) > 1e-4  # bf16 really
+
+
 def _merge_bn(bnp, S, nkb, C):
     """Per-slice (count, mean, M2) [S][3][C] (fp64) from BN partial slots [S][nkb][3][C] (count-0
     slots carry nothing), Chan's merge; the fused forward writes one slot per slice (nkb = 1)."""
