@@ -1071,9 +1071,11 @@ class Executor:
         hb = nt and self.head_bf16()
 
         def head_wgrad_bf16(dY, J, X, Kc, w, b, key, now=False):
-            # the bf16 mode: partials on bf16 operands (gwn_wgrad_bf16_partials), reduced with the
-            # deferred ones at the end of the backward, else (or now: end_conv_1, final at the head
-            # stage's yield, early_grad_range) right away
+            # the bf16 mode: partials on bf16 operands over row chunks (gwn_wgrad_bf16_partials),
+            # reduced with the deferred ones at the end of the backward, else (or now: end_conv_1,
+            # final at the head stage's yield, early_grad_range) right away.  (An fp32 form of this
+            # kernel for the fp32 head measured 94 + 58 us against the split-K GEMM's 57 + 38:
+            # latency-bound at one workgroup per CU)
             n = _lib.load().gwn_wgrad_bf16_partial_count(rows_f, J, Kc)
             part = sc.get(key)
             if part is None or part.numel() < n * (J * Kc + J):

@@ -495,9 +495,10 @@ def test_gemm_nt_bf16(gpu, M, N, K, epi):
 @pytest.mark.parametrize("R,J,Kc,pad", [(20800, 512, 256, 0), (13248, 256, 256, 4), (777, 256, 128, 0),
                                         (100, 128, 128, 8)])
 def test_wgrad_bf16_partials(gpu, R, J, Kc, pad):
-    """gwn_wgrad_bf16_partials + gwn_reduce_partials (the bf16 mode's head weight gradients) vs fp64
-    of the bf16-rounded operands: dW = bf16(dY)^T bf16(X) at the fp32 accumulation floor, db = the
-    unrounded column sums of dY; ragged row chunks, padded leading dimensions."""
+    """gwn_wgrad_bf16_partials + gwn_reduce_partials (the bf16 mode's end_conv_1 and skip-conv weight
+    gradients) vs fp64 of the bf16-rounded operands: dW = bf16(dY)^T bf16(X) at the fp32
+    accumulation floor, db = the unrounded column sums of dY; ragged row chunks, padded leading
+    dimensions."""
     from gwn_amd import _lib
     torch.manual_seed(R + J + Kc)
     dY = torch.randn(R, J + pad) * 2
