@@ -24,7 +24,7 @@ mkdir -p "$O"
 show() { python -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], d['value'], d['ms_per_step'], r['frac'], r.get('avg_launch_us'), d.get('mae12_delta'), (d.get('cpu_baseline') or {}).get('value'))" "$1" "$2"; }
 kernels() {  # PMC summary kernels per config
   case $1 in
-    pems) echo "gcn_fwd_t16b2_kernel gcn_fwd_t16b_kernel gcn_bwd_t16_kernel gram_cu_g4_kernel wgrad_group_kernel rowgemm_kernel" ;;
+    pems) echo "gcn_fwd_t16b2_kernel gcn_fwd_t16b_kernel gcn_bwd_t16_kernel gram_cu_g4_kernel wgrad_group_kernel rowgemm_kernel gemm_nt_bf16_kernel wgrad_bf16_kernel" ;;
     *) echo "gcn_fwd_t16_kernel gcn_bwd_t16_kernel gram_cu_kernel wgrad_group_kernel rowgemm_kernel gemm_nt_kernel gemm_kernel" ;;
   esac
 }
