@@ -300,6 +300,7 @@ class Executor:
         # instrumentation (bench.py): the training gcn forward launches store their workgroups' device
         # clock stamps (gwn_gcn_args.clock, per layer in acts.CLK)
         self.launch_clock = False
+        self.launch_clock_slots = 2  # u64 stamps per workgroup (gwn_gcn_args.clock: start, end)
 
     # ---------------------------------------------------------------------------------------
     def bind(self, device):
@@ -674,7 +675,7 @@ class Executor:
             if training and self.launch_clock:
                 if acts.CLK.get(i) is None:
                     cus = torch.cuda.get_device_properties(self.device).multi_processor_count
-                    acts.CLK[i] = torch.zeros(2 * cus, device=self.device, dtype=torch.int64)
+                    acts.CLK[i] = torch.zeros(self.launch_clock_slots * cus, device=self.device, dtype=torch.int64)
                 ga.clock = ptr(acts.CLK[i])
             rm, rv, mom, eps, nbt = bn_bufs[i]
             if fold and i == L - 1:
