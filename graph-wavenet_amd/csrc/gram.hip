@@ -585,11 +585,11 @@ __global__ __launch_bounds__(1024) void gram_cu_kernel(const GramCu g) {
 // The bf16 mode's CU-resident gram on the tiled bf16 operands (gwn_gram_g4_bf16's layout: a KiB per
 // (slice, 16-node tile), lane (g, j)'s 16 B its k-group of v_mfma_f32_16x16x32_bf16).  Like
 // gram_cu_kernel, but the 16x16 output tiles of one CU would need ~28 per wave at n = 325, so the
-// workgroups come in two halves (blockIdx & 1): half h keeps output tile rows [vt0, vt0 + R) of
+// workgroups come in two halves (blockIdx bit 3): half h keeps output tile rows [vt0, vt0 + R) of
 // every column (<= MAXT tiles per wave) and walks its own equal share of ALL the (layer, slice,
 // pair) steps; per step it stages R KiB of X and nt KiB of T (double-buffered, the next step's
 // 16-B loads in flight) and each wave runs one MFMA per tile, the X fragment reloaded only when
-// its row changes.  Partial slot kb = blockIdx >> 1 holds half 0's rows of share kb and half 1's
+// its row changes.  Partial slot kb (kernel) holds half 0's rows of share kb and half 1's
 // rows of share kb: [grid / 2][np][np], reduced in a fixed order.
 struct GramCuG4 {
   const char* X[GL]; const char* T[GL];  // layer l: pair p's operand at + p * slices * nt KiB
@@ -603,7 +603,11 @@ struct GramCuG4 {
 template <int MAXT>
 __global__ __launch_bounds__(1024) void gram_cu_g4_kernel(const GramCuG4 g) {
   extern __shared__ float4 gcg_lds4[];
-  const int h = blockIdx.x & 1, kb = blockIdx.x >> 1, nh = gridDim.x >> 1;
+  // the two halves of share kb are workgroups 16 q + x and 16 q + 8 + x (kb = 8 q + x): the same XCD
+  // (dispatch deals workgroups to the 8 XCDs round-robin), so the T stream both read per step comes
+  // from that XCD's L2 for the second of them (pairs 2 kb, 2 kb + 1 sat on two XCDs: 1.71x the
+  // algorithmic bytes, profiles/r04/pmc_pems_summary.txt)
+  const int h = (blockIdx.x >> 3) & 1, kb = ((blockIdx.x >> 4) << 3) | (blockIdx.x & 7), nh = gridDim.x >> 1;
   const int vt0 = h ? g.vmid : 0, R = h ? g.nt - g.vmid : g.vmid;
   const int nblk = R + g.nt;  // KiB staged per step
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -791,7 +795,7 @@ inline int gcg_need(int nt) { return (((nt + 1) / 2) * nt + 15) / 16; }
 long gwn_gram_g4_group_workspace_floats(int n, const int* slices, int nlayers) {
   if (n <= 0 || nlayers < 1 || nlayers > GL || !slices || gcg_need((n + 15) / 16) > 16) return 0;
   const long np = 32L * ((n + 31) / 32);
-  return (long)(gwn_device_cus() / 2) * np * np;
+  return (long)(gwn_device_cus() / 16 * 8) * np * np;
 }
 
 int gwn_gram_g4_group(const gwn_gram_layer* layers, int nlayers, int n, float* dA, int ld_dA, int accumulate,
@@ -817,7 +821,7 @@ int gwn_gram_g4_group(const gwn_gram_layer* layers, int nlayers, int n, float* d
   g.vmid = (nt + 1) / 2;
   g.np = 32L * ((n + 31) / 32);
   g.part = ws;
-  const int grid = (gwn_device_cus() / 2) * 2;
+  const int grid = (gwn_device_cus() / 16) * 16;  // (XCD-paired halves: a multiple of 16 workgroups)
   GWN_DEBUG_RANGE(ws, (long)(grid / 2) * g.np * g.np * 4, "gram_g4_group partials");
   GWN_DEBUG_RANGE(dA, ((long)(n - 1) * ld_dA + n) * 4, "gram_g4_group dA");
   const size_t lds = (size_t)(GCG_NB * (g.vmid + nt) + 1) * 1024;  // + the sink
