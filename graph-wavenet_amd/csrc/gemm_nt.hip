@@ -284,7 +284,11 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const WgB p) {
   __shared__ __attribute__((aligned(16))) __bf16 Xs[2][128 * WLD];
   __shared__ float bred[128];
   const int nkt = p.Kc / 128, ntiles = (p.J / 128) * nkt;
-  const int tile = blockIdx.x % ntiles, c = blockIdx.x / ntiles;
+  // the tiles of a row chunk on one XCD (workgroups are dealt to the 8 XCDs round-robin): its dY
+  // and X rows come from that XCD's L2 after the first tile's reads
+  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+  const int tile = q % ntiles, c = (q / ntiles) * 8 + xcd;
+  if (c >= p.nsplit) return;
   const int jt = tile / nkt, kt = tile - jt * nkt;
   const int j0 = 128 * jt, k0 = 128 * kt;
   const int r0 = (int)((long)p.R * c / p.nsplit), r1 = (int)((long)p.R * (c + 1) / p.nsplit);
@@ -588,7 +592,7 @@ extern "C" int gwn_wgrad_bf16_partials(const float* dY, long ldy, int J, const f
               "wgrad_bf16: operand beyond a 2 GB buffer window");
   const int ns = gwn_wgrad_bf16_partial_count(R, J, Kc);
   WgB p = {dY, ldy, X, ldx, part, J, Kc, R, ns};
-  wgrad_bf16_kernel<<<ns * (J / 128) * (Kc / 128), 256, 0, s>>>(p);
+  wgrad_bf16_kernel<<<(ns + 7) / 8 * 8 * (J / 128) * (Kc / 128), 256, 0, s>>>(p);
   GWN_CHECK_LAUNCH();
   return GWN_OK;
 }
