@@ -632,22 +632,40 @@ __global__ void loss_terms_kernel(const float* out, const float* real, long rsb,
   const float mask_scale = (cnt > 0.0f) ? label_total / cnt : 0.0f;  // 1 / mean(mask)
   const float inv_total = 1.0f / (float)total;
   float s_mae = 0.0f, s_mape = 0.0f, s_mse = 0.0f;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long)gridDim.x * blockDim.x) {
-    if (ROWS) {
-      const long r = idx / o;
-      const int oo = (int)(idx - r * o);
-      const int v = (int)(r % n);
-      const int b = (int)((r / n) % B);
-      const float gr = loss_term(out[r * ld_out + oo], real[b * rsb + v * rsn + oo * rso], mean, std, mask_scale,
-                                 inv_total, s_mae, s_mape, s_mse);
-      if (dout) {
-        float* row = dout + r * ld_dout;
-        row[oo] = gr;
-        if (oo == 0)
-          for (int c = o; c < ld_dout; ++c) row[c] = 0.0f;
+  const long stride = (long)gridDim.x * blockDim.x;
+  if (ROWS) {
+    // four grid-stride elements per pass, their loads first (the same elements in the same order
+    // as one at a time: the sums are unchanged)
+    for (long i0 = blockIdx.x * (long)blockDim.x + threadIdx.x; i0 < total; i0 += 4 * stride) {
+      float ov[4], yv[4];
+      long rr[4];
+      int oq[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long idx = i0 + u * stride;
+        const long r = idx / o;
+        const int oo = (int)(idx - r * o);
+        const int v = (int)(r % n);
+        const int b = (int)((r / n) % B);
+        rr[u] = r; oq[u] = oo;
+        ov[u] = idx < total ? out[r * ld_out + oo] : 0.0f;
+        yv[u] = idx < total ? real[b * rsb + v * rsn + oo * rso] : 0.0f;
       }
-    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (i0 + u * stride >= total) continue;
+        const float gr = loss_term(ov[u], yv[u], mean, std, mask_scale, inv_total, s_mae, s_mape, s_mse);
+        if (dout) {
+          float* row = dout + rr[u] * ld_dout;
+          row[oq[u]] = gr;
+          if (oq[u] == 0)
+            for (int c = o; c < ld_dout; ++c) row[c] = 0.0f;
+        }
+      }
+    }
+  }
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; !ROWS && idx < total; idx += stride) {
+    {
       const long r1 = idx / tf;
       const int v = (int)(r1 % n);
       const long r2 = r1 / n;
@@ -751,20 +769,36 @@ __global__ void adam_clipped_kernel(float* p, float* g, float* m, float* v, cons
   const double bc2 = 1.0 - pow((double)beta2, t);
   const float step_size = (float)((double)lr / bc1);
   const float bc2_sqrt = (float)sqrt(bc2);
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < active; i += (long)gridDim.x * blockDim.x) {
-    long k;
-    if (!range_index(lo, hi, nr, i, &k)) continue;
-    float gr = g[k] * coef;
-    g[k] = gr;
-    const float pv = p[k];
-    if (wd != 0.0f) gr = gr + wd * pv;
-    float mv = m[k];
-    mv = mv + (1.0f - beta1) * (gr - mv);
-    const float vv = v[k] * beta2 + (1.0f - beta2) * gr * gr;
-    m[k] = mv;
-    v[k] = vv;
-    const float denom = sqrtf(vv) / bc2_sqrt + eps;
-    p[k] = pv - step_size * (mv / denom);
+  // four grid-stride elements per pass, every load issued before the first update (few blocks keep
+  // the arrival count cheap; the passes were latency-bound one element at a time)
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i0 = blockIdx.x * (long)blockDim.x + threadIdx.x; i0 < active; i0 += 4 * stride) {
+    long kk[4];
+    bool ok[4];
+    float gv[4], pv[4], mv[4], vv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long i = i0 + u * stride;
+      ok[u] = i < active && range_index(lo, hi, nr, i, &kk[u]);
+      if (ok[u]) {
+        gv[u] = g[kk[u]]; pv[u] = p[kk[u]]; mv[u] = m[kk[u]]; vv[u] = v[kk[u]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!ok[u]) continue;
+      const long k = kk[u];
+      float gr = gv[u] * coef;
+      g[k] = gr;
+      if (wd != 0.0f) gr = gr + wd * pv[u];
+      float mq = mv[u];
+      mq = mq + (1.0f - beta1) * (gr - mq);
+      const float vq = vv[u] * beta2 + (1.0f - beta2) * gr * gr;
+      m[k] = mq;
+      v[k] = vq;
+      const float denom = sqrtf(vq) / bc2_sqrt + eps;
+      p[k] = pv[u] - step_size * (mq / denom);
+    }
   }
   // every block has read *step above: the last one to arrive advances it (and the dropout counter)
   __syncthreads();
@@ -784,10 +818,21 @@ __global__ void gather_sqnorm_kernel(const float* src, const int* idx, float* ds
   __shared__ float sh[256];
   if (blockIdx.x == 0 && threadIdx.x == 0) *(int*)(ws + RED_BLOCKS + 1) = 0;  // adam_clipped's counter
   float s = 0.0f;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
-    const float v = src[idx[i]];
-    dst[i] = v;
-    s += v * v;
+  // four grid-stride elements per pass: their indices, then their values (the same sum order)
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i0 = blockIdx.x * (long)blockDim.x + threadIdx.x; i0 < count; i0 += 4 * stride) {
+    int ix[4];
+    float xv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ix[u] = i0 + u * stride < count ? idx[i0 + u * stride] : 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xv[u] = i0 + u * stride < count ? src[ix[u]] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + u * stride >= count) continue;
+      dst[i0 + u * stride] = xv[u];
+      s += xv[u] * xv[u];
+    }
   }
   s = block_sum<256>(s, sh);
   if (threadIdx.x == 0) ws[blockIdx.x] = s;
@@ -810,8 +855,20 @@ __global__ void gather_sum_kernel(const float* src, const int* idx, float* dst, 
       if (i < sum_dst || i >= sum_dst + len) dst[i] = src[idx[i]];
     } else {
       const long j = i - count;
+      // the nvec source indices, then their values, eight at a time in flight (the same sum
+      // order; a dependent index -> value chain per term made this 2 x nvec memory latencies)
       float s = 0.0f;
-      for (int v = 0; v < nvec; ++v) s += src[idx[sum_src + (long)v * len + j]];
+      for (int v0 = 0; v0 < nvec; v0 += 8) {
+        int ix[8];
+        float xv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ix[u] = v0 + u < nvec ? idx[sum_src + (long)(v0 + u) * len + j] : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) xv[u] = v0 + u < nvec ? src[ix[u]] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (v0 + u < nvec) s += xv[u];
+      }
       dst[sum_dst + j] = s;
     }
   }
