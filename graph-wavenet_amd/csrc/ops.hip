@@ -587,11 +587,11 @@ __global__ void loss_count_kernel(const float* real, long rsb, long rsn, long rs
   if (blockIdx.x == 0 && threadIdx.x == 0) *(int*)(ws + LOSS_ARRIVE) = 0;
   const long total = (long)B * n * o;
   float cnt = 0.0f;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += 256L * gridDim.x) {
-    const int oo = (int)(i % o);
-    const long bv = i / o;
-    const int v = (int)(bv % n);
-    const int b = (int)(bv / n);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < (int)total; i += 256 * gridDim.x) {  // (total < 2^31)
+    const int oo = i % o;
+    const int bv = i / o;
+    const int v = bv % n;
+    const int b = bv / n;
     cnt += (real[b * rsb + v * rsn + oo * rso] != 0.0f) ? 1.0f : 0.0f;
   }
   cnt = block_sum<256>(cnt, sh);
@@ -632,40 +632,22 @@ __global__ void loss_terms_kernel(const float* out, const float* real, long rsb,
   const float mask_scale = (cnt > 0.0f) ? label_total / cnt : 0.0f;  // 1 / mean(mask)
   const float inv_total = 1.0f / (float)total;
   float s_mae = 0.0f, s_mape = 0.0f, s_mse = 0.0f;
-  const long stride = (long)gridDim.x * blockDim.x;
-  if (ROWS) {
-    // four grid-stride elements per pass, their loads first (the same elements in the same order
-    // as one at a time: the sums are unchanged)
-    for (long i0 = blockIdx.x * (long)blockDim.x + threadIdx.x; i0 < total; i0 += 4 * stride) {
-      float ov[4], yv[4];
-      long rr[4];
-      int oq[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const long idx = i0 + u * stride;
-        const long r = idx / o;
-        const int oo = (int)(idx - r * o);
-        const int v = (int)(r % n);
-        const int b = (int)((r / n) % B);
-        rr[u] = r; oq[u] = oo;
-        ov[u] = idx < total ? out[r * ld_out + oo] : 0.0f;
-        yv[u] = idx < total ? real[b * rsb + v * rsn + oo * rso] : 0.0f;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    if (ROWS) {
+      const long r = idx / o;
+      const int oo = (int)(idx - r * o);
+      const int v = (int)(r % n);
+      const int b = (int)((r / n) % B);
+      const float gr = loss_term(out[r * ld_out + oo], real[b * rsb + v * rsn + oo * rso], mean, std, mask_scale,
+                                 inv_total, s_mae, s_mape, s_mse);
+      if (dout) {
+        float* row = dout + r * ld_dout;
+        row[oo] = gr;
+        if (oo == 0)
+          for (int c = o; c < ld_dout; ++c) row[c] = 0.0f;
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (i0 + u * stride >= total) continue;
-        const float gr = loss_term(ov[u], yv[u], mean, std, mask_scale, inv_total, s_mae, s_mape, s_mse);
-        if (dout) {
-          float* row = dout + rr[u] * ld_dout;
-          row[oq[u]] = gr;
-          if (oq[u] == 0)
-            for (int c = o; c < ld_dout; ++c) row[c] = 0.0f;
-        }
-      }
-    }
-  }
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; !ROWS && idx < total; idx += stride) {
-    {
+    } else {
       const long r1 = idx / tf;
       const int v = (int)(r1 % n);
       const long r2 = r1 / n;
@@ -1553,7 +1535,7 @@ long gwn_masked_loss_workspace_floats(int B, int o, int n, int tf) {
 int gwn_masked_loss(const float* out, const float* real, long rsb, long rsn, long rso, int B, int o,
                     int n, int tf, float mean, float std, float* metrics, float* dout, float* ws,
                     hipStream_t s) {
-  GWN_REQUIRE(B > 0 && o > 0 && n > 0 && tf > 0, "masked_loss: bad shape");
+  GWN_REQUIRE(B > 0 && o > 0 && n > 0 && tf > 0 && (long)B * o * n * tf < (1L << 31), "masked_loss: bad shape");
   loss_count_kernel<<<LOSS_CNT_BLOCKS, 256, 0, s>>>(real, rsb, rsn, rso, B, n, o, ws);
   GWN_CHECK_LAUNCH();
   loss_terms_kernel<false><<<LOSS_TERM_BLOCKS, 256, 0, s>>>(out, real, rsb, rsn, rso, B, o, n, tf, mean, std, dout,
@@ -1565,7 +1547,8 @@ int gwn_masked_loss(const float* out, const float* real, long rsb, long rsn, lon
 int gwn_masked_loss_rows(const float* y, int ld_y, const float* real, long rsb, long rsn, long rso, int B, int o,
                          int n, int tf, float mean, float std, float* metrics, float* dy, int ld_dy, float* ws,
                          hipStream_t s) {
-  GWN_REQUIRE(B > 0 && o > 0 && n > 0 && tf > 0 && ld_y >= o && (!dy || ld_dy >= o), "masked_loss_rows: bad shape");
+  GWN_REQUIRE(B > 0 && o > 0 && n > 0 && tf > 0 && ld_y >= o && (!dy || ld_dy >= o) && (long)B * o * n * tf < (1L << 31),
+              "masked_loss_rows: bad shape");
   loss_count_kernel<<<LOSS_CNT_BLOCKS, 256, 0, s>>>(real, rsb, rsn, rso, B, n, o, ws);
   GWN_CHECK_LAUNCH();
   loss_terms_kernel<true><<<LOSS_TERM_BLOCKS, 256, 0, s>>>(y, real, rsb, rsn, rso, B, o, n, tf, mean, std, dy, ws,
