@@ -220,6 +220,67 @@ __global__ __launch_bounds__(SMALL_T) void wgrad_small_kernel(const float* dY, l
   }
 }
 
+// J = 32 with 16-B aligned dY rows (the start conv's weight gradient): lane (row slot, quad) owns
+// channels 4 quad .. +3 of every eighth row of its share (one 16-B dY load and one Kc-float X load
+// per row), the eight row slots of a wave summed by lane exchange, the sixteen waves through LDS in
+// a fixed order.  (The generic form: one channel per lane, 14.4 us per METR step.)
+__global__ __launch_bounds__(SMALL_T) void wgrad_small32_kernel(const float* dY, long ldy, const float* X, long ldx,
+                                                               int Kc, int R, float* part) {
+  __shared__ float sh[SMALL_T / 64][8][4 * (SMALL_KC + 1)];
+  const int qd = threadIdx.x & 7, slot = threadIdx.x >> 3, nslot = SMALL_T / 8;
+  const int r0 = (int)((long)R * blockIdx.x / gridDim.x), r1 = (int)((long)R * (blockIdx.x + 1) / gridDim.x);
+  float acc[4][SMALL_KC + 1];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int k = 0; k <= SMALL_KC; ++k) acc[e][k] = 0.0f;
+#pragma unroll 4
+  for (int r = r0 + slot; r < r1; r += nslot) {
+    const float4 dy = *(const float4*)(dY + (long)r * ldy + 4 * qd);
+    const float d4[4] = {dy.x, dy.y, dy.z, dy.w};
+    float xk[SMALL_KC];
+#pragma unroll
+    for (int k = 0; k < SMALL_KC; ++k) xk[k] = k < Kc ? X[(long)r * ldx + k] : 0.0f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+#pragma unroll
+      for (int k = 0; k < SMALL_KC; ++k) acc[e][k] = fmaf(d4[e], xk[k], acc[e][k]);
+      acc[e][SMALL_KC] += d4[e];
+    }
+  }
+  // the wave's eight row slots (lane bits 3..5) summed by exchange
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int k = 0; k <= SMALL_KC; ++k) {
+      float v = acc[e][k];
+      v += __shfl_xor(v, 8);
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      acc[e][k] = v;
+    }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int k = 0; k <= SMALL_KC; ++k) sh[wave][lane][e * (SMALL_KC + 1) + k] = acc[e][k];
+  }
+  __syncthreads();
+  if (threadIdx.x >= 32) return;
+  const int j = threadIdx.x, q = j >> 2, e = j & 3;
+  float* out = part + (long)blockIdx.x * (32 * Kc + 32);
+#pragma unroll
+  for (int k = 0; k <= SMALL_KC; ++k) {
+    if (k < Kc || k == SMALL_KC) {
+      float v = 0.0f;
+      for (int w = 0; w < SMALL_T / 64; ++w) v += sh[w][q][e * (SMALL_KC + 1) + k];
+      if (k < Kc) out[j * Kc + k] = v;
+      else out[32 * Kc + j] = v;
+    }
+  }
+}
+
 int wgrad_nblk(int R, int waves_per_blk) {
   // a whole number of workgroups per CU (256 CUs), ~WGRAD_WAVES_PER_CU waves per CU; >= 256 rows per workgroup
   int per_cu = WGRAD_WAVES_PER_CU / waves_per_blk;
@@ -290,7 +351,10 @@ int gwn_wgrad_partials(const float* dY, long ldy, int J, const float* X, long ld
   GWN_REQUIRE(part != nullptr, "wgrad_partials: part is required");
   if (Kt * ntaps <= SMALL_KC && J > 0 && J <= 256 && 256 % J == 0) {  // narrow inputs (1x1, no affine)
     GWN_REQUIRE(ntaps == 1 && !x_mean && !x_scale && !x_shift && x_rows >= R, "wgrad_partials: narrow form is 1x1, plain");
-    wgrad_small_kernel<<<gwn_wgrad_partial_count(R, J, Kt), SMALL_T, 0, s>>>(dY, ldy, J, X, ldx, Kt, R, part);
+    if (J == 32 && ldy % 4 == 0 && ((uintptr_t)dY & 15) == 0)
+      wgrad_small32_kernel<<<gwn_wgrad_partial_count(R, J, Kt), SMALL_T, 0, s>>>(dY, ldy, X, ldx, Kt, R, part);
+    else
+      wgrad_small_kernel<<<gwn_wgrad_partial_count(R, J, Kt), SMALL_T, 0, s>>>(dY, ldy, J, X, ldx, Kt, R, part);
     GWN_CHECK_LAUNCH();
     return GWN_OK;
   }
