@@ -1,13 +1,21 @@
 """One training step of a rocprofv3 kernel trace (bench.py run): the kernels between the last two
-adam_clipped_kernel launches of the timed region, in order, with durations and the idle gaps.
+adam_clipped_kernel launches of the timed region, in order, with durations and the idle gaps.  The
+timed region ends at the adam before the longest pause between adams (the MAE / oracle legs that
+follow it, before bench.py's extra clock-read steps).
   python tools/step_trace.py <run_kernel_trace.csv> [--list]"""
 import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 adam = [i for i, r in enumerate(rows) if "adam_clipped" in r["Kernel_Name"]]
-# the timed steps are followed by the roofline / MAE legs: take the step before the last adam
-a, b = adam[-2], adam[-1]
+# the timed steps are followed by the MAE legs and then the roofline's extra steps: take the step
+# that ends at the last adam before the longest pause between adams
+starts = [int(rows[i]["Start_Timestamp"]) for i in adam]
+gaps = [starts[k + 1] - starts[k] for k in range(len(starts) - 1)]
+kend = max(range(len(gaps)), key=lambda k: gaps[k]) if gaps else len(adam) - 1
+if len(gaps) < 3 or gaps[kend] < 3 * sorted(gaps)[len(gaps) // 2]:
+    kend = len(adam) - 1  # no pause: the last two adams
+a, b = adam[kend - 1], adam[kend]
 step = rows[a + 1:b + 1]
 t0, t1 = int(step[0]["Start_Timestamp"]), int(step[-1]["End_Timestamp"])
 busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in step)
