@@ -1648,7 +1648,7 @@ bool gwn_gcn_tcn_fusable(const gwn_gcn_args* g) {
 
 extern "C" int gwn_gcn_tcn_fused(const gwn_gcn_args* a) { return a && a->tcn && gwn_gcn_tcn_fusable(a) ? 1 : 0; }
 
-int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s) {
+int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s, int* used) {
   const int nwt = (g->n + 31) / 32;
   GWN_REQUIRE(g->ld_sup >= nwt * 32, "gcn_fwd (fused): supports must be padded to 32*ceil(n/32)");
   GWN_REQUIRE(g->layout == 0 || g->layout == 1, "gcn_fwd (fused): layout must be 0 or 1 (one wave per node tile)");
@@ -1735,9 +1735,12 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
         size_t lds2 = fixed + maximg2 * img;
         if (lds2 < 81 * 1024) lds2 = 81 * 1024;
         gcn_fwd_t16b2_kernel<768><<<grid2, 768, lds2, s>>>(a, p, maximg2);
-      } else if (g->split_planes == 2)
-        gcn_fwd_t16b_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
-      else gcn_fwd_t16b_kernel<1024><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+        if (used) *used = grid2;
+      } else {
+        if (g->split_planes == 2) gcn_fwd_t16b_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+        else gcn_fwd_t16b_kernel<1024><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+        if (used) *used = grid;
+      }
       GWN_CHECK_LAUNCH();
       return GWN_OK;
     }
@@ -1782,6 +1785,7 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
     // partial slot (gwn_bn_part_slots)
     a.bn_slots = (int)gwn_bn_part_slots(slices);
     gcn_fwd_t16_kernel<1024><<<pl.grid, 64 * T16_WAVES, pl.lds, s>>>(a, p, pl.maximg);
+    if (used) *used = pl.grid;
     GWN_CHECK_LAUNCH();
     return GWN_OK;
   }

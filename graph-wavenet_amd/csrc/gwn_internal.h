@@ -51,7 +51,9 @@ int gwn_gemm_launch(const GemmParams& p, hipStream_t stream);
 // Fused diffusion GCN (gcn_fused.hip)
 bool gwn_gcn_fused_eligible(int c, int n, int nsup, int ld_sup);
 // *folded: the launch also ran g->bn_fold (the 16-node tile kernels' last-workgroup finalize)
-int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s);
+// *used (optional): the leading BN partial slots that can hold rows (the t16 kernels' grid; else
+// gwn_bn_part_slots: the slots past it are written as zeros either way)
+int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t s, int* used = nullptr);
 bool gwn_gcn_tcn_fusable(const gwn_gcn_args* g);
 int gwn_device_cus();  // compute units of the current device (cached)
 // BatchNorm partial slots of a gwn_gcn_fwd launch over `slices` slices (every slot written)

@@ -1274,11 +1274,14 @@ int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
       a = &local;
     }
   }
+  int used = (int)gwn_bn_part_slots(a->rows / n);  // the slots that can hold rows (the t16 kernels: their grid)
   int rc = (co == c && gwn_gcn_fused_eligible(c, n, a->nsup, a->ld_sup))
-               ? gwn_gcn_fused_fwd_launch(a, a->bn_partials, s)
+               ? gwn_gcn_fused_fwd_launch(a, a->bn_partials, s, &used)
                : gcn_fwd_unfolded(a, s);
-  if (rc || !f) return rc;
-  return gwn_batchnorm_fwd_fold(a->bn_partials, (int)gwn_bn_part_slots(a->rows / n), co, f->gamma, f->beta,
+  if (rc) return rc;
+  if (a->bn_slots_used) *a->bn_slots_used = used;
+  if (!f) return rc;
+  return gwn_batchnorm_fwd_fold(a->bn_partials, used, co, f->gamma, f->beta,
                                 f->running_mean, f->running_var, f->momentum, f->eps, f->save_mean, f->save_rstd,
                                 f->scale, f->w_next, f->b_next, f->w_fold, f->b_fold, f->num_batches_tracked, s);
 }

@@ -108,6 +108,7 @@ class GcnArgs(ctypes.Structure):
         ("bn_fold", ctypes.POINTER(BnFold)),
         ("tcn", ctypes.POINTER(TcnArgs)),
         ("clock", c_void_p),
+        ("bn_slots_used", ctypes.POINTER(c_int)),
     ]
 
 

@@ -615,6 +615,7 @@ class Executor:
         if pieces_b and (getattr(acts, "HB", None) is None or len(acts.HB) != L - 1):
             acts.HB = [torch.empty(ts[i + 1] * P, 2 * cfg.nsup * cfg.D, device=self.device, dtype=torch.int16)
                        for i in range(L - 1)]
+        used_prev = 0  # the BN partial slots the previous gcn launch reported (gwn_gcn_args.bn_slots_used)
         for i in range(L):
             d, sh = cfg.dilations[i], cfg.shift(i)
             rows = ts[i + 1] * P
@@ -636,7 +637,7 @@ class Executor:
                                   w_fold=acts.w_fold[i].data_ptr(), b_fold=acts.b_fold[i].data_ptr(),
                                   num_batches_tracked=ptr(nbt_))
                 ta.bn, ta.bn_partials = ctypes.addressof(bfp), ptr(bnparts[(i - 1) % 2])
-                ta.bn_nparts = self._bn_parts(ts[i] * P)
+                ta.bn_nparts = used_prev or self._bn_parts(ts[i] * P)  # (the slots layer i-1's gcn filled)
                 ta._bn_keep = bfp  # (ctypes keeps no reference through the c_void_p field)
             if i == L - 1 and not training:
                 lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), st)
@@ -686,12 +687,15 @@ class Executor:
                                  save_mean=ptr(acts.mean[i]), save_rstd=ptr(acts.rstd[i]),
                                  scale=acts.bn_scale[i].data_ptr(), num_batches_tracked=ptr(nbt))
                 ga.bn_fold = ctypes.pointer(bf)
+            used = ctypes.c_int(0)
+            ga.bn_slots_used, ga._used = ctypes.pointer(used), used
             lib.call("gwn_gcn_fwd", ctypes.byref(ga), st)
+            used_prev = used.value  # the BN partial slots this launch can fill (the consumer's nparts)
             acts.gcn_args[i] = ga  # kept for bench.py's per-kernel timing
             if fold:
                 pass  # the BatchNorm finalize rides on the next TCN / this gcn call
             elif training:
-                lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnparts[i % 2]), self._bn_parts(rows),
+                lib.call("gwn_batchnorm_fwd_partials", ptr(acts.Z[i]), rows, C, ptr(bnparts[i % 2]), used_prev or self._bn_parts(rows),
                          ptr(self.pk("bn_g%d" % i)), ptr(self.pk("bn_b%d" % i)), ptr(rm), ptr(rv), mom, eps,
                          ptr(acts.X[i + 1]), ptr(acts.mean[i]), ptr(acts.rstd[i]), ptr(nbt), st)
             else:

@@ -353,6 +353,10 @@ typedef struct gwn_gcn_args {
    * clock[2*wg + 1] (wg < CUs: one workgroup per CU); each launch overwrites the previous one's.
    * Other forward paths write nothing (the caller zeroes it first to tell). */
   unsigned long long* clock;
+  /* bn_slots_used (optional, host int): set by gwn_gcn_fwd to the number of leading BN partial slots
+   * that can hold rows -- the 16-node tile kernels' workgroup count, else gwn_gcn_bn_partial_count's
+   * -- a consumer may pass it as nparts instead (the slots past it are zero-count) */
+  int* bn_slots_used;
 } gwn_gcn_args;
 /* gwn_batchnorm_fwd_fold's arguments (same meaning) for gwn_gcn_args.bn_fold */
 typedef struct gwn_bn_fold {
