@@ -873,6 +873,8 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn, planes):
             ga.tcn = ctypes.pointer(ta)
             clk = torch.zeros(2 * _cus(), device=gpu, dtype=torch.int64)
             ga.clock = clk.data_ptr()  # the instrumentation rides along (results compared as ever)
+            used = ctypes.c_int(-1)
+            ga.bn_slots_used = ctypes.pointer(used)
         else:
             _lib.call("gwn_gated_tcn_fwd", ctypes.byref(ta), _lib.stream())
         _lib.call("gwn_gcn_fwd", ctypes.byref(ga), _lib.stream())
@@ -880,9 +882,15 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn, planes):
         outs[fused] = (h, fg, skip[:, :C], z, _bn_all(bnp, rows, n, C, K, NP)) + (
             tuple(bo[k] for k in ("mean", "rstd", "scale", "rm", "rv", "nbt", "wf", "bf")) if bn else ())
     (h0, fg0, sk0, z0, st0), (h1, fg1, sk1, z1, st1) = outs[False][:5], outs[True][:5]
+    # gwn_gcn_args.bn_slots_used: the leading slots that can hold rows (the tile grid); the rest
+    # zero-count, so a consumer merging only those gets the same statistics
+    assert 1 <= used.value <= min(nparts, _cus())
+    assert torch.all(bnp.view(nparts, 3, C)[used.value:, 0] == 0)
+    assert int(bnp.view(nparts, 3, C)[:used.value, 0].sum(0)[0]) == rows
     # gwn_gcn_args.clock: every workgroup of the tile launch stamped (start, end), slots [0, grid)
     c = clk.cpu().reshape(-1, 2)
     g = int((c[:, 1] > 0).sum())
+    assert g == used.value
     assert 0 < g <= _cus() and bool((c[:g] > 0).all()) and bool((c[g:] == 0).all())
     assert bool((c[:g, 1] >= c[:g, 0]).all())
     span_ms = float(c[:g, 1].max() - c[:g, 0].min()) / lib.gwn_wall_clock_khz()
