@@ -196,6 +196,17 @@ def main():
     # captured graphs, each read after it (outside the timed region: the reads synchronize)
     roof = measure_dominant(eng, dev, bf16=bf16, steps=args.steps,
                             extra=lambda k: eng.train(xs[k % nb], ys[k % nb]), extra_n=9)
+    if dist_info is not None:
+        # the collectives' device time and how much of the early all-reduce the layers' backward
+        # hid (engine.trainer.dp_probe_summary), over 5 more steps outside the timed region
+        eng.dp_probe = []
+        for k in range(5):
+            eng.dp_probe.append({})
+            eng.train(xs[k % nb], ys[k % nb])
+        dist_info["allreduce"] = dict(eng.dp_probe_summary(), steps=5,
+                                      overlap=os.environ.get("GWN_DP_OVERLAP", "1") != "0",
+                                      grad_floats=int(eng.optimizer.grad_flat.numel()))
+        eng.dp_probe = None
     result = None
     if rank == 0:
         result = {

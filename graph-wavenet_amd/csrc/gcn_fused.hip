@@ -1632,7 +1632,9 @@ bool gwn_gcn_tcn_fusable(const gwn_gcn_args* g) {
   if (!t) return false;
   auto al = [](const void* q) { return (((uintptr_t)q) & 15) == 0; };
   const int slices = g->rows / g->n, nwt = (g->n + 31) / 32;
+  // (t16_tcn_load addresses the input rows with 32-bit byte offsets of one buffer resource)
   return t->c == CH && (t->ntaps == 0 || t->ntaps == 2) && (t->c_out == 0 || t->c_out == CH) &&
+         (long long)t->t_in * t->P * CH * 4 < 0x7fff0000LL &&
          t->xg == g->h && t->ld_xg == g->ld_h && (long)(t->t_in - t->dilation) * t->P == g->rows && t->dilation > 0 &&
          al(t->x) && t->w_fg && t->b_fg && (!t->fg || al(t->fg)) &&
          (!t->skipcat || (al(t->skipcat) && (t->ld_skip & 3) == 0)) && g->c == CH &&

@@ -94,6 +94,8 @@ __host__ __device__ inline unsigned gwn_mix32(unsigned h) {
   h ^= h >> 16;
   return h;
 }
+// idx < 2^32: the launches that apply dropout check rows * channels < 2^32 on the host
+// (gwn_gcn_fwd / gwn_gcn_bwd / gwn_batchnorm_bwd), so a mask never repeats within a tensor.
 __host__ __device__ inline float gwn_uniform(unsigned long long seed, unsigned long long salt,
                                              unsigned long long idx) {
   const unsigned key = gwn_mix32((unsigned)seed ^ gwn_mix32((unsigned)(seed >> 32) + 0x9E3779B9u * ((unsigned)salt + 1u)));

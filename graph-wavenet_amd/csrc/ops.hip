@@ -1252,6 +1252,8 @@ static int gcn_fwd_unfolded(const gwn_gcn_args* a, hipStream_t s);
 
 int gwn_gcn_fwd(const gwn_gcn_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_fwd: rows must be slices*n");
+  GWN_REQUIRE(a->drop_p <= 0.0f || (long long)a->rows * (a->c_out > 0 ? a->c_out : a->c) < (1LL << 32),
+              "gcn_fwd: dropout masks index rows*c_out elements in 32 bits (gwn_uniform)");
   const gwn_bn_fold* f = a->bn_fold;
   if (f) {
     const int co = a->c_out > 0 ? a->c_out : a->c;
@@ -1347,6 +1349,8 @@ long gwn_gcn_ksplit_ws_floats(int rows, int n, int nsup) {
 
 int gwn_gcn_bwd(const gwn_gcn_bwd_args* a, hipStream_t s) {
   GWN_REQUIRE(a && a->rows > 0 && a->n > 0 && a->rows % a->n == 0, "gcn_bwd: rows must be slices*n");
+  GWN_REQUIRE(a->drop_p <= 0.0f || (long long)a->rows * (a->c_out > 0 ? a->c_out : a->c) < (1LL << 32),
+              "gcn_bwd: dropout masks index rows*c_out elements in 32 bits (gwn_uniform)");
   const int c = a->c, n = a->n, slices = a->rows / n;
   GWN_REQUIRE(a->c_out >= 0, "gcn_bwd: bad c_out");
   const int co = a->c_out > 0 ? a->c_out : c;
@@ -1508,6 +1512,8 @@ int gwn_batchnorm_bwd(const float* dy, const float* z, int rows, int c, const fl
                       float* dres, int res_row0, float* dh, const unsigned long long* seed_ptr,
                       unsigned long long salt, float drop_p, int batch_stats, float* ws, hipStream_t s) {
   GWN_REQUIRE(rows > 0 && c > 0 && c <= 256 && 256 % c == 0, "batchnorm_bwd: c must divide 256");
+  GWN_REQUIRE(drop_p <= 0.0f || (long long)rows * c < (1LL << 32),
+              "batchnorm_bwd: dropout masks index rows*c elements in 32 bits (gwn_uniform)");
   float* part = ws;
   float* sums = ws + (long)RED_BLOCKS * 3 * c;  // [2][c]: sum dy, sum dy*xhat
   bn_bwd_partial_kernel<<<RED_BLOCKS, 256, 0, s>>>(dy, z, save_mean, save_rstd, rows, c, part);

@@ -122,6 +122,7 @@ class trainer():
         # HIP-graph replay of the fused training step (GWN_GRAPHS=0 disables): the ~240 launches
         # of a step are captured once per (shape, hyper-parameter) key and replayed
         self.use_graphs = os.environ.get("GWN_GRAPHS", "1") != "0"
+        self.dp_probe = None  # data-parallel collective timing (bench.py; _probe_event)
         self._graphs = {}
         self._eager_runs = {}
 
@@ -144,10 +145,10 @@ class trainer():
     def _early_range(self, acts):
         """Data parallel: the flat gradient range final after the backward's head stage
         (Executor.early_grad_range), whose all-reduce overlaps the layers' backward; None in a
-        single process, with the side-stream weight gradients of GWN_OVERLAP, or without one.
+        single process or without one.
         GWN_DP_OVERLAP=0: one all-reduce of the whole gradient after the backward."""
         ex = self.model._executor
-        if not self._distributed() or ex._overlap_ok(acts) or os.environ.get("GWN_DP_OVERLAP", "1") == "0":
+        if not self._distributed() or os.environ.get("GWN_DP_OVERLAP", "1") == "0":
             return None
         return ex.early_grad_range()
 
@@ -317,13 +318,47 @@ class trainer():
         if g1b is not None:
             hook = self._overlap_hook()
             hook(1)
+            self._probe_event("layers_0")
             g1b.replay()
+            self._probe_event("layers_1")
             hook(2)
             g2.replay()
         elif g2 is not None:
+            self._probe_event("rest_0")
             self._allreduce_grads()
+            self._probe_event("rest_1")
             g2.replay()
         return m
+
+    def _probe_event(self, name, stream=None):
+        """Data-parallel probe (bench.py, outside the timed region): with ``dp_probe`` a list, a
+        timing event per collective boundary into its last dict (dp_probe_summary)."""
+        if self.dp_probe is None or not self.dp_probe:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream if stream is not None else torch.cuda.current_stream())
+        self.dp_probe[-1][name] = ev
+
+    def dp_probe_summary(self):
+        """Mean device times (ms) over the probed steps: the early range's all-reduce on the side
+        stream (early_allreduce), the layers' backward it overlaps (layers_backward), the part of the
+        early all-reduce that ran inside that backward (early_overlapped), and the all-reduce of the
+        rest on the main stream plus the join (rest_allreduce)."""
+        torch.cuda.synchronize()
+        acc = {}
+        for evs in self.dp_probe or []:
+            def el(a, b):
+                return evs[a].elapsed_time(evs[b]) if a in evs and b in evs else None
+            vals = {"early_allreduce": el("early_0", "early_1"), "layers_backward": el("layers_0", "layers_1"),
+                    "rest_allreduce": el("rest_0", "rest_1")}
+            if vals["early_allreduce"] is not None and vals["layers_backward"] is not None:
+                # overlap of [early_0, early_1] with [layers_0, layers_1] on the device clock
+                s0, s1 = el("layers_0", "early_0"), el("layers_0", "early_1")
+                vals["early_overlapped"] = max(0.0, min(s1, vals["layers_backward"]) - max(s0, 0.0))
+            for k, v in vals.items():
+                if v is not None:
+                    acc.setdefault(k, []).append(v)
+        return {k + "_ms": round(sum(v) / len(v), 4) for k, v in acc.items()}
 
     def _overlap_hook(self):
         """between(part) for _backward_split in a data-parallel step: part 1 (after the head stage
@@ -342,13 +377,17 @@ class trainer():
             if part == 1:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
+                    self._probe_event("early_0", side)
                     self._allreduce(gf[a:b])
+                    self._probe_event("early_1", side)
             else:
+                self._probe_event("rest_0")
                 if a > 0:
                     self._allreduce(gf[:a])
                 if b < gf.numel():
                     self._allreduce(gf[b:])
                 main.wait_stream(side)
+                self._probe_event("rest_1")
 
         return between
 

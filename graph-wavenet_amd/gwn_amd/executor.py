@@ -368,10 +368,6 @@ class Executor:
             "dfg": e(maxrows, 2 * D),
             "dh": e(maxrows, C),
             "dhc": e(maxrows, cfg.W),
-            # second-parity buffers for the side-stream weight gradients (backward overlap)
-            "dfg2": e(maxrows, 2 * D),
-            "dh2": e(maxrows, C),
-            "dhc2": e(maxrows, cfg.W),
             "dadp": torch.zeros(cfg.NP, cfg.NP, device=self.device, dtype=F32),
             "metrics": e(4),
             "bnsums": e(2 * C),  # BN-backward statistics handed from a layer's TCN backward to the next
@@ -410,43 +406,36 @@ class Executor:
             s["part_mlp"], s["part_tcn"] = pm, pt
             # grouped weight gradients (gwn_wgrad_group): every layer's mlp / TCN dW in one launch
             # each at the end of the backward, so each layer keeps its own dh / dfg
-            if self._group_ok():
-                rows_l = [ts[i + 1] * P for i in range(L)]
-                gm = self._group_plan(rows_l[:L - 1], C, cfg.W, 1)
-                gt = self._group_plan(rows_l, 2 * C, C, 2)
-                if gm is not None and gt is not None and L >= 2:
-                    s["group_mlp"] = [e(n * (C * cfg.W + C)) for n in gm]
-                    s["group_tcn"] = [e(n * (4 * C * C + 2 * C)) for n in gt]
-                    s["group_np"] = (gm, gt)
-                    s["dh_l"] = [e(r, C) for r in rows_l]
-                    s["dfg_l"] = [e(r, 2 * D) for r in rows_l]
-                    s["aff_id"] = torch.cat([torch.zeros(C, device=self.device), torch.ones(C, device=self.device),
-                                             torch.zeros(C, device=self.device)])
-                # grouped adaptive-support gradient (gwn_gram_group, fp32 mode): each layer keeps its
-                # t1 / t2 ([rows][96]: the gcn backward's dhcat with only columns 32..96 written)
-                if cfg.adp_live and cfg.use_gcn and os.environ.get("GWN_GRAM_GROUP", "1") != "0":
-                    # a launch takes at most GRAM_GL layers: deeper stacks run several launches, the
-                    # later ones accumulating (the workspace: the largest chunk's need)
-                    need = [int(lib.gwn_gram_group_workspace_floats(
-                        N, (ctypes.c_int * len(ch))(*[rows_l[i] // N for i in ch]), len(ch)))
-                        for ch in _layer_chunks(L - 1)]
-                    if min(need) > 0:
-                        s["tt_l"] = [e(rows_l[i], 3 * C) for i in range(L - 1)]
-                        s["ws_gram_group"] = e(max(need) + 16)
+            rows_l = [ts[i + 1] * P for i in range(L)]
+            gm = self._group_plan(rows_l[:L - 1], C, cfg.W, 1)
+            gt = self._group_plan(rows_l, 2 * C, C, 2)
+            if gm is not None and gt is not None and L >= 2:
+                s["group_mlp"] = [e(n * (C * cfg.W + C)) for n in gm]
+                s["group_tcn"] = [e(n * (4 * C * C + 2 * C)) for n in gt]
+                s["group_np"] = (gm, gt)
+                s["dh_l"] = [e(r, C) for r in rows_l]
+                s["dfg_l"] = [e(r, 2 * D) for r in rows_l]
+                s["aff_id"] = torch.cat([torch.zeros(C, device=self.device), torch.ones(C, device=self.device),
+                                         torch.zeros(C, device=self.device)])
+            # grouped adaptive-support gradient (gwn_gram_group, fp32 mode): each layer keeps its
+            # t1 / t2 ([rows][96]: the gcn backward's dhcat with only columns 32..96 written)
+            if cfg.adp_live and cfg.use_gcn:
+                # a launch takes at most GRAM_GL layers: deeper stacks run several launches, the
+                # later ones accumulating (the workspace: the largest chunk's need)
+                need = [int(lib.gwn_gram_group_workspace_floats(
+                    N, (ctypes.c_int * len(ch))(*[rows_l[i] // N for i in ch]), len(ch)))
+                    for ch in _layer_chunks(L - 1)]
+                if min(need) > 0:
+                    s["tt_l"] = [e(rows_l[i], 3 * C) for i in range(L - 1)]
+                    s["ws_gram_group"] = e(max(need) + 16)
             if cfg.Cin <= 4 and 256 % C == 0:  # the start conv's weight gradient (narrow form)
                 s["part_start"] = e(max(1, lib.gwn_wgrad_partial_count(ts[0] * P, C, cfg.Cin)) * (C * cfg.Cin + C))
             if cfg.E % 32 == 0 and (cfg.OP // 32) * (cfg.E // 32) <= 16:  # end_conv_2's weight gradient
                 s["part_e2"] = e(max(1, lib.gwn_wgrad_partial_count(tf * P, cfg.OP, cfg.E)) * (cfg.OP * cfg.E + cfg.OP))
-            ge = self._group_plan([tf * P], cfg.OP, cfg.E, 1) if self._group_ok() else None
+            ge = self._group_plan([tf * P], cfg.OP, cfg.E, 1)
             if ge is not None:
                 s["part_e2g"] = (e(ge[0] * (cfg.OP * cfg.E + cfg.OP)), ge[0])
 
-        side_need = [lib.gwn_wgrad_workspace_floats(maxrows, C, cfg.W),
-                     lib.gwn_wgrad_workspace_floats(maxrows, 2 * C, 2 * C),
-                     lib.gwn_gram_workspace_floats(N, maxrows // N)]
-        for (M_, N_, K_) in ((cfg.O, cfg.E, tf * P), (cfg.E, cfg.S, tf * P), (cfg.S, L * D, tf * P)):
-            side_need.append(lib.gwn_gemm_workspace_floats(M_, N_, _ksplit(M_, N_, K_)))
-        s["ws_side"] = e(int(max(side_need)) + 16)
         # support split of the fused gcn kernels (gwn_gcn_args.ksplit): partial sums + per-slice
         # counters (zero, and left zero by every launch)
         if self._fused_gcn() and cfg.use_gcn and cfg.nsup >= 2:
@@ -592,25 +581,22 @@ class Executor:
         # bf16 mode: the adaptive-support gram on tiled operands -- the bf16 16-node tile kernels
         # write X and its hop 1 (forward) and t1 / t2 (backward) in gwn_gram_g4_bf16's layout
         gram_g4 = (training and cfg.adp_params and cfg.use_gcn and sup_batch <= 1 and self._fused_gcn()
-                   and os.environ.get("GWN_GRAM_G4", "1") != "0"
                    and acts.g4bf_arr is not None and acts.g4bt_arr is not None
                    and _lib.load().gwn_gcn_t16b_supported(N, cfg.nsup) == 1)
         acts.gram_g4 = gram_g4
         if getattr(acts, "XG4", None) is None:
             acts.XG4, acts.TG4, acts.CLK = {}, {}, {}
         # bf16 mode: every layer's adaptive-support gram in one gwn_gram_g4_group launch at the end
-        # of the backward (GWN_GRAM_GROUP=0: one gwn_gram_g4_bf16 per layer)
-        if gram_g4 and L >= 2 and getattr(acts, "ws_g4g", None) is None and os.environ.get("GWN_GRAM_GROUP", "1") != "0":
+        # of the backward
+        if gram_g4 and L >= 2 and getattr(acts, "ws_g4g", None) is None:
             need = [int(_lib.load().gwn_gram_g4_group_workspace_floats(
                 N, (ctypes.c_int * len(ch))(*[ts[i + 1] * P // N for i in ch]), len(ch)))
                 for ch in _layer_chunks(L - 1)]
             acts.ws_g4g = (torch.empty(max(need) + 16, device=self.device, dtype=F32) if min(need) > 0
                            else False)
         # bf16 mode: the hop pieces' only reader is then the grouped mlp weight gradient -- stored
-        # as bf16 (half the bytes written here and read there); GWN_BF16_PIECES=0 keeps them fp32
-        pieces_b = (gram_g4 and "group_mlp" in scr and self._group_ok() and self._defer_ok(scr)
-                    and not self._overlap_ok(acts) and self._fuse_ok(acts)
-                    and os.environ.get("GWN_BF16_PIECES", "1") != "0")
+        # as bf16 (half the bytes written here and read there)
+        pieces_b = gram_g4 and "group_mlp" in scr and self._defer_ok(scr) and self._fuse_ok(acts)
         acts.pieces_b = pieces_b
         if pieces_b and (getattr(acts, "HB", None) is None or len(acts.HB) != L - 1):
             acts.HB = [torch.empty(ts[i + 1] * P, 2 * cfg.nsup * cfg.D, device=self.device, dtype=torch.int16)
@@ -832,9 +818,8 @@ class Executor:
 
     def _bn_fold_ok(self, sup_batch):
         """BatchNorm on load needs the fused gcn forward (its epilogue applies the residual affine)
-        and C = 32 (the fold kernel); GWN_BN_FOLD=0 materialises bn(z) instead."""
-        cfg = self.cfg
-        return os.environ.get("GWN_BN_FOLD", "1") != "0" and self._fused_gcn()
+        and C = 32 (the fold kernel); otherwise bn(z) is materialised."""
+        return self._fused_gcn()
 
     def layer_input(self, acts, i):
         """(x, w_fg, b_fg, (mean, scale, shift)) of layer i's gated TCN / residual: the normalised
@@ -1032,17 +1017,14 @@ class Executor:
         if dout is not None:
             dout = dout.contiguous()
             lib.call("gwn_from_nchw_ld", ptr(dout), B, O, N, tf, ptr(sc["dy"]), OP, st)
-        # Weight / adjacency gradients (head wgrads, gwn_wgrad, gwn_gram: off the critical path)
-        # run on a second stream when the fused data path is on (C = 32), overlapping the input
-        # gradients that follow; in the layers the buffers they read (dh, dhcat, dfg) alternate by
-        # layer parity and a layer reuses its parity's buffers only after the side stream finished
-        # the layer + 2.
-        overlap = self._overlap_ok(acts)
+        # (Weight / adjacency gradients on a second stream beside the input gradients were measured
+        # slower in rounds 1, 2 and 5 -- the co-running launches slow the data path more than they
+        # hide, DESIGN.md section 4 -- and are not built.)
         # fused layer backward: BN backward in the gcn_bwd prologue, gate backward in its epilogue,
         # the next BN's statistics in the TCN input-gradient epilogue (3 launches fewer per layer)
         fuse = self._fuse_ok(acts)
         # weight / adjacency gradients as partials, one reduction launch for the whole backward
-        defer = not overlap and fuse and self._defer_ok(sc)
+        defer = fuse and self._defer_ok(sc)
         if getattr(acts, "pieces_b", False) and not (defer and "dh_l" in sc):
             raise RuntimeError("gwn_amd: the forward stored bf16 hop pieces for the grouped weight gradient, "
                                "which this backward does not run")
@@ -1056,21 +1038,12 @@ class Executor:
         gram_g4_group = (defer and getattr(acts, "gram_g4", False) and cfg.adp_live and L >= 2
                          and getattr(acts, "ws_g4g", None) is not None and acts.ws_g4g is not False
                          and len(acts.TG4) == L - 1)
-        main = torch.cuda.current_stream()
-        side = self._side_stream() if overlap else None
 
         def head_wgrad(dY, J, X, Kc, w, b, ldy=None):
             # (the head's weight gradients on a second stream beside its input gradients, joined
             # before the deferred reduction, measured slower: 24.4-24.7k vs 25.0k samples/s,
             # profiles/r05/head_side)
-            if not overlap:
-                wgrad(dY, J, X, Kc, rows_f, w, ws, b, ldy=ldy)
-                return
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                wgrad(dY, J, X, Kc, rows_f, w, sc["ws_side"], b, ldy=ldy)
+            wgrad(dY, J, X, Kc, rows_f, w, ws, b, ldy=ldy)
 
         nt = self._head_nt()
         hb = nt and self.head_bf16()
@@ -1136,7 +1109,6 @@ class Executor:
         else:
             gemm(sc["dsk"], S, 1, self.pk("skip_w"), L * D, 1, sc["dskipcat"], L * D, 1, M=rows_f, N=L * D, K=S)
         yield "head"
-        side_done = {}
         dnext = None
         bufs = [sc["dxa"], sc["dxb"]]
         first_adp = True
@@ -1145,16 +1117,13 @@ class Executor:
             d, sh = cfg.dilations[i], cfg.shift(i)
             rows = ts[i + 1] * P
             dx = bufs[i % 2]
-            par = "" if (i % 2 == 0 or not overlap) else "2"
-            dh, dhc, dfg = sc["dh" + par], sc["dhc" + par], sc["dfg" + par]
+            dh, dhc, dfg = sc["dh"], sc["dhc"], sc["dfg"]
             grouped = defer and "dh_l" in sc
             if grouped:  # this layer's own dh / dfg, read by the grouped weight gradients at the end
                 dh, dfg = sc["dh_l"][i], sc["dfg_l"][i]
             ld_dhc = cfg.W
             if gram_group and i < L - 1:  # this layer's own t1 / t2 (grouped gram at the end)
                 dhc, ld_dhc = sc["tt_l"][i], 3 * C
-            if overlap and (i + 2) in side_done:
-                main.wait_event(side_done[i + 2])
             dxg, ld_dxg, acc = None, 0, 0
             drop = float(self.dropout) if (acts.training and cfg.use_gcn) else 0.0
             if dnext is not None:
@@ -1173,14 +1142,12 @@ class Executor:
                                      accumulate_dadp=0 if first_adp else 1, workspace=ptr(ws),
                                      sup_t=ctypes.cast(acts.supT_arr, ctypes.POINTER(ctypes.c_void_p))
                                      if acts.supT_arr is not None else None,
-                                     skip_weight_grads=1 if (overlap or defer) else 0,
+                                     skip_weight_grads=1 if defer else 0,
                                      # power-schedule backward (the persistent 16-node tile
                                      # kernel: 750 vs 863 us per step for the chained one, 21.3k
-                                     # vs 20.5k samples/s); GWN_GCN_POW_BWD=0 selects the chain
-                                     sup2_t=self._arr_field(getattr(acts, "sup2t_arr", None))
-                                     if os.environ.get("GWN_GCN_POW_BWD", "1") != "0" else None,
-                                     sup_g4_t=self._arr_field(getattr(acts, "g4b_arr", None))
-                                     if os.environ.get("GWN_GCN_POW_BWD", "1") != "0" else None,
+                                     # vs 20.5k samples/s)
+                                     sup2_t=self._arr_field(getattr(acts, "sup2t_arr", None)),
+                                     sup_g4_t=self._arr_field(getattr(acts, "g4b_arr", None)),
                                      sup_g4b_t=self._arr_field(getattr(acts, "g4bt_arr", None)),
                                      tg4=(ptr(acts.TG4[i]) if gram_g4_group else ptr(sc["tg4"]))
                                      if (defer and getattr(acts, "gram_g4", False) and adp_index >= 0) else None,
@@ -1200,8 +1167,6 @@ class Executor:
                     gb.fg, gb.dskip, gb.ld_dskip = ptr(acts.FG[i]), sc["dskipcat"].data_ptr() + 4 * i * D, L * D
                     gb.skip_row0, gb.dfg = (ts[i + 1] - tf) * P, ptr(dfg)
                 lib.call("gwn_gcn_bwd", ctypes.byref(gb), st)
-                if overlap:
-                    self._side_gcn_grads(main, side, acts, i, rows, dh, dhc, adp_index, first_adp, sc)
                 if defer:
                     if not grouped:
                         self._defer_gcn_grads(acts, i, rows, dh, sc, segs, st)
@@ -1219,7 +1184,7 @@ class Executor:
                                  skip_row0=(ts[i + 1] - tf) * P, dfg=ptr(dfg),
                                  dw_fg=ptr(self.gk("fg_w%d" % i)), db_fg=ptr(self.gk("fg_b%d" % i)),
                                  dx=ptr(dx), accumulate_dx=acc, workspace=ptr(ws),
-                                 skip_weight_grads=1 if (overlap or defer) else 0)
+                                 skip_weight_grads=1 if defer else 0)
             if fuse:
                 if dnext is not None:
                     tb.dfg_ready, tb.acc_row0 = 1, sh * P
@@ -1227,8 +1192,6 @@ class Executor:
                     tb.bn_z, tb.bn_mean, tb.bn_rstd = ptr(acts.Z[i - 1]), ptr(acts.mean[i - 1]), ptr(acts.rstd[i - 1])
                     tb.bn_sums = ptr(sc["bnsums"])
             lib.call("gwn_gated_tcn_bwd", ctypes.byref(tb), st)
-            if overlap:
-                side_done[i] = self._side_tcn_grads(main, side, acts, i, rows, dfg, sc)
             if defer:
                 if not grouped:
                     part = sc["part_tcn"][i]
@@ -1243,8 +1206,6 @@ class Executor:
                     self._defer_gram(acts, i, rows, gram_now[0], adp_index, gram_now[1], sc, st)
                     gram_now = None
             dnext = dx
-        if overlap:
-            main.wait_event(side_done[0])  # dadp and every side-stream weight gradient are complete
         # start conv
         rows0 = ts[0] * P
         if defer and "part_start" in sc:
@@ -1288,19 +1249,10 @@ class Executor:
                      ptr(sc["dadp"]), N, 10, cfg.NP, ptr(self.gk("nv1")), ptr(self.gk("nv2")), ptr(ws), st)
 
     # ---------------------------------------------------------------------------------------
-    def _overlap_ok(self, acts):
-        """Weight gradients on a second stream (GWN_OVERLAP=1).  Off by default: with the fused
-        layer backward the main-stream kernels fill the chip, and the side stream's wgrad / gram
-        launches only contend with them (measured 16.62k vs 16.72k samples/s, round 1)."""
-        cfg = self.cfg
-        return (os.environ.get("GWN_OVERLAP", "0") != "0" and cfg.C == 32 and cfg.square and cfg.W % 32 == 0
-                and acts.supT_arr is not None)
-
     def _head_nt(self):
         """Row-tile NT GEMMs for the head (K dims / leading dims multiples of 4)."""
         cfg = self.cfg
-        return (os.environ.get("GWN_HEAD_NT", "1") != "0"
-                and all(v % 4 == 0 for v in (cfg.O, cfg.S, cfg.E, cfg.L * cfg.D)))
+        return all(v % 4 == 0 for v in (cfg.O, cfg.S, cfg.E, cfg.L * cfg.D))
 
     def head_bf16(self):
         """The bf16 mode's head (split_planes 2, configs[2]): the skip convs' and end_conv_1's GEMMs,
@@ -1316,20 +1268,10 @@ class Executor:
         return (os.environ.get("GWN_FUSE_BWD", "1") != "0" and cfg.use_gcn and cfg.C == 32 and cfg.square
                 and cfg.W % 32 == 0 and cfg.N <= 512 and acts.supT_arr is not None)
 
-    def _side_stream(self):
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=self.device)
-        return self._side
-
     def _defer_ok(self, sc):
-        """Deferred weight / adjacency gradients (GWN_DEFER_WGRAD=0: each reduced in its own
-        launches right after its layer)."""
-        return os.environ.get("GWN_DEFER_WGRAD", "1") != "0" and "part_mlp" in sc
-
-    def _group_ok(self):
-        """Grouped weight gradients (gwn_wgrad_group, one launch per weight family for all layers);
-        GWN_WGRAD_GROUP=0 keeps one gwn_wgrad_partials launch per layer (A/B measurements)."""
-        return os.environ.get("GWN_WGRAD_GROUP", "1") != "0"
+        """Deferred weight / adjacency gradients (the fused C = 32 shapes; otherwise each is
+        reduced in its own launches right after its layer)."""
+        return "part_mlp" in sc
 
     @staticmethod
     def _group_plan(rows, J, Kt, ntaps):
@@ -1408,40 +1350,6 @@ class Executor:
         fn = "gwn_gram_bf16" if getattr(acts, "g4bt_arr", None) is not None else "gwn_gram"
         _lib.call(fn, h, t + 4 * C, h + 4 * (1 + 2 * adp_index) * C, t + 4 * 2 * C, W, W, cfg.N, rows // cfg.N,
                   ptr(sc["dadp"]), cfg.NP, 0 if first_adp else 1, ptr(sc["ws"]), st)
-
-    def _side_gcn_grads(self, main, side, acts, i, rows, dh, dhc, adp_index, first_adp, sc):
-        """dW_mlp / db_mlp (gwn_wgrad) and the adaptive-support gradient (gwn_gram) of layer i on
-        the side stream, after the main stream's gcn data path of layer i."""
-        cfg = self.cfg
-        C, W = cfg.C, cfg.W
-        ev = torch.cuda.Event()
-        ev.record(main)
-        side.wait_event(ev)
-        sst, wss = side.cuda_stream, sc["ws_side"]
-        _lib.call("gwn_wgrad", ptr(dh), C, C, ptr(acts.H[i]), W, rows, W, 1, 0, rows,
-                  ptr(self.gk("mlp_w%d" % i)), W, ptr(self.gk("mlp_b%d" % i)), ptr(wss), sst)
-        if adp_index >= 0:
-            h = acts.H[i].data_ptr()
-            t = dhc.data_ptr()
-            _lib.call("gwn_gram", h, t + 4 * C, h + 4 * (1 + 2 * adp_index) * C, t + 4 * 2 * C, W, W, cfg.N,
-                      rows // cfg.N, ptr(sc["dadp"]), cfg.NP, 0 if first_adp else 1, ptr(wss), sst)
-
-    def _side_tcn_grads(self, main, side, acts, i, rows, dfg, sc):
-        """dW_fg / db_fg of layer i (gwn_wgrad over both taps) on the side stream; returns the
-        event that marks the end of layer i's side work."""
-        cfg = self.cfg
-        C = cfg.C
-        P = acts.P
-        ev = torch.cuda.Event()
-        ev.record(main)
-        side.wait_event(ev)
-        xin, _, _, raff = self.layer_input(acts, i)
-        _lib.call("gwn_wgrad_bn", ptr(dfg), 2 * C, 2 * C, xin, C, acts.ts[i] * P, C, 2,
-                  cfg.dilations[i] * P, rows, raff[0], raff[1], raff[2], ptr(self.gk("fg_w%d" % i)), 2 * C,
-                  ptr(self.gk("fg_b%d" % i)), ptr(sc["ws_side"]), side.cuda_stream)
-        done = torch.cuda.Event()
-        done.record(side)
-        return done
 
     def unpack_grads(self, gflat, norm_ws=None):
         """Kernel-layout gradients -> the flat buffer; with norm_ws also the clip-norm partials (the

@@ -154,7 +154,11 @@ class Bf16Pins:
         adopted with band = ``piece_band`` * sum|terms| (the fp32 accumulation error bound of the
         diffusion sum, sum|terms| = |rnd(g)| diffused through |rnd(A)|).
     Every difference that is not such a tie is counted in ``report`` as a violation (the tests
-    require none); adopted ties are counted too."""
+    require none); adopted ties are counted too, with the element count of each operand
+    (``<tag>_total``): the band is a bound per tensor (a fraction of max|g|), so for elements far
+    below the maximum it spans several ulps -- the tests also require the adopted ties to stay a
+    small fraction (1e-3) of the elements (``adopted_fraction``), so that a systematic rounding error
+    cannot be absorbed as ties."""
 
     def __init__(self, sup=None, g=None, pieces=None, sup_tol=1e-5, g_band=2.0 ** -16, piece_band=2.0 ** -19,
                  skr=None, head_band=2.0 ** -19, head_dy=None, head_dband=2.0 ** -18):
@@ -173,6 +177,7 @@ class Bf16Pins:
     def adopt(self, own_b, exact, hip_b, band, tag):
         """own_b = bf16(exact); hip_b = the HIP run's bf16 value: hip_b where it is a rounding tie."""
         diff = own_b != hip_b
+        self.report[tag + "_total"] = self.report.get(tag + "_total", 0) + own_b.numel()
         if not bool(diff.any()):
             return own_b
         _, e = torch.frexp(hip_b)  # hip = m 2^e, 0.5 <= |m| < 1: a bf16 ulp there is 2^(e - 8)
@@ -187,6 +192,11 @@ class Bf16Pins:
             det = list(zip(exact[bad].tolist()[:4], hip_b[bad].tolist()[:4], reach[bad].tolist()[:4]))
             self.report.setdefault(tag + "_bad_detail", []).extend(det)
         return torch.where(ok, hip_b, own_b)
+
+    def adopted_fraction(self):
+        """{tag: adopted / elements} of every operand the pins saw."""
+        return {k[:-len("_total")]: self.report[k[:-len("_total")] + "_adopted"] / max(v, 1)
+                for k, v in self.report.items() if k.endswith("_total")}
 
     def supports(self, sups):
         """the bf16 operands [(rnd(A), rnd(A^2))] of the HIP run's supports (checked)."""
@@ -465,27 +475,31 @@ def masked_metrics(pred, real, null_val=0.0, sign=None):
 
 
 def engine_loss(p, supports, x, real_val, cfg, scaler_mean, scaler_std, bn_state=None, training=True, masks=None,
-                record=None, pins=None):
+                record=None, pins=None, dropout_masks=None):
     """engine.py:41-51 up to the loss: pad 1, forward, inverse scale, masked MAE.
-    masks: optional branches (module docstring; "sign": [B,1,N,T_out] of pred - real)."""
+    masks: optional branches (module docstring; "sign": [B,1,N,T_out] of pred - real);
+    dropout_masks: optional per-layer keep masks [B,C,N,T_i] (forward's)."""
     x = torch.nn.functional.pad(x, (1, 0, 0, 0))
-    out = forward(p, supports, x, cfg, training, bn_state, masks=masks, record=record, pins=pins)
+    out = forward(p, supports, x, cfg, training, bn_state, dropout_masks=dropout_masks, masks=masks, record=record,
+                  pins=pins)
     pred = out.transpose(1, 3) * scaler_std + scaler_mean
     real = real_val.unsqueeze(1)
     mae, mape, rmse = masked_metrics(pred, real, sign=None if masks is None else masks.get("sign"))
     return out, mae, mape, rmse
 
 
-def grads(sd, supports, x, real_val, cfg, scaler_mean, scaler_std, dtype=F64, masks=None, record=None, pins=None):
+def grads(sd, supports, x, real_val, cfg, scaler_mean, scaler_std, dtype=F64, masks=None, record=None, pins=None,
+          dropout_masks=None):
     """Per-parameter gradients of the engine loss (train mode); params that do not reach the
     output get no entry (the reference leaves their .grad None).  masks: optional branch pinning
-    (module docstring)."""
+    (module docstring); dropout_masks: optional per-layer keep masks (``forward``)."""
     p = {k: torch.tensor(np.asarray(v), dtype=dtype, requires_grad=True) for k, v in sd.items()
          if not _is_buffer(k)}
     bn = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in sd.items() if "running" in k}
     sups = [torch.tensor(np.asarray(a), dtype=dtype) for a in supports]
     out, mae, mape, rmse = engine_loss(p, sups, torch.tensor(x, dtype=dtype), torch.tensor(real_val, dtype=dtype),
-                                       cfg, scaler_mean, scaler_std, bn, masks=masks, record=record, pins=pins)
+                                       cfg, scaler_mean, scaler_std, bn, masks=masks, record=record, pins=pins,
+                                       dropout_masks=dropout_masks)
     names = list(p.keys())
     gs = torch.autograd.grad(mae, [p[n] for n in names], allow_unused=True)
     g = {n: gi for n, gi in zip(names, gs) if gi is not None}

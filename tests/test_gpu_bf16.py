@@ -186,6 +186,7 @@ def test_bf16_eval_forward(gpu, name, n, xkey, okey):
     emu = _emulated(g, n, g[xkey], pins=pins).numpy()
     rep = pins.report
     assert rep["g_bad"] == 0 and rep["piece_bad"] == 0 and rep["skr_bad"] == 0 and rep["sup_err"] <= 1e-5, rep
+    assert all(f <= 1e-3 for f in pins.adopted_fraction().values()), pins.adopted_fraction()
     e_emu, e_full, e_f64 = (rel_err(out.cpu().numpy(), emu), rel_err(full.cpu().numpy(), emu),
                             rel_err(out.cpu().numpy(), g[okey]))
     print("bf16 eval forward N=%d: vs pinned bf16 emulation %.2e (full schedule %.2e; ties adopted: g %d, "
@@ -213,6 +214,8 @@ def test_bf16_train_step_grads(gpu, name, n, pre):
           % (name, rep["g_adopted"], rep["piece_adopted"], rep["skr_adopted"], rep["de1_adopted"], rep["dsk_adopted"],
              rep["sup_err"]))
     assert all(rep[k + "_bad"] == 0 for k in ("g", "piece", "skr", "de1", "dsk")) and rep["sup_err"] <= 1e-5, rep
+    print("adopted fractions", {k: "%.1e" % v for k, v in pins.adopted_fraction().items()})
+    assert all(f <= 1e-3 for f in pins.adopted_fraction().values()), pins.adopted_fraction()
     out = acts.y.detach().cpu().double().view(B, n, -1)  # [B, N, T_out] rows (b, n)
     e_fwd = rel_err(out.numpy(), eout[:, :, :, 0].permute(0, 2, 1).numpy())
     print("%s: train-mode output vs pinned emulation %.2e" % (name, e_fwd))
@@ -234,14 +237,15 @@ def test_bf16_train_step_grads(gpu, name, n, pre):
 def test_bf16_vs_fp32_kernels_small_graphs(gpu, n):
     """One- and two-tile graphs (every node-tile count has its own instantiation): a train step
     with dropout 0.3 in bf16 against fp32 on identical inputs and masks -- a sanity bound on the bf16
-    distance (the parity gates are the emulation tests above): worst 0.2, median REPORT_MEDIAN
-    (measured with the bf16 head: N=16 0.103 / 0.060, N=37 0.140 (bn.2.weight) -- B = 4 samples,
-    sign flips of |pred - real|)."""
+    distance (the parity gates are the emulation tests above): every gradient within REPORT_WORST
+    and the median within REPORT_MEDIAN, the reference's own distance under autocast(bfloat16).
+    B = 16 samples: at B = 4 (rounds 3-5) single sign flips of |pred - real| among 4*N*12 labels
+    dominated the distance (N=37: 0.140 on bn.2.weight), at 4x the labels each flip weighs 4x less."""
     from gwn_amd import synthetic, util
     from gwn_amd.engine import trainer
     adj = synthetic.random_sensor_graph(n, density=0.3, seed=n)
     sups = [torch.tensor(a, device=gpu) for a in synthetic.double_transition(adj)]
-    x, y = synthetic.synthetic_batch(4, n, 12, seed=n)
+    x, y = synthetic.synthetic_batch(16, n, 12, seed=n)
     res = []
     for dt in ("fp32", "bf16"):
         torch.manual_seed(999)
@@ -257,7 +261,7 @@ def test_bf16_vs_fp32_kernels_small_graphs(gpu, n):
         if k.endswith("mlp.bias") or np.linalg.norm(v) == 0:
             continue
         e = norm_rel(res[1][1][k], v)
-        assert e <= 0.2, (n, k, e)
+        assert e <= REPORT_WORST, (n, k, e)
         errs.append(e)
     print("bf16 vs fp32 kernels N=%d: worst %.2e, median %.2e" % (n, max(errs), np.median(errs)))
     assert np.median(errs) <= REPORT_MEDIAN
@@ -327,6 +331,32 @@ def test_bf16_training_tracks_fp32_over_30_steps(gpu, monkeypatch):
     assert tail_rel <= 5e-3
     # the floor is itself a draw of the chaos: 0.124 / 7.99e-3 with round 4's dropout stream, 0.044
     # with round 5's (the same arithmetic otherwise), while the bf16 drift measured 0.17 / 1.9e-2 on
-    # both -- so the bound is twice the floor or 6 % of the distance moved / 0.04, whichever is larger
-    assert drift <= max(2.0 * floor, 0.25)
+    # both.  So the rule is twice the floor, with the floor taken as the larger of this run's draw
+    # and the largest draw measured so far (0.124 -> a relative drift bound of 0.25; max-abs: twice
+    # 7.99e-3 is below the bf16 value measured on both streams, 1.9e-2, so that bound is 0.04, about
+    # twice the bf16 measurement, and documents the scale rather than a floor multiple)
+    assert drift <= 2.0 * max(floor, 0.124) + 1e-3
     assert max_abs <= max(2.0 * floor_abs, 0.04)
+
+
+def test_gwn_dtype_env_selects_bf16(gpu, monkeypatch):
+    """GWN_DTYPE=bf16 in the environment (model.py's default compute dtype) is the same mode as
+    gwnet.set_compute_dtype("bf16"): identical eval outputs, and different from fp32."""
+    from gwn_amd import synthetic
+    from gwn_amd.model import gwnet
+    g = load_golden("g13_train_n325.npz")
+    x, _ = synthetic.synthetic_batch(2, 325, 13, seed=4)
+    xd = torch.tensor(x, device=gpu)
+    outs = {}
+    for env, setter in (("bf16", None), ("fp32", "bf16"), ("fp32", None)):
+        monkeypatch.setenv("GWN_DTYPE", env)
+        m = gwnet(gpu, 325, 0.3, supports=[torch.tensor(g["sup0"], device=gpu), torch.tensor(g["sup1"], device=gpu)])
+        m.load_state_dict({k: torch.tensor(v) for k, v in state_dict_of(g).items()})
+        assert m.compute_dtype == env
+        if setter:
+            m.set_compute_dtype(setter)
+        m.eval()
+        with torch.no_grad():
+            outs[(env, setter)] = m(xd).cpu()
+    assert torch.equal(outs[("bf16", None)], outs[("fp32", "bf16")])
+    assert not torch.equal(outs[("bf16", None)], outs[("fp32", None)])

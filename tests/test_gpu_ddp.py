@@ -240,3 +240,9 @@ def test_bench_gpus_2_self_launch(gpu):
     assert dist["backend"] == "gloo" and dist["world_seen"] == 2
     assert 0 < dist["rank_seconds_min"] <= dist["rank_seconds_max"]
     assert abs(rec["ms_per_step"] - 1000.0 * dist["rank_seconds_max"] / 3) < 0.01
+    # the collectives' device time and the overlapped share of the early all-reduce (outside the
+    # timed region): the early range on the side stream, the rest on the main stream
+    ar = dist["allreduce"]
+    assert ar["overlap"] is True and ar["steps"] == 5 and ar["grad_floats"] > 0
+    assert ar["early_allreduce_ms"] > 0 and ar["rest_allreduce_ms"] > 0 and ar["layers_backward_ms"] > 0
+    assert 0 <= ar["early_overlapped_ms"] <= ar["early_allreduce_ms"] + 1e-3

@@ -35,12 +35,14 @@ def _loader_views(x, y, device):
     return tx, ty
 
 
-def _check(got, ref, tag):
+def _check(got, ref, tag, dropout=False):
+    """Every gradient norm-rel <= 1e-4; the gconv biases (BatchNorm cancels a per-channel constant:
+    analytically 0) absolutely -- unless dropout scales them per element (then they are live)."""
     assert set(got) == set(ref), (tag, sorted(set(got) ^ set(ref)))
     scale = max(float(np.max(np.abs(v))) for v in ref.values())
     for k, v in ref.items():
         g = got[k]
-        if k.startswith("gconv.") and k.endswith("mlp.bias"):
+        if k.startswith("gconv.") and k.endswith("mlp.bias") and not dropout:
             assert np.max(np.abs(g)) <= 1e-5 * scale, (tag, k)
         elif np.linalg.norm(v) > 0:
             assert norm_rel(g, v) <= 1e-4, (tag, k, norm_rel(g, v))
@@ -56,7 +58,7 @@ def _trainer(device, n, sups, sd, dropout=0.0):
     return eng
 
 
-def _untie(sd, sups, x, y, n, margin=1e-3):
+def _untie(sd, sups, x, y, n, margin=1e-3, cfg=None, dropout_masks=None):
     """Labels moved away from near-ties with the fp64 prediction.  The masked-MAE gradient is
     sign(pred - real) (util.py:524): a label within fp32 rounding of its prediction takes either
     sign in two equally valid fp32 evaluations, and one flipped element out of B*N*12 moves every
@@ -69,7 +71,8 @@ def _untie(sd, sups, x, y, n, margin=1e-3):
     bn = {k: torch.tensor(np.asarray(v), dtype=f64) for k, v in sd.items() if "running" in k}
     with torch.no_grad():
         out = orc.engine_loss(p, [torch.tensor(np.asarray(a), dtype=f64) for a in sups], torch.tensor(x, dtype=f64),
-                              torch.tensor(y, dtype=f64), orc.Cfg(n), 54.4, 19.5, bn)[0]
+                              torch.tensor(y, dtype=f64), cfg if cfg is not None else orc.Cfg(n), 54.4, 19.5, bn,
+                              dropout_masks=dropout_masks)[0]
     pred = (out.transpose(1, 3) * 19.5 + 54.4)[:, 0].numpy()
     d = pred - y
     tie = (np.abs(d) < margin) & (y != 0)
@@ -129,6 +132,69 @@ def test_headline_b64_train_step_grads_vs_oracle(gpu):
     got2 = {k: p.grad.detach().cpu().numpy() for k, p in eng.model.named_parameters() if p.grad is not None}
     for k in got:
         np.testing.assert_array_equal(got[k], got2[k], err_msg=k)
+
+
+def host_dropout_masks(seed, cfg, B, n, C, T0):
+    """libgwn's dropout keep masks of every layer, rebuilt on the host (gwn_uniform of the device
+    counter ``seed``, salt = layer, element index ((t*B + b)*N + node)*C + c of the layer's
+    [T][B][N][C] output rows), in the oracle's [B, C, N, T] layout."""
+    from test_gpu_model import _np_uniform
+    masks, T = [], T0
+    for i, d in enumerate(cfg.dilations):
+        T -= d
+        idx = np.arange(T * B * n * C, dtype=np.int64)
+        keep = (_np_uniform(seed, i, idx) >= np.float32(cfg.dropout)).reshape(T, B, n, C)
+        masks.append(torch.tensor(keep.transpose(1, 3, 2, 0).astype(np.float64)))
+    return masks
+
+
+def test_headline_b64_dropout_train_step_vs_oracle(gpu):
+    """The bench's own step: trainer.train at B=64, N=207, C=32 with dropout 0.3 -- the 16-node tile
+    forward (its fused gated TCN on the layers with a slice per CU or more) and backward apply the
+    counter masks.  The masks are rebuilt on the host from the step's seed and fed to the fp64
+    oracle (forward(dropout_masks=...)); output max-rel <= 1e-4, every gradient norm-rel <= 1e-4,
+    metrics and BN running stats as in the dropout-0 headline test, same branch pinning.  The
+    dropped fraction is ~0.3 per layer and the step advances the counter by one."""
+    from gwn_amd import synthetic
+    from oracle import gwnet_oracle as orc
+    n, B, drop = 207, 64, 0.3
+    g = load_golden("g12_metr_n207.npz")
+    sd = state_dict_of(g)
+    sups = [g["sup0"], g["sup1"]]
+    x, y = synthetic.synthetic_batch(B, n, 12, seed=66)
+    eng = _trainer(gpu, n, sups, sd, dropout=drop)
+    ex = eng.model.executor()
+    seed = int(ex.seed.item())
+    cfg = orc.Cfg(n, dropout=drop)
+    dmasks = host_dropout_masks(seed, cfg, B, n, 32, 13)
+    for mk in dmasks:
+        assert 0.29 < 1.0 - float(mk.mean()) < 0.31
+    y, _ = _untie(sd, sups, x, y, n, cfg=cfg, dropout_masks=dmasks)
+    tx, ty = _loader_views(x, y, gpu)
+    met = eng.train(tx, ty)
+    assert int(ex.seed.item()) == seed + 1
+    masks = _gpu_branch(eng, B, n)
+    (acts,) = list(eng._acts.values())
+    out_gpu = acts.y.detach().cpu().double().view(1, B, n, 12).permute(1, 3, 2, 0).numpy()
+    rec = {}
+    rout, rmet, rg, rbn = orc.grads(sd, sups, x, y, cfg, 54.4, 19.5, masks=masks, record=rec, dropout_masks=dmasks)
+    for key in ("skip", "e1"):
+        pre = rec[key].numpy()
+        flip = masks[key].numpy().astype(bool) != (pre > 0)
+        assert np.all(np.abs(pre[flip]) <= 1e-5 * float(np.max(np.abs(pre)))), (key, int(flip.sum()))
+    assert rel_err(out_gpu, rout.numpy()) <= 1e-4, rel_err(out_gpu, rout.numpy())
+    np.testing.assert_allclose(met, rmet, rtol=1e-4)
+    got = {k: p.grad.detach().cpu().numpy() for k, p in eng.model.named_parameters() if p.grad is not None}
+    _check(got, {k: v.numpy() for k, v in rg.items()}, "b64 dropout", dropout=True)
+    sdn = eng.model.state_dict()
+    for k, v in rbn.items():
+        assert rel_err(sdn[k].cpu().numpy(), v.numpy()) <= 1e-5, k
+    # a second (graph-captured) step draws the next masks: the output moves
+    eng.train(tx, ty)
+    assert int(ex.seed.item()) == seed + 2
+    (acts2,) = list(eng._acts.values())
+    out2 = acts2.y.detach().cpu().double().view(1, B, n, 12).permute(1, 3, 2, 0).numpy()
+    assert rel_err(out2, out_gpu) > 1e-3
 
 
 def test_pems_n325_train_step_grads_vs_reference(gpu):

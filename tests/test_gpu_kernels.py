@@ -769,7 +769,7 @@ def test_gcn_fused_schedules_agree(gpu, n, monkeypatch):
 
 @pytest.mark.parametrize("bn", [False, True])
 @pytest.mark.parametrize("n,B,t_out,d,planes", [(207, 32, 8, 2, 0), (37, 64, 5, 1, 0), (207, 8, 3, 1, 0),
-                                                (325, 32, 8, 1, 2)])
+                                                (325, 32, 8, 1, 2), (207, 64, 10, 1, 0)])
 # (planes 2: the bf16-mlp pair forward, where the TCN stays a separate launch -- fused there it was
 #  7.5 % slower per PEMS step, profiles/r05/tcn_fused -- so both sides of the comparison are the
 #  two-launch path and must agree bitwise)
@@ -785,7 +785,9 @@ def test_gcn_fwd_fused_tcn(gpu, n, B, t_out, d, bn, planes):
     workgroup of the fused launch, or gwn_batchnorm_fwd_fold first): its outputs (mean, rstd,
     scale, running statistics, num_batches_tracked, w_fold, b_fold) against fp64 as well.  planes 2:
     the bf16-mlp pair forward (configs[2]), which takes the TCN as its own launch.  The fused call
-    also carries gwn_gcn_args.clock (bench.py's timing): every workgroup's (start, end) stamped."""
+    also carries gwn_gcn_args.clock (bench.py's timing): every workgroup's (start, end) stamped.
+    (207, 64, 10): 640 slices, 2.5 per CU -- the tile ranges straddle slices, the pipelined staging's
+    ranges touch 3-4 slices (items of several slices interleaved, boundary slices' TCN in two CUs)."""
     import ctypes
     from gwn_amd import _lib
     lib = _lib.load()
@@ -1015,6 +1017,25 @@ def test_gcn_split_many_slices_bn_prologue_gate_epilogue(gpu, pw):
         assert int(kcnt.abs().sum()) == 0
         outs.append((h.clone(), z.clone(), _bn_all(bnp, rows, n, C, K, NP), dres.clone(), dh_out.clone(), dfg.clone(),
                      dhc[:, C:3 * C].clone(), dg.clone(), db.clone()))
+    # against fp64 with the host-rebuilt masks: the forward's dropout (salt 2) on the mlp output
+    # of the kernel's own pieces plus the BN-on-load residual; the backward's BN-backward prologue
+    # and its dropout (salt 4): dres = dz, dh_out = dz * keep / (1 - p)
+    from test_gpu_model import _np_uniform
+    for o in outs:
+        keep_f = torch.tensor(_np_uniform(5, 2, np.arange(rows * C, dtype=np.int64)).reshape(rows, C) >= 0.3,
+                              dtype=torch.float64)
+        zr = (o[0].double().cpu() @ wm.double().cpu().t() + bm.double().cpu()) * keep_f / 0.7 \
+            + (res.double().cpu() - rmean.double().cpu()) * rscale.double().cpu() + rshift.double().cpu()
+        assert rel_err(o[1].cpu().numpy(), zr.numpy()) <= 4e-6
+        zb, dyb = bn_z.double().cpu(), bn_dy.double().cpu()
+        k1, k2 = sums[:C].double().cpu() / rows, sums[C:].double().cpu() / rows
+        rs_, gm_ = brstd.double().cpu(), gamma.double().cpu()
+        dz = gm_ * rs_ * (dyb - k1 - (zb - bmean.double().cpu()) * rs_ * k2)
+        keep_b = torch.tensor(_np_uniform(5, 4, np.arange(rows * C, dtype=np.int64)).reshape(rows, C) >= 0.3,
+                              dtype=torch.float64)
+        assert rel_err(o[3].cpu().numpy(), dz.numpy()) <= 2e-6
+        assert rel_err(o[4].cpu().numpy(), (dz * keep_b / 0.7).numpy()) <= 2e-6
+        assert np.array_equal((o[4] == 0).cpu().numpy(), keep_b.numpy() == 0)
     # (pw: the whole slices run the 16-node tile kernels, the split the 32-node ones -- products
     # and BN merges in other orders than the split's)
     for a_, b_ in zip(*outs):
@@ -1090,7 +1111,16 @@ def test_gcn_pow_forward_modes(gpu, n):
     assert rel_err(z.cpu().numpy(), Z.numpy()) <= 4e-6
     _, zp, _ = run(True, drop=0.3)
     _, zc, _ = run(False, drop=0.3)
-    assert torch.equal(zp == res, zc == res)
+    # the dropped set is gwn_uniform(seed 99, salt 3, row*C + c) < p rebuilt on the host, and the
+    # kept values carry the 1/(1-p) scale (fp64 of the same pieces)
+    from test_gpu_model import _np_uniform
+    keep = _np_uniform(99, 3, np.arange(rows * C, dtype=np.int64)).reshape(rows, C) >= np.float32(0.3)
+    assert 0.28 < 1.0 - keep.mean() < 0.32
+    zd = (H @ wm.double().cpu().t() + bm.double().cpu()) * torch.tensor(keep, dtype=torch.float64) / 0.7 \
+        + res.double().cpu()
+    for zz in (zp, zc):
+        assert np.array_equal((zz == res).cpu().numpy(), ~keep)
+        assert rel_err(zz.cpu().numpy(), zd.numpy()) <= 4e-6
     assert rel_err(zp.cpu().numpy(), zc.cpu().numpy()) <= 1e-5
     rm, rv = torch.randn(C, device=gpu), torch.rand(C, device=gpu) + 0.5
     g_, b_ = torch.randn(C, device=gpu), torch.randn(C, device=gpu)

@@ -18,7 +18,7 @@ mkdir -p "$ROOT/graph-wavenet_amd/gwn_amd/exp"
 HIPCC=/opt/rocm/bin/hipcc
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I$ROOT/include"
 pids=()
-for f in $(cd "$ROOT/graph-wavenet_amd/csrc" && ls *.hip | sed 's/\.hip$//'); do
+for f in $(cd "$D/g/csrc" && ls *.hip | sed 's/\.hip$//'); do
   $HIPCC $FLAGS -c -o "$D/$f.o" "$D/g/csrc/$f.hip" & pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
