@@ -1231,10 +1231,13 @@ __device__ __forceinline__ void t16_bwd_put(float* img, int rows, int w, int q, 
 
 // t16_bwd_stage's BatchNorm prologue into the bf16 channel-major images: work unit = (slice, 4
 // consecutive nodes, channel quad), 4 dy / z row loads of 16 B, then dres / dh_out (the
-// workgroup's own rows) as 16-B stores and one 8-B LDS write per channel (4 nodes' bf16)
+// workgroup's own rows) as 16-B stores and one 8-B LDS write per channel (4 nodes' bf16).
+// pair_shift 1: rg ranges over (slice pair, tile) units (gcn_bwd_t16b2_kernel), the own rows of
+// slice s are its pair s >> 1's tiles in the range
 template <typename Mid>
 __device__ __forceinline__ void t16_bwd_stage_bn_bf16(const FusedBwd& a, __bf16* imgs, int imgb, int s0, int nsl,
-                                                      const T16Range& rg, int nt, int n, int s16, Mid mid) {
+                                                      const T16Range& rg, int nt, int n, int s16, Mid mid,
+                                                      int pair_shift = 0) {
   const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
   const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
   const int q = threadIdx.x & 7;  // blockDim % 8 == 0: every unit of a thread has channel quad q
@@ -1267,7 +1270,7 @@ __device__ __forceinline__ void t16_bwd_stage_bn_bf16(const FusedBwd& a, __bf16*
       first = false;
     }
     if (!ok) continue;
-    const long sb = (long)(s0 + sl) * nt;
+    const long sb = (long)((s0 + sl) >> pair_shift) * nt;
     const long t0 = max(rg.tb - sb, 0l), t1 = min(rg.te - sb, (long)nt);
     float v[4][4];  // [node][channel]
 #pragma unroll
@@ -1516,6 +1519,125 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
         }
         t16_st4(a.dfg + m * 2 * CH + 2 * c0, make_float4(o[0], o[1], o[2], o[3]));
         t16_st4(a.dfg + m * 2 * CH + 2 * c0 + 4, make_float4(o[4], o[5], o[6], o[7]));
+      }
+    }
+    p0 = p1;
+  }
+}
+
+// Two slices per wave in the bf16-mlp backward (gcn_fwd_t16b2_kernel's unit: slice pair 2q, 2q + 1
+// x node tile): each transposed-support fragment feeds both slices' diffusion MFMAs and each
+// channel-map fragment both mlps (W^T after diffusion, t1 / t2 of the adaptive support); the
+// BN-backward prologue stages the pairs' dh images (dres / dh_out for the workgroup's own pair
+// tiles), the epilogue is the gate backward (or the dxg store) of each slice.  12-wave workgroups
+// (the forward pair kernel's register budget).  An odd last slice: B diffuses A's image and stores
+// nothing.
+template <int MAXT>
+__global__ __launch_bounds__(MAXT) void gcn_bwd_t16b2_kernel(const FusedBwd a, const PowSup p, const int maximg) {
+  extern __shared__ float lds[];
+  const int n = a.n;
+  const int nt = (n + 15) >> 4;
+  const int s16 = t16b_s16(n), imgb = CH * s16;  // bf16 elements per image
+  float* ws = lds;
+  __bf16* imgs = (__bf16*)(ws + (2 * a.nsup + 1) * CH * LDW16 + T16_WAVES * 3 * CH);
+  const __bf16* maps = (const __bf16*)ws;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  const int nwaves = blockDim.x >> 6;
+  const int pairs = (a.slices + 1) / 2;
+  const T16Range rg = t16_range(pairs, nt);
+  if (a.bn_dy && blockIdx.x == 0 && threadIdx.x < CH) {
+    if (a.bn_dbeta) a.bn_dbeta[threadIdx.x] = a.bn_sums[threadIdx.x];
+    if (a.bn_dgamma) a.bn_dgamma[threadIdx.x] = a.bn_sums[CH + threadIdx.x];
+  }
+  for (long p0 = rg.tb; p0 < rg.te;) {
+    const int q0 = (int)(p0 / nt);
+    const long p1 = min(rg.te, (long)(q0 + maximg / 2) * nt);
+    const int q1 = (int)((p1 - 1) / nt);
+    const int s0 = 2 * q0, s1 = min(2 * q1 + 2, a.slices) - 1;
+    if (p0 != rg.tb) __syncthreads();
+    const bool first = p0 == rg.tb;
+    auto mid = [&] {
+      if (first) t16_stage_maps_bf16(a.w_mlp, a.ld_w, true, 2 * a.nsup + 1, (__bf16*)ws);
+    };
+    if (a.bn_dy) t16_bwd_stage_bn_bf16(a, imgs, imgb, s0, s1 - s0 + 1, rg, nt, n, s16, mid, 1);
+    else stage_bf16_octets(a.dh + (long)s0 * n * CH, CH, n, s16, s1 - s0 + 1, imgs, imgb, mid);
+    __syncthreads();
+    const int span = (int)(p1 - p0);
+    for (int tp = wave; tp < span; tp += nwaves) {
+      const long t = p0 + tp;
+      const int q = (int)(t / nt), tile = (int)(t - (long)q * nt);
+      const int sA = 2 * q, sB = 2 * q + 1;
+      const bool okB = sB < a.slices;
+      const __bf16* xsA = imgs + (sA - s0) * imgb;
+      const __bf16* xsB = okB ? imgs + (sB - s0) * imgb : xsA;
+      const int w0 = 16 * tile;
+      f32x4v dxA[2], dxB[2];
+      dxA[0] = dxA[1] = dxB[0] = dxB[1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      // the channel maps take bf16(dh): the staged images' node columns
+      const bf16x8m dbA = t16_img_col_b(xsA, s16, w0, lane), dbB = t16_img_col_b(xsB, s16, w0, lane);
+      t16_mlp_bp2(maps, 0, dbA, dbB, lane, dxA, dxB);
+      for (int k = 0; k < a.nsup; ++k) {
+        f32x4v eA[2][2], eB[2][2];
+        t16b_diffuse2(xsA, xsB, (const __bf16*)p.g4[2 * k], (const __bf16*)p.g4[2 * k + 1], n, tile, lane, eA, eB);
+        const bf16x8m e1A = t16_pack_b(eA[0]), e1B = t16_pack_b(eB[0]);
+        t16_mlp_bp2(maps, 1 + 2 * k, e1A, e1B, lane, dxA, dxB);
+        t16_mlp_bp2(maps, 2 + 2 * k, t16_pack_b(eA[1]), t16_pack_b(eB[1]), lane, dxA, dxB);
+        if (k == a.adp_index) {  // t1 = W1^T dh + W2^T (A dh), t2 = W2^T dh
+          f32x4v tA[2], tB[2];
+          tA[0] = tA[1] = tB[0] = tB[1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+          t16_mlp_bp2(maps, 1 + 2 * k, dbA, dbB, lane, tA, tB);
+          t16_mlp_bp2(maps, 2 + 2 * k, e1A, e1B, lane, tA, tB);
+          if (a.tg4) {
+            t16_store_g4(a.tg4, 0, a.slices, sA, nt, tile, lane, tA);
+            if (okB) t16_store_g4(a.tg4, 0, a.slices, sB, nt, tile, lane, tB);
+          } else {
+            t16_store(a.t1 + (long)sA * n * a.ld_t, a.ld_t, tA, w0, lane, n);
+            if (okB) t16_store(a.t1 + (long)sB * n * a.ld_t, a.ld_t, tB, w0, lane, n);
+          }
+          tA[0] = tA[1] = tB[0] = tB[1] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+          t16_mlp_bp2(maps, 2 + 2 * k, dbA, dbB, lane, tA, tB);
+          if (a.tg4) {
+            t16_store_g4(a.tg4, 1, a.slices, sA, nt, tile, lane, tA);
+            if (okB) t16_store_g4(a.tg4, 1, a.slices, sB, nt, tile, lane, tB);
+          } else {
+            t16_store(a.t2 + (long)sA * n * a.ld_t, a.ld_t, tA, w0, lane, n);
+            if (okB) t16_store(a.t2 + (long)sB * n * a.ld_t, a.ld_t, tB, w0, lane, n);
+          }
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !okB) break;
+        const long row0 = (long)(h ? sB : sA) * n;
+        const f32x4v* dx = h ? dxB : dxA;
+        if (!a.dfg) {
+          t16_store(a.dxg + row0 * a.ld_dxg, a.ld_dxg, dx, w0, lane, n);
+          continue;
+        }
+        // gate backward (gate_bwd_kernel's arithmetic): g = dxg (+ dskip) -> dfg via (tanh f, sigmoid s)
+        const int w = w0 + j;
+        if (w >= n) continue;
+        const long m = row0 + w;
+        const bool sk = a.dskip && m >= a.skip_row0;
+#pragma unroll
+        for (int oh = 0; oh < 2; ++oh) {
+          const int c0 = 16 * oh + 4 * g;
+          const float4 f0 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0);
+          const float4 f1 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0 + 4);
+          const float4 dq = sk ? *(const float4*)(a.dskip + (m - a.skip_row0) * a.ld_dskip + c0) : make_float4(0, 0, 0, 0);
+          const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+          const float dv[4] = {dq.x, dq.y, dq.z, dq.w};
+          float o[8];
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) {
+            const float gv = dx[oh][e2] + dv[e2];
+            const float f = fv[2 * e2], sg = fv[2 * e2 + 1];
+            o[2 * e2] = gv * sg * (1.0f - f * f);
+            o[2 * e2 + 1] = gv * f * sg * (1.0f - sg);
+          }
+          t16_st4(a.dfg + m * 2 * CH + 2 * c0, make_float4(o[0], o[1], o[2], o[3]));
+          t16_st4(a.dfg + m * 2 * CH + 2 * c0 + 4, make_float4(o[4], o[5], o[6], o[7]));
+        }
       }
     }
     p0 = p1;
@@ -1856,8 +1978,32 @@ int gwn_gcn_fused_bwd_launch(const gwn_gcn_bwd_args* g, const float* const* supT
       PowSup p = {};
       for (int k = 0; k < 2 * g->nsup; ++k) p.g4[k] = (const float*)g->sup_g4b_t[k];
       a.ksplit = 1;
-      if (g->split_planes == 2) gcn_bwd_t16_kernel<1024, true, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
-      else gcn_bwd_t16_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      // the bf16-mlp backward takes two slices per wave (gcn_bwd_t16b2_kernel, 12-wave workgroups)
+      const int pairs = (slices + 1) / 2;
+      const long units2 = (long)pairs * nt;
+      const int grid2 = (int)(units2 < gwn_device_cus() ? units2 : gwn_device_cus());
+      const long per2 = (units2 + grid2 - 1) / grid2;
+      int gmax2 = (int)((T16_LDS_MAX - fixed) / (2 * img));
+      gmax2 = gmax2 < T16_MAXIMG / 2 ? gmax2 : T16_MAXIMG / 2;
+      const int span2 = (int)((per2 - 1 + nt - 1) / nt) + 1;
+      const int maximg2 = 2 * (gmax2 < span2 ? gmax2 : span2);
+      // (pairs only from ~10 units per CU: at PEMS' 192-slice layer, 7.9 per CU, the pair kernel's
+      // 12 waves were 44.0 against 42.6 us; 256 slices 38.9 vs 42.8, 768 slices 92.8 vs 98.8)
+      if (g->split_planes == 2 && gmax2 >= 1 && units2 >= 10L * grid2) {
+        static bool attr2 = false;
+        if (!attr2) {
+          (void)hipFuncSetAttribute((const void*)gcn_bwd_t16b2_kernel<768>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    T16_LDS_MAX);
+          attr2 = true;
+        }
+        size_t lds2 = fixed + maximg2 * img;
+        if (lds2 < 81 * 1024) lds2 = 81 * 1024;
+        gcn_bwd_t16b2_kernel<768><<<grid2, 768, lds2, s>>>(a, p, maximg2);
+      } else if (g->split_planes == 2) {
+        gcn_bwd_t16_kernel<1024, true, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      } else {
+        gcn_bwd_t16_kernel<1024, true><<<grid, 64 * T16_WAVES, lds, s>>>(a, p, maximg);
+      }
       GWN_CHECK_LAUNCH();
       return GWN_OK;
     }

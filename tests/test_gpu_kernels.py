@@ -1548,7 +1548,8 @@ def _from_g4(buf, which, slices, n):
 
 
 @pytest.mark.parametrize("n", [16, 207, 325])
-@pytest.mark.parametrize("mode", ["bn_gate", "bn_gate_tg4", "plain", "bn_gate_tg4_mlp", "plain_mlp"])
+@pytest.mark.parametrize("mode", ["bn_gate", "bn_gate_tg4", "plain", "bn_gate_tg4_mlp", "plain_mlp",
+                                  "bn_gate_tg4_mlp_pairs", "plain_mlp_pairs"])
 def test_gcn_t16_bf16_backward(gpu, n, mode):
     """The bf16 16-node tile backward (gcn_bwd_t16_kernel<1024, true>: gwn_gcn_bwd_args.sup_g4b_t,
     split_planes 1) against fp64, kernel level (model.py:41-55 backward): the BN-backward prologue
@@ -1565,14 +1566,21 @@ def test_gcn_t16_bf16_backward(gpu, n, mode):
     diffusion of dh) within its accumulation error (2^-19 of the sum of |terms|) of a bf16 rounding
     boundary may round the other way in the kernel: each such tie is allowed its one bf16 ulp times
     |bf16(W_q)| in the outputs it feeds (_tie_allow), on top of the same 2e-5 -- per element, so a
-    wrong operand or product still fails (a fixed 3e-4 of the max had to grow with every new draw)."""
+    wrong operand or product still fails (a fixed 3e-4 of the max had to grow with every new draw).
+    *_pairs (n = 207): 2 * ceil(10 * CUs / 13) + 1 slices (395), so the launch takes
+    gcn_bwd_t16b2_kernel (two slices per wave from ~10 pair units per CU), with an odd last slice."""
     import ctypes
     from gwn_amd import _lib
     from test_gpu_model import _np_uniform
+    pairs = mode.endswith("_pairs")
+    if pairs and n != 207:
+        pytest.skip("the pair kernel's case runs at the bench's n = 207")
+    mode = mode.replace("_pairs", "")
     planes = 2 if mode.endswith("_mlp") else 1
     mode = mode.replace("_mlp", "")
     torch.manual_seed(n + 11)
-    C, K, S = 32, 3, 21
+    nt_ = (n + 15) // 16  # pairs: the fewest slices that give ~10 pair units per CU, odd
+    C, K, S = 32, 3, (2 * -(-10 * torch.cuda.get_device_properties(0).multi_processor_count // nt_) + 1 if pairs else 21)
     NP = (n + 31) // 32 * 32
     W = (2 * K + 1) * C
     rows = S * n
@@ -1630,6 +1638,13 @@ def test_gcn_t16_bf16_backward(gpu, n, mode):
                          **kw)
     _lib.call("gwn_gcn_bwd", ctypes.byref(gb), _lib.stream())
     torch.cuda.synchronize()
+    if pairs:  # bitwise the same on a second launch (build.sh: the packed-fp32 hazard it avoids)
+        keep_out = [t.clone() for t in (dhc, dfg if bn else dhc, tg4 if tg4 is not None else dhc)]
+        for _ in range(2):
+            _lib.call("gwn_gcn_bwd", ctypes.byref(gb), _lib.stream())
+            torch.cuda.synchronize()
+            for a_, b_ in zip(keep_out, (dhc, dfg if bn else dhc, tg4 if tg4 is not None else dhc)):
+                assert torch.equal(a_, b_)
     # fp64: the BN-backward prologue and dropout (gwn_uniform rebuilt on the host)
     if bn:
         z, dy = bn_z.double().cpu(), bn_dy.double().cpu()

@@ -19,7 +19,9 @@ HIPCC=/opt/rocm/bin/hipcc
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I$ROOT/include"
 pids=()
 for f in $(cd "$D/g/csrc" && ls *.hip | sed 's/\.hip$//'); do
-  $HIPCC $FLAGS -c -o "$D/$f.o" "$D/g/csrc/$f.hip" & pids+=($!)
+  fl="$FLAGS"  # as build.sh: no packed fp32 ops in the GCN tile kernels
+  case " gcn_fused gcn_slice " in *" $f "*) fl="$FLAGS -Xclang -target-feature -Xclang -packed-fp32-ops" ;; esac
+  $HIPCC $fl -c -o "$D/$f.o" "$D/g/csrc/$f.hip" 2>/dev/null & pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
 $HIPCC --offload-arch=gfx950 -shared -fPIC -o "$ROOT/graph-wavenet_amd/gwn_amd/exp/libgwn_$name.so" "$D"/*.o
