@@ -637,6 +637,9 @@ __device__ __forceinline__ void t16_tcn_load(const TcnLds* tp, int s, int w0, in
   const int off = node < n ? (int)((row * CH + 16 * (g & 1)) * 4) : 0x7ffffff0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) xq[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 16 * q, 0));
+  // all four in flight before the first use: left to the scheduler, each load was sunk next to
+  // its first product behind its own vmcnt(0) -- four serial memory round trips per unit
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // one unit: the products, the gate, the image rows (zero past n) and the global outputs
@@ -1407,6 +1410,39 @@ __device__ __forceinline__ void t16_store(float* out, long ld, const f32x4v* acc
   for (int oh = 0; oh < 2; ++oh) t16_st4(p + 16 * oh, make_float4(acc[oh][0], acc[oh][1], acc[oh][2], acc[oh][3]));
 }
 
+// the tile epilogue's gate backward for node row m (lane group g: channels 16 oh + 4 g .. + 3):
+// dfg = (g sigma (1 - f^2), g f sigma (1 - sigma)) with g = dx (+ dskip) and the saved (tanh f,
+// sigmoid sigma) pairs.  Both channel halves' fg / dskip rows are requested before the first
+// use: one memory round trip per tile instead of two.
+__device__ __forceinline__ void t16_gate_bwd(const FusedBwd& a, const f32x4v* dx, long m, int g) {
+  const bool sk = a.dskip && m >= a.skip_row0;
+  float4 f0[2], f1[2], dq[2];
+#pragma unroll
+  for (int oh = 0; oh < 2; ++oh) {
+    const int c0 = 16 * oh + 4 * g;
+    f0[oh] = *(const float4*)(a.fg + m * 2 * CH + 2 * c0);
+    f1[oh] = *(const float4*)(a.fg + m * 2 * CH + 2 * c0 + 4);
+    dq[oh] = sk ? *(const float4*)(a.dskip + (m - a.skip_row0) * a.ld_dskip + c0) : make_float4(0, 0, 0, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int oh = 0; oh < 2; ++oh) {
+    const int c0 = 16 * oh + 4 * g;
+    const float fv[8] = {f0[oh].x, f0[oh].y, f0[oh].z, f0[oh].w, f1[oh].x, f1[oh].y, f1[oh].z, f1[oh].w};
+    const float dv[4] = {dq[oh].x, dq[oh].y, dq[oh].z, dq[oh].w};
+    float o[8];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+      const float gv = dx[oh][e2] + dv[e2];
+      const float f = fv[2 * e2], sg = fv[2 * e2 + 1];
+      o[2 * e2] = gv * sg * (1.0f - f * f);
+      o[2 * e2 + 1] = gv * f * sg * (1.0f - sg);
+    }
+    t16_st4(a.dfg + m * 2 * CH + 2 * c0, make_float4(o[0], o[1], o[2], o[3]));
+    t16_st4(a.dfg + m * 2 * CH + 2 * c0 + 4, make_float4(o[4], o[5], o[6], o[7]));
+  }
+}
+
 // BF: bf16 operands in the diffusion (the bf16 forward's image / support layouts: sup_g4b_t), the
 // tile's fp32 dh rows for the channel maps of piece 0 and t1 / t2 read back from dh_out (written by
 // this workgroup's prologue for its own rows) or dh
@@ -1499,27 +1535,7 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16_kernel(const FusedBwd a, con
       // gate backward (gate_bwd_kernel's arithmetic): g = dxg (+ dskip) -> dfg via (tanh f, sigmoid s)
       const int w = w0 + j;
       if (w >= n) continue;
-      const long m = row0 + w;
-      const bool sk = a.dskip && m >= a.skip_row0;
-#pragma unroll
-      for (int oh = 0; oh < 2; ++oh) {
-        const int c0 = 16 * oh + 4 * g;
-        const float4 f0 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0);
-        const float4 f1 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0 + 4);
-        const float4 dq = sk ? *(const float4*)(a.dskip + (m - a.skip_row0) * a.ld_dskip + c0) : make_float4(0, 0, 0, 0);
-        const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-        const float dv[4] = {dq.x, dq.y, dq.z, dq.w};
-        float o[8];
-#pragma unroll
-        for (int e2 = 0; e2 < 4; ++e2) {
-          const float gv = dx[oh][e2] + dv[e2];
-          const float f = fv[2 * e2], sg = fv[2 * e2 + 1];
-          o[2 * e2] = gv * sg * (1.0f - f * f);
-          o[2 * e2 + 1] = gv * f * sg * (1.0f - sg);
-        }
-        t16_st4(a.dfg + m * 2 * CH + 2 * c0, make_float4(o[0], o[1], o[2], o[3]));
-        t16_st4(a.dfg + m * 2 * CH + 2 * c0 + 4, make_float4(o[4], o[5], o[6], o[7]));
-      }
+      t16_gate_bwd(a, dx, row0 + w, g);
     }
     p0 = p1;
   }
@@ -1617,27 +1633,7 @@ __global__ __launch_bounds__(MAXT) void gcn_bwd_t16b2_kernel(const FusedBwd a, c
         // gate backward (gate_bwd_kernel's arithmetic): g = dxg (+ dskip) -> dfg via (tanh f, sigmoid s)
         const int w = w0 + j;
         if (w >= n) continue;
-        const long m = row0 + w;
-        const bool sk = a.dskip && m >= a.skip_row0;
-#pragma unroll
-        for (int oh = 0; oh < 2; ++oh) {
-          const int c0 = 16 * oh + 4 * g;
-          const float4 f0 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0);
-          const float4 f1 = *(const float4*)(a.fg + m * 2 * CH + 2 * c0 + 4);
-          const float4 dq = sk ? *(const float4*)(a.dskip + (m - a.skip_row0) * a.ld_dskip + c0) : make_float4(0, 0, 0, 0);
-          const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-          const float dv[4] = {dq.x, dq.y, dq.z, dq.w};
-          float o[8];
-#pragma unroll
-          for (int e2 = 0; e2 < 4; ++e2) {
-            const float gv = dx[oh][e2] + dv[e2];
-            const float f = fv[2 * e2], sg = fv[2 * e2 + 1];
-            o[2 * e2] = gv * sg * (1.0f - f * f);
-            o[2 * e2 + 1] = gv * f * sg * (1.0f - sg);
-          }
-          t16_st4(a.dfg + m * 2 * CH + 2 * c0, make_float4(o[0], o[1], o[2], o[3]));
-          t16_st4(a.dfg + m * 2 * CH + 2 * c0 + 4, make_float4(o[4], o[5], o[6], o[7]));
-        }
+        t16_gate_bwd(a, dx, row0 + w, g);
       }
     }
     p0 = p1;
