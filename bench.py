@@ -386,7 +386,7 @@ def measure_dominant(eng, dev, rounds=5, bf16=False, steps=None, extra=None, ext
         # over this bench (tools/gpu.sh pmc:<cfg> + tools/pmc_summary.py: separate --pmc runs for
         # FETCH_SIZE, WRITE_SIZE and the SQ counters; FETCH x2 per the gfx950 correction)
         # (the newest round's committed passes)
-        for rnd in ("r05/final", "r04", "r03"):
+        for rnd in ("r06/final", "r05/final", "r04", "r03"):
             path = os.path.join(ROOT, "profiles", rnd, name)
             if os.path.exists(path):
                 with open(path) as f:
@@ -400,7 +400,7 @@ def measure_dominant(eng, dev, rounds=5, bf16=False, steps=None, extra=None, ext
         # run of this bench (tools/gpu.sh stats:<cfg>): its packet timestamps also hold the dispatch
         # before the first workgroup and the end-of-kernel release after the last
         import csv
-        for rnd in ("r05/final", "r04", "r03"):
+        for rnd in ("r06/final", "r05/final", "r04", "r03"):
             path = os.path.join(ROOT, "profiles", rnd, name)
             if os.path.exists(path):
                 with open(path) as f:

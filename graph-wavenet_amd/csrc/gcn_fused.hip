@@ -71,6 +71,9 @@ size_t t16_lds_bytes(int n, int nsup, int maximg, bool tcn = false) {
 // out] (t16_mlp's 16 ds_read_b32 per piece; the untransposed layout read as ds_read_b128 measured no
 // faster), from the mlp weights W [32][ld_w] (row = mlp output channel): forward M_p = W[:,
 // p-block] (strided 4-B loads), backward M_p = W[:, p-block]^T (rows of W, 16-B loads)
+// (Both of round 6's batched forms of this copy -- a thread's 7 strided loads in flight at once, or
+// W read row by row with 8 loads in flight -- measured 0.5-0.7 % slower per METR step than this
+// element loop, same box; profiles/r06/load_batching.)
 __device__ __forceinline__ void t16_stage_maps(const float* w, int ld_w, bool backward, int npieces, float* dst) {
   if (backward) {
     const int total = npieces * CH * 8;  // float4s
@@ -169,16 +172,20 @@ __device__ __forceinline__ void bn_init(BnRun& bn, float*) {
 // z tile epilogue (fwd_tile_epilogue's arithmetic on the 16-node tile layout): bias, dropout,
 // residual (BN of the layer below applied on load), z or eval-BN output store; the tile's BN
 // partial merged into the wave's running one
+// seed: *a.seed_ptr, read once per workgroup by the caller (t16_seed) -- per tile it was a dependent
+// global load in every epilogue
+__device__ __forceinline__ unsigned long long t16_seed(const FusedFwd& a) {
+  return (a.seed_ptr && a.drop_p > 0.0f) ? *a.seed_ptr : 0ull;
+}
 __device__ __forceinline__ void t16_epilogue(const FusedFwd& a, const f32x4v* hacc, long row0, int w0, int lane,
-                                             int n, BnRun& bn, const float* res_mean = nullptr,
-                                             const float* res_scale = nullptr) {
+                                             int n, BnRun& bn, unsigned long long seed,
+                                             const float* res_mean = nullptr, const float* res_scale = nullptr) {
   if (!res_mean) res_mean = a.res_mean;
   if (!res_scale) res_scale = a.res_scale;
   const int g = lane >> 4, j = lane & 15;
   const int w = w0 + j;
   const bool valid = w < n;
   const long m = row0 + min(w, n - 1);
-  const unsigned long long seed = a.seed_ptr ? *a.seed_ptr : 0ull;
   const float keep_scale = (a.drop_p > 0.0f) ? 1.0f / (1.0f - a.drop_p) : 1.0f;
   float* dst = a.x_out ? a.x_out : a.z;
   float v[8];
@@ -534,13 +541,16 @@ __device__ __forceinline__ void t16_tcn_bn_finalize(const FusedFwd& a, float* tw
   for (int i0 = sub; i0 < f.nparts; i0 += U * nsub) {
     float nb[U], mb[U], qb[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < U; ++u) {  // unconditional loads (a slot past nparts reads slot 0, then counts 0)
       const int i = i0 + u * nsub;
       const float* pp = f.part + (long)(i < f.nparts ? i : 0) * 3 * CH;
-      nb[u] = i < f.nparts ? pp[c] : 0.0f;
+      nb[u] = pp[c];
       mb[u] = pp[CH + c];
       qb[u] = pp[2 * CH + c];
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * nsub >= f.nparts) nb[u] = 0.0f;
 #pragma unroll
     for (int u = 0; u < U; ++u) merge(nb[u], mb[u], qb[u]);
   }
@@ -742,6 +752,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
   BnRun bn;
   bn_init(bn, wpart);
   t16_clock_start(a);
+  const unsigned long long seed = t16_seed(a);
   // the phase's slices staged in one pass (stage_rows4; the channel maps inside its first round
   // trip), else slice by slice; with the fused TCN computed from its inputs (the TCN weights in
   // the BN partials' region until the final flush)
@@ -808,7 +819,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16_kernel(const FusedFwd a, con
           }
         }
       }
-      t16_epilogue(a, hacc, row0, w0, lane, n, bn, res_mean, res_scale);
+      t16_epilogue(a, hacc, row0, w0, lane, n, bn, seed, res_mean, res_scale);
     }
     p0 = p1;
   }
@@ -975,6 +986,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
   BnRun bn;
   bn_init(bn, wpart);
   t16_clock_start(a);
+  const unsigned long long seed = t16_seed(a);
   const bool h16 = ((((uintptr_t)a.h) & 15) | (ldh & 3)) == 0;
   // the channel maps: f32 for t16_mlp, or bf16 MFMA operands for t16_mlp_b (MLPB)
   auto stage_maps = [&] {
@@ -1068,7 +1080,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b_kernel(const FusedFwd a, co
           }
         }
       }
-      t16_epilogue(a, hacc, row0, w0, lane, n, bn);
+      t16_epilogue(a, hacc, row0, w0, lane, n, bn, seed);
     }
     p0 = p1;
   }
@@ -1147,6 +1159,7 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b2_kernel(const FusedFwd a, c
   BnRun bn;
   bn_init(bn, wpart);
   t16_clock_start(a);
+  const unsigned long long seed = t16_seed(a);
   for (long p0 = rg.tb; p0 < rg.te;) {
     const int q0 = (int)(p0 / nt);
     const long p1 = min(rg.te, (long)(q0 + maximg / 2) * nt);
@@ -1210,8 +1223,8 @@ __global__ __launch_bounds__(MAXT) void gcn_fwd_t16b2_kernel(const FusedFwd a, c
           }
         }
       }
-      t16_epilogue(a, haccA, rowA, w0, lane, n, bn);
-      if (okB) t16_epilogue(a, haccB, rowB, w0, lane, n, bn);
+      t16_epilogue(a, haccA, rowA, w0, lane, n, bn, seed);
+      if (okB) t16_epilogue(a, haccB, rowB, w0, lane, n, bn, seed);
     }
     p0 = p1;
   }
@@ -1845,7 +1858,9 @@ int gwn_gcn_fused_fwd_launch(const gwn_gcn_args* g, float* bn_part, hipStream_t 
       const int span2 = (int)((per2 - 1 + nt - 1) / nt) + 1;
       const int maximg2 = 2 * (gmax2 < span2 ? gmax2 : span2);
       const bool h16 = ((((uintptr_t)a.h) & 15) | (a.ld_h & 3)) == 0;
-      if (g->split_planes == 2 && gmax2 >= 1 && h16) {
+      // (pairs from ~10 units per CU, as the backward: PEMS' 64-slice layer ran 25.2 us paired
+      // against 23.6 us with single slices)
+      if (g->split_planes == 2 && gmax2 >= 1 && h16 && units2 >= 10L * grid2) {
         static bool attr2 = false;
         if (!attr2) {
           (void)hipFuncSetAttribute((const void*)gcn_fwd_t16b2_kernel<768>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -110,19 +110,30 @@ __global__ void adp_bwd_kernel(const float* e1, const float* e2, const float* ad
   float dot = 0.0f;
   for (int w = threadIdx.x; w < n; w += 256) dot += adp[(long)v * ld + w] * dadp[(long)v * ld + w];
   dot = block_sum<256>(dot, sh);
-  float pe[ADP_MAXD];
+  float pe[ADP_MAXD], ev[ADP_MAXD];
 #pragma unroll
-  for (int k = 0; k < ADP_MAXD; ++k) pe[k] = 0.0f;
+  for (int k = 0; k < ADP_MAXD; ++k) {
+    pe[k] = 0.0f;
+    ev[k] = e1[(long)v * d + min(k, d - 1)];
+  }
   for (int w = threadIdx.x; w < ld; w += 256) {
+    // the column's embedding values and the row's adp / dadp all requested before the first use
+    // (the k loop loaded e2 one value per memory round trip)
+    const int wc = min(w, n - 1);
+    float e2v[ADP_MAXD];
+#pragma unroll
+    for (int k = 0; k < ADP_MAXD; ++k) e2v[k] = e2[(long)min(k, d - 1) * n + wc];
+    const float a = adp[(long)v * ld + wc], da = dadp[(long)v * ld + wc];
     float g = 0.0f;
     if (w < n) {
       float l = 0.0f;
-      for (int k = 0; k < d; ++k) l = fmaf(e1[(long)v * d + k], e2[(long)k * n + w], l);
-      const float a = adp[(long)v * ld + w];
-      g = (l > 0.0f) ? a * (dadp[(long)v * ld + w] - dot) : 0.0f;
 #pragma unroll
       for (int k = 0; k < ADP_MAXD; ++k)
-        if (k < d) pe[k] = fmaf(g, e2[(long)k * n + w], pe[k]);
+        if (k < d) l = fmaf(ev[k], e2v[k], l);
+      g = (l > 0.0f) ? a * (da - dot) : 0.0f;
+#pragma unroll
+      for (int k = 0; k < ADP_MAXD; ++k)
+        if (k < d) pe[k] = fmaf(g, e2v[k], pe[k]);
     }
     dl[(long)v * ld + w] = g;
   }
@@ -154,11 +165,23 @@ __global__ __launch_bounds__(1024) void adp_bwd_e2_kernel(const float* e1, const
 #pragma unroll
   for (int k = 0; k < ADP_MAXD; ++k) acc[k] = 0.0f;
   if (w < n) {
-    for (int v = tv; v < n; v += 64) {
-      const float g = dl[(long)v * ld + w];
+    // four rows' loads in flight per round (the same v order of the sums)
+    for (int v0 = tv; v0 < n; v0 += 4 * 64) {
+      float gq[4], eq[4][ADP_MAXD];
 #pragma unroll
-      for (int k = 0; k < ADP_MAXD; ++k)
-        if (k < d) acc[k] = fmaf(e1[(long)v * d + k], g, acc[k]);
+      for (int u = 0; u < 4; ++u) {
+        const int v = min(v0 + 64 * u, n - 1);
+        gq[u] = dl[(long)v * ld + w];
+#pragma unroll
+        for (int k = 0; k < ADP_MAXD; ++k) eq[u][k] = e1[(long)v * d + min(k, d - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (v0 + 64 * u >= n) break;
+#pragma unroll
+        for (int k = 0; k < ADP_MAXD; ++k)
+          if (k < d) acc[k] = fmaf(eq[u][k], gq[u], acc[k]);
+      }
     }
   }
 #pragma unroll
