@@ -1547,9 +1547,9 @@ def _from_g4(buf, which, slices, n):
     return x.reshape(slices, nt * 16, 32)
 
 
-@pytest.mark.parametrize("n", [16, 207, 325])
-@pytest.mark.parametrize("mode", ["bn_gate", "bn_gate_tg4", "plain", "bn_gate_tg4_mlp", "plain_mlp",
-                                  "bn_gate_tg4_mlp_pairs", "plain_mlp_pairs"])
+@pytest.mark.parametrize("n, mode", [(n, m) for n in (16, 207, 325)
+                                     for m in ("bn_gate", "bn_gate_tg4", "plain", "bn_gate_tg4_mlp", "plain_mlp")]
+                         + [(207, "bn_gate_tg4_mlp_pairs"), (207, "plain_mlp_pairs")])
 def test_gcn_t16_bf16_backward(gpu, n, mode):
     """The bf16 16-node tile backward (gcn_bwd_t16_kernel<1024, true>: gwn_gcn_bwd_args.sup_g4b_t,
     split_planes 1) against fp64, kernel level (model.py:41-55 backward): the BN-backward prologue
@@ -1572,9 +1572,7 @@ def test_gcn_t16_bf16_backward(gpu, n, mode):
     import ctypes
     from gwn_amd import _lib
     from test_gpu_model import _np_uniform
-    pairs = mode.endswith("_pairs")
-    if pairs and n != 207:
-        pytest.skip("the pair kernel's case runs at the bench's n = 207")
+    pairs = mode.endswith("_pairs")  # (the pair kernel's cases run at the bench's n = 207 only)
     mode = mode.replace("_pairs", "")
     planes = 2 if mode.endswith("_mlp") else 1
     mode = mode.replace("_mlp", "")
