@@ -470,8 +470,16 @@ def measure_dominant(eng, dev, rounds=5, bf16=False, steps=None, extra=None, ext
                 "timing": timing}
     t16 = fused and ex._pow_ok(1) and os.environ.get("GWN_GCN_T16", "1") != "0"
     traffic, mfma_busy, src = pmc("pmc_bench_metr.json", "gcn_fwd_t16_kernel") if t16 and N == 207 else (None,) * 3
-    timing["rocprof_avg_us"], timing["rocprof_source"] = (rocprof_avg("metr_kernel_stats.csv", "gcn_fwd_t16_kernel")
-                                                          if t16 and N == 207 else (None, None))
+    # (the committed rocprof pass of the driver's exact command, `python bench.py`, when present:
+    # the stats:metr pass also holds the post-timing legs' slower launches)
+    if t16 and N == 207:
+        timing["rocprof_avg_us"], timing["rocprof_source"] = rocprof_avg("default_cmd_kernel_stats.csv",
+                                                                         "gcn_fwd_t16_kernel")
+        if timing["rocprof_avg_us"] is None:
+            timing["rocprof_avg_us"], timing["rocprof_source"] = rocprof_avg("metr_kernel_stats.csv",
+                                                                             "gcn_fwd_t16_kernel")
+    else:
+        timing["rocprof_avg_us"], timing["rocprof_source"] = None, None
     if fused:
         kname = (("gcn_fwd_t16_kernel<1024> (fused diffusion GCN forward, power schedule, persistent 16-node "
                   "tile waves: one workgroup per CU over an equal tile range; the layer's gated TCN and the "
