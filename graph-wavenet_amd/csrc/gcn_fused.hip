@@ -529,14 +529,10 @@ __device__ __forceinline__ T tcn_uniform(const T& v) {  // an LDS-held value as 
 __device__ __forceinline__ void t16_tcn_bn_finalize(const FusedFwd& a, float* tw, float* scratch) {
   const auto& f = a.tcn.bn;
   const int c = threadIdx.x & 31, sub = threadIdx.x >> 5, nsub = blockDim.x >> 5;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  auto merge = [&](double nb, double mb, double qb) {
-    if (nb <= 0.0) return;
-    const double nn = n + nb, d = mb - mean, w = nb / nn;
-    mean += d * w;
-    m2 += qb + d * d * n * w;
-    n = nn;
-  };
+  // the partials (count, mean, M2) as fp64 sums n, S = sum n_b mean_b, Q = sum (M2_b + n_b mean_b^2):
+  // no division per merge (a Chan merge divides per partial, a serial chain per thread); mean = S/n,
+  // M2 = Q - S mean in fp64 (fp32 inputs: the cancellation costs ~1e-16 (1 + mean^2/var) of var)
+  double n = 0.0, s1 = 0.0, s2 = 0.0;
   constexpr int U = 4;
   for (int i0 = sub; i0 < f.nparts; i0 += U * nsub) {
     float nb[U], mb[U], qb[U];
@@ -552,15 +548,31 @@ __device__ __forceinline__ void t16_tcn_bn_finalize(const FusedFwd& a, float* tw
     for (int u = 0; u < U; ++u)
       if (i0 + u * nsub >= f.nparts) nb[u] = 0.0f;
 #pragma unroll
-    for (int u = 0; u < U; ++u) merge(nb[u], mb[u], qb[u]);
+    for (int u = 0; u < U; ++u) {
+      if (nb[u] <= 0.0f) continue;
+      const double nm = (double)nb[u] * (double)mb[u];
+      n += nb[u];
+      s1 += nm;
+      s2 += (double)qb[u] + nm * (double)mb[u];
+    }
   }
-  scratch[(sub * 3) * CH + c] = (float)n;
-  scratch[(sub * 3 + 1) * CH + c] = (float)mean;
-  scratch[(sub * 3 + 2) * CH + c] = (float)m2;
+  // the nsub sums of a channel: a fixed-order tree in LDS (fp64)
+  double* sd = (double*)scratch;
+  sd[(sub * 3) * CH + c] = n;
+  sd[(sub * 3 + 1) * CH + c] = s1;
+  sd[(sub * 3 + 2) * CH + c] = s2;
   __syncthreads();
+  for (int w = nsub >> 1; w > 0; w >>= 1) {
+    if (sub < w)
+#pragma unroll
+      for (int e = 0; e < 3; ++e) sd[(sub * 3 + e) * CH + c] += sd[((sub + w) * 3 + e) * CH + c];
+    __syncthreads();
+  }
   if (threadIdx.x < CH) {
-    n = mean = m2 = 0.0;
-    for (int q = 0; q < nsub; ++q) merge(scratch[(q * 3) * CH + c], scratch[(q * 3 + 1) * CH + c], scratch[(q * 3 + 2) * CH + c]);
+    n = sd[c];
+    const double mean = n > 0.0 ? sd[CH + c] / n : 0.0;
+    const double m2d = sd[2 * CH + c] - sd[CH + c] * mean;
+    const double m2 = m2d > 0.0 ? m2d : 0.0;
     const double var = n > 0.0 ? m2 / n : 0.0;
     const float rs = (float)(1.0 / sqrt(var + (double)f.eps));
     const float sc = rs * f.gamma[c];  // bn(z) = (z - mean) * sc + beta
@@ -1753,7 +1765,7 @@ T16Plan t16_plan(int n, int nsup, int slices, bool tcn = false) {
 // profiles/r05/tcn_fused)
 // the in-kernel finalize's merge: 32 channels x (blockDim / 32) slot lanes, exchanged through the
 // image space before the first phase is staged
-constexpr size_t T16_BN_SCRATCH = 3 * (64 * T16_WAVES / 32) * CH * sizeof(float);
+constexpr size_t T16_BN_SCRATCH = 3 * (64 * T16_WAVES / 32) * CH * sizeof(double);
 static bool bn_scratch_ok(int n, int nsup, int slices) {
   const T16Plan pl = t16_plan(n, nsup, slices, true);
   return pl.ok && pl.lds >= t16_lds_bytes(n, nsup, 0, true) + T16_BN_SCRATCH;

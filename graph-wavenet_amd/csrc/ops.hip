@@ -421,14 +421,15 @@ __global__ void bn_partial_kernel(const float* z, long rows, int c, float* part)
   }
 }
 
-// Chan merge of the per-chunk BatchNorm partials [nparts][3][c] of channel j over one 256-thread
-// block (strided subsets per thread, then a fixed-order tree); thread 0 returns the totals
+// The per-chunk BatchNorm partials [nparts][3][c] (count, mean, M2) of channel j merged over one
+// 256-thread block as fp64 sums n, S = sum n_b mean_b, Q = sum (M2_b + n_b mean_b^2) (strided subsets
+// per thread, then a fixed-order tree; no division per merge); thread 0 returns n, mean = S / n and
+// M2 = Q - S mean (fp32 inputs: the fp64 cancellation costs ~1e-16 (1 + mean^2 / var) of the variance)
 __device__ void bn_merge_channel(const float* part, int nparts, int c, int j, double& n_out, double& mean_out,
                                  double& m2_out) {
   __shared__ double sn[256], sm[256], sq[256];
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  // a thread's partials (i = tid, tid + 256, ...) are loaded four at a time before they are merged
-  // (same order as one at a time: identical results; the load -> merge loop waited per partial)
+  double n = 0.0, s1 = 0.0, s2 = 0.0;
+  // a thread's partials (i = tid, tid + 256, ...) are loaded four at a time before they are added
   constexpr int U = 4;
   for (int i0 = 0; i0 < nparts; i0 += 256 * U) {
     float nbv[U], mbv[U], m2v[U];
@@ -443,32 +444,27 @@ __device__ void bn_merge_channel(const float* part, int nparts, int c, int j, do
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const double nb = nbv[u];
-      if (nb <= 0.0) continue;
-      const double mb = mbv[u], m2b = m2v[u];
-      const double nn = n + nb;
-      const double delta = mb - mean;
-      mean += delta * nb / nn;
-      m2 += m2b + delta * delta * n * nb / nn;
-      n = nn;
+      if (nbv[u] <= 0.0f) continue;
+      const double nm = (double)nbv[u] * (double)mbv[u];
+      n += nbv[u];
+      s1 += nm;
+      s2 += (double)m2v[u] + nm * (double)mbv[u];
     }
   }
-  sn[threadIdx.x] = n; sm[threadIdx.x] = mean; sq[threadIdx.x] = m2;
+  sn[threadIdx.x] = n; sm[threadIdx.x] = s1; sq[threadIdx.x] = s2;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) {
-      const double na = sn[threadIdx.x], nb = sn[threadIdx.x + w];
-      const double nn = na + nb;
-      if (nb > 0.0) {
-        const double delta = sm[threadIdx.x + w] - sm[threadIdx.x];
-        sm[threadIdx.x] += delta * nb / nn;
-        sq[threadIdx.x] += sq[threadIdx.x + w] + delta * delta * na * nb / nn;
-        sn[threadIdx.x] = nn;
-      }
+      sn[threadIdx.x] += sn[threadIdx.x + w];
+      sm[threadIdx.x] += sm[threadIdx.x + w];
+      sq[threadIdx.x] += sq[threadIdx.x + w];
     }
     __syncthreads();
   }
-  n_out = sn[0]; mean_out = sm[0]; m2_out = sq[0];
+  n_out = sn[0];
+  mean_out = n_out > 0.0 ? sm[0] / n_out : 0.0;
+  const double m2 = sq[0] - sm[0] * mean_out;
+  m2_out = m2 > 0.0 ? m2 : 0.0;
 }
 
 __global__ void bn_finalize_kernel(const float* part, int nparts, int c, float momentum, float eps,
