@@ -533,7 +533,7 @@ __device__ __forceinline__ void t16_tcn_bn_finalize(const FusedFwd& a, float* tw
   // no division per merge (a Chan merge divides per partial, a serial chain per thread); mean = S/n,
   // M2 = Q - S mean in fp64 (fp32 inputs: the cancellation costs ~1e-16 (1 + mean^2/var) of var)
   double n = 0.0, s1 = 0.0, s2 = 0.0;
-  constexpr int U = 4;
+  constexpr int U = 12;  // (768 partials: two rounds of loads per thread)
   for (int i0 = sub; i0 < f.nparts; i0 += U * nsub) {
     float nb[U], mb[U], qb[U];
 #pragma unroll
