@@ -76,6 +76,30 @@ __global__ void adp_fwd_kernel(const float* e1, const float* e2, int n, int d, f
   e1 += (long)blockIdx.y * n * d;
   e2 += (long)blockIdx.y * d * n;
   adp += (long)blockIdx.y * adp_bstride;
+  if (n <= 256 && d <= 16) {
+    // one column per thread: its d embedding loads issued together, the logit kept in a register
+    // (the loop form below re-derived it per pass with a memory round trip per k); the same fma
+    // order, exp and scaling, so the same values
+    const int w = threadIdx.x;
+    const bool on = w < n;
+    float e1v[16], e2v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      e1v[k] = k < d ? e1[(long)v * d + k] : 0.0f;
+      e2v[k] = (k < d && on) ? e2[(long)k * n + w] : 0.0f;
+    }
+    float l = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < d) l = fmaf(e1v[k], e2v[k], l);
+    l = fmaxf(l, 0.0f);
+    const float mx = block_max<256>(on ? l : -INFINITY, sh);
+    const float ex = on ? expf(l - mx) : 0.0f;
+    const float sum = block_sum<256>(ex, sh);
+    const float inv = 1.0f / sum;
+    for (int c = threadIdx.x; c < ld; c += 256) adp[(long)v * ld + c] = (c < n) ? ex * inv : 0.0f;
+    return;
+  }
   float mx = -INFINITY;
   for (int w = threadIdx.x; w < n; w += 256) {
     float l = 0.0f;
